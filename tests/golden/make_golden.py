@@ -1,0 +1,356 @@
+#!/usr/bin/env python3
+"""Generate the committed golden fixtures by running the REFERENCE's own code (this container only).
+
+Run:  python tests/golden/make_golden.py   (needs /root/reference; never runs on the GPU box)
+
+The reference is imported from /root/reference with the stubs of _refstubs.py;
+its pure-Torch CPU path (tinycudann absent) is the parity oracle.  Only inputs and outputs are
+written (npz, loadable with allow_pickle=False) plus scene geometry as JSON; no reference source
+is copied.  Hash tables are formula-filled (adaptive_city_nerf_amd/synthetic.py) so the 128 MiB
+tables are regenerated from (seed, scale) instead of stored.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+HERE = Path(__file__).resolve().parent
+REPO = HERE.parent.parent
+REF = Path(os.environ.get("ACN_REFERENCE", "/root/reference"))
+sys.path.insert(0, str(REPO))
+sys.path.insert(0, str(HERE))
+
+import _refstubs  # noqa: E402
+
+_refstubs.install()
+sys.path.insert(0, str(REF))
+
+import warnings  # noqa: E402
+
+warnings.filterwarnings("ignore")
+
+from adaptive_city_nerf_amd.synthetic import formula_table  # noqa: E402
+from models.encodings import HashGridEncoder, SHEncoder  # noqa: E402
+from models.inr.meta_container import MetaContainer  # noqa: E402
+from nerfs.ray_rendering import render_rays, volume_render, render_image  # noqa: E402
+from nerfs.ray_sampling import clamp_rays_near_far, get_ray_directions, get_rays  # noqa: E402
+from nerfs.scene_box import SceneBox  # noqa: E402
+
+DATA = REF / "data" / "drz" / "out" / "example"
+TABLE_SCALE = 0.5          # U(-0.5, 0.5) so sigma/colour vary
+BM_RUNTIME = 1.05          # nerf_runner.py:150  min(max(1, --bm=1.05), params 1.1)
+F32 = np.float32
+
+
+def _np(t: torch.Tensor) -> np.ndarray:
+    return t.detach().cpu().numpy().copy()
+
+
+def save(name: str, **arrays) -> None:
+    meta = {"torch": torch.__version__, "numpy": np.__version__, "generator": "tests/golden/make_golden.py"}
+    arrays["_meta"] = np.array(json.dumps(meta))
+    np.savez_compressed(HERE / f"{name}.npz", **arrays)
+    print("wrote", name, {k: getattr(v, "shape", None) for k, v in arrays.items()})
+
+
+# ----------------------------------------------------------------------------------------------
+def scene_json() -> dict:
+    coords = torch.load(DATA / "coordinates.pt", map_location="cpu", weights_only=True)
+    vmeta = torch.load(DATA / "val" / "metadata" / "000000.pt", map_location="cpu", weights_only=True)
+    out = {
+        "pose_scale_factor": float(coords["pose_scale_factor"]),
+        "val_cam0": {
+            "H": int(vmeta["H"]), "W": int(vmeta["W"]),
+            "c2w": _np(vmeta["c2w"].float()).tolist(),
+            "intrinsics": _np(vmeta["intrinsics"].float()).tolist(),
+        },
+        "masks": {},
+    }
+    for mask in ["g11_grid_bm110_ss11", "g22_grid_bm110_ss11"]:
+        p = torch.load(DATA / "masks" / mask / "params.pt", map_location="cpu", weights_only=True)
+        b = torch.load(DATA / "masks" / mask / "scene_boxes.pt", map_location="cpu", weights_only=True)
+        out["masks"][mask] = {
+            "centroids": _np(p["centroids"].float()).tolist(),
+            "cluster_2d": bool(p["cluster_2d"]),
+            "boundary_margin": float(p["boundary_margin"]),
+            "aabb_global": _np(b["aabb_global"].float()).tolist(),
+            "mins": _np(b["mins"].float()).tolist(),
+            "maxs": _np(b["maxs"].float()).tolist(),
+        }
+    return out
+
+
+def build_container(scene: dict, mask: str, seed: int = 0, table_seed0: int = 100):
+    m = scene["masks"][mask]
+    K = len(m["centroids"])
+    gbox = SceneBox(aabb=torch.tensor(m["aabb_global"], dtype=torch.float32))
+    boxes = [SceneBox(aabb=torch.tensor([m["mins"][k], m["maxs"][k]], dtype=torch.float32)) for k in range(K)]
+    hash_conf = {"levels": 16, "features_per_level": 2, "log2_hashmap_size": 20,
+                 "max_res": 4096, "min_res": 16, "interpolation": "Linear"}
+    torch.manual_seed(seed)
+    model = MetaContainer(
+        num_submodules=K, centroids=torch.tensor(m["centroids"], dtype=torch.float32),
+        aabb=gbox.aabb, nerf_variant="instant", boundary_margin=min(max(1.0, BM_RUNTIME), m["boundary_margin"]),
+        cluster_2d=m["cluster_2d"], joint_training=False, use_bg_nerf=True, bg_hidden=32,
+        bg_encoding="spherical", occ_conf={"use_occ": False}, expert_box_list=boxes, hidden=64,
+        sigma_depth=2, color_depth=2, dir_encoding="spherical", color_hidden=64,
+        use_sigmoid_rgb=True, hash_enc_conf=hash_conf,
+    )
+    with torch.no_grad():
+        for k, sub in enumerate(model.submodules):
+            tab = formula_table(16, 20, 2, seed=table_seed0 + k, scale=TABLE_SCALE)
+            sub.xyz_encoder.hash_table.data.copy_(torch.from_numpy(tab))
+    model.eval()
+    return model, gbox
+
+
+def weights_dict(model) -> dict:
+    """MLP + background weights keyed by the reference state-dict names (tables excluded)."""
+    out = {}
+    for k, v in model.state_dict().items():
+        if k.endswith("hash_table"):
+            continue
+        out["w:" + k] = _np(v.float()).copy()   # copy: state_dict tensors alias live params
+    return out
+
+
+def val_rays(scene: dict, mask: str, downscale: float) -> torch.Tensor:
+    cam = scene["val_cam0"]
+    H = int(round(cam["H"] * downscale)); W = int(round(cam["W"] * downscale))
+    fx, fy, cx, cy = (torch.tensor(cam["intrinsics"]) * downscale).tolist()
+    intr = torch.tensor(cam["intrinsics"], dtype=torch.float32) * downscale
+    fx, fy, cx, cy = [float(v) for v in intr]
+    dirs = get_ray_directions(H, W, fx, fy, cx, cy, True, device=torch.device("cpu"))
+    m = scene["masks"][mask]
+    gbox = SceneBox(aabb=torch.tensor(m["aabb_global"], dtype=torch.float32))
+    rays = get_rays(dirs, torch.tensor(cam["c2w"], dtype=torch.float32), scene_box=gbox).view(-1, 8)
+    psf = scene["pose_scale_factor"]
+    rays, valid = clamp_rays_near_far(rays, near_far_override=(0.0 / psf, 100000 / psf))
+    return rays, valid, (H, W, fx, fy, cx, cy)
+
+
+# ----------------------------------------------------------------------------------------------
+def gen_hashgrid() -> None:
+    g = torch.Generator().manual_seed(0)
+    x = torch.rand(4096, 3, generator=g)
+    edge = torch.tensor([[0.0, 0.0, 0.0], [1.0, 1.0, 1.0], [1e-6, 1e-6, 1e-6], [1 - 1e-6, 0.5, 1e-6],
+                         [0.5, 0.5, 0.5], [0.25, 0.75, 0.125], [1.0 / 16, 2.0 / 23, 3.0 / 33],
+                         [4095.0 / 4095, 7.0 / 4095, 0.999999]], dtype=torch.float32)
+    x = torch.cat([x, edge], 0)
+    variants = [
+        ("lin_L16_T20", dict(levels=16, min_res=16, max_res=4096, log2_hashmap_size=20, interpolation="Linear"), 7),
+        ("near_L16_T12", dict(levels=16, min_res=16, max_res=4096, log2_hashmap_size=12, interpolation="Nearest"), 8),
+        ("smooth_L16_T12", dict(levels=16, min_res=16, max_res=4096, log2_hashmap_size=12, interpolation="Smoothstep"), 9),
+        ("lin_L4_T19", dict(levels=4, min_res=16, max_res=4096, log2_hashmap_size=19, interpolation="Linear"), 10),
+        ("lin_L8_T14_r2_512", dict(levels=8, min_res=2, max_res=512, log2_hashmap_size=14, interpolation="Linear"), 11),
+    ]
+    out = {"x01": _np(x)}
+    for name, kw, seed in variants:
+        enc = HashGridEncoder(features_per_level=2, implementation="torch", **kw)
+        tab = formula_table(kw["levels"], kw["log2_hashmap_size"], 2, seed=seed, scale=TABLE_SCALE)
+        with torch.no_grad():
+            enc.hash_table.data.copy_(torch.from_numpy(tab))
+            y = enc(x)
+        out[f"{name}:y"] = _np(y)
+        out[f"{name}:resolutions"] = _np(enc.level_resolutions)
+        out[f"{name}:cfg"] = np.array([kw["levels"], kw["min_res"], kw["max_res"], kw["log2_hashmap_size"], seed,
+                                       {"Nearest": 0, "Linear": 1, "Smoothstep": 2}[kw["interpolation"]]], np.int64)
+        # backward: d/dtable of <y, g> for a fixed cotangent (scatter-add semantics of index backward)
+        if kw["log2_hashmap_size"] <= 14:
+            enc.hash_table.grad = None
+            gy = torch.randn(y.shape, generator=g)
+            y2 = enc(x)
+            (y2 * gy).sum().backward()
+            out[f"{name}:gy"] = _np(gy)
+            out[f"{name}:gtable"] = _np(enc.hash_table.grad)
+    save("hashgrid", **out)
+
+
+def gen_sh() -> None:
+    g = torch.Generator().manual_seed(1)
+    d = torch.randn(1024, 3, generator=g) * 3.0
+    d[0] = torch.tensor([0.0, 0.0, 0.0]); d[1] = torch.tensor([0.0, 0.0, -1.0]); d[2] = torch.tensor([1e-12, 0, 0])
+    out = {"d": _np(d)}
+    for lv in range(1, 6):
+        enc = SHEncoder(levels=lv, implementation="torch")
+        out[f"levels{lv}"] = _np(enc(d))
+    save("sh", **out)
+
+
+def gen_volume_render() -> None:
+    g = torch.Generator().manual_seed(2)
+    N, S = 256, 64
+    rgb = torch.rand(N, S, 3, generator=g) * 1.4 - 0.2                 # exercises clamp(0,1)
+    sig = torch.exp(torch.rand(N, S, generator=g) * 14 - 7) - 0.01     # (-0.01, ~1e3): clamp_min(0)
+    sig[:8] *= 1e3                                                      # saturated rays
+    rgb_sigma = torch.cat([rgb, sig[..., None]], -1)
+    near = torch.rand(N, 1, generator=g) * 0.1
+    steps = torch.rand(N, S, generator=g) * 0.01
+    steps[:, 5] = 1e-6                                                  # exercises the 1e-4 clamp
+    t_vals = near + torch.cumsum(steps, 1)
+    bg = torch.rand(N, 3, generator=g)
+    a = volume_render(rgb_sigma, t_vals, bg_rgb=bg)
+    b = volume_render(rgb_sigma * 3 - 1, t_vals, bg_rgb=None, raw_rgb=True, raw_sigma=True, sigma_scale=2.0)
+    out = {"rgb_sigma": _np(rgb_sigma), "t_vals": _np(t_vals), "bg": _np(bg)}
+    for tag, res in (("a", a), ("b", b)):
+        for nm, v in zip(("rgb", "depth", "weights", "acc"), res):
+            out[f"{tag}:{nm}"] = _np(v)
+    save("volume_render", **out)
+
+
+def gen_field_and_render(scene: dict) -> None:
+    # --- single expert (g11): field forward on random points + end-to-end render --------------
+    for mask, tag in (("g11_grid_bm110_ss11", "k1"), ("g22_grid_bm110_ss11", "k4")):
+        model, gbox = build_container(scene, mask)
+        K = len(model.submodules)
+        w = weights_dict(model)
+        g = torch.Generator().manual_seed(3)
+        out = dict(w)
+        # field samples inside the global box (+ a few outside to exercise the clamp)
+        lo = gbox.min; hi = gbox.max
+        x = lo + (hi - lo) * (torch.rand(4096, 3, generator=g) * 1.1 - 0.05)
+        d = torch.randn(4096, 3, generator=g)
+        x_d = torch.cat([x, d], -1)
+        with torch.no_grad():
+            y_expert0 = model.submodules[0](x_d)
+            y_cont = model(x_d)
+        out.update({"field:x_d": _np(x_d), "field:y_expert0": _np(y_expert0), "field:y_container": _np(y_cont)})
+        # rays from val camera 0 at downscale 0.25, 512 seeded rays, S=64
+        rays, valid, cam = val_rays(scene, mask, 0.25)
+        rv = rays[valid]
+        perm = torch.randperm(rv.shape[0], generator=torch.Generator().manual_seed(0))[:512]
+        r512 = rv[perm].contiguous()
+        with torch.no_grad():
+            res = render_rays(model, r512, ray_samples=64, params=None, active_module=None,
+                              bg_color_default="white", chunk=1_000_000)
+            res_a0 = render_rays(model, r512, ray_samples=64, params=None, active_module=0,
+                                 bg_color_default="white", chunk=1_000_000)
+        out["render:rays"] = _np(r512)
+        for nm, v in zip(("rgb", "depth", "weights", "acc"), res):
+            out[f"render:{nm}"] = _np(v)
+        for nm, v in zip(("rgb", "depth", "weights", "acc"), res_a0):
+            out[f"render_a0:{nm}"] = _np(v)
+        # fast weights: perturbed MLP params passed through `params` (meta_core.py:26-66 style)
+        gp = torch.Generator().manual_seed(4)
+        fast = {}
+        for name, p in model.meta_named_parameters():
+            fast[name] = (p.detach() + 0.05 * torch.randn(p.shape, generator=gp)).float()
+        with torch.no_grad():
+            resf = render_rays(model, r512, ray_samples=64, params=fast, active_module=None,
+                               bg_color_default="white", chunk=1_000_000)
+        for name, v in fast.items():
+            out["fast:" + name] = _np(v)
+        for nm, v in zip(("rgb", "depth", "weights", "acc"), resf):
+            out[f"render_fast:{nm}"] = _np(v)
+        # high-contrast variant: MLP weights scaled x3 in place, so sigma spans orders of magnitude
+        # and colours saturate (a far stronger parity check than the near-constant default init)
+        with torch.no_grad():
+            for name, p in model.meta_named_parameters():
+                if name.endswith("weight"):
+                    p.mul_(3.0)
+            for sub in model.submodules:
+                sub.sigma_head.bias.fill_(0.5)
+            resh = render_rays(model, r512, ray_samples=64, params=None, active_module=None,
+                               bg_color_default="white", chunk=1_000_000)
+            y_hi = model(x_d)
+        for k2, v2 in weights_dict(model).items():
+            out["hi" + k2] = v2
+        out["field_hi:y_container"] = _np(y_hi)
+        for nm, v in zip(("rgb", "depth", "weights", "acc"), resh):
+            out[f"render_hi:{nm}"] = _np(v)
+        # full (small) frame through render_image at downscale 1/32 (48x64 rays, S=32)
+        cam0 = scene["val_cam0"]; ds = 1.0 / 32
+        H = int(round(cam0["H"] * ds)); W = int(round(cam0["W"] * ds))
+        intr = torch.tensor(cam0["intrinsics"], dtype=torch.float32) * ds
+        with torch.no_grad():
+            img, dep, acc = render_image(model, H=H, W=W, fx=float(intr[0]), fy=float(intr[1]), cx=float(intr[2]),
+                                         cy=float(intr[3]), c2w=torch.tensor(cam0["c2w"], dtype=torch.float32),
+                                         scene_box=gbox, ray_samples=32, chunk_points=1 << 16)
+        out.update({"image:rgb": _np(img), "image:depth": _np(dep), "image:acc": _np(acc),
+                    "image:hw": np.array([H, W], np.int64)})
+        out["table_seeds"] = np.array([100 + k for k in range(K)], np.int64)
+        out["table_scale"] = np.array(TABLE_SCALE, np.float64)
+        out["bm"] = np.array(model.boundary_margin, np.float64)
+        save(f"render_{tag}", **out)
+        del model
+
+
+def gen_routing(scene: dict) -> None:
+    m = scene["masks"]["g22_grid_bm110_ss11"]
+    K = len(m["centroids"])
+    gbox = SceneBox(aabb=torch.tensor(m["aabb_global"], dtype=torch.float32))
+    boxes = [SceneBox(aabb=torch.tensor([m["mins"][k], m["maxs"][k]], dtype=torch.float32)) for k in range(K)]
+    g = torch.Generator().manual_seed(5)
+    n = 8192
+    pts = torch.empty(n, 3)
+    pts[:, 0] = torch.rand(n, generator=g) * 0.5
+    yz = torch.rand(n, 2, generator=g) * 2.2 - 1.1
+    # concentrate half of the points in a thin band around the Voronoi bisectors y=0 / z=0
+    band = torch.rand(n // 2, 2, generator=g) * 0.1 - 0.05
+    yz[: n // 4, 0] = band[: n // 4, 0]
+    yz[n // 4: n // 2, 1] = band[n // 4:, 1]
+    pts[:, 1:] = yz
+    out = {"pts": _np(pts)}
+    for bm in (1.05, 1.0):
+        torch.manual_seed(0)
+        cont = MetaContainer(
+            num_submodules=K, centroids=torch.tensor(m["centroids"]), aabb=gbox.aabb, boundary_margin=bm,
+            cluster_2d=True, use_bg_nerf=False, occ_conf={"use_occ": False}, expert_box_list=boxes,
+            hidden=8, sigma_depth=1, color_depth=1, color_hidden=8, geo_feat_dim=3,
+            hash_enc_conf={"levels": 2, "log2_hashmap_size": 8},
+        )
+        W, hard = cont._routing(pts)
+        if W is not None:
+            out[f"bm{bm}:W"] = _np(W)
+        else:
+            out[f"bm{bm}:hard"] = _np(hard)
+    out["centroids"] = np.array(m["centroids"], F32)
+    save("routing", **out)
+
+
+def gen_rays(scene: dict) -> None:
+    out = {}
+    for ds, tag in ((1.0 / 16, "ds16"), (0.25, "ds4")):
+        rays, valid, cam = val_rays(scene, "g22_grid_bm110_ss11", ds)
+        H, W, fx, fy, cx, cy = cam
+        dirs = get_ray_directions(H, W, fx, fy, cx, cy, True, device=torch.device("cpu"))
+        if tag == "ds4":       # keep the fixture small: every 7th ray of the 384x512 frame
+            sel = torch.arange(0, rays.shape[0], 7)
+            out[f"{tag}:sel"] = _np(sel)
+            rays = rays[sel]; valid = valid[sel]; dirs = dirs.view(-1, 3)[sel]
+        out[f"{tag}:rays"] = _np(rays)
+        out[f"{tag}:valid"] = _np(valid)
+        out[f"{tag}:dirs"] = _np(dirs.reshape(-1, 3))
+        out[f"{tag}:cam"] = np.array([H, W, fx, fy, cx, cy], np.float64)
+    # a synthetic camera whose rays miss the box (invalid -> +inf near/far; NaN downstream, §8(a3))
+    m = scene["masks"]["g22_grid_bm110_ss11"]
+    gbox = SceneBox(aabb=torch.tensor(m["aabb_global"], dtype=torch.float32))
+    c2w = torch.tensor([[1.0, 0, 0, 5.0], [0, 1.0, 0, 5.0], [0, 0, 1.0, 5.0]])
+    dirs = get_ray_directions(8, 8, 4.0, 4.0, 4.0, 4.0, False, device=torch.device("cpu"))
+    r = get_rays(dirs, c2w, scene_box=gbox).view(-1, 8)
+    r2, v2 = clamp_rays_near_far(r, near_far_override=(None, None))
+    out.update({"miss:rays_raw": _np(r), "miss:rays": _np(r2), "miss:valid": _np(v2)})
+    save("rays", **out)
+
+
+def main() -> None:
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    scene = scene_json()
+    (HERE / "scene_drz_example.json").write_text(json.dumps(scene, indent=1))
+    print("wrote scene_drz_example.json")
+    which = sys.argv[1:] or ["hashgrid", "sh", "volume_render", "routing", "rays", "render"]
+    if "hashgrid" in which: gen_hashgrid()
+    if "sh" in which: gen_sh()
+    if "volume_render" in which: gen_volume_render()
+    if "routing" in which: gen_routing(scene)
+    if "rays" in which: gen_rays(scene)
+    if "render" in which: gen_field_and_render(scene)
+
+
+if __name__ == "__main__":
+    main()
