@@ -1,0 +1,123 @@
+"""ctypes binding of libacnerf.so (the C ABI declared in include/acnerf.h).
+
+This is the Python-side FFI stub of the drop-in boundary: every call passes raw device pointers
+of torch tensors (owned by PyTorch's caching allocator) plus the current HIP stream.  There is no
+CPU fallback: if the library or a HIP device is missing, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+from pathlib import Path
+
+import torch  # must be imported before the library: libacnerf.so binds torch's libamdhip64.so.7
+
+PKG = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("ACNERF_LIB", PKG / "libacnerf.so"))
+
+ACN_MAX_LEVELS = 32
+ACN_MAX_EXPERTS = 16
+ACN_BG_NONE, ACN_BG_CONST, ACN_BG_MLP = 0, 1, 2
+INTERP = {"Nearest": 0, "Linear": 1, "Smoothstep": 2}
+
+
+class AcnError(RuntimeError):
+    pass
+
+
+class acn_expert(C.Structure):
+    _fields_ = [
+        ("table", C.c_void_p),
+        ("L", C.c_int32), ("log2T", C.c_int32), ("F", C.c_int32), ("interp", C.c_int32),
+        ("res", C.c_int32 * ACN_MAX_LEVELS),
+        ("aabb_min", C.c_float * 3), ("aabb_extent", C.c_float * 3),
+        ("sig_w0", C.c_void_p), ("sig_b0", C.c_void_p),
+        ("sig_w1", C.c_void_p), ("sig_b1", C.c_void_p),
+        ("sigh_w", C.c_void_p), ("sigh_b", C.c_void_p),
+        ("geo_w", C.c_void_p), ("geo_b", C.c_void_p),
+        ("col_w0", C.c_void_p), ("col_b0", C.c_void_p),
+        ("col_w1", C.c_void_p), ("col_b1", C.c_void_p),
+        ("col_w2", C.c_void_p), ("col_b2", C.c_void_p),
+    ]
+
+
+class acn_routing(C.Structure):
+    _fields_ = [("K", C.c_int32), ("cluster_2d", C.c_int32), ("boundary_margin", C.c_float),
+                ("centroids", (C.c_float * 3) * ACN_MAX_EXPERTS)]
+
+
+class acn_background(C.Structure):
+    _fields_ = [("mode", C.c_int32), ("hidden", C.c_int32), ("color", C.c_float * 3),
+                ("w1", C.c_void_p), ("b1", C.c_void_p), ("w2", C.c_void_p), ("b2", C.c_void_p)]
+
+
+_lib = None
+_lock = threading.Lock()
+vp, i64, i32, f32, sz = C.c_void_p, C.c_int64, C.c_int, C.c_float, C.c_size_t
+
+SIGNATURES = {
+    "acn_version": ([], C.c_int),
+    "acn_last_error": ([C.c_char_p, sz], C.c_int),
+    "acn_hashgrid_fwd": ([vp, i64, vp, vp, i32, i32, i32, i32, vp, vp], C.c_int),
+    "acn_hashgrid_bwd": ([vp, i64, vp, vp, i32, i32, i32, i32, vp, vp], C.c_int),
+    "acn_sh_fwd": ([vp, i64, i32, vp, vp], C.c_int),
+    "acn_workspace_bytes": ([i32], sz),
+    "acn_field_fwd": ([vp, i64, i64, vp, vp, i32, vp, sz, vp, vp], C.c_int),
+    "acn_volume_render_fwd": ([vp, vp, vp, i64, i32, i32, i32, f32, vp, vp, vp, vp, vp], C.c_int),
+    "acn_render_stratified_fwd": ([vp, i64, i32, vp, vp, vp, i32, vp, f32, f32, vp, sz, vp, vp, vp, vp, vp],
+                                  C.c_int),
+    "acn_get_rays": ([i32, i32, f32, f32, f32, f32, i32, vp, vp, f32, f32, i32, f32, i32, f32, i32, vp, vp, vp],
+                     C.c_int),
+    "acn_ray_directions": ([i32, i32, f32, f32, f32, f32, i32, vp, vp], C.c_int),
+    "acn_rays_from_dirs": ([vp, i64, vp, vp, f32, f32, f32, f32, f32, vp, vp], C.c_int),
+    "acn_ray_aabb": ([vp, vp, i64, vp, f32, f32, f32, vp, vp, vp], C.c_int),
+    "acn_clamp_rays": ([vp, i64, i32, i32, f32, i32, f32, f32, f32, vp, vp], C.c_int),
+    "acn_routing_fwd": ([vp, i64, i64, vp, vp, vp, vp], C.c_int),
+    "acn_background_fwd": ([vp, i64, vp, vp, vp], C.c_int),
+}
+
+
+def lib():
+    """Load libacnerf.so (once).  Raises if it is missing: there is no fallback path."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not LIB_PATH.exists():
+                raise AcnError(f"libacnerf.so not found at {LIB_PATH}; build it with "
+                               f"`python -c 'import __graft_entry__ as g; g.build()'` (or make -C "
+                               f"adaptive_city_nerf_amd/csrc)")
+            L = C.CDLL(str(LIB_PATH))
+            for name, (args, res) in SIGNATURES.items():
+                fn = getattr(L, name)
+                fn.argtypes = args
+                fn.restype = res
+            _lib = L
+    return _lib
+
+
+def exported_symbols():
+    return list(SIGNATURES)
+
+
+def check(status: int, what: str) -> None:
+    if status != 0:
+        buf = C.create_string_buffer(512)
+        lib().acn_last_error(buf, 512)
+        raise AcnError(f"{what} failed (status {status}): {buf.value.decode(errors='replace')}")
+
+
+def ptr(t) -> int:
+    return 0 if t is None else int(t.data_ptr())
+
+
+def stream_of(t: torch.Tensor) -> int:
+    return int(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def require_hip(t: torch.Tensor, what: str) -> None:
+    if not (isinstance(t, torch.Tensor) and t.is_cuda):
+        raise AcnError(f"{what}: the HIP implementation needs tensors on a HIP device (got "
+                       f"{getattr(t, 'device', type(t))}); there is no CPU fallback")

@@ -1,0 +1,206 @@
+// encoders.hip -- standalone HashGridEncoder forward/backward and SHEncoder forward (gfx950).
+//
+// Replaces models/encodings.py:331-381 (HashGridEncoder._torch_forward, _hash :308-316, _gather
+// :318-329) and :133-151 (SHEncoder.forward).  One lane per (point, level): the L lanes of a
+// point are adjacent, so the (M, L*F) output row of a point is written as one contiguous
+// L*F*4-byte segment (128 B for the reference's L=16, F=2) and the point's x01 is a broadcast.
+#include "acn_device.h"
+#include "acn_internal.h"
+
+namespace {
+
+struct Res32 {
+    int32_t v[ACN_MAX_LEVELS];
+};
+
+template <int INTERP>
+__global__ void __launch_bounds__(256) hashgrid_fwd_f2(const float* __restrict__ x01, int64_t M,
+                                                       const float2* __restrict__ table, Res32 res,
+                                                       int L, int log2T, float2* __restrict__ out) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t m = gid / L;
+    const int l = (int)(gid - m * L);
+    if (m >= M) return;
+    const float r = (float)res.v[l];
+    const float sx = x01[3 * m] * r, sy = x01[3 * m + 1] * r, sz = x01[3 * m + 2] * r;
+    const uint32_t mask = (uint32_t)((1ull << log2T) - 1ull);
+    const float2* tl = table + ((int64_t)l << log2T);
+    float o0, o1;
+    acn::hash_level_f2<INTERP>(tl, sx, sy, sz, mask, o0, o1);
+    out[m * L + l] = make_float2(o0, o1);
+}
+
+// generic feature count (F != 2)
+template <int INTERP>
+__global__ void __launch_bounds__(256) hashgrid_fwd_gen(const float* __restrict__ x01, int64_t M,
+                                                        const float* __restrict__ table, Res32 res, int L,
+                                                        int log2T, int F, float* __restrict__ out) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t m = gid / L;
+    const int l = (int)(gid - m * L);
+    if (m >= M) return;
+    const float r = (float)res.v[l];
+    const float sx = x01[3 * m] * r, sy = x01[3 * m + 1] * r, sz = x01[3 * m + 2] * r;
+    const uint32_t mask = (uint32_t)((1ull << log2T) - 1ull);
+    const float* tl = table + ((int64_t)l << log2T) * F;
+    float* o = out + (m * L + l) * F;
+    if (INTERP == 0) {
+        const uint32_t ix = (uint32_t)(int)rintf(sx), iy = (uint32_t)(int)rintf(sy), iz = (uint32_t)(int)rintf(sz);
+        const float* e = tl + (int64_t)((ix ^ (iy * acn::kP1) ^ (iz * acn::kP2)) & mask) * F;
+        for (int f = 0; f < F; ++f) o[f] = e[f];
+        return;
+    }
+    const float fx = floorf(sx), fy = floorf(sy), fz = floorf(sz);
+    float wx = sx - fx, wy = sy - fy, wz = sz - fz;
+    if (INTERP == 2) {
+        wx = (wx * wx) * (3.0f - 2.0f * wx);
+        wy = (wy * wy) * (3.0f - 2.0f * wy);
+        wz = (wz * wz) * (3.0f - 2.0f * wz);
+    }
+    const uint32_t x0 = (uint32_t)(int)fx, x1 = x0 + 1u;
+    const uint32_t y0 = (uint32_t)(int)fy * acn::kP1, y1 = y0 + acn::kP1;
+    const uint32_t z0 = (uint32_t)(int)fz * acn::kP2, z1 = z0 + acn::kP2;
+    const float* c[8];
+    c[0] = tl + (int64_t)((x0 ^ y0 ^ z0) & mask) * F;  // f000
+    c[1] = tl + (int64_t)((x0 ^ y0 ^ z1) & mask) * F;  // f001
+    c[2] = tl + (int64_t)((x0 ^ y1 ^ z0) & mask) * F;  // f010
+    c[3] = tl + (int64_t)((x0 ^ y1 ^ z1) & mask) * F;  // f011
+    c[4] = tl + (int64_t)((x1 ^ y0 ^ z0) & mask) * F;  // f100
+    c[5] = tl + (int64_t)((x1 ^ y0 ^ z1) & mask) * F;  // f101
+    c[6] = tl + (int64_t)((x1 ^ y1 ^ z0) & mask) * F;  // f110
+    c[7] = tl + (int64_t)((x1 ^ y1 ^ z1) & mask) * F;  // f111
+    const float ax = 1.0f - wx, ay = 1.0f - wy, az = 1.0f - wz;
+    for (int f = 0; f < F; ++f) {
+        const float c00 = c[0][f] * ax + c[4][f] * wx;
+        const float c01 = c[1][f] * ax + c[5][f] * wx;
+        const float c10 = c[2][f] * ax + c[6][f] * wx;
+        const float c11 = c[3][f] * ax + c[7][f] * wx;
+        const float c0 = c00 * ay + c10 * wy;
+        const float c1 = c01 * ay + c11 * wy;
+        o[f] = c0 * az + c1 * wz;
+    }
+}
+
+// Backward: autograd of the 8 gathers + lerps.  The gradient of corner (bx,by,bz) is
+// ((g * wz') * wy') * wx' in the chain-rule order of the forward lerps, scatter-added with
+// no-return fp32 atomics (global_atomic_add_f32), as torch's index_put_(accumulate=True).
+template <int INTERP>
+__global__ void __launch_bounds__(256) hashgrid_bwd_gen(const float* __restrict__ x01, int64_t M,
+                                                        const float* __restrict__ gout, Res32 res, int L,
+                                                        int log2T, int F, float* __restrict__ gtable) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t m = gid / L;
+    const int l = (int)(gid - m * L);
+    if (m >= M) return;
+    const float r = (float)res.v[l];
+    const float sx = x01[3 * m] * r, sy = x01[3 * m + 1] * r, sz = x01[3 * m + 2] * r;
+    const uint32_t mask = (uint32_t)((1ull << log2T) - 1ull);
+    float* tl = gtable + ((int64_t)l << log2T) * F;
+    const float* g = gout + (m * L + l) * F;
+    if (INTERP == 0) {
+        const uint32_t ix = (uint32_t)(int)rintf(sx), iy = (uint32_t)(int)rintf(sy), iz = (uint32_t)(int)rintf(sz);
+        float* e = tl + (int64_t)((ix ^ (iy * acn::kP1) ^ (iz * acn::kP2)) & mask) * F;
+        for (int f = 0; f < F; ++f) unsafeAtomicAdd(e + f, g[f]);
+        return;
+    }
+    const float fx = floorf(sx), fy = floorf(sy), fz = floorf(sz);
+    float wx = sx - fx, wy = sy - fy, wz = sz - fz;
+    if (INTERP == 2) {
+        wx = (wx * wx) * (3.0f - 2.0f * wx);
+        wy = (wy * wy) * (3.0f - 2.0f * wy);
+        wz = (wz * wz) * (3.0f - 2.0f * wz);
+    }
+    const float ax = 1.0f - wx, ay = 1.0f - wy, az = 1.0f - wz;
+    const uint32_t x0 = (uint32_t)(int)fx;
+    const uint32_t y0 = (uint32_t)(int)fy * acn::kP1;
+    const uint32_t z0 = (uint32_t)(int)fz * acn::kP2;
+#pragma unroll
+    for (int cidx = 0; cidx < 8; ++cidx) {
+        const int bx = cidx >> 2, by = (cidx >> 1) & 1, bz = cidx & 1;
+        const uint32_t h = ((x0 + (uint32_t)bx) ^ (y0 + (by ? acn::kP1 : 0u)) ^ (z0 + (bz ? acn::kP2 : 0u))) & mask;
+        float* e = tl + (int64_t)h * F;
+        for (int f = 0; f < F; ++f) {
+            const float gv = ((g[f] * (bz ? wz : az)) * (by ? wy : ay)) * (bx ? wx : ax);
+            unsafeAtomicAdd(e + f, gv);
+        }
+    }
+}
+
+template <int DEGREE>
+__global__ void __launch_bounds__(256) sh_fwd_kernel(const float* __restrict__ d, int64_t M,
+                                                     float* __restrict__ out) {
+    constexpr int C = (DEGREE + 1) * (DEGREE + 1);
+    const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= M) return;
+    float c[C];
+    acn::sh_encode<DEGREE>(d[3 * m], d[3 * m + 1], d[3 * m + 2], c);
+#pragma unroll
+    for (int i = 0; i < C; ++i) out[m * C + i] = c[i];
+}
+
+}  // namespace
+
+extern "C" int acn_hashgrid_fwd(const float* x01, int64_t M, const float* table, const int32_t* res, int L,
+                                int log2T, int F, int interp, float* out, void* stream) {
+    ACN_REQUIRE(M >= 0, "acn_hashgrid_fwd: M must be >= 0");
+    ACN_REQUIRE(L >= 1 && L <= ACN_MAX_LEVELS, "acn_hashgrid_fwd: levels must be in [1, %d], got %d", ACN_MAX_LEVELS, L);
+    ACN_REQUIRE(log2T >= 1 && log2T <= 30, "acn_hashgrid_fwd: log2_hashmap_size must be in [1, 30], got %d", log2T);
+    ACN_REQUIRE(F >= 1 && F <= 64, "acn_hashgrid_fwd: features_per_level must be in [1, 64], got %d", F);
+    ACN_REQUIRE(interp >= 0 && interp <= 2, "acn_hashgrid_fwd: bad interpolation %d", interp);
+    ACN_REQUIRE(res != nullptr, "acn_hashgrid_fwd: res is NULL");
+    if (M == 0) return ACN_OK;
+    ACN_REQUIRE(x01 && table && out, "acn_hashgrid_fwd: NULL pointer");
+    Res32 r{};
+    for (int i = 0; i < L; ++i) r.v[i] = res[i];
+    const int64_t threads = M * L;
+    const dim3 grid((unsigned)((threads + 255) / 256)), block(256);
+    hipStream_t s = (hipStream_t)stream;
+    if (F == 2) {
+        if (interp == 0) hipLaunchKernelGGL(hashgrid_fwd_f2<0>, grid, block, 0, s, x01, M, (const float2*)table, r, L, log2T, (float2*)out);
+        else if (interp == 1) hipLaunchKernelGGL(hashgrid_fwd_f2<1>, grid, block, 0, s, x01, M, (const float2*)table, r, L, log2T, (float2*)out);
+        else hipLaunchKernelGGL(hashgrid_fwd_f2<2>, grid, block, 0, s, x01, M, (const float2*)table, r, L, log2T, (float2*)out);
+    } else {
+        if (interp == 0) hipLaunchKernelGGL(hashgrid_fwd_gen<0>, grid, block, 0, s, x01, M, table, r, L, log2T, F, out);
+        else if (interp == 1) hipLaunchKernelGGL(hashgrid_fwd_gen<1>, grid, block, 0, s, x01, M, table, r, L, log2T, F, out);
+        else hipLaunchKernelGGL(hashgrid_fwd_gen<2>, grid, block, 0, s, x01, M, table, r, L, log2T, F, out);
+    }
+    return acn_check_launch("acn_hashgrid_fwd");
+}
+
+extern "C" int acn_hashgrid_bwd(const float* x01, int64_t M, const float* grad_out, const int32_t* res, int L,
+                                int log2T, int F, int interp, float* grad_table, void* stream) {
+    ACN_REQUIRE(M >= 0, "acn_hashgrid_bwd: M must be >= 0");
+    ACN_REQUIRE(L >= 1 && L <= ACN_MAX_LEVELS, "acn_hashgrid_bwd: levels must be in [1, %d], got %d", ACN_MAX_LEVELS, L);
+    ACN_REQUIRE(log2T >= 1 && log2T <= 30, "acn_hashgrid_bwd: log2_hashmap_size must be in [1, 30], got %d", log2T);
+    ACN_REQUIRE(F >= 1 && F <= 64, "acn_hashgrid_bwd: features_per_level must be in [1, 64], got %d", F);
+    ACN_REQUIRE(interp >= 0 && interp <= 2, "acn_hashgrid_bwd: bad interpolation %d", interp);
+    ACN_REQUIRE(res != nullptr, "acn_hashgrid_bwd: res is NULL");
+    if (M == 0) return ACN_OK;
+    ACN_REQUIRE(x01 && grad_out && grad_table, "acn_hashgrid_bwd: NULL pointer");
+    Res32 r{};
+    for (int i = 0; i < L; ++i) r.v[i] = res[i];
+    const int64_t threads = M * L;
+    const dim3 grid((unsigned)((threads + 255) / 256)), block(256);
+    hipStream_t s = (hipStream_t)stream;
+    if (interp == 0) hipLaunchKernelGGL(hashgrid_bwd_gen<0>, grid, block, 0, s, x01, M, grad_out, r, L, log2T, F, grad_table);
+    else if (interp == 1) hipLaunchKernelGGL(hashgrid_bwd_gen<1>, grid, block, 0, s, x01, M, grad_out, r, L, log2T, F, grad_table);
+    else hipLaunchKernelGGL(hashgrid_bwd_gen<2>, grid, block, 0, s, x01, M, grad_out, r, L, log2T, F, grad_table);
+    return acn_check_launch("acn_hashgrid_bwd");
+}
+
+extern "C" int acn_sh_fwd(const float* d, int64_t M, int levels, float* out, void* stream) {
+    ACN_REQUIRE(levels >= 1 && levels <= 5, "acn_sh_fwd: Supported levels in [1, 5], got %d", levels);
+    ACN_REQUIRE(M >= 0, "acn_sh_fwd: M must be >= 0");
+    if (M == 0) return ACN_OK;
+    ACN_REQUIRE(d && out, "acn_sh_fwd: NULL pointer");
+    const dim3 grid((unsigned)((M + 255) / 256)), block(256);
+    hipStream_t s = (hipStream_t)stream;
+    switch (levels) {
+        case 1: hipLaunchKernelGGL(sh_fwd_kernel<0>, grid, block, 0, s, d, M, out); break;
+        case 2: hipLaunchKernelGGL(sh_fwd_kernel<1>, grid, block, 0, s, d, M, out); break;
+        case 3: hipLaunchKernelGGL(sh_fwd_kernel<2>, grid, block, 0, s, d, M, out); break;
+        case 4: hipLaunchKernelGGL(sh_fwd_kernel<3>, grid, block, 0, s, d, M, out); break;
+        default: hipLaunchKernelGGL(sh_fwd_kernel<4>, grid, block, 0, s, d, M, out); break;
+    }
+    return acn_check_launch("acn_sh_fwd");
+}

@@ -1,0 +1,875 @@
+// render.hip -- fused field (hash grid -> sigma MLP -> colour MLP) and fused stratified render
+// for gfx950 (MI355X).  Replaces the chunked torch-op chains of
+//   nerfs/ray_rendering.py:290-345 render_rays_stratified (+ stratified_t_vals :262-287,
+//   _get_bg_rgb :23-45, volume_render :114-165),
+//   models/inr/meta_container.py:275-343 MetaContainer.forward (+ _routing :97-134,
+//   background_color :347-382),
+//   models/inr/meta_ngp.py:155-241 MetaNGP._world_to_unit / density / color / forward.
+//
+// Execution model: one wave owns one ray at a time and walks it front to back in tiles of 32
+// samples.  Inside a tile the 64 lanes are (sample j = lane & 31, half h = lane >> 5); half h
+// hash-encodes levels 8h..8h+7 of sample j, which is exactly the B-operand layout of
+// v_mfma_f32_32x32x2_f32 for the first layer (k-step s pairs feature 16*0+s with 16*1+s).  Every
+// MLP layer is H^T = W . X^T on fp32 MFMA (exact fp32 fma chains: parity mode), with the layer's
+// accumulator registers feeding the next layer's B operand directly (no LDS round trip).  The
+// packed weights of up to two experts sit in LDS (58 KB each); more experts read them from L2.
+// Compositing uses a 32-lane exclusive prefix product of (1 - alpha + 1e-10) in double (torch's
+// CPU cumprod accumulates in double), carries transmittance across tiles, and stops the ray once
+// T < tau (early ray termination; tau = 0 disables it).
+#include "acn_device.h"
+#include "acn_internal.h"
+
+using namespace acn;
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+namespace {
+
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ int rho(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// An opaque zero / copy produced inside the loop body: the packed-weight reads and per-lane
+// level selections derived from it cannot be hoisted out of the ray/tile loops by LICM (the
+// hoisted values would exceed the 128-VGPR budget of 4 waves/SIMD and get spilled to scratch).
+__device__ __forceinline__ int opaque_s(int v) {
+    asm volatile("" : "+s"(v));
+    return v;
+}
+__device__ __forceinline__ int opaque_v(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
+// ------------------------------------------------------------------------------------------
+// weight packing
+struct PackSrc {
+    const float *sig_w0, *sig_b0, *sig_w1, *sig_b1, *sigh_w, *sigh_b, *geo_w, *geo_b;
+    const float *col_w0, *col_b0, *col_w1, *col_b1, *col_w2, *col_b2;
+};
+struct PackArgs {
+    PackSrc e[kMaxK];
+};
+
+// decode a local index of an A-operand segment with NS k-steps per tile
+__device__ __forceinline__ void decode_a(int li, int NS, int& t, int& s, int& i, int& h) {
+    const int q = li & 3, lane = (li >> 2) & 63, tg = li >> 8;
+    const int g = tg % (NS / 4);
+    t = tg / (NS / 4);
+    s = 4 * g + q;
+    i = lane & 31;
+    h = lane >> 5;
+}
+
+__device__ float pack_value(const PackSrc& p, int idx) {
+    int t, s, i, h;
+    if (idx < PK_W2) {  // sigma_trunk.0 (64, 32): k = 16h + s
+        decode_a(idx - PK_W1, 16, t, s, i, h);
+        return p.sig_w0[(i + 32 * t) * 32 + 16 * h + s];
+    }
+    if (idx < PK_WH) {  // sigma_trunk.1 (64, 64): k = rho(r, h) + 32 Tin, s = 16 Tin + r
+        decode_a(idx - PK_W2, 32, t, s, i, h);
+        return p.sig_w1[(i + 32 * t) * 64 + rho(s & 15, h) + 32 * (s >> 4)];
+    }
+    if (idx < PK_WC1) {  // [sigma_head; geo_head; 0] (32 rows) x 64
+        decode_a(idx - PK_WH, 32, t, s, i, h);
+        const int k = rho(s & 15, h) + 32 * (s >> 4);
+        if (i == 0) return p.sigh_w[k];
+        if (i <= kGeo) return p.geo_w[(i - 1) * 64 + k];
+        return 0.0f;
+    }
+    if (idx < PK_WC2) {  // color_mlp.0 (64, 31) on head rows rho: 0 -> sigma_raw (weight 0),
+        decode_a(idx - PK_WC1, 16, t, s, i, h);  // 1..15 geo, 16..31 SH  => column rho - 1
+        const int r = rho(s, h);
+        return r == 0 ? 0.0f : p.col_w0[(i + 32 * t) * 31 + (r - 1)];
+    }
+    if (idx < PK_WC3) {  // color_mlp.1 (64, 64)
+        decode_a(idx - PK_WC2, 32, t, s, i, h);
+        return p.col_w1[(i + 32 * t) * 64 + rho(s & 15, h) + 32 * (s >> 4)];
+    }
+    if (idx < PK_B) {  // color_mlp.2 (3, 64), VALU layout [h][c][T*16 + r]
+        const int li = idx - PK_WC3;
+        const int hh = li / 96, c = (li % 96) / 32, tr = li % 32;
+        return p.col_w2[c * 64 + rho(tr & 15, hh) + 32 * (tr >> 4)];
+    }
+    if (idx < PK_BC3) {  // bias fragments [tile][h][r]
+        const int li = idx - PK_B;
+        const int tile = li / 32, hh = (li / 16) & 1, r = li & 15;
+        const int row = rho(r, hh);
+        switch (tile) {
+            case 0: case 1: return p.sig_b0[row + 32 * (tile - 0)];
+            case 2: case 3: return p.sig_b1[row + 32 * (tile - 2)];
+            case 4: return row == 0 ? p.sigh_b[0] : (row <= kGeo ? p.geo_b[row - 1] : 0.0f);
+            case 5: case 6: return p.col_b0[row + 32 * (tile - 5)];
+            default: return p.col_b1[row + 32 * (tile - 7)];
+        }
+    }
+    const int li = idx - PK_BC3;
+    return li < 3 ? p.col_b2[li] : 0.0f;
+}
+
+__global__ void __launch_bounds__(256) pack_kernel(PackArgs args, int K, float* __restrict__ out) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    const int k = blockIdx.y;
+    if (idx >= PK_FLOATS || k >= K) return;
+    out[(size_t)k * PK_FLOATS + idx] = pack_value(args.e[k], idx);
+}
+
+// ------------------------------------------------------------------------------------------
+// one 32-sample tile of one expert's field.  W: packed image (LDS or global, by inlining).
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+
+__device__ __forceinline__ f32x16 bias_frag(const float* W, int tile, int h) {
+    const float* b = W + PK_B + (tile * 2 + h) * 16;
+    const f32x4 a = ld4(b), c = ld4(b + 4), d = ld4(b + 8), e = ld4(b + 12);
+    f32x16 v;
+    v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+    v[4] = c[0]; v[5] = c[1]; v[6] = c[2]; v[7] = c[3];
+    v[8] = d[0]; v[9] = d[1]; v[10] = d[2]; v[11] = d[3];
+    v[12] = e[0]; v[13] = e[1]; v[14] = e[2]; v[15] = e[3];
+    return v;
+}
+
+__device__ __forceinline__ void relu16(f32x16& v) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = v[i] < 0.0f ? 0.0f : v[i];  // NaN propagates like torch.relu
+}
+
+// 64 -> 64 layer: out tiles (o0, o1) = bias + W . [in0; in1].  A fragments are double
+// buffered one 4-k-step group ahead; the scheduling barrier stops the compiler from hoisting
+// every ds_read of the layer (64 VGPRs) above the MFMAs.
+__device__ __forceinline__ void layer64x64(const float* W, int seg, int btile, int lane, int h,
+                                           const f32x16& in0, const f32x16& in1, f32x16& o0, f32x16& o1) {
+    o0 = bias_frag(W, btile, h);
+    o1 = bias_frag(W, btile + 1, h);
+    f32x4 n0 = ld4(W + seg + ((0 * 8 + 0) * 64 + lane) * 4);
+    f32x4 n1 = ld4(W + seg + ((1 * 8 + 0) * 64 + lane) * 4);
+#pragma unroll
+    for (int gi = 0; gi < 8; ++gi) {
+        const f32x4 a0 = n0, a1 = n1;
+        if (gi < 7) {
+            n0 = ld4(W + seg + ((0 * 8 + gi + 1) * 64 + lane) * 4);
+            n1 = ld4(W + seg + ((1 * 8 + gi + 1) * 64 + lane) * 4);
+        }
+        const int tin = gi >> 2, g = gi & 3;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float b = tin ? in1[4 * g + q] : in0[4 * g + q];
+            o0 = mfma32(a0[q], b, o0);
+            o1 = mfma32(a1[q], b, o1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// Field of one expert on this lane's sample (x world point, shv = this half's SH rows).
+// Returns rgb (after sigmoid) on every lane and sigma_raw on every lane.
+template <int INTERP>
+__device__ __forceinline__ void field_tile(const float* W, const ExpertMeta& em, int log2T, float px, float py,
+                                           float pz, const float (&shv)[8], int lane, float& rr, float& rg, float& rb,
+                                           float& sraw) {
+    W = W + opaque_s(0);
+    const int h = opaque_v(lane >> 5);
+    // _world_to_unit (meta_ngp.py:155-158)
+    const float eps = 1e-6f, hi = 1.0f - 1e-6f;
+    const float x0 = clamp_nan((px - em.amin[0]) / em.ext[0], eps, hi);
+    const float x1 = clamp_nan((py - em.amin[1]) / em.ext[1], eps, hi);
+    const float x2 = clamp_nan((pz - em.amin[2]) / em.ext[2], eps, hi);
+    // hash grid: this half encodes levels 8h .. 8h+7 (encodings.py:331-381)
+    const uint32_t mask = (uint32_t)((1ull << log2T) - 1ull);
+    float feat[16];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+        const float res = (float)(h ? em.res[8 + l] : em.res[l]);
+        const float2* tl = reinterpret_cast<const float2*>(em.table) + ((size_t)(l + 8 * h) << log2T);
+        hash_level_f2<INTERP>(tl, x0 * res, x1 * res, x2 * res, mask, feat[2 * l], feat[2 * l + 1]);
+        if (l & 1) __builtin_amdgcn_sched_barrier(0);  // <= 16 gathers in flight per lane (VGPR budget)
+    }
+    // sigma_trunk.0: 32 -> 64 (ReLU)
+    f32x16 a0 = bias_frag(W, BT_L1, h), a1 = bias_frag(W, BT_L1 + 1, h);
+    {
+        f32x4 n0 = ld4(W + PK_W1 + ((0 * 4 + 0) * 64 + lane) * 4);
+        f32x4 n1 = ld4(W + PK_W1 + ((1 * 4 + 0) * 64 + lane) * 4);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const f32x4 w0 = n0, w1 = n1;
+            if (g < 3) {
+                n0 = ld4(W + PK_W1 + ((0 * 4 + g + 1) * 64 + lane) * 4);
+                n1 = ld4(W + PK_W1 + ((1 * 4 + g + 1) * 64 + lane) * 4);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                a0 = mfma32(w0[q], feat[4 * g + q], a0);
+                a1 = mfma32(w1[q], feat[4 * g + q], a1);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    relu16(a0);
+    relu16(a1);
+    // sigma_trunk.1: 64 -> 64 (ReLU)
+    f32x16 b0, b1;
+    layer64x64(W, PK_W2, BT_L2, lane, h, a0, a1, b0, b1);
+    relu16(b0);
+    relu16(b1);
+    // heads: rows 0 sigma_head, 1..15 geo_head; rows 16..31 carry the SH features through
+    // (zero weights, accumulator initialised with SH): the colour MLP input [geo, sh].
+    f32x16 hd = bias_frag(W, BT_H, h);
+#pragma unroll
+    for (int r = 8; r < 16; ++r) hd[r] = shv[r - 8];
+    {
+        f32x4 n = ld4(W + PK_WH + (0 * 64 + lane) * 4);
+#pragma unroll
+        for (int gi = 0; gi < 8; ++gi) {
+            const f32x4 w = n;
+            if (gi < 7) n = ld4(W + PK_WH + ((gi + 1) * 64 + lane) * 4);
+            const int tin = gi >> 2, g = gi & 3;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) hd = mfma32(w[q], tin ? b1[4 * g + q] : b0[4 * g + q], hd);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    // sigma_raw = row 0, held by lane j of half 0
+    sraw = __shfl(hd[0], lane & 31);
+    // color_mlp.0: [geo(15), sh(16)] -> 64 (ReLU)
+    f32x16 c0 = bias_frag(W, BT_C1, h), c1 = bias_frag(W, BT_C1 + 1, h);
+    {
+        f32x4 n0 = ld4(W + PK_WC1 + ((0 * 4 + 0) * 64 + lane) * 4);
+        f32x4 n1 = ld4(W + PK_WC1 + ((1 * 4 + 0) * 64 + lane) * 4);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const f32x4 w0 = n0, w1 = n1;
+            if (g < 3) {
+                n0 = ld4(W + PK_WC1 + ((0 * 4 + g + 1) * 64 + lane) * 4);
+                n1 = ld4(W + PK_WC1 + ((1 * 4 + g + 1) * 64 + lane) * 4);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                c0 = mfma32(w0[q], hd[4 * g + q], c0);
+                c1 = mfma32(w1[q], hd[4 * g + q], c1);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    relu16(c0);
+    relu16(c1);
+    // color_mlp.1: 64 -> 64 (ReLU)
+    f32x16 d0, d1;
+    layer64x64(W, PK_WC2, BT_C2, lane, h, c0, c1, d0, d1);
+    relu16(d0);
+    relu16(d1);
+    // color_mlp.2: 64 -> 3 on the VALU (a 3-row MFMA tile would waste 29/32 of the pipe):
+    // each half dots its 32 features, the halves are summed with a cross-half swap.
+    const float* w3 = W + PK_WC3 + h * 96;
+    float o[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const f32x4 wa = ld4(w3 + c * 32 + 4 * g);
+            const f32x4 wb = ld4(w3 + c * 32 + 16 + 4 * g);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                acc = fmaf(wa[q], d0[4 * g + q], acc);
+                acc = fmaf(wb[q], d1[4 * g + q], acc);
+            }
+        }
+        o[c] = acc;
+    }
+    const f32x4 b3 = ld4(W + PK_BC3);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) o[c] = (o[c] + __shfl_xor(o[c], 32)) + b3[c];
+    rr = sigmoidf_(o[0]);
+    rg = sigmoidf_(o[1]);
+    rb = sigmoidf_(o[2]);
+}
+
+// Routing (meta_container.py:97-134), cdist mm-path restated exactly as in the oracle.
+// Computed without per-expert arrays (runtime-indexed arrays would live in scratch): a first
+// pass gives min distance / denominator (soft) or argmin (hard), then w_k is recomputed per k.
+__device__ __forceinline__ float route_dist(const FieldCfg& cfg, int k, float px, float py, float pz) {
+    float s = 0.0f, xn, cn;
+    if (cfg.cluster_2d) {
+        const float cy = cfg.cent[k][1], cz = cfg.cent[k][2];
+        xn = py * py + pz * pz;
+        cn = cy * cy + cz * cz;
+        s = fmaf(-2.0f * py, cy, s);
+        s = fmaf(-2.0f * pz, cz, s);
+    } else {
+        const float cx = cfg.cent[k][0], cy = cfg.cent[k][1], cz = cfg.cent[k][2];
+        xn = (px * px + py * py) + pz * pz;
+        cn = (cx * cx + cy * cy) + cz * cz;
+        s = fmaf(-2.0f * px, cx, s);
+        s = fmaf(-2.0f * py, cy, s);
+        s = fmaf(-2.0f * pz, cz, s);
+    }
+    s = s + xn;
+    s = s + cn;
+    return sqrtf(s > 0.0f ? s : 0.0f);
+}
+
+struct RouteState {
+    float thr, den;  // soft: bm * min dist, sum of masked inverse distances
+    int hard;        // hard: argmin
+};
+
+template <int ROUTE>
+__device__ __forceinline__ RouteState route_prep(const FieldCfg& cfg, float px, float py, float pz) {
+    RouteState st{0.0f, 0.0f, 0};
+    if (ROUTE == 1) {
+        float mind = INFINITY;
+        for (int k = 0; k < cfg.K; ++k) {
+            float d = route_dist(cfg, k, px, py, pz);
+            d = d < 1e-6f ? 1e-6f : d;
+            mind = fminf(mind, d);
+        }
+        st.thr = cfg.bm * mind;
+        float den = 0.0f;
+        for (int k = 0; k < cfg.K; ++k) {
+            float d = route_dist(cfg, k, px, py, pz);
+            d = d < 1e-6f ? 1e-6f : d;
+            den = den + ((d <= st.thr) ? 1.0f / d : 0.0f);
+        }
+        st.den = den < 1e-6f ? 1e-6f : den;
+    } else if (ROUTE == 2) {
+        float best = INFINITY;
+        for (int k = 0; k < cfg.K; ++k) {
+            const float d = route_dist(cfg, k, px, py, pz);
+            if (d < best || k == 0) { best = d; st.hard = k; }
+        }
+    }
+    return st;
+}
+
+__device__ __forceinline__ float route_weight(const FieldCfg& cfg, const RouteState& st, int k, float px, float py,
+                                              float pz) {
+    float d = route_dist(cfg, k, px, py, pz);
+    d = d < 1e-6f ? 1e-6f : d;
+    return ((d <= st.thr) ? 1.0f / d : 0.0f) / st.den;
+}
+
+// Container forward of this lane's sample over all experts (meta_container.py:300-343):
+// soft: y = sum_k (y_k * w_k) accumulated in expert order from zero (index_add_); hard: copy.
+template <int INTERP, int ROUTE>
+__device__ __forceinline__ void container_tile(const FieldCfg& cfg, const float* Wbase, float px, float py, float pz,
+                                               const float (&shv)[8], int lane, float& yr, float& yg, float& yb,
+                                               float& ys) {
+    if (ROUTE == 0) {
+        field_tile<INTERP>(Wbase, cfg.ex[0], cfg.log2T, px, py, pz, shv, lane, yr, yg, yb, ys);
+        ys = trunc_exp(ys);
+        return;
+    }
+    const RouteState st = route_prep<ROUTE>(cfg, px, py, pz);
+    yr = yg = yb = ys = 0.0f;
+    for (int k = 0; k < cfg.K; ++k) {
+        const float wk = (ROUTE == 1) ? route_weight(cfg, st, k, px, py, pz) : 0.0f;
+        const bool need = (ROUTE == 1) ? (wk > 0.0f) : (st.hard == k);
+        if (__ballot(need) == 0ull) continue;  // wave-uniform skip of experts no sample needs
+        float r, g, b, s;
+        field_tile<INTERP>(Wbase + (size_t)k * PK_FLOATS, cfg.ex[k], cfg.log2T, px, py, pz, shv, lane, r, g, b, s);
+        s = trunc_exp(s);
+        if (need) {
+            if (ROUTE == 1) {
+                yr = yr + r * wk;
+                yg = yg + g * wk;
+                yb = yb + b * wk;
+                ys = ys + s * wk;
+            } else {
+                yr = r; yg = g; yb = b; ys = s;
+            }
+        }
+    }
+}
+
+// SH rows of the head tile held by half h: rows 16+4h..19+4h and 24+4h..27+4h
+__device__ __forceinline__ void sh_rows_for_half(const float (&sh)[16], int h, float (&shv)[8]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        shv[i] = h ? sh[4 + i] : sh[i];
+        shv[4 + i] = h ? sh[12 + i] : sh[8 + i];
+    }
+}
+
+// colour-branch direction encoding (meta_ngp.py:165-168 then encodings.py:144-151)
+__device__ __forceinline__ void dir_sh(float dx, float dy, float dz, float (&sh)[16]) {
+    const float n = clamp_min_nan(norm3(dx, dy, dz), 1e-9f);
+    sh_encode<3>(dx / n, dy / n, dz / n, sh);
+}
+
+// ------------------------------------------------------------------------------------------
+template <int KL>
+__device__ __forceinline__ void stage_weights(float* smem, const float* __restrict__ packed) {
+    const f32x4* src = reinterpret_cast<const f32x4*>(packed);
+    f32x4* dst = reinterpret_cast<f32x4*>(smem);
+    for (int i = threadIdx.x; i < KL * PK_FLOATS / 4; i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
+}
+
+struct FieldParams {
+    const float* x;
+    int64_t M, ld;
+    const float* packed;
+    float* out;
+};
+
+// acn_field_fwd: 32 points per wave-tile, grid-stride over tiles.
+template <int INTERP, int KL, int ROUTE>
+__global__ void __launch_bounds__(1024, 4) field_kernel(FieldCfg cfg, FieldParams p) {
+    __shared__ __attribute__((aligned(16))) float smem[(KL > 0 ? KL : 1) * PK_FLOATS];
+    const float* W = p.packed;
+    if (KL > 0) {
+        stage_weights<KL>(smem, p.packed);
+        W = smem;
+    }
+    const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    const int64_t ntiles = (p.M + 31) / 32;
+    for (int64_t tile = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave; tile < ntiles; tile += nw) {
+        const int64_t m = tile * 32 + j;
+        const int64_t mc = m < p.M ? m : p.M - 1;
+        const float* xr = p.x + mc * p.ld;
+        const float px = xr[0], py = xr[1], pz = xr[2];
+        float sh[16], shv[8];
+        dir_sh(xr[3], xr[4], xr[5], sh);
+        sh_rows_for_half(sh, h, shv);
+        float yr, yg, yb, ys;
+        container_tile<INTERP, ROUTE>(cfg, W, px, py, pz, shv, lane, yr, yg, yb, ys);
+        if (h == 0 && m < p.M) {
+            f32x4 v;
+            v[0] = yr; v[1] = yg; v[2] = yb; v[3] = ys;
+            *reinterpret_cast<f32x4*>(p.out + 4 * m) = v;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// compositing of one 32-sample tile (ray_rendering.py:137-159).  Transmittance is carried in
+// double (torch's CPU cumprod accumulates in double); the weighted sums are kept as per-lane
+// float partials across tiles and reduced across lanes once per ray, in double.
+struct RayAcc {
+    double T;
+    float r, g, b, d, a;
+};
+
+__device__ __forceinline__ double wave32_sum(double v) {
+#pragma unroll
+    for (int off = 16; off >= 1; off >>= 1) v += __shfl_xor(v, off, 32);
+    return v;
+}
+
+__device__ __forceinline__ void composite_tile(RayAcc& acc, bool valid, float cr, float cg, float cb, float sig,
+                                               float t, float dist, int j, float* wout) {
+    // rgb.clamp(0,1), sigma.clamp_min(0) (* sigma_scale) are applied by the caller
+    dist = clamp_min_nan(dist, 1e-4f);
+    float alpha = 1.0f - expf(-sig * dist);
+    alpha = clamp_nan(alpha, 0.0f, (float)(1.0 - 1e-7));
+    float x = (1.0f - alpha) + 1e-10f;
+    if (!valid) { x = 1.0f; alpha = 0.0f; }
+    double incl = (double)x;
+#pragma unroll
+    for (int off = 1; off < 32; off <<= 1) {
+        const double y = __shfl_up(incl, off, 32);
+        if (j >= off) incl *= y;
+    }
+    double excl = __shfl_up(incl, 1, 32);
+    if (j == 0) excl = 1.0;
+    const float Ts = (float)(acc.T * excl);
+    const float w = alpha * Ts;
+    if (wout) *wout = w;
+    if (valid) {
+        acc.r += w * cr;
+        acc.g += w * cg;
+        acc.b += w * cb;
+        acc.d += w * t;
+        acc.a += w;
+    }
+    acc.T = acc.T * __shfl(incl, 31, 32);
+}
+
+__device__ __forceinline__ void finish_ray(const RayAcc& acc, float& r, float& g, float& b, float& d, float& a) {
+    r = (float)wave32_sum((double)acc.r);
+    g = (float)wave32_sum((double)acc.g);
+    b = (float)wave32_sum((double)acc.b);
+    d = (float)wave32_sum((double)acc.d);
+    a = (float)wave32_sum((double)acc.a);
+}
+
+// t value of sample s (stratified_t_vals, ray_rendering.py:278-287); linspace as torch CPU
+__device__ __forceinline__ float lin01(int i, int S) {
+    if (S == 1) return 0.0f;
+    const float step = 1.0f / (float)(S - 1);
+    return i < S / 2 ? fmaf(step, (float)i, 0.0f) : fmaf(-step, (float)(S - 1 - i), 1.0f);
+}
+__device__ __forceinline__ float tlin(float near, float far, int i, int S) {
+    const float u = lin01(i, S);
+    return near * (1.0f - u) + far * u;
+}
+__device__ __forceinline__ float tval(float near, float far, int s, int S, const float* jit) {
+    const float ts = tlin(near, far, s, S);
+    if (!jit) return ts;
+    const float lo = s == 0 ? ts : 0.5f * (tlin(near, far, s - 1, S) + ts);
+    const float hi = s == S - 1 ? ts : 0.5f * (ts + tlin(near, far, s + 1, S));
+    return lo + (hi - lo) * jit[s];
+}
+
+struct BgArgs {
+    int32_t mode, hidden;
+    float color[3];
+    const float *w1, *b1, *w2, *b2;
+};
+
+// background_color (meta_container.py:360-367): F.normalize -> SH(4) -> Linear ReLU -> Linear Sigmoid
+__device__ __forceinline__ void background(const BgArgs& bg, float dx, float dy, float dz, int lane, float (&out)[3]) {
+    if (bg.mode == ACN_BG_CONST) { out[0] = bg.color[0]; out[1] = bg.color[1]; out[2] = bg.color[2]; return; }
+    if (bg.mode != ACN_BG_MLP) { out[0] = out[1] = out[2] = 0.0f; return; }
+    const float n = clamp_min_nan(norm3(dx, dy, dz), 1e-12f);
+    float sh[16];
+    sh_encode<3>(dx / n, dy / n, dz / n, sh);
+    float hv = 0.0f;
+    if (lane < bg.hidden) {
+        float s = 0.0f;
+        for (int k = 0; k < 16; ++k) s = fmaf(sh[k], bg.w1[lane * 16 + k], s);
+        hv = s + bg.b1[lane];
+        hv = hv < 0.0f ? 0.0f : hv;
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        float v = lane < bg.hidden ? hv * bg.w2[c * bg.hidden + lane] : 0.0f;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+        out[c] = sigmoidf_(v + bg.b2[c]);
+    }
+}
+
+struct RenderParams {
+    const float* rays;
+    int64_t N;
+    int32_t S;
+    const float* jitter;
+    const float* packed;
+    float sigma_scale, tau;
+    float *rgb, *depth, *weights, *acc;
+};
+
+template <int INTERP, int KL, int ROUTE>
+__global__ void __launch_bounds__(1024, 4) render_kernel(FieldCfg cfg, BgArgs bg, RenderParams p) {
+    __shared__ __attribute__((aligned(16))) float smem[(KL > 0 ? KL : 1) * PK_FLOATS];
+    const float* W = p.packed;
+    if (KL > 0) {
+        stage_weights<KL>(smem, p.packed);
+        W = smem;
+    }
+    const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // provably uniform: ray data in SGPRs
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    const int S = p.S;
+    for (int64_t ray = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave; ray < p.N; ray += nw) {
+        const float* rp = p.rays + ray * 8;
+        const float ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
+        const float near = rp[6], far = rp[7];
+        const float* jit = p.jitter ? p.jitter + ray * S : nullptr;
+        float sh[16], shv[8];
+        dir_sh(dx, dy, dz, sh);
+        sh_rows_for_half(sh, h, shv);
+        RayAcc acc{1.0, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+        int s0 = 0;
+        for (; s0 < S; s0 += 32) {
+            const int s = s0 + j;
+            const bool valid = s < S;
+            const int sc = valid ? s : S - 1;
+            const float t = tval(near, far, sc, S, jit);
+            const float tn = (sc < S - 1) ? tval(near, far, sc + 1, S, jit) : t;
+            const float tp = (sc == S - 1 && S > 1) ? tval(near, far, sc - 1, S, jit) : t;
+            const float dist = (sc < S - 1) ? (tn - t) : (t - tp);
+            const float px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;
+            float yr, yg, yb, ys;
+            container_tile<INTERP, ROUTE>(cfg, W, px, py, pz, shv, lane, yr, yg, yb, ys);
+            // volume_render input conditioning (:140-143)
+            yr = clamp_nan(yr, 0.0f, 1.0f);
+            yg = clamp_nan(yg, 0.0f, 1.0f);
+            yb = clamp_nan(yb, 0.0f, 1.0f);
+            float sig = clamp_min_nan(ys, 0.0f);
+            if (p.sigma_scale != 1.0f) sig = sig * p.sigma_scale;
+            float wv;
+            composite_tile(acc, valid, yr, yg, yb, sig, t, dist, j, &wv);
+            if (p.weights && valid && h == 0) p.weights[ray * S + s] = wv;
+            const int stop = __builtin_amdgcn_readfirstlane((int)(acc.T < (double)p.tau));
+            if (stop) { s0 += 32; break; }
+        }
+        if (p.weights && h == 0)  // samples skipped by early termination carry zero weight
+            for (int s = s0 + j; s < S; s += 32) p.weights[ray * S + s] = 0.0f;
+        float bgc[3];
+        background(bg, dx, dy, dz, lane, bgc);
+        float r, g, b, dd, a;
+        finish_ray(acc, r, g, b, dd, a);
+        if (lane == 0) {
+            if (bg.mode != ACN_BG_NONE) {
+                const float om = 1.0f - a;
+                r = r + om * bgc[0];
+                g = g + om * bgc[1];
+                b = b + om * bgc[2];
+            }
+            p.rgb[ray * 3 + 0] = r;
+            p.rgb[ray * 3 + 1] = g;
+            p.rgb[ray * 3 + 2] = b;
+            p.depth[ray] = dd;
+            p.acc[ray] = a;
+        }
+    }
+}
+
+// standalone volume_render: one wave per ray, 32-sample tiles
+__global__ void __launch_bounds__(256) volume_render_kernel(const float* __restrict__ rs, const float* __restrict__ tv,
+                                                            const float* __restrict__ bgp, int64_t N, int S,
+                                                            int raw_rgb, int raw_sigma, float sigma_scale,
+                                                            float* rgb, float* depth, float* weights, float* accp) {
+    const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t ray = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); ray < N; ray += nw) {
+        RayAcc acc{1.0, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+        const float* t = tv + ray * S;
+        for (int s0 = 0; s0 < S; s0 += 32) {
+            const int s = s0 + j;
+            const bool valid = s < S;
+            const int sc = valid ? s : S - 1;
+            const float* v = rs + (ray * S + sc) * 4;
+            float cr = v[0], cg = v[1], cb = v[2], sg = v[3];
+            if (raw_rgb) { cr = sigmoidf_(cr); cg = sigmoidf_(cg); cb = sigmoidf_(cb); }
+            else { cr = clamp_nan(cr, 0.0f, 1.0f); cg = clamp_nan(cg, 0.0f, 1.0f); cb = clamp_nan(cb, 0.0f, 1.0f); }
+            sg = raw_sigma ? trunc_exp(sg) : clamp_min_nan(sg, 0.0f);
+            if (sigma_scale != 1.0f) sg = sg * sigma_scale;
+            const float dist = (sc < S - 1) ? (t[sc + 1] - t[sc]) : (t[sc] - t[sc - 1]);
+            float wv;
+            composite_tile(acc, valid, cr, cg, cb, sg, t[sc], dist, j, &wv);
+            if (weights && valid && h == 0) weights[ray * S + s] = wv;
+        }
+        float r, g, b, dd, a;
+        finish_ray(acc, r, g, b, dd, a);
+        if (lane == 0) {
+            if (bgp) {
+                const float om = 1.0f - a;
+                r = r + om * bgp[3 * ray];
+                g = g + om * bgp[3 * ray + 1];
+                b = b + om * bgp[3 * ray + 2];
+            }
+            rgb[3 * ray] = r; rgb[3 * ray + 1] = g; rgb[3 * ray + 2] = b;
+            depth[ray] = dd;
+            accp[ray] = a;
+        }
+    }
+}
+
+// MetaContainer._routing as a standalone op: W (M, K) soft weights, or hard (M) argmin
+__global__ void __launch_bounds__(256) routing_kernel(FieldCfg cfg, const float* __restrict__ pts, int64_t M, int64_t ld,
+                                                      float* __restrict__ W, int32_t* __restrict__ hard) {
+    const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= M) return;
+    const float px = pts[m * ld], py = pts[m * ld + 1], pz = pts[m * ld + 2];
+    if (cfg.routing == 1) {
+        const RouteState st = route_prep<1>(cfg, px, py, pz);
+        for (int k = 0; k < cfg.K; ++k) W[m * cfg.K + k] = route_weight(cfg, st, k, px, py, pz);
+    } else {
+        const RouteState st = route_prep<2>(cfg, px, py, pz);
+        hard[m] = st.hard;
+    }
+}
+
+// MetaContainer.background_color for N directions: one wave per direction
+__global__ void __launch_bounds__(256) background_kernel(BgArgs bg, const float* __restrict__ d, int64_t N,
+                                                         float* __restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t i = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < N; i += nw) {
+        float c[3];
+        background(bg, d[3 * i], d[3 * i + 1], d[3 * i + 2], lane, c);
+        if (lane < 3) out[3 * i + lane] = lane == 0 ? c[0] : (lane == 1 ? c[1] : c[2]);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+int g_num_cus = 0;
+int num_cus() {
+    if (g_num_cus == 0) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+            g_num_cus = n;
+        else
+            g_num_cus = 256;
+    }
+    return g_num_cus;
+}
+
+int check_expert(const acn_expert& e, int k) {
+    ACN_REQUIRE(e.table, "expert %d: hash table is NULL", k);
+    if (e.L != 16 || e.F != 2)
+        return acn_set_error(ACN_ERR_UNSUPPORTED, "expert %d: fused path needs levels*features = 16*2 (got %d*%d)", k, e.L, e.F);
+    ACN_REQUIRE(e.log2T >= 1 && e.log2T <= 30, "expert %d: log2_hashmap_size must be in [1, 30]", k);
+    ACN_REQUIRE(e.interp >= 0 && e.interp <= 2, "expert %d: bad interpolation", k);
+    const float* ptrs[] = {e.sig_w0, e.sig_b0, e.sig_w1, e.sig_b1, e.sigh_w, e.sigh_b, e.geo_w,
+                           e.geo_b, e.col_w0, e.col_b0, e.col_w1, e.col_b1, e.col_w2, e.col_b2};
+    for (const float* q : ptrs) ACN_REQUIRE(q, "expert %d: NULL MLP weight/bias pointer", k);
+    return ACN_OK;
+}
+
+// Builds FieldCfg + packs weights into the workspace.  Returns status; sets *interp.
+int prepare(const acn_expert* experts, const acn_routing* routing, int active_module, void* workspace,
+            size_t workspace_bytes, hipStream_t s, FieldCfg& cfg, int& interp, int& Keval) {
+    ACN_REQUIRE(experts && routing, "NULL experts/routing");
+    const int K = routing->K;
+    ACN_REQUIRE(K >= 1 && K <= ACN_MAX_EXPERTS, "routing.K must be in [1, %d], got %d", ACN_MAX_EXPERTS, K);
+    ACN_REQUIRE(active_module < K, "active_module %d out of range for K=%d", active_module, K);
+    const int k0 = active_module >= 0 ? active_module : 0;
+    Keval = active_module >= 0 ? 1 : K;
+    ACN_REQUIRE(workspace && workspace_bytes >= (size_t)Keval * PK_BYTES, "workspace too small: need %zu bytes",
+                (size_t)Keval * PK_BYTES);
+    ACN_REQUIRE(((uintptr_t)workspace & 15) == 0, "workspace must be 16-byte aligned");
+    interp = experts[k0].interp;
+    const int log2T = experts[k0].log2T;
+    PackArgs pa{};
+    for (int i = 0; i < Keval; ++i) {
+        const acn_expert& e = experts[k0 + i];
+        int st = check_expert(e, k0 + i);
+        if (st) return st;
+        if (e.interp != interp || e.log2T != log2T)
+            return acn_set_error(ACN_ERR_UNSUPPORTED, "experts must share interpolation and log2_hashmap_size");
+        ExpertMeta& m = cfg.ex[i];
+        m.table = e.table;
+        for (int a = 0; a < 3; ++a) { m.amin[a] = e.aabb_min[a]; m.ext[a] = e.aabb_extent[a]; }
+        for (int l = 0; l < 16; ++l) m.res[l] = e.res[l];
+        pa.e[i] = PackSrc{e.sig_w0, e.sig_b0, e.sig_w1, e.sig_b1, e.sigh_w, e.sigh_b, e.geo_w, e.geo_b,
+                          e.col_w0, e.col_b0, e.col_w1, e.col_b1, e.col_w2, e.col_b2};
+    }
+    cfg.K = Keval;
+    cfg.log2T = log2T;
+    cfg.cluster_2d = routing->cluster_2d;
+    cfg.bm = routing->boundary_margin;
+    // single expert (active_module, or K == 1 whose soft weight is exactly 1 / argmin is 0): no routing
+    if (active_module >= 0 || K == 1) cfg.routing = 0;
+    else cfg.routing = routing->boundary_margin > 1.0f ? 1 : 2;
+    for (int k = 0; k < K && active_module < 0; ++k)
+        for (int a = 0; a < 3; ++a) cfg.cent[k][a] = routing->centroids[k][a];
+    hipLaunchKernelGGL(pack_kernel, dim3((PK_FLOATS + 255) / 256, Keval), dim3(256), 0, s, pa, Keval,
+                       (float*)workspace);
+    return acn_check_launch("acn pack_kernel");
+}
+
+}  // namespace
+
+// interpolation x weight residency x routing.  Single-expert launches (ROUTE 0) use one LDS image;
+// routed launches keep K <= 2 experts in LDS and read K > 2 packed images from L2.
+#define ACN_DISPATCH_I(L, I)                                           \
+    do {                                                               \
+        if (cfg.routing == 0) L(I, 1, 0);                              \
+        else if (cfg.routing == 1) { if (K == 2) L(I, 2, 1); else L(I, 0, 1); } \
+        else { if (K == 2) L(I, 2, 2); else L(I, 0, 2); }              \
+    } while (0)
+#define ACN_DISPATCH(L)                                                \
+    do {                                                               \
+        if (interp == 1) ACN_DISPATCH_I(L, 1);                         \
+        else if (interp == 0) ACN_DISPATCH_I(L, 0);                    \
+        else ACN_DISPATCH_I(L, 2);                                     \
+    } while (0)
+
+extern "C" size_t acn_workspace_bytes(int K) { return (size_t)(K < 1 ? 1 : K) * PK_BYTES; }
+
+extern "C" int acn_field_fwd(const float* x, int64_t M, int64_t ld, const acn_expert* experts,
+                             const acn_routing* routing, int active_module, void* workspace, size_t workspace_bytes,
+                             float* out, void* stream) {
+    ACN_REQUIRE(M >= 0 && ld >= 6, "acn_field_fwd: x must be (N, D>=6)");
+    if (M == 0) return ACN_OK;
+    ACN_REQUIRE(x && out, "acn_field_fwd: NULL pointer");
+    hipStream_t s = (hipStream_t)stream;
+    FieldCfg cfg{};
+    int interp, K;
+    int st = prepare(experts, routing, active_module, workspace, workspace_bytes, s, cfg, interp, K);
+    if (st) return st;
+    FieldParams p{x, M, ld, (const float*)workspace, out};
+    const int64_t ntiles = (M + 31) / 32;
+    const int64_t wgs = (ntiles + 15) / 16;
+    const dim3 grid((unsigned)(wgs < num_cus() ? wgs : num_cus())), block(1024);
+#define ACN_FIELD_LAUNCH(I, KL, R) hipLaunchKernelGGL((field_kernel<I, KL, R>), grid, block, 0, s, cfg, p)
+    ACN_DISPATCH(ACN_FIELD_LAUNCH);
+#undef ACN_FIELD_LAUNCH
+    return acn_check_launch("acn_field_fwd");
+}
+
+extern "C" int acn_render_stratified_fwd(const float* rays, int64_t N, int S, const float* jitter,
+                                         const acn_expert* experts, const acn_routing* routing, int active_module,
+                                         const acn_background* bg, float sigma_scale, float tau, void* workspace,
+                                         size_t workspace_bytes, float* rgb, float* depth, float* weights, float* acc,
+                                         void* stream) {
+    ACN_REQUIRE(N >= 0, "acn_render_stratified_fwd: N must be >= 0");
+    ACN_REQUIRE(S >= 2, "acn_render_stratified_fwd: ray_samples must be >= 2, got %d", S);
+    if (N == 0) return ACN_OK;
+    ACN_REQUIRE(rays && rgb && depth && acc, "acn_render_stratified_fwd: NULL pointer");
+    ACN_REQUIRE(bg, "acn_render_stratified_fwd: NULL background");
+    if (bg->mode == ACN_BG_MLP) {
+        ACN_REQUIRE(bg->w1 && bg->b1 && bg->w2 && bg->b2, "background MLP pointers are NULL");
+        ACN_REQUIRE(bg->hidden >= 1 && bg->hidden <= 64, "bg_hidden must be in [1, 64], got %d", bg->hidden);
+    }
+    hipStream_t s = (hipStream_t)stream;
+    FieldCfg cfg{};
+    int interp, K;
+    int st = prepare(experts, routing, active_module, workspace, workspace_bytes, s, cfg, interp, K);
+    if (st) return st;
+    BgArgs b{bg->mode, bg->hidden, {bg->color[0], bg->color[1], bg->color[2]}, bg->w1, bg->b1, bg->w2, bg->b2};
+    RenderParams p{rays, N, S, jitter, (const float*)workspace, sigma_scale, tau, rgb, depth, weights, acc};
+    const int64_t wgs = (N + 15) / 16;
+    const dim3 grid((unsigned)(wgs < num_cus() ? wgs : num_cus())), block(1024);
+#define ACN_RENDER_LAUNCH(I, KL, R) hipLaunchKernelGGL((render_kernel<I, KL, R>), grid, block, 0, s, cfg, b, p)
+    ACN_DISPATCH(ACN_RENDER_LAUNCH);
+#undef ACN_RENDER_LAUNCH
+    return acn_check_launch("acn_render_stratified_fwd");
+}
+
+extern "C" int acn_volume_render_fwd(const float* rgb_sigma, const float* t_vals, const float* bg, int64_t N, int S,
+                                     int raw_rgb, int raw_sigma, float sigma_scale, float* rgb, float* depth,
+                                     float* weights, float* acc, void* stream) {
+    ACN_REQUIRE(N >= 0 && S >= 2, "acn_volume_render_fwd: need N >= 0 and S >= 2 (got S=%d)", S);
+    if (N == 0) return ACN_OK;
+    ACN_REQUIRE(rgb_sigma && t_vals && rgb && depth && acc, "acn_volume_render_fwd: NULL pointer");
+    const int64_t wgs = (N + 3) / 4;
+    const dim3 grid((unsigned)(wgs < 4096 ? wgs : 4096)), block(256);
+    hipLaunchKernelGGL(volume_render_kernel, grid, block, 0, (hipStream_t)stream, rgb_sigma, t_vals, bg, N, S, raw_rgb,
+                       raw_sigma, sigma_scale, rgb, depth, weights, acc);
+    return acn_check_launch("acn_volume_render_fwd");
+}
+
+extern "C" int acn_routing_fwd(const float* pts, int64_t M, int64_t ld, const acn_routing* routing, float* weights,
+                               int32_t* hard, void* stream) {
+    ACN_REQUIRE(routing && routing->K >= 1 && routing->K <= ACN_MAX_EXPERTS, "acn_routing_fwd: bad routing");
+    ACN_REQUIRE(M >= 0 && ld >= 3, "acn_routing_fwd: pts must be (N, >=3)");
+    if (M == 0) return ACN_OK;
+    const bool soft = routing->boundary_margin > 1.0f;
+    ACN_REQUIRE(pts && (soft ? weights != nullptr : hard != nullptr), "acn_routing_fwd: NULL pointer");
+    FieldCfg cfg{};
+    cfg.K = routing->K;
+    cfg.cluster_2d = routing->cluster_2d;
+    cfg.bm = routing->boundary_margin;
+    cfg.routing = soft ? 1 : 2;
+    for (int k = 0; k < cfg.K; ++k)
+        for (int a = 0; a < 3; ++a) cfg.cent[k][a] = routing->centroids[k][a];
+    hipLaunchKernelGGL(routing_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, (hipStream_t)stream, cfg, pts, M,
+                       ld, weights, hard);
+    return acn_check_launch("acn_routing_fwd");
+}
+
+extern "C" int acn_background_fwd(const float* dirs, int64_t N, const acn_background* bg, float* out, void* stream) {
+    ACN_REQUIRE(N >= 0 && bg, "acn_background_fwd: bad arguments");
+    if (N == 0) return ACN_OK;
+    ACN_REQUIRE(dirs && out, "acn_background_fwd: NULL pointer");
+    if (bg->mode == ACN_BG_MLP) {
+        ACN_REQUIRE(bg->w1 && bg->b1 && bg->w2 && bg->b2, "background MLP pointers are NULL");
+        ACN_REQUIRE(bg->hidden >= 1 && bg->hidden <= 64, "bg_hidden must be in [1, 64], got %d", bg->hidden);
+    }
+    BgArgs b{bg->mode, bg->hidden, {bg->color[0], bg->color[1], bg->color[2]}, bg->w1, bg->b1, bg->w2, bg->b2};
+    const int64_t wgs = (N + 3) / 4;
+    hipLaunchKernelGGL(background_kernel, dim3((unsigned)(wgs < 8192 ? wgs : 8192)), dim3(256), 0, (hipStream_t)stream,
+                       b, dirs, N, out);
+    return acn_check_launch("acn_background_fwd");
+}

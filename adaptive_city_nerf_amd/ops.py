@@ -1,0 +1,232 @@
+"""Tensor-level wrappers over libacnerf.so (include/acnerf.h).
+
+Each function validates shapes the way the reference's asserts do, makes inputs contiguous fp32
+device tensors, allocates outputs with the caching allocator and launches on the current stream.
+No CPU path exists: CPU tensors raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, Optional, Sequence
+
+import torch
+
+from . import _lib
+from ._lib import (ACN_BG_CONST, ACN_BG_MLP, ACN_BG_NONE, AcnError, acn_background, acn_expert,
+                   acn_routing, check, ptr, require_hip, stream_of)
+
+MLP_KEYS = (
+    ("sig_w0", "sigma_trunk.0.linear.weight"), ("sig_b0", "sigma_trunk.0.linear.bias"),
+    ("sig_w1", "sigma_trunk.1.linear.weight"), ("sig_b1", "sigma_trunk.1.linear.bias"),
+    ("sigh_w", "sigma_head.weight"), ("sigh_b", "sigma_head.bias"),
+    ("geo_w", "geo_head.weight"), ("geo_b", "geo_head.bias"),
+    ("col_w0", "color_mlp.0.linear.weight"), ("col_b0", "color_mlp.0.linear.bias"),
+    ("col_w1", "color_mlp.1.linear.weight"), ("col_b1", "color_mlp.1.linear.bias"),
+    ("col_w2", "color_mlp.2.weight"), ("col_b2", "color_mlp.2.bias"),
+)
+MLP_SHAPES = {
+    "sigma_trunk.0.linear.weight": (64, 32), "sigma_trunk.0.linear.bias": (64,),
+    "sigma_trunk.1.linear.weight": (64, 64), "sigma_trunk.1.linear.bias": (64,),
+    "sigma_head.weight": (1, 64), "sigma_head.bias": (1,),
+    "geo_head.weight": (15, 64), "geo_head.bias": (15,),
+    "color_mlp.0.linear.weight": (64, 31), "color_mlp.0.linear.bias": (64,),
+    "color_mlp.1.linear.weight": (64, 64), "color_mlp.1.linear.bias": (64,),
+    "color_mlp.2.weight": (3, 64), "color_mlp.2.bias": (3,),
+}
+
+
+def _f32(t: torch.Tensor) -> torch.Tensor:
+    return t.detach().to(torch.float32).contiguous()
+
+
+# ---------------------------------------------------------------------------------------------
+def hashgrid_fwd(x01: torch.Tensor, table: torch.Tensor, resolutions: Sequence[int], log2T: int,
+                 F: int, interp: int) -> torch.Tensor:
+    require_hip(x01, "HashGridEncoder")
+    assert x01.shape[-1] == 3, f"Expected (...,3), got {tuple(x01.shape)}"
+    L = len(resolutions)
+    x = _f32(x01).view(-1, 3)
+    tab = _f32(table)
+    if tab.shape != (L << log2T, F):
+        raise AcnError(f"hash table must be ({L << log2T}, {F}), got {tuple(tab.shape)}")
+    out = torch.empty(x.shape[0], L * F, device=x.device, dtype=torch.float32)
+    res = (C.c_int32 * L)(*[int(r) for r in resolutions])
+    check(_lib.lib().acn_hashgrid_fwd(ptr(x), x.shape[0], ptr(tab), res, L, log2T, F, interp, ptr(out),
+                                      stream_of(x)), "acn_hashgrid_fwd")
+    return out.view(*x01.shape[:-1], L * F)
+
+
+def hashgrid_bwd(x01: torch.Tensor, grad_out: torch.Tensor, resolutions: Sequence[int], log2T: int, F: int,
+                 interp: int) -> torch.Tensor:
+    L = len(resolutions)
+    x = _f32(x01).view(-1, 3)
+    g = _f32(grad_out).view(-1, L * F)
+    gt = torch.zeros(L << log2T, F, device=x.device, dtype=torch.float32)
+    res = (C.c_int32 * L)(*[int(r) for r in resolutions])
+    check(_lib.lib().acn_hashgrid_bwd(ptr(x), x.shape[0], ptr(g), res, L, log2T, F, interp, ptr(gt),
+                                      stream_of(x)), "acn_hashgrid_bwd")
+    return gt
+
+
+def sh_fwd(d: torch.Tensor, levels: int) -> torch.Tensor:
+    require_hip(d, "SHEncoder")
+    assert d.shape[-1] == 3, f"Expected (...,3); got {tuple(d.shape)}"
+    x = _f32(d).view(-1, 3)
+    out = torch.empty(x.shape[0], levels * levels, device=x.device, dtype=torch.float32)
+    check(_lib.lib().acn_sh_fwd(ptr(x), x.shape[0], levels, ptr(out), stream_of(x)), "acn_sh_fwd")
+    return out.view(*d.shape[:-1], levels * levels)
+
+
+# ---------------------------------------------------------------------------------------------
+class ExpertSpec:
+    """The device-side description of one MetaNGP expert: hash table + level resolutions + AABB +
+    the 14 MLP tensors (module parameters or fast weights from a `params` dict)."""
+
+    def __init__(self, table: torch.Tensor, resolutions: Sequence[int], log2T: int, interp: int,
+                 aabb_min: Sequence[float], aabb_extent: Sequence[float], mlp: Dict[str, torch.Tensor],
+                 F: int = 2):
+        self.keep = []
+        s = acn_expert()
+        tab = _f32(table)
+        self.keep.append(tab)
+        s.table = ptr(tab)
+        s.L = len(resolutions)
+        s.log2T = int(log2T)
+        s.F = int(F)
+        s.interp = int(interp)
+        for i, r in enumerate(resolutions):
+            s.res[i] = int(r)
+        s.aabb_min[:] = [float(v) for v in aabb_min]
+        s.aabb_extent[:] = [float(v) for v in aabb_extent]
+        for field, key in MLP_KEYS:
+            if key not in mlp:
+                raise AcnError(f"missing MLP tensor {key!r}")
+            t = _f32(mlp[key])
+            if tuple(t.shape) != MLP_SHAPES[key]:
+                raise AcnError(f"the fused HIP field supports the reference architecture (nerf_runner.py:102-121); "
+                               f"{key} has shape {tuple(t.shape)}, expected {MLP_SHAPES[key]}")
+            self.keep.append(t)
+            setattr(s, field, ptr(t))
+        self.s = s
+        self.device = tab.device
+
+
+def make_routing(centroids: torch.Tensor, K: int, cluster_2d: bool, boundary_margin: float) -> acn_routing:
+    r = acn_routing()
+    r.K = int(K)
+    r.cluster_2d = int(bool(cluster_2d))
+    r.boundary_margin = float(boundary_margin)
+    c = centroids.detach().float().cpu()
+    for k in range(K):
+        for a in range(3):
+            r.centroids[k][a] = float(c[k, a])
+    return r
+
+
+def make_background(mode: str, color=None, mlp: Optional[Dict[str, torch.Tensor]] = None):
+    b = acn_background()
+    keep = []
+    if mode == "mlp":
+        b.mode = ACN_BG_MLP
+        w1 = _f32(mlp["0.weight"]); b1 = _f32(mlp["0.bias"]); w2 = _f32(mlp["2.weight"]); b2 = _f32(mlp["2.bias"])
+        if w1.shape[1] != 16 or w2.shape[0] != 3:
+            raise AcnError("background MLP must be Linear(16, H) -> Linear(H, 3)")
+        keep += [w1, b1, w2, b2]
+        b.hidden = int(w1.shape[0])
+        b.w1, b.b1, b.w2, b.b2 = ptr(w1), ptr(b1), ptr(w2), ptr(b2)
+    elif mode == "const":
+        b.mode = ACN_BG_CONST
+        b.color[:] = [float(v) for v in color]
+    else:
+        b.mode = ACN_BG_NONE
+    return b, keep
+
+
+def _experts_array(experts: Sequence[ExpertSpec]):
+    return (acn_expert * len(experts))(*[e.s for e in experts])
+
+
+def field_fwd(x: torch.Tensor, experts: Sequence[ExpertSpec], routing: acn_routing,
+              active_module: Optional[int] = None) -> torch.Tensor:
+    require_hip(x, "MetaContainer.forward")
+    assert x.dim() == 2 and x.shape[-1] >= 6, "x must be (N,D>=6)"
+    xx = _f32(x)
+    M = xx.shape[0]
+    out = torch.empty(M, 4, device=xx.device, dtype=torch.float32)
+    if M == 0:
+        return out
+    K = 1 if active_module is not None else routing.K
+    ws = torch.empty(int(_lib.lib().acn_workspace_bytes(K)) // 4, device=xx.device, dtype=torch.float32)
+    arr = _experts_array(experts)
+    check(_lib.lib().acn_field_fwd(ptr(xx), M, xx.shape[1], arr, C.byref(routing),
+                                   -1 if active_module is None else int(active_module), ptr(ws),
+                                   ws.numel() * 4, ptr(out), stream_of(xx)), "acn_field_fwd")
+    return out
+
+
+def render_stratified(rays: torch.Tensor, S: int, experts: Sequence[ExpertSpec], routing: acn_routing,
+                      active_module: Optional[int], background, sigma_scale: float = 1.0, tau: float = 0.0,
+                      jitter: Optional[torch.Tensor] = None, want_weights: bool = True):
+    require_hip(rays, "render_rays")
+    assert rays.dim() == 2 and rays.shape[-1] == 8, "rays must be (N,8)"
+    r = _f32(rays)
+    N = r.shape[0]
+    dev = r.device
+    rgb = torch.empty(N, 3, device=dev, dtype=torch.float32)
+    depth = torch.empty(N, device=dev, dtype=torch.float32)
+    acc = torch.empty(N, device=dev, dtype=torch.float32)
+    weights = torch.empty(N, S, device=dev, dtype=torch.float32) if want_weights else None
+    if N == 0:
+        return rgb, depth, weights, acc
+    K = 1 if active_module is not None else routing.K
+    ws = torch.empty(int(_lib.lib().acn_workspace_bytes(K)) // 4, device=dev, dtype=torch.float32)
+    arr = _experts_array(experts)
+    jit = None if jitter is None else _f32(jitter)
+    check(_lib.lib().acn_render_stratified_fwd(
+        ptr(r), N, int(S), ptr(jit), arr, C.byref(routing), -1 if active_module is None else int(active_module),
+        C.byref(background), float(sigma_scale), float(tau), ptr(ws), ws.numel() * 4, ptr(rgb), ptr(depth),
+        ptr(weights), ptr(acc), stream_of(r)), "acn_render_stratified_fwd")
+    return rgb, depth, weights, acc
+
+
+def volume_render(rgb_sigma: torch.Tensor, t_vals: torch.Tensor, bg_rgb: Optional[torch.Tensor] = None,
+                  raw_rgb: bool = False, raw_sigma: bool = False, sigma_scale: float = 1.0):
+    require_hip(rgb_sigma, "volume_render")
+    rs = _f32(rgb_sigma)
+    t = _f32(t_vals)
+    N, S = t.shape
+    assert rs.shape == (N, S, 4), f"rgb_sigma must be (N,S,4), got {tuple(rs.shape)}"
+    dev = rs.device
+    bg = None if bg_rgb is None else _f32(bg_rgb.to(dev)).view(N, 3)
+    rgb = torch.empty(N, 3, device=dev, dtype=torch.float32)
+    depth = torch.empty(N, device=dev, dtype=torch.float32)
+    w = torch.empty(N, S, device=dev, dtype=torch.float32)
+    acc = torch.empty(N, device=dev, dtype=torch.float32)
+    check(_lib.lib().acn_volume_render_fwd(ptr(rs), ptr(t), ptr(bg), N, S, int(raw_rgb), int(raw_sigma),
+                                           float(sigma_scale), ptr(rgb), ptr(depth), ptr(w), ptr(acc),
+                                           stream_of(rs)), "acn_volume_render_fwd")
+    return rgb, depth, w, acc
+
+
+def get_rays_image(H: int, W: int, fx: float, fy: float, cx: float, cy: float, c2w: torch.Tensor,
+                   aabb: Optional[torch.Tensor], device, center_pixels: bool = True, near: Optional[float] = None,
+                   far: Optional[float] = None, near_far_override=None, apply_clamp: bool = True):
+    c = c2w.detach().float().cpu().contiguous()[:3, :4].contiguous()
+    c_arr = (C.c_float * 12)(*c.view(-1).tolist())
+    a_arr = None
+    if aabb is not None:
+        a = aabb.detach().float().cpu().contiguous().view(-1)
+        a_arr = (C.c_float * 6)(*a.tolist())
+    hn = hf = 0
+    nv = fv = 0.0
+    if near_far_override is not None:
+        if near_far_override[0] is not None:
+            hn, nv = 1, float(near_far_override[0])
+        if near_far_override[1] is not None:
+            hf, fv = 1, float(near_far_override[1])
+    rays = torch.empty(H * W, 8, device=device, dtype=torch.float32)
+    valid = torch.empty(H * W, device=device, dtype=torch.uint8)
+    check(_lib.lib().acn_get_rays(int(H), int(W), float(fx), float(fy), float(cx), float(cy), int(center_pixels),
+                                  c_arr, a_arr, float(near or 0.0), float(far or 0.0), hn, nv, hf, fv,
+                                  int(apply_clamp), ptr(rays), ptr(valid), stream_of(rays)), "acn_get_rays")
+    return rays, valid.bool()

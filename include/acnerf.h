@@ -1,0 +1,170 @@
+/*
+ * acnerf.h -- C ABI of libacnerf.so, the MI355X (gfx950) volumetric ray renderer for the
+ * psklavos1/adaptive-city-nerf stratified render hot path.
+ *
+ * Every entry point takes plain device pointers + sizes + a hipStream_t (as void*), launches
+ * hand-written CDNA4 kernels on that stream and returns an int status: 0 = ok, > 0 = hipError_t,
+ * < 0 = argument / unsupported-configuration error.  No C++ exception crosses the ABI; the
+ * message of the last failure on the calling thread is available from acn_last_error().
+ *
+ * Ownership: the caller owns every buffer (inputs, outputs and the workspace); the library
+ * never allocates or frees device memory and keeps no pointer past the call.  Functions are
+ * stateless and reentrant (the reference's viewer renders from a callback thread while an
+ * adaptation thread runs: viewer/viewer.py:712-848, viewer/engine/controller.py:220).
+ *
+ * Each function names the reference interface it replaces (file:line under the reference repo).
+ */
+#ifndef ACNERF_H
+#define ACNERF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ACN_ABI_VERSION 1
+
+#define ACN_OK 0
+#define ACN_ERR_ARG (-1)          /* shape / argument error (mirrors the reference's asserts) */
+#define ACN_ERR_UNSUPPORTED (-2)  /* configuration the fused kernels do not implement */
+
+#define ACN_MAX_LEVELS 32
+#define ACN_MAX_EXPERTS 16
+
+/* interpolation modes of HashGridEncoder (models/encodings.py:158, :340-364) */
+#define ACN_INTERP_NEAREST 0
+#define ACN_INTERP_LINEAR 1
+#define ACN_INTERP_SMOOTHSTEP 2
+
+/* One Instant-NGP expert (MetaNGP, models/inr/meta_ngp.py:15-241).  Pointers are device memory
+ * holding the reference's own tensors (state-dict layout, nn.Linear weights (out, in) row-major),
+ * or the fast weights of a `params` dict (models/metamodule/metamodule.py:140-156).
+ * The fused kernels implement the reference's configured architecture (nerf_runner.py:102-121):
+ * L*F = 32 hash features, sigma_trunk 2 x 64 (ReLU), sigma_head 64->1, geo_head 64->15,
+ * SH levels 4 (16 comps), color_mlp 31->64->64 (ReLU) ->3, sigmoid rgb.                       */
+typedef struct acn_expert {
+    const float* table;            /* xyz_encoder.hash_table (L << log2T, F) */
+    int32_t L, log2T, F, interp;
+    int32_t res[ACN_MAX_LEVELS];   /* xyz_encoder.level_resolutions (host values) */
+    float aabb_min[3];             /* scene_box.min               (meta_ngp.py:157) */
+    float aabb_extent[3];          /* aabb_extent buffer          (meta_ngp.py:37)  */
+    const float *sig_w0, *sig_b0;  /* sigma_trunk.0.linear  (64, 32), (64,) */
+    const float *sig_w1, *sig_b1;  /* sigma_trunk.1.linear  (64, 64), (64,) */
+    const float *sigh_w, *sigh_b;  /* sigma_head            (1, 64),  (1,)  */
+    const float *geo_w, *geo_b;    /* geo_head              (15, 64), (15,) */
+    const float *col_w0, *col_b0;  /* color_mlp.0.linear    (64, 31), (64,) */
+    const float *col_w1, *col_b1;  /* color_mlp.1.linear    (64, 64), (64,) */
+    const float *col_w2, *col_b2;  /* color_mlp.2           (3, 64),  (3,)  */
+} acn_expert;
+
+/* MetaContainer routing (models/inr/meta_container.py:97-134): soft inverse-distance weights
+ * when boundary_margin > 1, else nearest centroid.                                           */
+typedef struct acn_routing {
+    int32_t K;                     /* number of experts */
+    int32_t cluster_2d;            /* 1: route on (y, z) (coord idx (1, 2)), 0: on (x, y, z) */
+    float boundary_margin;         /* bm (>= 1) */
+    float centroids[ACN_MAX_EXPERTS][3];
+} acn_routing;
+
+/* Background (ray_rendering.py:23-79 _get_bg_rgb / get_bg_default_color, and
+ * MetaContainer.background_color meta_container.py:347-382).                                */
+#define ACN_BG_NONE 0              /* bg_color_default == "none" */
+#define ACN_BG_CONST 1             /* white / black */
+#define ACN_BG_MLP 2               /* use_bg_nerf: SH(4) -> Linear(16,H) ReLU -> Linear(H,3) Sigmoid */
+typedef struct acn_background {
+    int32_t mode;
+    int32_t hidden;                /* H (bg_hidden, default 32; <= 64) */
+    float color[3];                /* ACN_BG_CONST */
+    const float *w1, *b1;          /* bg_mlp.0 (H, 16), (H,) device */
+    const float *w2, *b2;          /* bg_mlp.2 (3, H),  (3,) device */
+} acn_background;
+
+/* ---------------------------------------------------------------------------------------- */
+int acn_version(void);                              /* ACN_ABI_VERSION */
+int acn_last_error(char* buf, size_t n);            /* thread-local message of the last failure */
+
+/* HashGridEncoder._torch_forward (models/encodings.py:331-381): x01 (M,3) -> out (M, L*F),
+ * level-major / feature-minor.  res: host pointer to L level resolutions.                     */
+int acn_hashgrid_fwd(const float* x01, int64_t M, const float* table, const int32_t* res, int L,
+                     int log2T, int F, int interp, float* out, void* stream);
+
+/* Backward of the same gathers (autograd of table[idx], encodings.py:324-327): grad_table +=
+ * scatter of grad_out (M, L*F).  grad_table must be zero-initialised by the caller.           */
+int acn_hashgrid_bwd(const float* x01, int64_t M, const float* grad_out, const int32_t* res,
+                     int L, int log2T, int F, int interp, float* grad_table, void* stream);
+
+/* SHEncoder.forward torch fallback (models/encodings.py:133-151, :27-81): d (M,3) unnormalised
+ * -> out (M, levels^2), levels in [1, 5].                                                     */
+int acn_sh_fwd(const float* d, int64_t M, int levels, float* out, void* stream);
+
+/* Bytes of device workspace the fused field / render entry points need for K experts. */
+size_t acn_workspace_bytes(int K);
+
+/* MetaContainer.forward / MetaNGP.forward (meta_container.py:275-343, meta_ngp.py:226-241):
+ * x (M, ld>=6) rows [xyz, dir, ...] -> out (M, 4) = [rgb, sigma].  active_module >= 0 runs only
+ * that expert (no routing), as the reference's `active_module` argument does.                */
+int acn_field_fwd(const float* x, int64_t M, int64_t ld, const acn_expert* experts,
+                  const acn_routing* routing, int active_module, void* workspace,
+                  size_t workspace_bytes, float* out, void* stream);
+
+/* volume_render (nerfs/ray_rendering.py:114-165): rgb_sigma (N,S,4), t_vals (N,S), bg (N,3) or
+ * NULL -> rgb (N,3), depth (N), weights (N,S) or NULL, acc (N).                              */
+int acn_volume_render_fwd(const float* rgb_sigma, const float* t_vals, const float* bg, int64_t N,
+                          int S, int raw_rgb, int raw_sigma, float sigma_scale, float* rgb,
+                          float* depth, float* weights, float* acc, void* stream);
+
+/* Fused render_rays_stratified (ray_rendering.py:290-345 + stratified_t_vals :262-287 +
+ * _get_bg_rgb :23-45 + volume_render :114-165) with the field of every expert evaluated in the
+ * same kernel.  rays (N,8) [o, d, near, far]; jitter (N,S) uniforms of the training-mode draw
+ * (:286) or NULL for eval; tau: early-ray-termination threshold on transmittance (0 = off; the
+ * reference has none, the composite error is bounded by 2*tau).  Outputs as volume_render.     */
+int acn_render_stratified_fwd(const float* rays, int64_t N, int S, const float* jitter,
+                              const acn_expert* experts, const acn_routing* routing,
+                              int active_module, const acn_background* bg, float sigma_scale,
+                              float tau, void* workspace, size_t workspace_bytes, float* rgb,
+                              float* depth, float* weights, float* acc, void* stream);
+
+/* get_ray_directions + get_rays + clamp_rays_near_far (nerfs/ray_sampling.py:111-136, :50-108,
+ * :139-176) with SceneBox.ray_aabb_intersect (nerfs/scene_box.py:45-107).  c2w: host (3,4)
+ * row-major; aabb: host (2,3) or NULL (then near/far constants are used); the override flags
+ * reproduce near_far_override=(n|None, f|None); apply_clamp=0 reproduces override None.
+ * Writes rays (H*W, 8) and valid (H*W) bytes (valid may be NULL).                             */
+int acn_get_rays(int H, int W, float fx, float fy, float cx, float cy, int center_pixels,
+                 const float* c2w, const float* aabb, float near_c, float far_c, int has_near_ovr,
+                 float near_ovr, int has_far_ovr, float far_ovr, int apply_clamp, float* rays,
+                 uint8_t* valid, void* stream);
+
+/* get_ray_directions (ray_sampling.py:111-136): dirs (H*W, 3) unit camera-frame directions. */
+int acn_ray_directions(int H, int W, float fx, float fy, float cx, float cy, int center_pixels, float* dirs,
+                       void* stream);
+
+/* get_rays (ray_sampling.py:50-108) for given directions (N,3): rays (N,8).  c2w host (3,4);
+ * aabb host (2,3) -> SceneBox.ray_aabb_intersect(eps, max_bound, invalid_value), or NULL ->
+ * constant near_c / far_c.                                                                   */
+int acn_rays_from_dirs(const float* dirs, int64_t N, const float* c2w, const float* aabb, float near_c,
+                       float far_c, float eps, float max_bound, float invalid_value, float* rays,
+                       void* stream);
+
+/* SceneBox.ray_aabb_intersect (nerfs/scene_box.py:45-107): origins, dirs (N,3) -> tmin, tmax (N). */
+int acn_ray_aabb(const float* origins, const float* dirs, int64_t N, const float* aabb, float eps,
+                 float max_bound, float invalid_value, float* tmin, float* tmax, void* stream);
+
+/* clamp_rays_near_far (ray_sampling.py:139-176) in place on rays (N,8); apply=0 reproduces
+ * near_far_override=None (valid mask only).  valid (N) bytes may be NULL.                     */
+int acn_clamp_rays(float* rays, int64_t N, int apply, int has_near_ovr, float near_ovr, int has_far_ovr,
+                   float far_ovr, float eps, float invalid_value, uint8_t* valid, void* stream);
+
+/* MetaContainer._routing (meta_container.py:97-134): pts (M, ld>=3) -> soft weights (M, K) when
+ * boundary_margin > 1, else hard assignment (M) int32.                                        */
+int acn_routing_fwd(const float* pts, int64_t M, int64_t ld, const acn_routing* routing, float* weights,
+                    int32_t* hard, void* stream);
+
+/* MetaContainer.background_color (meta_container.py:347-382): dirs (N,3) -> rgb (N,3). */
+int acn_background_fwd(const float* dirs, int64_t N, const acn_background* bg, float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ACNERF_H */
