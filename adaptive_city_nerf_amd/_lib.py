@@ -63,6 +63,7 @@ SIGNATURES = {
     "acn_hashgrid_bwd": ([vp, i64, vp, vp, i32, i32, i32, i32, vp, vp], C.c_int),
     "acn_sh_fwd": ([vp, i64, i32, vp, vp], C.c_int),
     "acn_workspace_bytes": ([i32], sz),
+    "acn_pack_experts": ([vp, vp, i32, vp, sz, vp], C.c_int),
     "acn_field_fwd": ([vp, i64, i64, vp, vp, i32, vp, sz, vp, vp], C.c_int),
     "acn_volume_render_fwd": ([vp, vp, vp, i64, i32, i32, i32, f32, vp, vp, vp, vp, vp], C.c_int),
     "acn_render_stratified_fwd": ([vp, i64, i32, vp, vp, vp, i32, vp, f32, f32, vp, sz, vp, vp, vp, vp, vp],

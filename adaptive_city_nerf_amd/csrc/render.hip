@@ -718,7 +718,7 @@ int check_expert(const acn_expert& e, int k) {
 
 // Builds FieldCfg + packs weights into the workspace.  Returns status; sets *interp.
 int prepare(const acn_expert* experts, const acn_routing* routing, int active_module, void* workspace,
-            size_t workspace_bytes, hipStream_t s, FieldCfg& cfg, int& interp, int& Keval) {
+            size_t workspace_bytes, hipStream_t s, FieldCfg& cfg, int& interp, int& Keval, bool do_pack) {
     ACN_REQUIRE(experts && routing, "NULL experts/routing");
     const int K = routing->K;
     ACN_REQUIRE(K >= 1 && K <= ACN_MAX_EXPERTS, "routing.K must be in [1, %d], got %d", ACN_MAX_EXPERTS, K);
@@ -753,9 +753,12 @@ int prepare(const acn_expert* experts, const acn_routing* routing, int active_mo
     else cfg.routing = routing->boundary_margin > 1.0f ? 1 : 2;
     for (int k = 0; k < K && active_module < 0; ++k)
         for (int a = 0; a < 3; ++a) cfg.cent[k][a] = routing->centroids[k][a];
-    hipLaunchKernelGGL(pack_kernel, dim3((PK_FLOATS + 255) / 256, Keval), dim3(256), 0, s, pa, Keval,
-                       (float*)workspace);
-    return acn_check_launch("acn pack_kernel");
+    if (do_pack) {
+        hipLaunchKernelGGL(pack_kernel, dim3((PK_FLOATS + 255) / 256, Keval), dim3(256), 0, s, pa, Keval,
+                           (float*)workspace);
+        return acn_check_launch("acn_pack_experts");
+    }
+    return ACN_OK;
 }
 
 }  // namespace
@@ -777,6 +780,14 @@ int prepare(const acn_expert* experts, const acn_routing* routing, int active_mo
 
 extern "C" size_t acn_workspace_bytes(int K) { return (size_t)(K < 1 ? 1 : K) * PK_BYTES; }
 
+extern "C" int acn_pack_experts(const acn_expert* experts, const acn_routing* routing, int active_module,
+                                void* workspace, size_t workspace_bytes, void* stream) {
+    FieldCfg cfg{};
+    int interp, K;
+    return prepare(experts, routing, active_module, workspace, workspace_bytes, (hipStream_t)stream, cfg, interp, K,
+                   true);
+}
+
 extern "C" int acn_field_fwd(const float* x, int64_t M, int64_t ld, const acn_expert* experts,
                              const acn_routing* routing, int active_module, void* workspace, size_t workspace_bytes,
                              float* out, void* stream) {
@@ -786,7 +797,7 @@ extern "C" int acn_field_fwd(const float* x, int64_t M, int64_t ld, const acn_ex
     hipStream_t s = (hipStream_t)stream;
     FieldCfg cfg{};
     int interp, K;
-    int st = prepare(experts, routing, active_module, workspace, workspace_bytes, s, cfg, interp, K);
+    int st = prepare(experts, routing, active_module, workspace, workspace_bytes, s, cfg, interp, K, false);
     if (st) return st;
     FieldParams p{x, M, ld, (const float*)workspace, out};
     const int64_t ntiles = (M + 31) / 32;
@@ -815,7 +826,7 @@ extern "C" int acn_render_stratified_fwd(const float* rays, int64_t N, int S, co
     hipStream_t s = (hipStream_t)stream;
     FieldCfg cfg{};
     int interp, K;
-    int st = prepare(experts, routing, active_module, workspace, workspace_bytes, s, cfg, interp, K);
+    int st = prepare(experts, routing, active_module, workspace, workspace_bytes, s, cfg, interp, K, false);
     if (st) return st;
     BgArgs b{bg->mode, bg->hidden, {bg->color[0], bg->color[1], bg->color[2]}, bg->w1, bg->b1, bg->w2, bg->b2};
     RenderParams p{rays, N, S, jitter, (const float*)workspace, sigma_scale, tau, rgb, depth, weights, acc};

@@ -146,8 +146,40 @@ def _experts_array(experts: Sequence[ExpertSpec]):
     return (acn_expert * len(experts))(*[e.s for e in experts])
 
 
+def pack_experts(experts: Sequence[ExpertSpec], routing: acn_routing, active_module: Optional[int] = None,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """MFMA-ordered weight image of the experts the next fused call evaluates (acn_pack_experts)."""
+    K = 1 if active_module is not None else routing.K
+    nbytes = int(_lib.lib().acn_workspace_bytes(K))
+    dev = experts[0].device
+    if out is None or out.numel() * 4 < nbytes or out.device != dev:
+        out = torch.empty(nbytes // 4, device=dev, dtype=torch.float32)
+    arr = _experts_array(experts)
+    check(_lib.lib().acn_pack_experts(arr, C.byref(routing), -1 if active_module is None else int(active_module),
+                                      ptr(out), out.numel() * 4, int(torch.cuda.current_stream(dev).cuda_stream)),
+          "acn_pack_experts")
+    return out
+
+
+class PackCache:
+    """Re-packs only when the (module-owned) weights changed: the key is built from the identity,
+    storage and version counter of every packed tensor (in-place updates and load_state_dict bump
+    the version).  Fast-weight dicts are never cached (their storage is recycled per step)."""
+
+    def __init__(self):
+        self.key = None
+        self.ws = None
+
+    def get(self, experts: Sequence[ExpertSpec], routing: acn_routing, active_module: Optional[int], key):
+        if key is not None and key == self.key and self.ws is not None:
+            return self.ws
+        self.ws = pack_experts(experts, routing, active_module, out=self.ws)
+        self.key = key
+        return self.ws
+
+
 def field_fwd(x: torch.Tensor, experts: Sequence[ExpertSpec], routing: acn_routing,
-              active_module: Optional[int] = None) -> torch.Tensor:
+              active_module: Optional[int] = None, packed: Optional[torch.Tensor] = None) -> torch.Tensor:
     require_hip(x, "MetaContainer.forward")
     assert x.dim() == 2 and x.shape[-1] >= 6, "x must be (N,D>=6)"
     xx = _f32(x)
@@ -155,8 +187,7 @@ def field_fwd(x: torch.Tensor, experts: Sequence[ExpertSpec], routing: acn_routi
     out = torch.empty(M, 4, device=xx.device, dtype=torch.float32)
     if M == 0:
         return out
-    K = 1 if active_module is not None else routing.K
-    ws = torch.empty(int(_lib.lib().acn_workspace_bytes(K)) // 4, device=xx.device, dtype=torch.float32)
+    ws = packed if packed is not None else pack_experts(experts, routing, active_module)
     arr = _experts_array(experts)
     check(_lib.lib().acn_field_fwd(ptr(xx), M, xx.shape[1], arr, C.byref(routing),
                                    -1 if active_module is None else int(active_module), ptr(ws),
@@ -164,9 +195,15 @@ def field_fwd(x: torch.Tensor, experts: Sequence[ExpertSpec], routing: acn_routi
     return out
 
 
+# Optional timing hook (bench.py): when set to a list, render_stratified appends a pair of
+# recorded HIP events bracketing exactly the fused render kernel on the launch stream.
+EVENT_HOOK = None
+
+
 def render_stratified(rays: torch.Tensor, S: int, experts: Sequence[ExpertSpec], routing: acn_routing,
                       active_module: Optional[int], background, sigma_scale: float = 1.0, tau: float = 0.0,
-                      jitter: Optional[torch.Tensor] = None, want_weights: bool = True):
+                      jitter: Optional[torch.Tensor] = None, want_weights: bool = True,
+                      packed: Optional[torch.Tensor] = None):
     require_hip(rays, "render_rays")
     assert rays.dim() == 2 and rays.shape[-1] == 8, "rays must be (N,8)"
     r = _f32(rays)
@@ -178,14 +215,21 @@ def render_stratified(rays: torch.Tensor, S: int, experts: Sequence[ExpertSpec],
     weights = torch.empty(N, S, device=dev, dtype=torch.float32) if want_weights else None
     if N == 0:
         return rgb, depth, weights, acc
-    K = 1 if active_module is not None else routing.K
-    ws = torch.empty(int(_lib.lib().acn_workspace_bytes(K)) // 4, device=dev, dtype=torch.float32)
+    ws = packed if packed is not None else pack_experts(experts, routing, active_module)
     arr = _experts_array(experts)
     jit = None if jitter is None else _f32(jitter)
+    hook = EVENT_HOOK
+    if hook is not None:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record()
     check(_lib.lib().acn_render_stratified_fwd(
         ptr(r), N, int(S), ptr(jit), arr, C.byref(routing), -1 if active_module is None else int(active_module),
         C.byref(background), float(sigma_scale), float(tau), ptr(ws), ws.numel() * 4, ptr(rgb), ptr(depth),
         ptr(weights), ptr(acc), stream_of(r)), "acn_render_stratified_fwd")
+    if hook is not None:
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        hook.append((e0, e1))
     return rgb, depth, weights, acc
 
 
@@ -230,3 +274,84 @@ def get_rays_image(H: int, W: int, fx: float, fy: float, cx: float, cy: float, c
                                   c_arr, a_arr, float(near or 0.0), float(far or 0.0), hn, nv, hf, fv,
                                   int(apply_clamp), ptr(rays), ptr(valid), stream_of(rays)), "acn_get_rays")
     return rays, valid.bool()
+
+
+def _host_f32(t, n):
+    v = t.detach().float().cpu().contiguous().view(-1)
+    if v.numel() != n:
+        raise AcnError(f"expected {n} values, got {v.numel()}")
+    return (C.c_float * n)(*v.tolist())
+
+
+def ray_directions(H: int, W: int, fx: float, fy: float, cx: float, cy: float, center_pixels: bool, device):
+    dirs = torch.empty(H, W, 3, device=device, dtype=torch.float32)
+    check(_lib.lib().acn_ray_directions(int(H), int(W), float(fx), float(fy), float(cx), float(cy),
+                                        int(center_pixels), ptr(dirs), stream_of(dirs)), "acn_ray_directions")
+    return dirs
+
+
+def rays_from_dirs(dirs: torch.Tensor, c2w: torch.Tensor, aabb: Optional[torch.Tensor], near_c: float = 0.0,
+                   far_c: float = 0.0, eps: float = 1e-8, max_bound: float = 1e10, invalid_value: float = 1e10):
+    require_hip(dirs, "get_rays")
+    d = _f32(dirs).view(-1, 3)
+    rays = torch.empty(d.shape[0], 8, device=d.device, dtype=torch.float32)
+    c = _host_f32(c2w[:3, :4], 12)
+    a = None if aabb is None else _host_f32(aabb, 6)
+    check(_lib.lib().acn_rays_from_dirs(ptr(d), d.shape[0], c, a, float(near_c), float(far_c), float(eps),
+                                        float(max_bound), float(invalid_value), ptr(rays), stream_of(d)),
+          "acn_rays_from_dirs")
+    return rays
+
+
+def ray_aabb(origins: torch.Tensor, dirs: torch.Tensor, aabb: torch.Tensor, eps: float, max_bound: float,
+             invalid_value: float):
+    require_hip(origins, "SceneBox.ray_aabb_intersect")
+    o = _f32(origins).view(-1, 3)
+    d = _f32(dirs.to(o.device)).view(-1, 3)
+    tmin = torch.empty(o.shape[0], device=o.device, dtype=torch.float32)
+    tmax = torch.empty_like(tmin)
+    check(_lib.lib().acn_ray_aabb(ptr(o), ptr(d), o.shape[0], _host_f32(aabb, 6), float(eps), float(max_bound),
+                                  float(invalid_value), ptr(tmin), ptr(tmax), stream_of(o)), "acn_ray_aabb")
+    return tmin, tmax
+
+
+def clamp_rays(rays: torch.Tensor, near_far_override, eps: float = 1e-6, invalid_value: float = float("inf")):
+    """Returns (rays', valid).  rays' is a new tensor unless override is None (then rays itself)."""
+    require_hip(rays, "clamp_rays_near_far")
+    apply = near_far_override is not None
+    r = _f32(rays).clone() if apply else _f32(rays)
+    hn = hf = 0
+    nv = fv = 0.0
+    if apply:
+        if near_far_override[0] is not None:
+            hn, nv = 1, float(near_far_override[0])
+        if near_far_override[1] is not None:
+            hf, fv = 1, float(near_far_override[1])
+    valid = torch.empty(r.shape[0], device=r.device, dtype=torch.uint8)
+    check(_lib.lib().acn_clamp_rays(ptr(r), r.shape[0], int(apply), hn, nv, hf, fv, float(eps), float(invalid_value),
+                                    ptr(valid), stream_of(r)), "acn_clamp_rays")
+    return (r if apply else rays), valid.bool()
+
+
+def routing_fwd(pts: torch.Tensor, routing: acn_routing):
+    require_hip(pts, "MetaContainer._routing")
+    p = _f32(pts)
+    M = p.shape[0]
+    if routing.boundary_margin > 1.0:
+        W = torch.empty(M, routing.K, device=p.device, dtype=torch.float32)
+        check(_lib.lib().acn_routing_fwd(ptr(p), M, p.shape[1], C.byref(routing), ptr(W), None, stream_of(p)),
+              "acn_routing_fwd")
+        return W, None
+    hard = torch.empty(M, device=p.device, dtype=torch.int32)
+    check(_lib.lib().acn_routing_fwd(ptr(p), M, p.shape[1], C.byref(routing), None, ptr(hard), stream_of(p)),
+          "acn_routing_fwd")
+    return None, hard.long()
+
+
+def background_fwd(dirs: torch.Tensor, background) -> torch.Tensor:
+    require_hip(dirs, "MetaContainer.background_color")
+    d = _f32(dirs).view(-1, 3)
+    out = torch.empty(d.shape[0], 3, device=d.device, dtype=torch.float32)
+    check(_lib.lib().acn_background_fwd(ptr(d), d.shape[0], C.byref(background), ptr(out), stream_of(d)),
+          "acn_background_fwd")
+    return out

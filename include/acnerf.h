@@ -102,9 +102,17 @@ int acn_sh_fwd(const float* d, int64_t M, int levels, float* out, void* stream);
 /* Bytes of device workspace the fused field / render entry points need for K experts. */
 size_t acn_workspace_bytes(int K);
 
+/* Pack the MLP weights of the experts the next field/render call evaluates (all K, or only
+ * experts[active_module] when active_module >= 0) into the workspace, in the MFMA operand order
+ * the fused kernels stage into LDS.  Must be re-run whenever any of those weights change (the
+ * Python layer re-packs when a tensor's version counter moves or fast weights are passed).    */
+int acn_pack_experts(const acn_expert* experts, const acn_routing* routing, int active_module,
+                     void* workspace, size_t workspace_bytes, void* stream);
+
 /* MetaContainer.forward / MetaNGP.forward (meta_container.py:275-343, meta_ngp.py:226-241):
  * x (M, ld>=6) rows [xyz, dir, ...] -> out (M, 4) = [rgb, sigma].  active_module >= 0 runs only
- * that expert (no routing), as the reference's `active_module` argument does.                */
+ * that expert (no routing), as the reference's `active_module` argument does.  `experts` holds
+ * routing->K entries; `workspace` must hold acn_pack_experts() output for the same arguments. */
 int acn_field_fwd(const float* x, int64_t M, int64_t ld, const acn_expert* experts,
                   const acn_routing* routing, int active_module, void* workspace,
                   size_t workspace_bytes, float* out, void* stream);
@@ -119,7 +127,8 @@ int acn_volume_render_fwd(const float* rgb_sigma, const float* t_vals, const flo
  * _get_bg_rgb :23-45 + volume_render :114-165) with the field of every expert evaluated in the
  * same kernel.  rays (N,8) [o, d, near, far]; jitter (N,S) uniforms of the training-mode draw
  * (:286) or NULL for eval; tau: early-ray-termination threshold on transmittance (0 = off; the
- * reference has none, the composite error is bounded by 2*tau).  Outputs as volume_render.     */
+ * reference has none, the composite error is bounded by 2*tau).  Outputs as volume_render.
+ * `workspace` must hold acn_pack_experts() output for the same experts / routing / module.    */
 int acn_render_stratified_fwd(const float* rays, int64_t N, int S, const float* jitter,
                               const acn_expert* experts, const acn_routing* routing,
                               int active_module, const acn_background* bg, float sigma_scale,
