@@ -82,6 +82,184 @@ __device__ __forceinline__ void sh_encode(float dx, float dy, float dz, float* c
     sh_components<DEGREE>(dx / n, dy / n, dz / n, c);
 }
 
+// One level of HashGridEncoder._torch_forward split in two halves so that callers can keep the
+// gathers of several levels in flight: hash_issue computes the 8 corner rows and issues their
+// loads, hash_finish interpolates once they have landed.  Same arithmetic as hash_level_f2.
+// 8-byte table-row load with a cache policy: 0 plain, 1 non-temporal (nt), 2 L1-bypassing
+// (relaxed agent-scope atomic load -> global_load_dwordx2 sc1, served by the L2)
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+template <int POL>
+__device__ __forceinline__ float2 ld_row(const float2* p) {
+    if (POL == 1) {
+        const f32x2_t v = __builtin_nontemporal_load(reinterpret_cast<const f32x2_t*>(p));
+        return make_float2(v[0], v[1]);
+    }
+    if (POL == 2) {
+        const uint64_t u = __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        return make_float2(__uint_as_float((uint32_t)u), __uint_as_float((uint32_t)(u >> 32)));
+    }
+    return *p;
+}
+
+struct HashPending {
+    float2 f[8];
+    float wx, wy, wz;
+};
+
+template <int INTERP, int POL = 0>
+__device__ __forceinline__ void hash_issue(const float2* __restrict__ tl, float sx, float sy, float sz,
+                                           uint32_t mask, HashPending& p) {
+    if (INTERP == 0) {
+        const uint32_t ix = (uint32_t)(int)rintf(sx), iy = (uint32_t)(int)rintf(sy), iz = (uint32_t)(int)rintf(sz);
+        p.f[0] = ld_row<POL>(tl + ((ix ^ (iy * kP1) ^ (iz * kP2)) & mask));
+        return;
+    }
+    const float fx = floorf(sx), fy = floorf(sy), fz = floorf(sz);
+    float wx = sx - fx, wy = sy - fy, wz = sz - fz;
+    const uint32_t x0 = (uint32_t)(int)fx;
+    const uint32_t y0 = (uint32_t)(int)fy * kP1, y1 = y0 + kP1;
+    const uint32_t z0 = (uint32_t)(int)fz * kP2, z1 = z0 + kP2;
+    const uint32_t x1 = x0 + 1u;
+    if (INTERP == 2) {
+        wx = (wx * wx) * (3.0f - 2.0f * wx);
+        wy = (wy * wy) * (3.0f - 2.0f * wy);
+        wz = (wz * wz) * (3.0f - 2.0f * wz);
+    }
+    const uint32_t a00 = y0 ^ z0, a01 = y0 ^ z1, a10 = y1 ^ z0, a11 = y1 ^ z1;
+#if ACN_XPAIR
+    // The x-neighbours of a (y, z) corner pair hash to rows i0 = x0^a and i1 = x1^a.  For even x0,
+    // i1 = i0 ^ 1: both rows sit in ONE 16-byte block, fetched by a single dwordx4 gather; only
+    // lanes with odd x0 issue a second (dwordx2) gather for i1.
+    const bool xodd = (x0 & 1u) != 0u;
+    const uint32_t aa[4] = {a00, a01, a10, a11};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const uint32_t i0 = (x0 ^ aa[c]) & mask;
+        const float4 q = *reinterpret_cast<const float4*>(tl + (i0 & ~1u));
+        const bool hi = (i0 & 1u) != 0u;
+        p.f[2 * c] = hi ? make_float2(q.z, q.w) : make_float2(q.x, q.y);
+        p.f[2 * c + 1] = hi ? make_float2(q.x, q.y) : make_float2(q.z, q.w);
+    }
+    if (xodd) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) p.f[2 * c + 1] = tl[(x1 ^ aa[c]) & mask];
+    }
+#else
+    p.f[0] = ld_row<POL>(tl + ((x0 ^ a00) & mask));
+    p.f[1] = ld_row<POL>(tl + ((x1 ^ a00) & mask));
+    p.f[2] = ld_row<POL>(tl + ((x0 ^ a01) & mask));
+    p.f[3] = ld_row<POL>(tl + ((x1 ^ a01) & mask));
+    p.f[4] = ld_row<POL>(tl + ((x0 ^ a10) & mask));
+    p.f[5] = ld_row<POL>(tl + ((x1 ^ a10) & mask));
+    p.f[6] = ld_row<POL>(tl + ((x0 ^ a11) & mask));
+    p.f[7] = ld_row<POL>(tl + ((x1 ^ a11) & mask));
+#endif
+    p.wx = wx;
+    p.wy = wy;
+    p.wz = wz;
+}
+
+template <int INTERP>
+__device__ __forceinline__ void hash_finish(const HashPending& p, float& o0, float& o1) {
+    if (INTERP == 0) {
+        o0 = p.f[0].x;
+        o1 = p.f[0].y;
+        return;
+    }
+    const float wx = p.wx, wy = p.wy, wz = p.wz;
+    const float ax = 1.0f - wx, ay = 1.0f - wy, az = 1.0f - wz;
+    // f index: bit0 = x1, bit1 = z1, bit2 = y1 (issue order above)
+    {
+        const float c00 = p.f[0].x * ax + p.f[1].x * wx;
+        const float c01 = p.f[2].x * ax + p.f[3].x * wx;
+        const float c10 = p.f[4].x * ax + p.f[5].x * wx;
+        const float c11 = p.f[6].x * ax + p.f[7].x * wx;
+        const float c0 = c00 * ay + c10 * wy;
+        const float c1 = c01 * ay + c11 * wy;
+        o0 = c0 * az + c1 * wz;
+    }
+    {
+        const float c00 = p.f[0].y * ax + p.f[1].y * wx;
+        const float c01 = p.f[2].y * ax + p.f[3].y * wx;
+        const float c10 = p.f[4].y * ax + p.f[5].y * wx;
+        const float c11 = p.f[6].y * ax + p.f[7].y * wx;
+        const float c0 = c00 * ay + c10 * wy;
+        const float c1 = c01 * ay + c11 * wy;
+        o1 = c0 * az + c1 * wz;
+    }
+}
+
+// Buffer-resource form of hash_issue/hash_finish (Linear/Smoothstep).  The x-neighbours of a
+// (y, z) corner pair hash to rows i0 = x0^a and i1 = x1^a; for even x0, i1 = i0 ^ 1, so ONE
+// 16-byte gather of the aligned block holding i0 returns both.  The second gather (8 bytes, row
+// i1) is only needed by lanes with odd x0: the other lanes pass an out-of-range offset, which the
+// buffer's range check turns into a no-op (no cache access).
+#ifndef ACN_XPAIR_NOSKIP
+#define ACN_XPAIR_NOSKIP 0
+#endif
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+struct HashPendingX {
+    u32x4_t q[4];
+    u32x2_t r[4];
+    float wx, wy, wz;
+    uint32_t sel;  // bit c: row i0 of corner pair c is the odd row of its block; bit 4: x0 odd
+};
+
+template <int INTERP>
+__device__ __forceinline__ void hash_issue_x(__amdgpu_buffer_rsrc_t rs, uint32_t lvbase, float sx, float sy, float sz,
+                                             uint32_t mask, HashPendingX& p) {
+    const float fx = floorf(sx), fy = floorf(sy), fz = floorf(sz);
+    float wx = sx - fx, wy = sy - fy, wz = sz - fz;
+    const uint32_t x0 = (uint32_t)(int)fx;
+    const uint32_t y0 = (uint32_t)(int)fy * kP1, y1 = y0 + kP1;
+    const uint32_t z0 = (uint32_t)(int)fz * kP2, z1 = z0 + kP2;
+    const uint32_t x1 = x0 + 1u;
+    if (INTERP == 2) {
+        wx = (wx * wx) * (3.0f - 2.0f * wx);
+        wy = (wy * wy) * (3.0f - 2.0f * wy);
+        wz = (wz * wz) * (3.0f - 2.0f * wz);
+    }
+    const uint32_t aa[4] = {y0 ^ z0, y0 ^ z1, y1 ^ z0, y1 ^ z1};
+    const bool xodd = (x0 & 1u) != 0u;
+    uint32_t sel = xodd ? 16u : 0u;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const uint32_t i0 = (x0 ^ aa[c]) & mask;
+        sel |= (i0 & 1u) << c;
+        p.q[c] = __builtin_amdgcn_raw_buffer_load_b128(rs, lvbase + ((i0 & ~1u) << 3), 0, 0);
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const uint32_t i1 = (x1 ^ aa[c]) & mask;
+        p.r[c] = __builtin_amdgcn_raw_buffer_load_b64(rs, (xodd || ACN_XPAIR_NOSKIP) ? lvbase + (i1 << 3) : 0xFFFFFFF0u, 0, 0);
+    }
+    p.wx = wx;
+    p.wy = wy;
+    p.wz = wz;
+    p.sel = sel;
+}
+
+template <int INTERP>
+__device__ __forceinline__ void hash_finish_x(const HashPendingX& p, float& o0, float& o1) {
+    HashPending h;
+    const bool xodd = (p.sel & 16u) != 0u;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const bool hi = ((p.sel >> c) & 1u) != 0u;
+        const u32x4_t q = p.q[c];
+        const uint32_t l0 = hi ? q[2] : q[0], l1 = hi ? q[3] : q[1];
+        const uint32_t e0 = hi ? q[0] : q[2], e1 = hi ? q[1] : q[3];
+        h.f[2 * c] = make_float2(__uint_as_float(l0), __uint_as_float(l1));
+        h.f[2 * c + 1] = make_float2(__uint_as_float(xodd ? p.r[c][0] : e0), __uint_as_float(xodd ? p.r[c][1] : e1));
+    }
+    h.wx = p.wx;
+    h.wy = p.wy;
+    h.wz = p.wz;
+    hash_finish<INTERP>(h, o0, o1);
+}
+
 // One level of HashGridEncoder._torch_forward (encodings.py:331-381) for one point.
 // tl: this level's table base (row = F floats).  INTERP: 0 nearest, 1 linear, 2 smoothstep.
 // Linear/Smoothstep lerp order x -> y -> z exactly as encodings.py:373-379.

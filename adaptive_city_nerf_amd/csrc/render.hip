@@ -21,6 +21,17 @@
 
 using namespace acn;
 
+#ifndef ACN_LEVEL_PARITY
+#define ACN_LEVEL_PARITY 0  // 1: half h encodes levels 2i+h (instruction i = two adjacent levels)
+#endif
+#ifndef ACN_FINE_POL
+#define ACN_FINE_POL 0      // load policy (ld_row) of the gathers of the finest levels
+#endif
+#ifndef ACN_FINE_FROM
+#define ACN_FINE_FROM 8     // first gather step i (0..7) that uses ACN_FINE_POL
+#endif
+
+
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -68,7 +79,8 @@ __device__ float pack_value(const PackSrc& p, int idx) {
     int t, s, i, h;
     if (idx < PK_W2) {  // sigma_trunk.0 (64, 32): k = 16h + s
         decode_a(idx - PK_W1, 16, t, s, i, h);
-        return p.sig_w0[(i + 32 * t) * 32 + 16 * h + s];
+        const int col = ACN_LEVEL_PARITY ? 4 * (s >> 1) + 2 * h + (s & 1) : 16 * h + s;
+        return p.sig_w0[(i + 32 * t) * 32 + col];
     }
     if (idx < PK_WH) {  // sigma_trunk.1 (64, 64): k = rho(r, h) + 32 Tin, s = 16 Tin + r
         decode_a(idx - PK_W2, 32, t, s, i, h);
@@ -133,6 +145,50 @@ __device__ __forceinline__ f32x16 bias_frag(const float* W, int tile, int h) {
     return v;
 }
 
+// a [tile][h][16] fragment image (per-ray folded colour bias)
+__device__ __forceinline__ f32x16 bias_frag_at(const float* cb, int tile, int h) {
+    const float* b = cb + (tile * 2 + h) * 16;
+    const f32x4 a = ld4(b), c = ld4(b + 4), d = ld4(b + 8), e = ld4(b + 12);
+    f32x16 v;
+    v[0] = a[0]; v[1] = a[1]; v[2] = a[2]; v[3] = a[3];
+    v[4] = c[0]; v[5] = c[1]; v[6] = c[2]; v[7] = c[3];
+    v[8] = d[0]; v[9] = d[1]; v[10] = d[2]; v[11] = d[3];
+    v[12] = e[0]; v[13] = e[1]; v[14] = e[2]; v[15] = e[3];
+    return v;
+}
+
+// Per-ray fold of colour layer 0's SH columns (meta_ngp.py:171-190: the direction, hence its SH
+// encoding, is constant along a ray): cb[tile][h][r] = b_c0[row] + sum_m W_c0[row][15+m] sh[m]
+// for row = rho(r, h) + 32 tile, computed once per ray with the 8 SH k-steps of the packed
+// colour-layer-0 image (B = this half's SH rows, identical in every column).  Lanes j == 0 of
+// each half store the fragment; the wave reads it back per tile instead of the plain bias.
+__device__ __forceinline__ void fold_sh_bias(const float* W, const float (&shv)[8], int lane, float* cb) {
+    const int h = lane >> 5;
+    f32x16 q0 = bias_frag(W, BT_C1, h), q1 = bias_frag(W, BT_C1 + 1, h);
+#pragma unroll
+    for (int g = 2; g < 4; ++g) {
+        const f32x4 w0 = ld4(W + PK_WC1 + ((0 * 4 + g) * 64 + lane) * 4);
+        const f32x4 w1 = ld4(W + PK_WC1 + ((1 * 4 + g) * 64 + lane) * 4);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            q0 = mfma32(w0[q], shv[4 * (g - 2) + q], q0);
+            q1 = mfma32(w1[q], shv[4 * (g - 2) + q], q1);
+        }
+    }
+    if ((lane & 31) == 0) {
+        f32x4* d0 = reinterpret_cast<f32x4*>(cb + (0 * 2 + h) * 16);
+        f32x4* d1 = reinterpret_cast<f32x4*>(cb + (1 * 2 + h) * 16);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            f32x4 a, b;
+            a[0] = q0[4 * i]; a[1] = q0[4 * i + 1]; a[2] = q0[4 * i + 2]; a[3] = q0[4 * i + 3];
+            b[0] = q1[4 * i]; b[1] = q1[4 * i + 1]; b[2] = q1[4 * i + 2]; b[3] = q1[4 * i + 3];
+            d0[i] = a;
+            d1[i] = b;
+        }
+    }
+}
+
 __device__ __forceinline__ void relu16(f32x16& v) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) v[i] = v[i] < 0.0f ? 0.0f : v[i];  // NaN propagates like torch.relu
@@ -165,12 +221,77 @@ __device__ __forceinline__ void layer64x64(const float* W, int seg, int btile, i
     }
 }
 
+#ifndef ACN_HASH_DEPTH
+#define ACN_HASH_DEPTH 2  // levels whose gathers are in flight together (1 = issue + wait per level)
+#endif
+
+#if ACN_DIAG_PHASE  // diagnostic build only: per-wave timestamp taken right after the hash phase
+__shared__ uint64_t g_diag_stamp[16];
+#endif
+
+// level encoded by half h at gather step i (its features sit at feat[2i], feat[2i+1])
+__device__ __forceinline__ int level_of(int i, int h) { return ACN_LEVEL_PARITY ? 2 * i + h : i + 8 * h; }
+
+// Hash-encode this half's 8 levels (encodings.py:331-381) with the gathers of ACN_HASH_DEPTH
+// levels in flight: level step i+D-1 is issued before step i is interpolated.
+template <int INTERP>
+__device__ __forceinline__ void hash_levels8(const ExpertMeta& em, int log2T, int h, float x0, float x1, float x2,
+                                             float (&feat)[16]) {
+    constexpr int D = ACN_HASH_DEPTH;
+    const uint32_t mask = (uint32_t)((1ull << log2T) - 1ull);
+#if ACN_XPAIR == 2
+    if (INTERP != 0) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)em.table, (short)0, (int)(uint32_t)((16ull << log2T) * 8ull), 0x00020000);
+        HashPendingX px[D];
+        auto issue_x = [&](int i, HashPendingX& pp) {
+            const int lv = level_of(i, h);
+            const float res = (float)(ACN_LEVEL_PARITY ? (h ? em.res[2 * i + 1] : em.res[2 * i])
+                                                       : (h ? em.res[8 + i] : em.res[i]));
+            hash_issue_x<INTERP>(rs, (uint32_t)lv << (log2T + 3), x0 * res, x1 * res, x2 * res, mask, pp);
+        };
+#pragma unroll
+        for (int l = 0; l < D - 1; ++l) issue_x(l, px[l]);
+#pragma unroll
+        for (int l = 0; l < 8; ++l) {
+            if (l + D - 1 < 8) issue_x(l + D - 1, px[(l + D - 1) % D]);
+            __builtin_amdgcn_sched_barrier(0);
+            hash_finish_x<INTERP>(px[l % D], feat[2 * l], feat[2 * l + 1]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        return;
+    }
+#endif
+    HashPending pend[D];
+    auto issue = [&](int i, HashPending& pp) {
+        const int lv = level_of(i, h);
+        const float res = (float)(ACN_LEVEL_PARITY ? (h ? em.res[2 * i + 1] : em.res[2 * i])
+                                                   : (h ? em.res[8 + i] : em.res[i]));
+        const float2* tl = reinterpret_cast<const float2*>(em.table) + ((size_t)lv << log2T);
+        if (i >= ACN_FINE_FROM)
+            hash_issue<INTERP, ACN_FINE_POL>(tl, x0 * res, x1 * res, x2 * res, mask, pp);
+        else
+            hash_issue<INTERP, 0>(tl, x0 * res, x1 * res, x2 * res, mask, pp);
+    };
+#pragma unroll
+    for (int l = 0; l < D - 1; ++l) issue(l, pend[l]);
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+        if (l + D - 1 < 8) issue(l + D - 1, pend[(l + D - 1) % D]);
+        __builtin_amdgcn_sched_barrier(0);
+        hash_finish<INTERP>(pend[l % D], feat[2 * l], feat[2 * l + 1]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 // Field of one expert on this lane's sample (x world point, shv = this half's SH rows).
 // Returns rgb (after sigmoid) on every lane and sigma_raw on every lane.
-template <int INTERP>
+// FOLD: the colour MLP's SH columns + bias were folded per ray into cb (LDS, [tile][h][16],
+// see fold_sh_bias): colour layer 0 then only runs the 8 k-steps of the [sigma_raw, geo] rows.
+template <int INTERP, bool FOLD>
 __device__ __forceinline__ void field_tile(const float* W, const ExpertMeta& em, int log2T, float px, float py,
-                                           float pz, const float (&shv)[8], int lane, float& rr, float& rg, float& rb,
-                                           float& sraw) {
+                                           float pz, const float (&shv)[8], const float* cb, int lane, float& rr,
+                                           float& rg, float& rb, float& sraw) {
     W = W + opaque_s(0);
     const int h = opaque_v(lane >> 5);
     // _world_to_unit (meta_ngp.py:155-158)
@@ -178,16 +299,28 @@ __device__ __forceinline__ void field_tile(const float* W, const ExpertMeta& em,
     const float x0 = clamp_nan((px - em.amin[0]) / em.ext[0], eps, hi);
     const float x1 = clamp_nan((py - em.amin[1]) / em.ext[1], eps, hi);
     const float x2 = clamp_nan((pz - em.amin[2]) / em.ext[2], eps, hi);
-    // hash grid: this half encodes levels 8h .. 8h+7 (encodings.py:331-381)
-    const uint32_t mask = (uint32_t)((1ull << log2T) - 1ull);
     float feat[16];
+#if ACN_DIAG_NOHASH  // diagnostic build only: no gathers
 #pragma unroll
-    for (int l = 0; l < 8; ++l) {
-        const float res = (float)(h ? em.res[8 + l] : em.res[l]);
-        const float2* tl = reinterpret_cast<const float2*>(em.table) + ((size_t)(l + 8 * h) << log2T);
-        hash_level_f2<INTERP>(tl, x0 * res, x1 * res, x2 * res, mask, feat[2 * l], feat[2 * l + 1]);
-        if (l & 1) __builtin_amdgcn_sched_barrier(0);  // <= 16 gathers in flight per lane (VGPR budget)
+    for (int i = 0; i < 16; ++i) feat[i] = x0 * (float)(i + 1) - x1 + x2 * (float)i;
+#else
+    hash_levels8<INTERP>(em, log2T, h, x0, x1, x2, feat);
+#endif
+#if ACN_DIAG_PHASE
+    {
+        const uint64_t tnow = __builtin_amdgcn_s_memtime();
+        if (lane == 0) g_diag_stamp[threadIdx.x >> 6] = tnow;
     }
+#endif
+#if ACN_DIAG_NOMLP  // diagnostic build only: no MLP
+    {
+        float a = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) a += feat[i];
+        rr = a; rg = feat[1]; rb = feat[2]; sraw = __shfl(feat[3], lane & 31);
+        return;
+    }
+#endif
     // sigma_trunk.0: 32 -> 64 (ReLU)
     f32x16 a0 = bias_frag(W, BT_L1, h), a1 = bias_frag(W, BT_L1 + 1, h);
     {
@@ -218,8 +351,10 @@ __device__ __forceinline__ void field_tile(const float* W, const ExpertMeta& em,
     // heads: rows 0 sigma_head, 1..15 geo_head; rows 16..31 carry the SH features through
     // (zero weights, accumulator initialised with SH): the colour MLP input [geo, sh].
     f32x16 hd = bias_frag(W, BT_H, h);
+    if (!FOLD) {
 #pragma unroll
-    for (int r = 8; r < 16; ++r) hd[r] = shv[r - 8];
+        for (int r = 8; r < 16; ++r) hd[r] = shv[r - 8];
+    }
     {
         f32x4 n = ld4(W + PK_WH + (0 * 64 + lane) * 4);
 #pragma unroll
@@ -234,15 +369,23 @@ __device__ __forceinline__ void field_tile(const float* W, const ExpertMeta& em,
     }
     // sigma_raw = row 0, held by lane j of half 0
     sraw = __shfl(hd[0], lane & 31);
-    // color_mlp.0: [geo(15), sh(16)] -> 64 (ReLU)
-    f32x16 c0 = bias_frag(W, BT_C1, h), c1 = bias_frag(W, BT_C1 + 1, h);
+    // color_mlp.0: [geo(15), sh(16)] -> 64 (ReLU); with FOLD only the 8 k-steps of rows 0..15
+    f32x16 c0, c1;
+    if (FOLD) {
+        c0 = bias_frag_at(cb, 0, h);
+        c1 = bias_frag_at(cb, 1, h);
+    } else {
+        c0 = bias_frag(W, BT_C1, h);
+        c1 = bias_frag(W, BT_C1 + 1, h);
+    }
     {
+        constexpr int NG = FOLD ? 2 : 4;
         f32x4 n0 = ld4(W + PK_WC1 + ((0 * 4 + 0) * 64 + lane) * 4);
         f32x4 n1 = ld4(W + PK_WC1 + ((1 * 4 + 0) * 64 + lane) * 4);
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
+        for (int g = 0; g < NG; ++g) {
             const f32x4 w0 = n0, w1 = n1;
-            if (g < 3) {
+            if (g < NG - 1) {
                 n0 = ld4(W + PK_WC1 + ((0 * 4 + g + 1) * 64 + lane) * 4);
                 n1 = ld4(W + PK_WC1 + ((1 * 4 + g + 1) * 64 + lane) * 4);
             }
@@ -354,12 +497,18 @@ __device__ __forceinline__ float route_weight(const FieldCfg& cfg, const RouteSt
 
 // Container forward of this lane's sample over all experts (meta_container.py:300-343):
 // soft: y = sum_k (y_k * w_k) accumulated in expert order from zero (index_add_); hard: copy.
-template <int INTERP, int ROUTE>
+// FOLD: cb points at this wave's per-expert folded colour biases ([k][64] floats in LDS) and
+// *folded is the wave-uniform mask of experts already folded for the current ray.
+template <int INTERP, int ROUTE, bool FOLD>
 __device__ __forceinline__ void container_tile(const FieldCfg& cfg, const float* Wbase, float px, float py, float pz,
-                                               const float (&shv)[8], int lane, float& yr, float& yg, float& yb,
-                                               float& ys) {
+                                               const float (&shv)[8], float* cb, uint32_t* folded, int lane,
+                                               float& yr, float& yg, float& yb, float& ys) {
     if (ROUTE == 0) {
-        field_tile<INTERP>(Wbase, cfg.ex[0], cfg.log2T, px, py, pz, shv, lane, yr, yg, yb, ys);
+        if (FOLD && !(*folded & 1u)) {
+            fold_sh_bias(Wbase, shv, lane, cb);
+            *folded |= 1u;
+        }
+        field_tile<INTERP, FOLD>(Wbase, cfg.ex[0], cfg.log2T, px, py, pz, shv, cb, lane, yr, yg, yb, ys);
         ys = trunc_exp(ys);
         return;
     }
@@ -369,8 +518,14 @@ __device__ __forceinline__ void container_tile(const FieldCfg& cfg, const float*
         const float wk = (ROUTE == 1) ? route_weight(cfg, st, k, px, py, pz) : 0.0f;
         const bool need = (ROUTE == 1) ? (wk > 0.0f) : (st.hard == k);
         if (__ballot(need) == 0ull) continue;  // wave-uniform skip of experts no sample needs
+        const float* Wk = Wbase + (size_t)k * PK_FLOATS;
+        float* cbk = FOLD ? cb + k * 64 : nullptr;
+        if (FOLD && !((*folded >> k) & 1u)) {
+            fold_sh_bias(Wk, shv, lane, cbk);
+            *folded |= 1u << k;
+        }
         float r, g, b, s;
-        field_tile<INTERP>(Wbase + (size_t)k * PK_FLOATS, cfg.ex[k], cfg.log2T, px, py, pz, shv, lane, r, g, b, s);
+        field_tile<INTERP, FOLD>(Wk, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbk, lane, r, g, b, s);
         s = trunc_exp(s);
         if (need) {
             if (ROUTE == 1) {
@@ -438,7 +593,7 @@ __global__ void __launch_bounds__(1024, 4) field_kernel(FieldCfg cfg, FieldParam
         dir_sh(xr[3], xr[4], xr[5], sh);
         sh_rows_for_half(sh, h, shv);
         float yr, yg, yb, ys;
-        container_tile<INTERP, ROUTE>(cfg, W, px, py, pz, shv, lane, yr, yg, yb, ys);
+        container_tile<INTERP, ROUTE, false>(cfg, W, px, py, pz, shv, nullptr, nullptr, lane, yr, yg, yb, ys);
         if (h == 0 && m < p.M) {
             f32x4 v;
             v[0] = yr; v[1] = yg; v[2] = yb; v[3] = ys;
@@ -556,9 +711,24 @@ struct RenderParams {
     float *rgb, *depth, *weights, *acc;
 };
 
+#ifndef ACN_SHFOLD
+#define ACN_SHFOLD 1
+#endif
+
+// t of sample i without jitter, branch-free (same roundings as lin01/tlin)
+__device__ __forceinline__ float tlin_sel(float near, float far, int i, int S, float step) {
+    const float a = fmaf(step, (float)i, 0.0f);
+    const float b = fmaf(-step, (float)(S - 1 - i), 1.0f);
+    const float u = i < S / 2 ? a : b;
+    return near * (1.0f - u) + far * u;
+}
+
 template <int INTERP, int KL, int ROUTE>
 __global__ void __launch_bounds__(1024, 4) render_kernel(FieldCfg cfg, BgArgs bg, RenderParams p) {
+    constexpr bool FOLD = ACN_SHFOLD != 0;
+    constexpr int KF = ROUTE == 0 ? 1 : (KL == 2 ? 2 : kMaxK);  // experts a ray may fold
     __shared__ __attribute__((aligned(16))) float smem[(KL > 0 ? KL : 1) * PK_FLOATS];
+    __shared__ __attribute__((aligned(16))) float cbuf[FOLD ? 16 * KF * 64 : 4];
     const float* W = p.packed;
     if (KL > 0) {
         stage_weights<KL>(smem, p.packed);
@@ -566,8 +736,13 @@ __global__ void __launch_bounds__(1024, 4) render_kernel(FieldCfg cfg, BgArgs bg
     }
     const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // provably uniform: ray data in SGPRs
+    float* cb = FOLD ? cbuf + wave * KF * 64 : nullptr;
     const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
     const int S = p.S;
+    const float step = 1.0f / (float)(S - 1);
+#if ACN_DIAG_CLOCK  // diagnostic build only: depth[ray] <- in-kernel shader clock (MHz) over the ray
+    const uint64_t diag_t0 = __builtin_amdgcn_s_memtime(), diag_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
     for (int64_t ray = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave; ray < p.N; ray += nw) {
         const float* rp = p.rays + ray * 8;
         const float ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
@@ -576,19 +751,41 @@ __global__ void __launch_bounds__(1024, 4) render_kernel(FieldCfg cfg, BgArgs bg
         float sh[16], shv[8];
         dir_sh(dx, dy, dz, sh);
         sh_rows_for_half(sh, h, shv);
+        uint32_t folded = 0u;
+#if ACN_DIAG_PHASE
+        uint32_t dg_hash = 0u, dg_mlp = 0u, dg_comp = 0u, dg_n = 0u;
+#endif
         RayAcc acc{1.0, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
         int s0 = 0;
         for (; s0 < S; s0 += 32) {
             const int s = s0 + j;
             const bool valid = s < S;
             const int sc = valid ? s : S - 1;
-            const float t = tval(near, far, sc, S, jit);
-            const float tn = (sc < S - 1) ? tval(near, far, sc + 1, S, jit) : t;
-            const float tp = (sc == S - 1 && S > 1) ? tval(near, far, sc - 1, S, jit) : t;
-            const float dist = (sc < S - 1) ? (tn - t) : (t - tp);
+            float t, dist;
+            if (!jit) {  // eval: dist = t[i+1] - t[i], the last one repeated (ray_rendering.py:144-145)
+                const int i0 = sc < S - 1 ? sc : S - 2;
+                const float ta = tlin_sel(near, far, i0, S, step), tb = tlin_sel(near, far, i0 + 1, S, step);
+                t = sc < S - 1 ? ta : tb;
+                dist = tb - ta;
+            } else {
+                t = tval(near, far, sc, S, jit);
+                const float tn = (sc < S - 1) ? tval(near, far, sc + 1, S, jit) : t;
+                const float tp = (sc == S - 1 && S > 1) ? tval(near, far, sc - 1, S, jit) : t;
+                dist = (sc < S - 1) ? (tn - t) : (t - tp);
+            }
             const float px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;
             float yr, yg, yb, ys;
-            container_tile<INTERP, ROUTE>(cfg, W, px, py, pz, shv, lane, yr, yg, yb, ys);
+#if ACN_DIAG_PHASE
+            const uint64_t dA = __builtin_amdgcn_s_memtime();
+#endif
+            container_tile<INTERP, ROUTE, FOLD>(cfg, W, px, py, pz, shv, cb, &folded, lane, yr, yg, yb, ys);
+#if ACN_DIAG_PHASE
+            const uint64_t dB = __builtin_amdgcn_s_memtime();
+            const uint32_t dS = __builtin_amdgcn_readfirstlane((uint32_t)g_diag_stamp[wave]);
+            dg_hash += dS - (uint32_t)dA;
+            dg_mlp += (uint32_t)dB - dS;
+            dg_n += 1u;
+#endif
             // volume_render input conditioning (:140-143)
             yr = clamp_nan(yr, 0.0f, 1.0f);
             yg = clamp_nan(yg, 0.0f, 1.0f);
@@ -598,6 +795,9 @@ __global__ void __launch_bounds__(1024, 4) render_kernel(FieldCfg cfg, BgArgs bg
             float wv;
             composite_tile(acc, valid, yr, yg, yb, sig, t, dist, j, &wv);
             if (p.weights && valid && h == 0) p.weights[ray * S + s] = wv;
+#if ACN_DIAG_PHASE
+            dg_comp += (uint32_t)__builtin_amdgcn_s_memtime() - (uint32_t)dB;
+#endif
             const int stop = __builtin_amdgcn_readfirstlane((int)(acc.T < (double)p.tau));
             if (stop) { s0 += 32; break; }
         }
@@ -619,6 +819,15 @@ __global__ void __launch_bounds__(1024, 4) render_kernel(FieldCfg cfg, BgArgs bg
             p.rgb[ray * 3 + 2] = b;
             p.depth[ray] = dd;
             p.acc[ray] = a;
+#if ACN_DIAG_CLOCK
+            p.depth[ray] = (float)(__builtin_amdgcn_s_memtime() - diag_t0) * 100.0f /
+                           (float)(__builtin_amdgcn_s_memrealtime() - diag_r0);
+#endif
+#if ACN_DIAG_PHASE  // cycles per tile: depth <- hash phase, acc <- MLP phase, rgb.r <- compositing
+            p.depth[ray] = (float)dg_hash / (float)dg_n;
+            p.acc[ray] = (float)dg_mlp / (float)dg_n;
+            p.rgb[ray * 3] = (float)dg_comp / (float)dg_n;
+#endif
         }
     }
 }
