@@ -171,6 +171,7 @@ def render_rays_stratified(model, rays: Tensor, ray_samples: int, params=None, a
                            bg_color_default: str = "white", chunk: int = 1_000_000, sigma_scale=1.0, **kwargs):
     """Stratified renderer: rgb (N,3), depth (N,), weights (N,S), acc (N,) (:290-345)."""
     tau = float(kwargs.get("early_stop_tau", 0.0))
+    want_weights = bool(kwargs.get("_want_weights", True))  # render_image drops the (N,S) weights
     N = rays.shape[0]
     if rays.is_cuda:
         fe = _fused_experts(model, params, active_module)
@@ -182,8 +183,9 @@ def render_rays_stratified(model, rays: Tensor, ray_samples: int, params=None, a
             rgb, depth, w, acc = ops.render_stratified(rays, ray_samples, specs, routing,
                                                        0 if len(specs) == 1 else None, bg,
                                                        sigma_scale=float(sigma_scale), tau=tau, jitter=jitter,
-                                                       packed=packed)
-            return rgb.to(rays.dtype), depth.to(rays.dtype), w.to(rays.dtype), acc.to(rays.dtype)
+                                                       packed=packed, want_weights=want_weights)
+            return (rgb.to(rays.dtype), depth.to(rays.dtype), None if w is None else w.to(rays.dtype),
+                    acc.to(rays.dtype))
     # composed (differentiable) path -- same structure as the reference
     o, d = rays[:, :3], rays[:, 3:6]
     near, far = rays[:, 6], rays[:, 7]
@@ -217,6 +219,6 @@ def render_image(model, *, H: int, W: int, fx: float, fy: float, cx: float, cy: 
                                  near_far_override=(None, None), apply_clamp=True)
     rgb_lin, depth, _, acc = render_rays(model, rays, ray_samples=ray_samples, params=params,
                                          active_module=active_module, bg_color_default=bg_color_default,
-                                         chunk=chunk_points, **kwargs)
+                                         chunk=chunk_points, _want_weights=False, **kwargs)
     rgb_lin = rgb_lin.view(H, W, 3).float().clamp_(0, 1)
     return rgb_lin, (None if depth is None else depth.view(-1)), (None if acc is None else acc.view(-1))

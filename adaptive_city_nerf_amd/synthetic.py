@@ -58,3 +58,35 @@ def formula_table_rows(rows: np.ndarray, features: int, seed: int, scale: float)
     with np.errstate(over="ignore"):
         u = (splitmix64(flat + np.uint64(seed) * _SEED_MUL) >> np.uint64(40)).astype(np.float64)
     return (((u / 16777216.0) * 2.0 - 1.0) * float(scale)).astype(np.float32)
+
+
+def grid_layout(gy: int, gz: int, example: dict, margin_frac: float = 0.0284) -> dict:
+    """Synthetic ``g{gy}{gz}`` expert layout for configs the reference ships no mask set for
+    (4x2).  Centroids follow ``_grid_centroids`` (scripts/create_clusters.py:298-323,
+    cluster_2d): cell centres of a gy x gz grid over the camera-position box, x at its centre.
+    The camera box is recovered from the shipped 2x2 layout (its centroids sit at 1/4 and 3/4 of
+    the box).  Per-expert AABBs: the axis-aligned Voronoi cell of the grid, clipped to the global
+    AABB and widened on interior faces by ``margin_frac`` of the global extent (the 2x2 example's
+    boundary widening, scene_drz_example.json g22), x spanning the global box."""
+    g22 = example["masks"]["g22_grid_bm110_ss11"]
+    c = np.asarray(g22["centroids"], np.float64)
+    lo_g, hi_g = np.asarray(g22["aabb_global"][0], np.float64), np.asarray(g22["aabb_global"][1], np.float64)
+    ymin, ymax = c[:, 1].min(), c[:, 1].max()
+    zmin, zmax = c[:, 2].min(), c[:, 2].max()
+    ry, rz = 2.0 * (ymax - ymin), 2.0 * (zmax - zmin)          # centroids at 1/4, 3/4 of the range
+    y0, z0 = ymin - ry / 4.0, zmin - rz / 4.0
+    ys = y0 + (np.arange(gy) + 0.5) * ry / gy
+    zs = z0 + (np.arange(gz) + 0.5) * rz / gz
+    xc = float(c[0, 0])
+    ybounds = np.concatenate([[lo_g[1]], 0.5 * (ys[1:] + ys[:-1]), [hi_g[1]]])
+    zbounds = np.concatenate([[lo_g[2]], 0.5 * (zs[1:] + zs[:-1]), [hi_g[2]]])
+    my, mz = margin_frac * (hi_g[1] - lo_g[1]), margin_frac * (hi_g[2] - lo_g[2])
+    cents, mins, maxs = [], [], []
+    for i in range(gy):
+        for j in range(gz):
+            cents.append([xc, ys[i], zs[j]])
+            mins.append([lo_g[0], ybounds[i] - (my if i > 0 else 0.0), zbounds[j] - (mz if j > 0 else 0.0)])
+            maxs.append([hi_g[0], ybounds[i + 1] + (my if i < gy - 1 else 0.0), zbounds[j + 1] + (mz if j < gz - 1 else 0.0)])
+    f32 = lambda a: np.asarray(a, np.float32).tolist()  # noqa: E731
+    return {"centroids": f32(cents), "cluster_2d": True, "boundary_margin": 1.1, "aabb_global": g22["aabb_global"],
+            "mins": f32(mins), "maxs": f32(maxs)}

@@ -13,6 +13,14 @@ Multi-GPU (torch.distributed.run, one process per GPU): rays are independent, so
 its own 4096 x 256 batch (weak scaling, no collective in the data path); barrier + synchronize
 bracket the K timed steps and the max over ranks is reported.
 
+Other BASELINE configs (``--workload``):
+  c3  2x2 Voronoi grid -> 4 experts (soft routing, boundary_margin 1.05); a global batch of
+      world x 4096 rays x 256 samples is sharded by owning expert (parallel.expert_sorted_plan),
+      each rank renders its 4096 rays and the rendered rays are all-gathered over RCCL (weak).
+  c4  4x2 grid -> 8 experts (synthetic layout, synthetic.grid_layout), one 800x800 frame x 256
+      samples: rays generated on device, sharded by expert, rendered, all-gathered, PSNR
+      all-reduced (parallel.render_image_sharded) -- strong scaling.
+
 Also reported: roofline of the fused render kernel (HIP events bracketing exactly that launch on
 its stream), and on rank 0 at N=1 a CPU baseline: the C oracle (oracle/, a fixture-pinned port of
 the reference CPU path) rendering the same batch on the host cores, whose output also gives the
@@ -42,10 +50,14 @@ HBM_PEAK_GBS = 8000.0
 
 def build_model(device, n_experts=1, seed=0, table_seed=100, table_scale=0.5):
     from adaptive_city_nerf_amd import MetaContainer, SceneBox
-    from adaptive_city_nerf_amd.synthetic import formula_table
+    from adaptive_city_nerf_amd.synthetic import formula_table, grid_layout
     scene = json.loads((REPO / "tests" / "golden" / "scene_drz_example.json").read_text())
-    mask = "g11_grid_bm110_ss11" if n_experts == 1 else "g22_grid_bm110_ss11"
-    sc = scene["masks"][mask]
+    if n_experts in (1, 4):
+        sc = scene["masks"]["g11_grid_bm110_ss11" if n_experts == 1 else "g22_grid_bm110_ss11"]
+    elif n_experts == 8:
+        sc = grid_layout(4, 2, scene)
+    else:
+        raise ValueError("n_experts must be 1 (g11), 4 (g22) or 8 (synthetic g42)")
     K = len(sc["centroids"])
     gbox = SceneBox(aabb=torch.tensor(sc["aabb_global"], dtype=torch.float32))
     boxes = [SceneBox(aabb=torch.tensor([sc["mins"][k], sc["maxs"][k]], dtype=torch.float32)) for k in range(K)]
@@ -63,14 +75,22 @@ def build_model(device, n_experts=1, seed=0, table_seed=100, table_scale=0.5):
     return m.to(device).eval(), gbox, scene, sc
 
 
+def frame_camera(scene, H=None, W=None, ds=0.25):
+    """Validation camera 0: at downscale ds, or with intrinsics rescaled to an H x W frame
+    centred at (W/2, H/2) (800x800, cx = cy = 400)."""
+    cam = scene["val_cam0"]
+    intr = torch.tensor(cam["intrinsics"], dtype=torch.float32)
+    if H is None:
+        return int(round(cam["H"] * ds)), int(round(cam["W"] * ds)), (intr * ds).tolist(), torch.tensor(cam["c2w"])
+    s = min(H / cam["H"], W / cam["W"])
+    return H, W, [float(intr[0] * s), float(intr[1] * s), W / 2.0, H / 2.0], torch.tensor(cam["c2w"])
+
+
 def make_rays(scene, gbox, device, n_rays, seed):
     from adaptive_city_nerf_amd import ops
-    cam = scene["val_cam0"]
-    ds = 0.25
-    H, W = int(round(cam["H"] * ds)), int(round(cam["W"] * ds))
-    intr = (torch.tensor(cam["intrinsics"], dtype=torch.float32) * ds).tolist()
+    H, W, intr, c2w = frame_camera(scene)
     psf = scene["pose_scale_factor"]
-    rays, valid = ops.get_rays_image(H, W, *intr, torch.tensor(cam["c2w"]), gbox.aabb, device,
+    rays, valid = ops.get_rays_image(H, W, *intr, c2w, gbox.aabb, device,
                                      near_far_override=(0.0 / psf, 100000 / psf))
     vi = torch.nonzero(valid).squeeze(1).cpu()
     g = torch.Generator().manual_seed(seed)
@@ -81,17 +101,19 @@ def make_rays(scene, gbox, device, n_rays, seed):
 def cpu_baseline(model, sc, rays, S, gpu_rgb, min_seconds):
     """C oracle on the host cores over the same batch, repeated until >= min_seconds."""
     from oracle import oracle as O
-    sub = model.submodules[0]
-    w = {n: p.detach().cpu().numpy() for n, p in sub.meta_named_parameters()}
-    e = O.Expert(w, sub.xyz_encoder.hash_table.detach().cpu().numpy(), np.array(sub.xyz_encoder._res_host, np.int32),
-                 sub.scene_box.min.cpu().numpy(), sub.aabb_extent.cpu().numpy())
+    experts = []
+    for sub in model.submodules:
+        w = {n: p.detach().cpu().numpy() for n, p in sub.meta_named_parameters()}
+        experts.append(O.Expert(w, sub.xyz_encoder.hash_table.detach().cpu().numpy(),
+                                np.array(sub.xyz_encoder._res_host, np.int32), sub.scene_box.min.cpu().numpy(),
+                                sub.aabb_extent.cpu().numpy()))
     bg = {f"bg_mlp.{k}": v.detach().cpu().numpy() for k, v in model.bg_mlp.state_dict().items()}
     r = rays.cpu().numpy()
     cores = O.max_threads()
     reps, t0 = 0, time.perf_counter()
     while True:
-        orgb, _, _, _ = O.render_stratified(r, S, [e], np.array(sc["centroids"], np.float32), bm=model.boundary_margin,
-                                            bg_mlp=bg, want_weights=False)
+        orgb, _, _, _ = O.render_stratified(r, S, experts, np.array(sc["centroids"], np.float32),
+                                            bm=model.boundary_margin, bg_mlp=bg, want_weights=False)
         reps += 1
         if time.perf_counter() - t0 >= min_seconds:
             break
@@ -119,10 +141,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--rays", type=int, default=4096)
+    ap.add_argument("--workload", choices=["c2", "c3", "c4"], default="c2")
+    ap.add_argument("--rays", type=int, default=4096, help="rays per GPU (c2, c3)")
     ap.add_argument("--samples", type=int, default=256)
-    ap.add_argument("--experts", type=int, default=1)
+    ap.add_argument("--frame", type=int, default=800, help="frame side (c4)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-rays", type=int, default=4096, help="rays in the CPU-baseline / PSNR sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     a = ap.parse_args()
 
@@ -136,14 +160,44 @@ def main():
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
-    from adaptive_city_nerf_amd import ops, render_rays
-    model, gbox, scene, sc = build_model(device, a.experts)
-    rays = make_rays(scene, gbox, device, a.rays, 1234 + rank)
+    from adaptive_city_nerf_amd import ops, parallel, render_rays
     S = a.samples
+    K = {"c2": 1, "c3": 4, "c4": 8}[a.workload]
+    model, gbox, scene, sc = build_model(device, K)
 
-    def step():
-        with torch.no_grad():
-            return render_rays(model, rays, ray_samples=S, bg_color_default="white")
+    if a.workload == "c2":
+        rays = make_rays(scene, gbox, device, a.rays, 1234 + rank)
+        samples_per_step = world * a.rays * S
+
+        def step():
+            with torch.no_grad():
+                return render_rays(model, rays, ray_samples=S, bg_color_default="white")
+        sample_rays = rays
+    elif a.workload == "c3":
+        # global batch (identical on every rank), sharded by owning expert; gather of rendered rays
+        grays = make_rays(scene, gbox, device, world * a.rays, 1234)
+        plan = parallel.expert_sorted_plan(parallel.dominant_expert(grays, model), world)
+        samples_per_step = grays.shape[0] * S
+
+        def render_fn(r):
+            rgb, depth, _, acc = render_rays(model, r, ray_samples=S, bg_color_default="white", _want_weights=False)
+            return rgb, depth, acc
+
+        def step():
+            with torch.no_grad():
+                return parallel.render_rays_sharded(grays, render_fn, plan)
+        sample_rays = grays
+    else:
+        H, W, intr, c2w = frame_camera(scene, a.frame, a.frame)
+        samples_per_step = H * W * S
+        gt = torch.rand(H, W, 3, device=device, generator=torch.Generator(device).manual_seed(7))
+
+        def step():
+            with torch.no_grad():
+                return parallel.render_image_sharded(model, H=H, W=W, fx=intr[0], fy=intr[1], cx=intr[2], cy=intr[3],
+                                                     c2w=c2w, scene_box=gbox, ray_samples=S, gt_srgb=gt)
+        frays, fvalid = ops.get_rays_image(H, W, *intr, c2w, gbox.aabb, device, near_far_override=(None, None))
+        sample_rays = frays
 
     for _ in range(a.warmup):
         out = step()
@@ -160,43 +214,67 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     kernel_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in ops.EVENT_HOOK]))
+    kernel_launches = len(ops.EVENT_HOOK) // max(a.steps, 1)
     ops.EVENT_HOOK = None
     if world > 1:
         t = torch.tensor([dt, kernel_ms], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt, kernel_ms = float(t[0]), float(t[1])
 
-    samples_per_step = a.rays * S
-    value = world * samples_per_step * a.steps / dt
+    value = samples_per_step * a.steps / dt
     ms_per_step = dt / a.steps * 1e3
-    achieved = FLOP_PER_SAMPLE * samples_per_step / (kernel_ms * 1e-3) / 1e12
-    tr = load_traffic()
+    # samples one launch of the dominant kernel processes on this rank
+    launch_samples = samples_per_step // world // max(kernel_launches, 1)
+    achieved = FLOP_PER_SAMPLE * launch_samples / (kernel_ms * 1e-3) / 1e12
+    tr = load_traffic() if a.workload == "c2" else None
+    kname = {"c2": "render_kernel<1,1,0> (fused stratified render, 1 expert)",
+             "c3": "render_kernel<1,0,1> (fused stratified render, soft routing over 4 experts)",
+             "c4": "render_kernel<1,0,1> (fused stratified render, soft routing over 8 experts)"}[a.workload]
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
                 "traffic": (tr or {}).get("hbm_bytes_per_launch"),
-                "kernel": "render_kernel<1,1,0> (fused stratified render)", "kernel_ms": round(kernel_ms, 4),
-                "hash_bytes_algorithmic_per_launch": int(BYTES_PER_SAMPLE * samples_per_step),
-                "hash_gbs_algorithmic": round(BYTES_PER_SAMPLE * samples_per_step / (kernel_ms * 1e-3) / 1e9, 1)}
+                "kernel": kname, "kernel_ms": round(kernel_ms, 4), "samples_per_launch": int(launch_samples),
+                "flop_per_sample": FLOP_PER_SAMPLE,
+                "hash_bytes_algorithmic_per_launch": int(BYTES_PER_SAMPLE * launch_samples),
+                "hash_gbs_algorithmic": round(BYTES_PER_SAMPLE * launch_samples / (kernel_ms * 1e-3) / 1e9, 1)}
 
     cpu, psnr, rmse, maxerr = None, None, None, None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu, psnr, rmse, maxerr = cpu_baseline(model, sc, rays, S, out[0].cpu().numpy(), a.cpu_seconds)
+    if rank == 0 and not a.no_cpu_baseline:
+        rgb_all = out[0].reshape(-1, 3)
+        if a.workload == "c2":
+            idx = torch.arange(rays.shape[0], device=device)[: a.cpu_rays]
+        else:  # a bounded random sample of the gathered frame / batch (valid rays)
+            fin = torch.nonzero(torch.isfinite(sample_rays[:, 7])).squeeze(1).cpu()
+            g = torch.Generator().manual_seed(99)
+            idx = fin[torch.randperm(fin.numel(), generator=g)[: a.cpu_rays]].to(device)
+        cpu, psnr, rmse, maxerr = cpu_baseline(model, sc, sample_rays[idx], S, rgb_all[idx].cpu().numpy(),
+                                               a.cpu_seconds)
 
     if rank == 0:
+        cfg = {"c2": {"workload": "C2: single Instant-NGP expert, 4096 rays x 256 samples per GPU, eval, fused "
+                                  "render_rays", "rays_per_gpu": a.rays, "experts": 1},
+               "c3": {"workload": "C3: 2x2 Voronoi grid -> 4 experts (soft routing bm 1.05), 4096 rays x 256 samples "
+                                  "per GPU sharded by owning expert, RCCL all-gather of rendered rays",
+                      "rays_per_gpu": a.rays, "experts": 4},
+               "c4": {"workload": f"C4: 4x2 grid -> 8 experts (synthetic layout), {a.frame}x{a.frame} frame x "
+                                  f"{S} samples, expert-sharded, RCCL all-gather + PSNR all-reduce",
+                      "frame": [a.frame, a.frame], "experts": 8}}[a.workload]
+        cfg.update({"samples_per_ray": S, "parallelism": f"ray-sharded x{world}"})
         line = {
             "metric": "ray-samples/sec + PSNR, 4096 rays×256 samples, 1/2/4/8 MI355X",
             "value": round(value, 1), "unit": "ray-samples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-            "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "strong" if a.workload == "c4" else "weak", "vs_baseline": None,
             "dtype": "f32", "data": "synthetic (formula-filled hash table, seeded MLP init; rays from the "
                                     "reference's validation camera geometry)",
-            "config": {"workload": "C2: single Instant-NGP expert, 4096 rays x 256 samples per GPU, eval, fused "
-                                   "render_rays", "rays_per_gpu": a.rays, "samples_per_ray": S,
-                       "experts": a.experts, "parallelism": f"ray-sharded x{world}"},
+            "config": cfg,
             "roofline": roofline,
             "cpu_baseline": cpu,
             "psnr_vs_cpu_path_db": None if psnr is None else round(psnr, 2),
             "rgb_max_abs_err_vs_cpu_path": maxerr,
         }
+        if a.workload == "c4":
+            line["psnr_vs_synthetic_gt_db"] = round(float(out[3]), 4)
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
