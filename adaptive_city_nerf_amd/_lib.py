@@ -52,6 +52,15 @@ class acn_background(C.Structure):
                 ("w1", C.c_void_p), ("b1", C.c_void_p), ("w2", C.c_void_p), ("b2", C.c_void_p)]
 
 
+ACN_OPTIM_CHUNK = 65536
+ACN_OPTIM_MAX_GROUPS = 8
+
+
+class acn_adam_group(C.Structure):
+    _fields_ = [("lr", C.c_double), ("beta1", C.c_double), ("beta2", C.c_double), ("eps", C.c_double),
+                ("weight_decay", C.c_double), ("step", C.c_int32), ("pad", C.c_int32)]
+
+
 _lib = None
 _lock = threading.Lock()
 vp, i64, i32, f32, sz = C.c_void_p, C.c_int64, C.c_int, C.c_float, C.c_size_t
@@ -76,6 +85,9 @@ SIGNATURES = {
     "acn_clamp_rays": ([vp, i64, i32, i32, f32, i32, f32, f32, f32, vp, vp], C.c_int),
     "acn_routing_fwd": ([vp, i64, i64, vp, vp, vp, vp], C.c_int),
     "acn_background_fwd": ([vp, i64, vp, vp, vp], C.c_int),
+    "acn_grad_sumsq": ([vp, vp, i64, vp, vp, vp], C.c_int),
+    "acn_clip_coef": ([vp, f32, vp, vp], C.c_int),
+    "acn_adam_step": ([vp, vp, i64, vp, i32, vp, vp], C.c_int),
 }
 
 

@@ -126,6 +126,41 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_gen(const float* __restrict_
     }
 }
 
+// F == 2, Linear/Smoothstep: one lane per (point, level, corner, feature).  A wave covers 4
+// consecutive points at ONE level, lanes ordered (point, y/z corner, x corner, feature), so each
+// no-return atomic instruction touches ~16 table row pairs (the x-neighbours of a corner pair
+// share a 128-B line) instead of the 64 unrelated rows of the lane-per-(point, level) mapping
+// (MI355X_MICROARCH.md "Global float atomics": rate set by distinct rows per instruction).  The
+// per-corner gradient keeps the forward's chain-rule order ((g * wz) * wy) * wx.
+template <int INTERP>
+__global__ void __launch_bounds__(256) hashgrid_bwd_f2(const float* __restrict__ x01, int64_t M,
+                                                       const float* __restrict__ gout, Res32 res, int L,
+                                                       int log2T, float* __restrict__ gtable) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t groups = (M + 3) >> 2;               // groups of 4 points
+    const int l = (int)(wave / groups);
+    const int64_t m = (wave - (int64_t)l * groups) * 4 + (lane >> 4);
+    if (l >= L || m >= M) return;
+    const int f = lane & 1, bx = (lane >> 1) & 1, by = (lane >> 3) & 1, bz = (lane >> 2) & 1;
+    const float r = (float)res.v[l];
+    const float sx = x01[3 * m] * r, sy = x01[3 * m + 1] * r, sz = x01[3 * m + 2] * r;
+    const uint32_t mask = (uint32_t)((1ull << log2T) - 1ull);
+    const float fx = floorf(sx), fy = floorf(sy), fz = floorf(sz);
+    float wx = sx - fx, wy = sy - fy, wz = sz - fz;
+    if (INTERP == 2) {
+        wx = (wx * wx) * (3.0f - 2.0f * wx);
+        wy = (wy * wy) * (3.0f - 2.0f * wy);
+        wz = (wz * wz) * (3.0f - 2.0f * wz);
+    }
+    const uint32_t xi = (uint32_t)(int)fx + (uint32_t)bx;
+    const uint32_t yi = (uint32_t)(int)fy * acn::kP1 + (by ? acn::kP1 : 0u);
+    const uint32_t zi = (uint32_t)(int)fz * acn::kP2 + (bz ? acn::kP2 : 0u);
+    const uint32_t h = (xi ^ yi ^ zi) & mask;
+    const float gv = ((gout[(m * L + l) * 2 + f] * (bz ? wz : 1.0f - wz)) * (by ? wy : 1.0f - wy)) * (bx ? wx : 1.0f - wx);
+    unsafeAtomicAdd(gtable + (((int64_t)l << log2T) + h) * 2 + f, gv);
+}
+
 template <int DEGREE>
 __global__ void __launch_bounds__(256) sh_fwd_kernel(const float* __restrict__ d, int64_t M,
                                                      float* __restrict__ out) {
@@ -179,9 +214,16 @@ extern "C" int acn_hashgrid_bwd(const float* x01, int64_t M, const float* grad_o
     ACN_REQUIRE(x01 && grad_out && grad_table, "acn_hashgrid_bwd: NULL pointer");
     Res32 r{};
     for (int i = 0; i < L; ++i) r.v[i] = res[i];
+    hipStream_t s = (hipStream_t)stream;
+    if (F == 2 && interp != 0) {
+        const int64_t waves = ((M + 3) / 4) * L;
+        const dim3 grid((unsigned)((waves + 3) / 4)), block(256);
+        if (interp == 1) hipLaunchKernelGGL(hashgrid_bwd_f2<1>, grid, block, 0, s, x01, M, grad_out, r, L, log2T, grad_table);
+        else hipLaunchKernelGGL(hashgrid_bwd_f2<2>, grid, block, 0, s, x01, M, grad_out, r, L, log2T, grad_table);
+        return acn_check_launch("acn_hashgrid_bwd");
+    }
     const int64_t threads = M * L;
     const dim3 grid((unsigned)((threads + 255) / 256)), block(256);
-    hipStream_t s = (hipStream_t)stream;
     if (interp == 0) hipLaunchKernelGGL(hashgrid_bwd_gen<0>, grid, block, 0, s, x01, M, grad_out, r, L, log2T, F, grad_table);
     else if (interp == 1) hipLaunchKernelGGL(hashgrid_bwd_gen<1>, grid, block, 0, s, x01, M, grad_out, r, L, log2T, F, grad_table);
     else hipLaunchKernelGGL(hashgrid_bwd_gen<2>, grid, block, 0, s, x01, M, grad_out, r, L, log2T, F, grad_table);

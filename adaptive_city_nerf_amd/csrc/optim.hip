@@ -1,0 +1,194 @@
+// optim.hip -- the optimizer step of the online adaptation loop on gfx950:
+//   torch.nn.utils.clip_grad_norm_(params, max_norm)      (runtime_adapt.py:305-307)
+//   torch.optim.Adam(param_groups).step()                  (common/utils.py:57-62, runtime_adapt.py:309)
+// over every parameter of the model in ONE launch each (multi-tensor), instead of per-tensor op
+// chains.  The reference runs dense Adam over 134M parameters per step (4 experts x 2^24 table
+// rows x 2): this step is HBM-bound (28 B moved per parameter: read p, g, m, v; write p, m, v),
+// so the kernels stream 16-B vectors with every lane busy and fold the clip coefficient into the
+// Adam pass (the clipped gradient is never written back).
+//
+// Work decomposition: every tensor is cut into chunks of ACN_OPTIM_CHUNK elements; the caller
+// passes a device array of tensor descriptors and a chunk -> tensor map, so one grid covers all
+// tensors (and no host synchronisation is needed between the norm, the coefficient and the step).
+#include "acn_internal.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ double block_sum(double v) {
+    __shared__ double red[kThreads / 64];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double t = 0.0;
+    if (threadIdx.x == 0)
+        for (int i = 0; i < kThreads / 64; ++i) t += red[i];
+    return t;  // valid on thread 0
+}
+
+// per-chunk sum of squared gradients (double accumulation)
+__global__ void __launch_bounds__(kThreads) sumsq_kernel(const acn_param_desc* __restrict__ descs,
+                                                         const int32_t* __restrict__ chunk_tensor,
+                                                         double* __restrict__ partials) {
+    const acn_param_desc d = descs[chunk_tensor[blockIdx.x]];
+    const int64_t base = (int64_t)(blockIdx.x - d.first_chunk) * ACN_OPTIM_CHUNK;
+    const int64_t n = d.numel - base < ACN_OPTIM_CHUNK ? d.numel - base : ACN_OPTIM_CHUNK;
+    const float* g = d.grad + base;
+    double acc = 0.0;
+    if (d.grad != nullptr) {
+        const bool vec = ((reinterpret_cast<uintptr_t>(g) & 15) == 0);
+        if (vec) {
+            const int64_t n4 = n >> 2;
+            const f4* g4 = reinterpret_cast<const f4*>(g);
+            for (int64_t i = threadIdx.x; i < n4; i += kThreads) {
+                const f4 v = g4[i];
+                acc += (double)v[0] * v[0] + (double)v[1] * v[1] + (double)v[2] * v[2] + (double)v[3] * v[3];
+            }
+            for (int64_t i = (n4 << 2) + threadIdx.x; i < n; i += kThreads) acc += (double)g[i] * g[i];
+        } else {
+            for (int64_t i = threadIdx.x; i < n; i += kThreads) acc += (double)g[i] * g[i];
+        }
+    }
+    const double t = block_sum(acc);
+    if (threadIdx.x == 0) partials[blockIdx.x] = t;
+}
+
+__global__ void __launch_bounds__(kThreads) reduce_kernel(const double* __restrict__ partials, int64_t n,
+                                                          double* __restrict__ total) {
+    double acc = 0.0;
+    for (int64_t i = threadIdx.x; i < n; i += kThreads) acc += partials[i];
+    const double t = block_sum(acc);
+    if (threadIdx.x == 0) total[0] = t;
+}
+
+// clip_grad_norm_ (torch/nn/utils/clip_grad.py): total_norm, clip_coef = max_norm / (total_norm +
+// 1e-6) clamped to <= 1 (fp32 arithmetic, as the tensor ops there).
+__global__ void clip_coef_kernel(const double* __restrict__ total_sumsq, float max_norm, float* __restrict__ out) {
+    const float norm = (float)sqrt(total_sumsq[0]);
+    float coef = max_norm / (norm + 1e-6f);
+    coef = coef > 1.0f ? 1.0f : coef;  // NaN passes through, like torch.clamp
+    out[0] = norm;
+    out[1] = coef;
+}
+
+struct GroupK {
+    float lr_neg_step, w1, beta2, one_m_beta2, bc2s, eps, wd;
+};
+struct GroupsArg {
+    GroupK g[ACN_OPTIM_MAX_GROUPS];
+};
+
+// torch.optim.Adam, single-tensor semantics (torch/optim/adam.py _single_tensor_adam):
+//   g = grad * clip (+ wd * p); m = lerp(m, g, 1 - beta1); v = v * beta2 + (1 - beta2) * g * g
+//   p += (-lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
+__device__ __forceinline__ void adam_elem(float& p, float gr, float& m, float& v, float scale, const GroupK& k) {
+    float g = gr * scale;
+    if (k.wd != 0.0f) g = fmaf(k.wd, p, g);       // grad.add(param, alpha=wd) (vectorised fmadd)
+    m = fmaf(k.w1, g - m, m);                    // at::lerp, |weight| < 0.5 branch (vectorised fmadd)
+    v = v * k.beta2;
+    v = v + (k.one_m_beta2 * g) * g;             // addcmul_(g, g, value = 1 - beta2)
+    const float denom = sqrtf(v) / k.bc2s + k.eps;
+    p = p + (k.lr_neg_step * m) / denom;         // addcdiv_(m, denom, value = -step_size)
+}
+
+__global__ void __launch_bounds__(kThreads) adam_kernel(const acn_param_desc* __restrict__ descs,
+                                                        const int32_t* __restrict__ chunk_tensor, GroupsArg ga,
+                                                        const float* __restrict__ grad_scale) {
+    const acn_param_desc d = descs[chunk_tensor[blockIdx.x]];
+    if (d.grad == nullptr) return;  // parameter without gradient: torch skips it
+    const GroupK k = ga.g[d.group];
+    const float scale = grad_scale ? grad_scale[1] : 1.0f;
+    const int64_t base = (int64_t)(blockIdx.x - d.first_chunk) * ACN_OPTIM_CHUNK;
+    const int64_t n = d.numel - base < ACN_OPTIM_CHUNK ? d.numel - base : ACN_OPTIM_CHUNK;
+    float* p = d.param + base;
+    const float* g = d.grad + base;
+    float* m = d.exp_avg + base;
+    float* v = d.exp_avg_sq + base;
+    const uintptr_t align = reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) |
+                            reinterpret_cast<uintptr_t>(m) | reinterpret_cast<uintptr_t>(v);
+    int64_t done = 0;
+    if ((align & 15) == 0) {
+        const int64_t n4 = n >> 2;
+        f4* p4 = reinterpret_cast<f4*>(p);
+        const f4* g4 = reinterpret_cast<const f4*>(g);
+        f4* m4 = reinterpret_cast<f4*>(m);
+        f4* v4 = reinterpret_cast<f4*>(v);
+        for (int64_t i = threadIdx.x; i < n4; i += kThreads) {
+            f4 pp = p4[i], mm = m4[i], vv = v4[i];
+            const f4 gg = g4[i];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                float a = pp[c], b = mm[c], e = vv[c];
+                adam_elem(a, gg[c], b, e, scale, k);
+                pp[c] = a; mm[c] = b; vv[c] = e;
+            }
+            p4[i] = pp;
+            m4[i] = mm;
+            v4[i] = vv;
+        }
+        done = n4 << 2;
+    }
+    for (int64_t i = done + threadIdx.x; i < n; i += kThreads) {
+        float a = p[i], b = m[i], e = v[i];
+        adam_elem(a, g[i], b, e, scale, k);
+        p[i] = a; m[i] = b; v[i] = e;
+    }
+}
+
+}  // namespace
+
+extern "C" int acn_grad_sumsq(const acn_param_desc* descs, const int32_t* chunk_tensor, int64_t nchunks,
+                              double* partials, double* total, void* stream) {
+    ACN_REQUIRE(nchunks >= 0, "acn_grad_sumsq: nchunks must be >= 0");
+    ACN_REQUIRE(total, "acn_grad_sumsq: NULL total");
+    hipStream_t s = (hipStream_t)stream;
+    if (nchunks == 0) {
+        const hipError_t e = hipMemsetAsync(total, 0, sizeof(double), s);
+        return e == hipSuccess ? ACN_OK : acn_set_error((int)e, "acn_grad_sumsq: %s", hipGetErrorString(e));
+    }
+    ACN_REQUIRE(descs && chunk_tensor && partials, "acn_grad_sumsq: NULL pointer");
+    ACN_REQUIRE(nchunks <= 0x7fffffff, "acn_grad_sumsq: too many chunks");
+    hipLaunchKernelGGL(sumsq_kernel, dim3((unsigned)nchunks), dim3(kThreads), 0, s, descs, chunk_tensor, partials);
+    hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(kThreads), 0, s, partials, nchunks, total);
+    return acn_check_launch("acn_grad_sumsq");
+}
+
+extern "C" int acn_clip_coef(const double* total_sumsq, float max_norm, float* out, void* stream) {
+    ACN_REQUIRE(total_sumsq && out, "acn_clip_coef: NULL pointer");
+    hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, total_sumsq, max_norm, out);
+    return acn_check_launch("acn_clip_coef");
+}
+
+extern "C" int acn_adam_step(const acn_param_desc* descs, const int32_t* chunk_tensor, int64_t nchunks,
+                             const acn_adam_group* groups, int ngroups, const float* grad_scale, void* stream) {
+    ACN_REQUIRE(nchunks >= 0 && nchunks <= 0x7fffffff, "acn_adam_step: bad nchunks");
+    if (nchunks == 0) return ACN_OK;
+    ACN_REQUIRE(descs && chunk_tensor && groups, "acn_adam_step: NULL pointer");
+    ACN_REQUIRE(ngroups >= 1 && ngroups <= ACN_OPTIM_MAX_GROUPS, "acn_adam_step: ngroups must be in [1, %d]",
+                ACN_OPTIM_MAX_GROUPS);
+    GroupsArg ga{};
+    for (int i = 0; i < ngroups; ++i) {
+        const acn_adam_group& g = groups[i];
+        ACN_REQUIRE(g.step >= 1, "acn_adam_step: group %d step must be >= 1 (incremented before the update)", i);
+        // python-float (double) scalars of _single_tensor_adam, cast to fp32 where they meet tensors
+        const double b1 = g.beta1, b2 = g.beta2;
+        const double bc1 = 1.0 - pow(b1, (double)g.step);
+        const double bc2 = 1.0 - pow(b2, (double)g.step);
+        const double step_size = (double)g.lr / bc1;
+        GroupK& k = ga.g[i];
+        k.lr_neg_step = (float)(-step_size);
+        k.w1 = (float)(1.0 - b1);
+        k.beta2 = (float)b2;
+        k.one_m_beta2 = (float)(1.0 - b2);
+        k.bc2s = (float)sqrt(bc2);
+        k.eps = (float)g.eps;
+        k.wd = (float)g.weight_decay;
+    }
+    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)nchunks), dim3(kThreads), 0, (hipStream_t)stream, descs,
+                       chunk_tensor, ga, grad_scale);
+    return acn_check_launch("acn_adam_step");
+}

@@ -1,0 +1,220 @@
+"""Optimizer step of the online adaptation loop on the HIP kernels of csrc/optim.hip.
+
+Reference: ``torch.nn.utils.clip_grad_norm_(base.parameters(), grad_clip)`` then
+``optimizer.step()`` with ``torch.optim.Adam(param_groups)`` (pipelines/online_stage/
+runtime_adapt.py:305-309, common/utils.py:16-62).  ``FusedAdam`` keeps torch.optim.Adam's
+constructor, param-group and state layout (``state[p] = {"step", "exp_avg", "exp_avg_sq"}``, so
+state dicts load either way) but performs the whole step -- every tensor of every group -- in one
+multi-tensor launch, optionally with the clip coefficient of ``clip_grad_norm_`` folded in
+(``step(max_norm=...)``: norm -> coefficient -> update, three launches, no host synchronisation).
+There is no CPU path: parameters must live on a HIP device.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Iterable, Optional
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+from ._lib import ACN_OPTIM_CHUNK, ACN_OPTIM_MAX_GROUPS, AcnError, acn_adam_group, check, require_hip
+
+
+class _Plan:
+    """Device descriptors (acn_param_desc) + chunk -> tensor map for a list of (p, g, m, v, key)."""
+
+    def __init__(self, rows, device):
+        self.key = tuple((p.data_ptr(), 0 if g is None else g.data_ptr(), m.data_ptr(), v.data_ptr(), k)
+                         for p, g, m, v, k in rows)
+        descs, owners, first = [], [], 0
+        for t, (p, g, m, v, k) in enumerate(rows):
+            n = p.numel()
+            nch = (n + ACN_OPTIM_CHUNK - 1) // ACN_OPTIM_CHUNK
+            descs.append([p.data_ptr(), 0 if g is None else g.data_ptr(), m.data_ptr(), v.data_ptr(), n,
+                          (first << 32) | k])
+            owners.append(torch.full((nch,), t, dtype=torch.int32))
+            first += nch
+        self.nchunks = first
+        host = torch.tensor(descs, dtype=torch.int64).pin_memory() if descs else torch.zeros(0, 6, dtype=torch.int64)
+        self.descs = host.to(device, non_blocking=True)
+        own = torch.cat(owners) if owners else torch.zeros(0, dtype=torch.int32)
+        self.chunk_tensor = own.pin_memory().to(device, non_blocking=True) if own.numel() else own.to(device)
+        self.partials = torch.empty(max(first, 1), dtype=torch.float64, device=device)
+        self._keep = (host, own)
+
+
+# Optional timing hook (bench.py): when set to a list, FusedAdam.step appends a pair of recorded
+# HIP events bracketing exactly the Adam launch on the current stream.
+EVENT_HOOK = None
+
+
+def _stream(device) -> int:
+    return int(torch.cuda.current_stream(device).cuda_stream)
+
+
+def grad_sumsq(params, device, plan: Optional[_Plan] = None) -> torch.Tensor:
+    """Sum of squared gradients of ``params`` as a 1-element float64 device tensor."""
+    if plan is None:
+        rows = [(p, p.grad, p, p, 0) for p in params if p.grad is not None]
+        plan = _Plan(rows, device)
+    total = torch.empty(1, dtype=torch.float64, device=device)
+    check(_lib.lib().acn_grad_sumsq(plan.descs.data_ptr() if plan.nchunks else None,
+                                    plan.chunk_tensor.data_ptr() if plan.nchunks else None, plan.nchunks,
+                                    plan.partials.data_ptr(), total.data_ptr(), _stream(device)), "acn_grad_sumsq")
+    return total
+
+
+def clip_coef(total_sumsq: torch.Tensor, max_norm: float) -> torch.Tensor:
+    """(total_norm, clip coefficient) as a 2-element float32 device tensor."""
+    out = torch.empty(2, dtype=torch.float32, device=total_sumsq.device)
+    check(_lib.lib().acn_clip_coef(total_sumsq.data_ptr(), float(max_norm), out.data_ptr(),
+                                   _stream(total_sumsq.device)), "acn_clip_coef")
+    return out
+
+
+def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0, group=None) -> torch.Tensor:
+    """torch.nn.utils.clip_grad_norm_ (2-norm) with the norm reduced by one HIP launch pair;
+    gradients are scaled in place.  ``group``: all-reduce the squared norm over ranks first."""
+    if norm_type != 2.0:
+        raise AcnError("clip_grad_norm_: only the 2-norm (the reference's) is implemented on the HIP path")
+    params = [p for p in (parameters if not isinstance(parameters, torch.Tensor) else [parameters])]
+    grads = [p.grad for p in params if p.grad is not None]
+    if not grads:
+        return torch.tensor(0.0)
+    device = grads[0].device
+    require_hip(grads[0], "clip_grad_norm_")
+    total = grad_sumsq([p for p in params if p.grad is not None], device)
+    if group is not None and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(total, group=group)
+    nc = clip_coef(total, max_norm)
+    torch._foreach_mul_(grads, nc[1])
+    return nc[0]
+
+
+class FusedAdam(torch.optim.Optimizer):
+    """torch.optim.Adam (amsgrad=False, maximize=False) as one multi-tensor HIP step."""
+
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
+                 amsgrad: bool = False, **unused):
+        if amsgrad:
+            raise AcnError("FusedAdam: amsgrad is not implemented (the reference does not use it)")
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False, maximize=False,
+                        foreach=None, capturable=False, differentiable=False, fused=None)
+        super().__init__(params, defaults)
+        self._plan = None
+        self._splans = None
+        self.last_norm: Optional[torch.Tensor] = None   # (total_norm, coef) of the last clipped step
+        # parameters replicated across an expert-parallel group (e.g. the shared background head):
+        # their squared norm is added once, after the all-reduce of everyone else's
+        self.shared_params = set()
+
+    def _rows(self):
+        """(p, grad, exp_avg, exp_avg_sq, kind) rows; kind indexes distinct (group, step) pairs."""
+        rows, kinds = [], []
+        for gi, group in enumerate(self.param_groups):
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                require_hip(p, "FusedAdam")
+                if p.grad.is_sparse:
+                    raise AcnError("FusedAdam: sparse gradients are not supported")
+                st = self.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.tensor(0.0, dtype=torch.float32)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["step"] += 1
+                key = (gi, int(st["step"].item()))
+                if key not in kinds:
+                    kinds.append(key)
+                g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+                if not (p.is_contiguous() and st["exp_avg"].is_contiguous() and st["exp_avg_sq"].is_contiguous()):
+                    raise AcnError("FusedAdam: parameters and state must be contiguous")
+                if p.dtype != torch.float32 or g.dtype != torch.float32:
+                    raise AcnError("FusedAdam: fp32 parameters/gradients only")
+                rows.append((p, g, st["exp_avg"], st["exp_avg_sq"], kinds.index(key)))
+        if len(kinds) > ACN_OPTIM_MAX_GROUPS:
+            raise AcnError(f"FusedAdam: at most {ACN_OPTIM_MAX_GROUPS} distinct (group, step) pairs per step")
+        return rows, kinds
+
+    @torch.no_grad()
+    def step(self, closure=None, max_norm: Optional[float] = None, sumsq_group=None):
+        """One Adam step.  ``max_norm``: apply clip_grad_norm_(all params, max_norm) first (fused:
+        the coefficient scales the gradients inside the update).  ``sumsq_group``: all-reduce the
+        squared gradient norm over this process group before the coefficient (expert parallel)."""
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        rows, kinds = self._rows()
+        if not rows:
+            return loss
+        device = rows[0][0].device
+        key = tuple((p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), k) for p, g, m, v, k in rows)
+        if self._plan is None or self._plan.key != key:
+            self._plan = _Plan(rows, device)
+        plan = self._plan
+        scale = None
+        if max_norm is not None:
+            distributed = sumsq_group is not None and dist.is_initialized() and dist.get_world_size(sumsq_group) > 1
+            if distributed and self.shared_params:
+                own = [r for r in rows if id(r[0]) not in self.shared_params]
+                shr = [r for r in rows if id(r[0]) in self.shared_params]
+                skey = (key, "split")
+                if self._splans is None or self._splans[0] != skey:
+                    self._splans = (skey, _Plan(own, device), _Plan(shr, device))
+                total = grad_sumsq(None, device, self._splans[1])
+                dist.all_reduce(total, group=sumsq_group)
+                total = total + grad_sumsq(None, device, self._splans[2])
+            else:
+                total = grad_sumsq(None, device, plan)
+                if distributed:
+                    dist.all_reduce(total, group=sumsq_group)
+            scale = clip_coef(total, max_norm)
+            self.last_norm = scale
+        groups = (acn_adam_group * len(kinds))()
+        for i, (gi, step) in enumerate(kinds):
+            g = self.param_groups[gi]
+            b1, b2 = g["betas"]
+            groups[i] = acn_adam_group(float(g["lr"]), float(b1), float(b2), float(g["eps"]),
+                                       float(g["weight_decay"]), int(step), 0)
+        hook = EVENT_HOOK
+        if hook is not None:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+        check(_lib.lib().acn_adam_step(plan.descs.data_ptr(), plan.chunk_tensor.data_ptr(), plan.nchunks, groups,
+                                       len(kinds), None if scale is None else scale.data_ptr(), _stream(device)),
+              "acn_adam_step")
+        if hook is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            hook.append((e0, e1))
+        return loss
+
+
+def build_optimizer(P, model, fused: bool = True):
+    """get_optimizer (common/utils.py:16-75) with FusedAdam for 'adam' (the online-stage config)."""
+    base_lr = getattr(P, "lr", 1e-3)
+    wd = getattr(P, "weight_decay", 0.0)
+    groups = model.get_param_groups()
+    pg = []
+    for name, attr in (("encoding", "encoding_lr"), ("sigma", "sigma_lr"), ("color", "color_lr"),
+                       ("background", "bg_lr")):
+        if name in groups:
+            lr = getattr(P, attr, None)
+            pg.append({"params": list(groups[name]["params"]), "lr": float(base_lr if lr is None else lr), "name": name})
+    opt = str(getattr(P, "optimizer", "adamw")).lower()
+    if opt == "adam" and fused:
+        return FusedAdam(pg, lr=base_lr, weight_decay=wd)
+    if opt == "adam":
+        return torch.optim.Adam(pg, lr=base_lr, weight_decay=wd)
+    if opt == "adamw":
+        return torch.optim.AdamW(pg, lr=base_lr, weight_decay=wd)
+    if opt == "sgd":
+        return torch.optim.SGD(pg, lr=base_lr, momentum=getattr(P, "momentum", 0.9), weight_decay=wd)
+    raise ValueError(f"Unknown optimizer: {opt}")
+
+
+def iter_params(model) -> Iterable[torch.nn.Parameter]:
+    return [p for p in model.parameters() if p.requires_grad]

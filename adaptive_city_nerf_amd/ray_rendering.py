@@ -9,8 +9,10 @@ materialises never exist.  With autograd (training) the call composes the differ
 per-expert forward (HIP hash grid + fast-weight MetaLinear chain) with the reference's
 compositing formulas.
 
-Extension (not in the reference): ``early_stop_tau`` (default 0 = off) stops a ray once its
+Extensions (not in the reference): ``early_stop_tau`` (default 0 = off) stops a ray once its
 transmittance drops below tau; the composite then differs from the reference by at most 2*tau.
+``jitter_u`` (N, S) supplies the uniforms of the training-mode jitter (the reference draws them
+with torch.rand_like, ray_rendering.py:286) so a training step can be reproduced exactly.
 """
 from __future__ import annotations
 
@@ -179,7 +181,11 @@ def render_rays_stratified(model, rays: Tensor, ray_samples: int, params=None, a
         if fe is not None and fb is not None:
             specs, routing, packed = fe
             bg, keep = fb
-            jitter = torch.rand(N, ray_samples, device=rays.device) if model.training else None
+            jitter = None
+            if model.training:
+                ju = kwargs.get("jitter_u")
+                jitter = ju.to(rays.device, torch.float32).contiguous() if ju is not None else \
+                    torch.rand(N, ray_samples, device=rays.device)
             rgb, depth, w, acc = ops.render_stratified(rays, ray_samples, specs, routing,
                                                        0 if len(specs) == 1 else None, bg,
                                                        sigma_scale=float(sigma_scale), tau=tau, jitter=jitter,
@@ -189,7 +195,7 @@ def render_rays_stratified(model, rays: Tensor, ray_samples: int, params=None, a
     # composed (differentiable) path -- same structure as the reference
     o, d = rays[:, :3], rays[:, 3:6]
     near, far = rays[:, 6], rays[:, 7]
-    t_vals = stratified_t_vals(near, far, ray_samples, randomized=model.training)
+    t_vals = stratified_t_vals(near, far, ray_samples, randomized=model.training, u=kwargs.get("jitter_u"))
     pts = o.unsqueeze(1) + d.unsqueeze(1) * t_vals.unsqueeze(-1)
     dirs = d.unsqueeze(1).expand_as(pts)
     id6 = torch.cat([pts, dirs], dim=-1).reshape(-1, 6)

@@ -1,0 +1,99 @@
+"""Online adaptation step (reference: pipelines/online_stage/runtime_adapt.py:213-315 ``runtime_adapt``,
+nerfs/losses.py:10-32 ``compute_mse_loss``) on the HIP path.
+
+One step = ``render_rays`` in training mode (stratified jitter) through the differentiable
+per-expert forward -> sRGB/linear colour transform -> MSE -> backward (the hash-grid gather
+backward is a HIP scatter-add kernel) -> ``clip_grad_norm_`` + Adam as one fused multi-tensor HIP
+step (optim.FusedAdam).  The reference wraps the forward in fp16 autocast with a GradScaler; this
+build computes in fp32 (SURVEY §8(b) "Autocast / dtype"), so the scaler is the identity.
+
+Expert-parallel use: with ``active_module=k`` the step touches only expert k
+(the reference adapts ``model.submodules[active_module]``, whose render has no background head),
+so rank k can adapt expert k with no collective at all.
+"""
+from __future__ import annotations
+
+from typing import Dict, Iterable, Optional
+
+import torch
+import torch.nn.functional as F
+
+from .color_space import color_space_transformer
+from .optim import FusedAdam
+from .ray_rendering import render_rays
+
+
+def compute_mse_loss(P, model, data, params=None, active_module=None, reduction: str = "mean", **render_kwargs):
+    """losses.py:10-32: MSE between render_rays(...) rgb and data['rgbs'] in P.color_space."""
+    gt_rgb = data["rgbs"]
+    rays = data["rays"]
+    pred_rgb, *_ = render_rays(model, rays, ray_samples=P.ray_samples, params=params, active_module=active_module,
+                               chunk=P.chunk_points, **render_kwargs)
+    pred_rgb, gt_rgb = color_space_transformer(pred_rgb, gt_rgb, color_space=P.color_space)
+    return F.mse_loss(pred_rgb, gt_rgb, reduction=reduction)
+
+
+def adapt_step(P, base, rays, rgbs, optimizer, active_module=None, grad_clip: Optional[float] = 1.0,
+               group=None, shared: Optional[list] = None, **render_kwargs) -> torch.Tensor:
+    """One optimizer update of runtime_adapt (runtime_adapt.py:288-313).  Returns the loss (device).
+
+    Expert parallel (``group``): rank k renders through ``active_module=k``; the gradients of the
+    ``shared`` parameters (the background head every rank renders with) are averaged over the
+    group (one small RCCL all-reduce) and the clip norm is the global one (an all-reduce of one
+    double), so the shared replicas stay bit-identical and every expert sees the clip coefficient a
+    single process adapting all of them would apply."""
+    optimizer.zero_grad()
+    loss = compute_mse_loss(P, model=base, data={"rays": rays, "rgbs": rgbs}, params=None,
+                            active_module=active_module, reduction="mean", **render_kwargs)
+    loss.backward()
+    if group is not None and torch.distributed.is_initialized() and torch.distributed.get_world_size(group) > 1:
+        grads = [p.grad for p in (shared or []) if p.grad is not None]
+        if grads:
+            flat = torch.cat([g.reshape(-1) for g in grads])
+            torch.distributed.all_reduce(flat, group=group)
+            flat.div_(torch.distributed.get_world_size(group))
+            off = 0
+            for g in grads:
+                g.copy_(flat[off: off + g.numel()].view_as(g))
+                off += g.numel()
+    if isinstance(optimizer, FusedAdam):
+        if shared:
+            optimizer.shared_params = {id(p) for p in shared}
+        optimizer.step(max_norm=grad_clip, sumsq_group=group)  # clip_grad_norm_ folded into the fused step
+    else:
+        if grad_clip is not None:
+            torch.nn.utils.clip_grad_norm_(base.parameters(), grad_clip)
+        optimizer.step()
+    return loss.detach()
+
+
+def runtime_adapt(*, P, model, data_loader: Iterable, optimizer, steps: Optional[int] = None,
+                  active_module: Optional[int] = None, grad_clip: Optional[float] = 1.0) -> Dict[str, float]:
+    """runtime_adapt.py:213-315: adapt in place; one pass over the loader (steps=None) or exactly
+    ``steps`` updates cycling over it."""
+    device = next(model.parameters()).device
+    model.train()
+    # the reference clips base.parameters(); parameters outside base get no gradient from the loss
+    # (zero_grad sets them to None), so FusedAdam's norm over gradient-carrying tensors is the same
+    base = model.submodules[active_module] if active_module is not None else model
+    last_loss, step_count = None, 0
+
+    def run(rays, rgbs):
+        nonlocal last_loss, step_count
+        rays, rgbs = rays.to(device, non_blocking=True), rgbs.to(device, non_blocking=True)
+        last_loss = adapt_step(P, base, rays, rgbs, optimizer, active_module=active_module, grad_clip=grad_clip)
+        step_count += 1
+
+    if steps is None:
+        for rays, rgbs in data_loader:
+            run(rays, rgbs)
+    else:
+        it = iter(data_loader)
+        while step_count < int(steps):
+            try:
+                rays, rgbs = next(it)
+            except StopIteration:
+                it = iter(data_loader)
+                rays, rgbs = next(it)
+            run(rays, rgbs)
+    return {"loss": 0.0 if last_loss is None else float(last_loss), "steps": step_count}

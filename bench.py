@@ -20,6 +20,10 @@ Other BASELINE configs (``--workload``):
   c4  4x2 grid -> 8 experts (synthetic layout, synthetic.grid_layout), one 800x800 frame x 256
       samples: rays generated on device, sharded by expert, rendered, all-gathered, PSNR
       all-reduced (parallel.render_image_sharded) -- strong scaling.
+  c5  online adaptation (runtime_adapt.py:288-313): 8-expert container, rank r adapts expert r
+      (active_module) on batches of 1000 rays x 96 samples: training render -> MSE -> backward ->
+      clip_grad_norm_ + Adam (one fused HIP step); shared background-head gradients and the clip
+      norm all-reduced over RCCL (weak).  metric value = trained ray-samples/s (fwd+bwd+update).
 
 Also reported: roofline of the fused render kernel (HIP events bracketing exactly that launch on
 its stream), and on rank 0 at N=1 a CPU baseline: the C oracle (oracle/, a fixture-pinned port of
@@ -48,7 +52,7 @@ FP32_MFMA_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 matrix = vector pea
 HBM_PEAK_GBS = 8000.0
 
 
-def build_model(device, n_experts=1, seed=0, table_seed=100, table_scale=0.5):
+def build_model(device, n_experts=1, seed=0, table_seed=100, table_scale=0.5, fill=None):
     from adaptive_city_nerf_amd import MetaContainer, SceneBox
     from adaptive_city_nerf_amd.synthetic import formula_table, grid_layout
     scene = json.loads((REPO / "tests" / "golden" / "scene_drz_example.json").read_text())
@@ -71,7 +75,8 @@ def build_model(device, n_experts=1, seed=0, table_seed=100, table_scale=0.5):
                                      "max_res": 4096, "min_res": 16, "interpolation": "Linear"})
     with torch.no_grad():
         for k, sub in enumerate(m.submodules):
-            sub.xyz_encoder.hash_table.copy_(torch.from_numpy(formula_table(16, 20, 2, table_seed + k, table_scale)))
+            if fill is None or k in fill:
+                sub.xyz_encoder.hash_table.copy_(torch.from_numpy(formula_table(16, 20, 2, table_seed + k, table_scale)))
     return m.to(device).eval(), gbox, scene, sc
 
 
@@ -141,7 +146,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["c2", "c3", "c4"], default="c2")
+    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c2")
     ap.add_argument("--rays", type=int, default=4096, help="rays per GPU (c2, c3)")
     ap.add_argument("--samples", type=int, default=256)
     ap.add_argument("--frame", type=int, default=800, help="frame side (c4)")
@@ -162,8 +167,8 @@ def main():
 
     from adaptive_city_nerf_amd import ops, parallel, render_rays
     S = a.samples
-    K = {"c2": 1, "c3": 4, "c4": 8}[a.workload]
-    model, gbox, scene, sc = build_model(device, K)
+    K = {"c2": 1, "c3": 4, "c4": 8, "c5": 8}[a.workload]
+    model, gbox, scene, sc = build_model(device, K, fill=[rank % K] if a.workload == "c5" else None)
 
     if a.workload == "c2":
         rays = make_rays(scene, gbox, device, a.rays, 1234 + rank)
@@ -187,6 +192,31 @@ def main():
             with torch.no_grad():
                 return parallel.render_rays_sharded(grays, render_fn, plan)
         sample_rays = grays
+    elif a.workload == "c5":
+        from types import SimpleNamespace
+        from adaptive_city_nerf_amd import optim as aoptim
+        from adaptive_city_nerf_amd.train import adapt_step
+        S = 96 if a.samples == 256 else a.samples      # configs/eval.json:15 ray_samples
+        P = SimpleNamespace(ray_samples=S, chunk_points=4000000, color_space="linear", optimizer="adam", lr=1e-4,
+                            encoding_lr=0.01, sigma_lr=0.002, color_lr=0.002, bg_lr=0.001, weight_decay=0.0)
+        nb, bsz = 32, 1000
+        pool = make_rays(scene, gbox, device, nb * bsz, 4321 + rank).view(nb, bsz, 8)
+        gtp = torch.rand(nb, bsz, 3, device=device, generator=torch.Generator(device).manual_seed(5 + rank))
+        model.train()
+        opt = aoptim.build_optimizer(P, model)
+        shared = list(model.bg_mlp.parameters())
+        pg = dist.group.WORLD if world > 1 else None
+        expert = rank % K
+        samples_per_step = world * bsz * S
+        it = [0]
+
+        def step():
+            i = it[0] % nb
+            it[0] += 1
+            return adapt_step(P, model, pool[i], gtp[i], opt, active_module=expert, grad_clip=1.0, group=pg,
+                              shared=shared)
+        sample_rays = pool[0]
+        aoptim.EVENT_HOOK = []
     else:
         H, W, intr, c2w = frame_camera(scene, a.frame, a.frame)
         samples_per_step = H * W * S
@@ -213,8 +243,14 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    kernel_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in ops.EVENT_HOOK]))
-    kernel_launches = len(ops.EVENT_HOOK) // max(a.steps, 1)
+    if a.workload == "c5":
+        from adaptive_city_nerf_amd import optim as aoptim
+        hook = aoptim.EVENT_HOOK[-a.steps:]
+        aoptim.EVENT_HOOK = None
+    else:
+        hook = ops.EVENT_HOOK
+    kernel_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in hook]))
+    kernel_launches = len(hook) // max(a.steps, 1)
     ops.EVENT_HOOK = None
     if world > 1:
         t = torch.tensor([dt, kernel_ms], device=device, dtype=torch.float64)
@@ -223,11 +259,16 @@ def main():
 
     value = samples_per_step * a.steps / dt
     ms_per_step = dt / a.steps * 1e3
+    if a.workload == "c5":
+        nparam = sum(p.numel() for p in model.submodules[expert].parameters()) + sum(p.numel() for p in shared)
+        adam_bytes = 28 * nparam            # read p, g, m, v + write p, m, v (fp32)
+        achieved_gbs = adam_bytes / (kernel_ms * 1e-3) / 1e9
     # samples one launch of the dominant kernel processes on this rank
     launch_samples = samples_per_step // world // max(kernel_launches, 1)
     achieved = FLOP_PER_SAMPLE * launch_samples / (kernel_ms * 1e-3) / 1e12
     tr = load_traffic() if a.workload == "c2" else None
-    kname = {"c2": "render_kernel<1,1,0> (fused stratified render, 1 expert)",
+    kname = {"c5": "adam_kernel (fused clip + Adam over the adapted expert + background head)",
+             "c2": "render_kernel<1,1,0> (fused stratified render, 1 expert)",
              "c3": "render_kernel<1,0,1> (fused stratified render, soft routing over 4 experts)",
              "c4": "render_kernel<1,0,1> (fused stratified render, soft routing over 8 experts)"}[a.workload]
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -237,9 +278,14 @@ def main():
                 "flop_per_sample": FLOP_PER_SAMPLE,
                 "hash_bytes_algorithmic_per_launch": int(BYTES_PER_SAMPLE * launch_samples),
                 "hash_gbs_algorithmic": round(BYTES_PER_SAMPLE * launch_samples / (kernel_ms * 1e-3) / 1e9, 1)}
+    if a.workload == "c5":
+        roofline = {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kname,
+                    "kernel_ms": round(kernel_ms, 4), "params_per_launch": int(nparam),
+                    "bytes_per_param": 28, "bytes_algorithmic_per_launch": int(adam_bytes)}
 
     cpu, psnr, rmse, maxerr = None, None, None, None
-    if rank == 0 and not a.no_cpu_baseline:
+    if rank == 0 and not a.no_cpu_baseline and a.workload != "c5":
         rgb_all = out[0].reshape(-1, 3)
         if a.workload == "c2":
             idx = torch.arange(rays.shape[0], device=device)[: a.cpu_rays]
@@ -258,7 +304,11 @@ def main():
                       "rays_per_gpu": a.rays, "experts": 4},
                "c4": {"workload": f"C4: 4x2 grid -> 8 experts (synthetic layout), {a.frame}x{a.frame} frame x "
                                   f"{S} samples, expert-sharded, RCCL all-gather + PSNR all-reduce",
-                      "frame": [a.frame, a.frame], "experts": 8}}[a.workload]
+                      "frame": [a.frame, a.frame], "experts": 8},
+               "c5": {"workload": f"C5: online adaptation, 8-expert container, rank r adapts expert r on 1000-ray x "
+                                  f"{S}-sample batches (train render + MSE + backward + fused clip/Adam), shared "
+                                  f"background grads + clip norm all-reduced", "rays_per_step_per_gpu": 1000,
+                      "experts": 8}}[a.workload]
         cfg.update({"samples_per_ray": S, "parallelism": f"ray-sharded x{world}"})
         line = {
             "metric": "ray-samples/sec + PSNR, 4096 rays×256 samples, 1/2/4/8 MI355X",

@@ -173,6 +173,45 @@ int acn_routing_fwd(const float* pts, int64_t M, int64_t ld, const acn_routing* 
 /* MetaContainer.background_color (meta_container.py:347-382): dirs (N,3) -> rgb (N,3). */
 int acn_background_fwd(const float* dirs, int64_t N, const acn_background* bg, float* out, void* stream);
 
+/* ---------------------------------------------------------------------------------------- */
+/* Optimizer step of the online adaptation loop (pipelines/online_stage/runtime_adapt.py:305-309):
+ * torch.nn.utils.clip_grad_norm_(params, max_norm) followed by torch.optim.Adam(param_groups)
+ * .step() (common/utils.py:57-62), multi-tensor.  The caller keeps, in DEVICE memory, one
+ * descriptor per parameter tensor and a chunk -> tensor map: tensor t covers chunks
+ * [first_chunk, first_chunk + ceil(numel / ACN_OPTIM_CHUNK)).                                   */
+#define ACN_OPTIM_CHUNK 65536
+#define ACN_OPTIM_MAX_GROUPS 8
+typedef struct acn_param_desc {
+    float* param;                  /* the parameter (updated in place) */
+    const float* grad;             /* its gradient, or NULL (parameter skipped, as torch does) */
+    float* exp_avg;                /* Adam state 'exp_avg'    (same numel) */
+    float* exp_avg_sq;             /* Adam state 'exp_avg_sq' (same numel) */
+    int64_t numel;
+    int32_t group;                 /* index into the acn_adam_group array */
+    int32_t first_chunk;
+} acn_param_desc;
+
+/* One torch.optim.Adam param group (host memory).  `step` is the value AFTER this step's
+ * increment (torch increments state['step'] before the update).                                */
+typedef struct acn_adam_group {
+    double lr, beta1, beta2, eps, weight_decay;
+    int32_t step, pad;
+} acn_adam_group;
+
+/* Sum of squared gradients over all described tensors: per-chunk partials (nchunks doubles,
+ * caller workspace) then *total (device double).                                               */
+int acn_grad_sumsq(const acn_param_desc* descs, const int32_t* chunk_tensor, int64_t nchunks,
+                   double* partials, double* total, void* stream);
+
+/* clip_grad_norm_ coefficient from a (possibly all-reduced) total: out[0] = total_norm (fp32),
+ * out[1] = min(1, max_norm / (total_norm + 1e-6)).  Device pointers.                            */
+int acn_clip_coef(const double* total_sumsq, float max_norm, float* out, void* stream);
+
+/* Adam update of every described tensor (torch.optim.Adam single-tensor arithmetic), gradients
+ * multiplied on the fly by grad_scale[1] (the clip coefficient) when grad_scale != NULL.        */
+int acn_adam_step(const acn_param_desc* descs, const int32_t* chunk_tensor, int64_t nchunks,
+                  const acn_adam_group* groups, int ngroups, const float* grad_scale, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -338,18 +338,85 @@ def gen_rays(scene: dict) -> None:
     save("rays", **out)
 
 
+def gen_train(scene: dict) -> None:
+    """SURVEY §8(c) fixture (7): runtime_adapt steps (runtime_adapt.py:288-313) of the K=4
+    container on 256 rays x 32 samples, with the training-mode jitter injected (the reference draws
+    it with torch.rand_like, ray_rendering.py:286): loss, clip norm, gradients (MLP tensors whole,
+    hash-table rows sampled + per-level checksums) and parameters after each Adam step."""
+    from types import SimpleNamespace
+    from common.utils import get_optimizer
+    from nerfs.losses import compute_mse_loss
+    mask = "g22_grid_bm110_ss11"
+    model, gbox = build_container(scene, mask)
+    K = len(model.submodules)
+    out = dict(weights_dict(model))
+    P = SimpleNamespace(ray_samples=32, chunk_points=1 << 20, color_space="linear", optimizer="adam", lr=1e-4,
+                        encoding_lr=0.01, sigma_lr=0.002, color_lr=0.002, bg_lr=0.001, weight_decay=0.0)
+    opt = get_optimizer(P, model)
+    rays, valid, _ = val_rays(scene, mask, 0.25)
+    rv = rays[valid]
+    g = torch.Generator().manual_seed(11)
+    rows_g = torch.Generator().manual_seed(12)
+    sample_rows = torch.randint(0, 16 << 20, (K, 4096), generator=rows_g)
+    out["train:rows"] = _np(sample_rows)
+    model.train()
+    real_rand_like = torch.rand_like
+    for step in range(2):
+        perm = torch.randperm(rv.shape[0], generator=g)[:256]
+        r = rv[perm].contiguous()
+        rgbs = torch.rand(256, 3, generator=g)
+        u = torch.rand(256, 32, generator=g)
+        torch.rand_like = lambda t, *a, **k: u.clone() if tuple(t.shape) == tuple(u.shape) else real_rand_like(t, *a, **k)
+        try:
+            opt.zero_grad()
+            loss = compute_mse_loss(P, model=model, data={"rays": r, "rgbs": rgbs}, params=None, active_module=None,
+                                    reduction="mean")
+            loss.backward()
+        finally:
+            torch.rand_like = real_rand_like
+        pre = f"train{step}:"
+        out[pre + "rays"] = _np(r); out[pre + "rgbs"] = _np(rgbs); out[pre + "u"] = _np(u)
+        out[pre + "loss"] = np.array(float(loss.detach()), np.float64)
+        for name, prm in model.named_parameters():
+            if prm.grad is None:
+                continue
+            if name.endswith("hash_table"):
+                k = int(name.split(".")[1])
+                gt = prm.grad.detach()
+                out[pre + f"grad_rows:{k}"] = _np(gt[sample_rows[k]])
+                lv = gt.view(16, -1)
+                out[pre + f"grad_level_sum:{k}"] = _np(lv.double().sum(1))
+                out[pre + f"grad_level_sumsq:{k}"] = _np((lv.double() ** 2).sum(1))
+                out[pre + f"grad_nnz:{k}"] = np.array(int((gt != 0).sum()), np.int64)
+            else:
+                out[pre + "grad:" + name] = _np(prm.grad)
+        total = torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        out[pre + "total_norm"] = np.array(float(total), np.float64)
+        opt.step()
+        for name, prm in model.named_parameters():
+            if name.endswith("hash_table"):
+                k = int(name.split(".")[1])
+                out[pre + f"table_rows:{k}"] = _np(prm.detach()[sample_rows[k]])
+            else:
+                out[pre + "param:" + name] = _np(prm)
+    out["table_seeds"] = np.array([100 + k for k in range(K)], np.int64)
+    out["table_scale"] = np.array(TABLE_SCALE, np.float64)
+    save("train_k4", **out)
+
+
 def main() -> None:
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     scene = scene_json()
     (HERE / "scene_drz_example.json").write_text(json.dumps(scene, indent=1))
     print("wrote scene_drz_example.json")
-    which = sys.argv[1:] or ["hashgrid", "sh", "volume_render", "routing", "rays", "render"]
+    which = sys.argv[1:] or ["hashgrid", "sh", "volume_render", "routing", "rays", "render", "train"]
     if "hashgrid" in which: gen_hashgrid()
     if "sh" in which: gen_sh()
     if "volume_render" in which: gen_volume_render()
     if "routing" in which: gen_routing(scene)
     if "rays" in which: gen_rays(scene)
     if "render" in which: gen_field_and_render(scene)
+    if "train" in which: gen_train(scene)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,162 @@
+"""Online adaptation step (adaptive_city_nerf_amd/train.py + optim.py) against the reference.
+
+CPU tests cover the host logic (param groups, descriptor plans).  GPU tests compare the fused
+HIP optimizer with torch.optim.Adam / clip_grad_norm_ (the reference's own optimizer, CPU fp32),
+and two full runtime_adapt steps of the K=4 container with the reference's fixture
+(tests/golden/train_k4.npz, made by tests/golden/make_golden.py from the reference itself with the
+training jitter injected): loss, clip norm, gradients and parameters after each Adam step.
+Tolerances: fp32 sums in a different order (MKL vs rocBLAS / atomics) -> relative 1e-4 on the
+loss and gradients; Adam's first steps move every parameter by ~lr * sign(g), so parameters are
+compared to 1e-3 * lr plus a 0.1% allowance of sign-ambiguous (|g| ~ 0) elements.
+"""
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+
+import goldens as G
+
+P = SimpleNamespace(ray_samples=32, chunk_points=1 << 20, color_space="linear", optimizer="adam", lr=1e-4,
+                    encoding_lr=0.01, sigma_lr=0.002, color_lr=0.002, bg_lr=0.001, weight_decay=0.0)
+
+
+def test_build_optimizer_groups_match_reference_config():
+    from test_module_api import build_model
+    from adaptive_city_nerf_amd.optim import FusedAdam, build_optimizer
+    m, _ = build_model("k4")
+    opt = build_optimizer(P, m)
+    assert isinstance(opt, FusedAdam)
+    names = [g["name"] for g in opt.param_groups]
+    assert names == ["encoding", "sigma", "color", "background"]
+    assert [g["lr"] for g in opt.param_groups] == [0.01, 0.002, 0.002, 0.001]
+    n = sum(p.numel() for g in opt.param_groups for p in g["params"])
+    assert n == sum(p.numel() for p in m.parameters())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wd", [0.0, 0.01])
+def test_fused_adam_matches_torch_adam(wd):
+    from adaptive_city_nerf_amd.optim import FusedAdam
+    g = torch.Generator().manual_seed(5)
+    shapes = [(1 << 18, 2), (64, 32), (64,), (3,), (1, 64), (70001,)]   # chunk tails and tiny tensors
+    ref = [torch.randn(s, generator=g) for s in shapes]
+    dev = [p.clone().cuda().requires_grad_(True) for p in ref]
+    ref = [p.clone().requires_grad_(True) for p in ref]
+    groups_r = [{"params": ref[:2], "lr": 0.01}, {"params": ref[2:], "lr": 0.002}]
+    groups_d = [{"params": dev[:2], "lr": 0.01}, {"params": dev[2:], "lr": 0.002}]
+    opt_r = torch.optim.Adam(groups_r, lr=1e-4, weight_decay=wd, foreach=False)
+    opt_d = FusedAdam(groups_d, lr=1e-4, weight_decay=wd)
+    for step in range(3):
+        for pr, pd in zip(ref, dev):
+            gr = torch.randn(pr.shape, generator=g) * (10.0 ** (step - 1))
+            if step == 1:
+                gr[..., :1] = 0.0
+            pr.grad = gr.clone()
+            pd.grad = gr.clone().cuda()
+        opt_r.step()
+        opt_d.step()
+        for pr, pd in zip(ref, dev):
+            # elements whose (weight-decayed) gradient cancels to ~0 are sign-ambiguous under one
+            # rounding difference: allow 1e-5 of them
+            assert _close_frac(pd.detach().cpu().numpy(), pr.detach().numpy(), 2e-7, 2e-6) >= 1 - 1e-5
+            np.testing.assert_allclose(opt_d.state[pd]["exp_avg_sq"].cpu().numpy(),
+                                       opt_r.state[pr]["exp_avg_sq"].numpy(), rtol=2e-6, atol=1e-12)
+    # state layout is torch's: the fused optimizer's state dict loads into torch.optim.Adam
+    sd = opt_d.state_dict()
+    assert set(sd["state"][0]) == {"step", "exp_avg", "exp_avg_sq"} and float(sd["state"][0]["step"]) == 3.0
+
+
+@pytest.mark.gpu
+def test_fused_clip_matches_torch_clip_grad_norm():
+    from adaptive_city_nerf_amd.optim import FusedAdam, clip_grad_norm_
+    g = torch.Generator().manual_seed(6)
+    shapes = [(100000,), (64, 64), (3,)]
+    grads = [torch.randn(s, generator=g) for s in shapes]
+    ref = [torch.zeros(s, requires_grad=True) for s in shapes]
+    for p, gr in zip(ref, grads):
+        p.grad = gr.clone()
+    tn_ref = torch.nn.utils.clip_grad_norm_(ref, 1.0)
+    dev = [torch.zeros(s, device="cuda", requires_grad=True) for s in shapes]
+    for p, gr in zip(dev, grads):
+        p.grad = gr.clone().cuda()
+    tn = clip_grad_norm_(dev, 1.0)
+    assert abs(float(tn) - float(tn_ref)) <= 1e-5 * float(tn_ref)
+    for pr, pd in zip(ref, dev):
+        np.testing.assert_allclose(pd.grad.cpu().numpy(), pr.grad.numpy(), rtol=1e-5, atol=1e-9)
+    # fused clip inside the step == clip then step
+    a = [torch.ones(s, device="cuda", requires_grad=True) for s in shapes]
+    b = [torch.ones(s, device="cuda", requires_grad=True) for s in shapes]
+    for x, y, gr in zip(a, b, grads):
+        x.grad = gr.clone().cuda()
+        y.grad = gr.clone().cuda()
+    oa, ob = FusedAdam(a, lr=0.01), FusedAdam(b, lr=0.01)
+    oa.step(max_norm=1.0)
+    clip_grad_norm_(b, 1.0)
+    ob.step()
+    for x, y in zip(a, b):
+        np.testing.assert_allclose(x.detach().cpu().numpy(), y.detach().cpu().numpy(), rtol=1e-6, atol=1e-8)
+
+
+def _close_frac(a, b, atol, rtol):
+    a = np.asarray(a, np.float64); b = np.asarray(b, np.float64)
+    return float(np.mean(np.abs(a - b) <= atol + rtol * np.abs(b)))
+
+
+@pytest.mark.gpu
+def test_adapt_steps_match_reference_fixture():
+    from test_module_api import build_model, reference_state_dict
+    from adaptive_city_nerf_amd.optim import build_optimizer
+    from adaptive_city_nerf_amd.train import adapt_step
+    d = G.load("train_k4")
+    m, _ = build_model("k4")
+    K = len(m.submodules)
+    m.load_state_dict(reference_state_dict(d, K, "w:"))
+    m = m.cuda().train()
+    opt = build_optimizer(P, m)
+    rows = d["train:rows"]
+    lrs = {"encoding": 0.01, "sigma": 0.002, "color": 0.002, "background": 0.001}
+    for step in range(2):
+        pre = f"train{step}:"
+        rays = torch.from_numpy(d[pre + "rays"]).cuda()
+        rgbs = torch.from_numpy(d[pre + "rgbs"]).cuda()
+        u = torch.from_numpy(d[pre + "u"]).cuda()
+        loss = adapt_step(P, m, rays, rgbs, opt, grad_clip=1.0, jitter_u=u)
+        torch.cuda.synchronize()
+        ref_loss = float(d[pre + "loss"])
+        assert abs(float(loss) - ref_loss) <= 1e-5 * ref_loss, (float(loss), ref_loss)
+        assert abs(float(opt.last_norm[0]) - float(d[pre + "total_norm"])) <= 1e-4 * float(d[pre + "total_norm"])
+        named = dict(m.named_parameters())
+        for name, p in named.items():
+            gkey = pre + "grad:" + name
+            if name.endswith("hash_table"):
+                k = int(name.split(".")[1])
+                if (pre + f"grad_rows:{k}") not in d:
+                    assert p.grad is None or float(p.grad.abs().max()) == 0.0
+                    continue
+                gt = p.grad.detach()
+                np.testing.assert_allclose(gt[torch.from_numpy(rows[k]).cuda()].cpu().numpy(), d[pre + f"grad_rows:{k}"],
+                                           rtol=1e-4, atol=1e-9)
+                lv = gt.view(16, -1).double()
+                np.testing.assert_allclose(lv.sum(1).cpu().numpy(), d[pre + f"grad_level_sum:{k}"], rtol=1e-4,
+                                           atol=1e-9)
+                np.testing.assert_allclose((lv ** 2).sum(1).cpu().numpy(), d[pre + f"grad_level_sumsq:{k}"],
+                                           rtol=1e-4, atol=1e-15)
+                assert int((gt != 0).sum()) == int(d[pre + f"grad_nnz:{k}"])
+            elif gkey in d:
+                ref = d[gkey]
+                scale = float(np.abs(ref).max()) + 1e-12
+                np.testing.assert_allclose(p.grad.detach().cpu().numpy(), ref, rtol=0, atol=1e-4 * scale)
+        for name, p in named.items():
+            group = "encoding" if name.endswith("hash_table") else \
+                "background" if name.startswith("bg_mlp") else \
+                "color" if ".color_mlp." in name else "sigma"
+            lr = lrs[group]
+            if name.endswith("hash_table"):
+                k = int(name.split(".")[1])
+                got = p.detach()[torch.from_numpy(rows[k]).cuda()].cpu().numpy()
+                ref = d[pre + f"table_rows:{k}"]
+            else:
+                got = p.detach().cpu().numpy()
+                ref = d[pre + "param:" + name]
+            assert _close_frac(got, ref, 1e-3 * lr, 1e-6) >= 0.999, name

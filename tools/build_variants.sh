@@ -10,6 +10,6 @@ for spec in "$@"; do
   name=${spec%%:*}; defs=${spec#*:}
   ( /opt/rocm/bin/hipcc $F $defs -c render.hip -o /tmp/render_$name.o &&
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../build_variants/libacnerf_$name.so \
-      build/capi_common.cpp.o build/encoders.hip.o build/rays.hip.o /tmp/render_$name.o && echo "built $name" ) &
+      build/capi_common.cpp.o build/encoders.hip.o build/rays.hip.o build/optim.hip.o /tmp/render_$name.o && echo "built $name" ) &
 done
 wait
