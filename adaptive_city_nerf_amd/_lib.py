@@ -85,6 +85,7 @@ SIGNATURES = {
     "acn_clamp_rays": ([vp, i64, i32, i32, f32, i32, f32, f32, f32, vp, vp], C.c_int),
     "acn_routing_fwd": ([vp, i64, i64, vp, vp, vp, vp], C.c_int),
     "acn_background_fwd": ([vp, i64, vp, vp, vp], C.c_int),
+    "acn_volume_render_bwd": ([vp, vp, vp, i64, i32, f32, vp, vp, vp, vp, vp, vp, vp], C.c_int),
     "acn_grad_sumsq": ([vp, vp, i64, vp, vp, vp], C.c_int),
     "acn_clip_coef": ([vp, f32, vp, vp], C.c_int),
     "acn_adam_step": ([vp, vp, i64, vp, i32, vp, vp], C.c_int),

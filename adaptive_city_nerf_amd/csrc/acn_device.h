@@ -146,6 +146,13 @@ __device__ __forceinline__ void hash_issue(const float2* __restrict__ tl, float 
         for (int c = 0; c < 4; ++c) p.f[2 * c + 1] = tl[(x1 ^ aa[c]) & mask];
     }
 #else
+#if ACN_DIAG_HALF_CORNERS  // diagnostic build only: 4 gathers per level (wrong values)
+    p.f[0] = ld_row<POL>(tl + ((x0 ^ a00) & mask));
+    p.f[2] = ld_row<POL>(tl + ((x0 ^ a01) & mask));
+    p.f[4] = ld_row<POL>(tl + ((x0 ^ a10) & mask));
+    p.f[6] = ld_row<POL>(tl + ((x0 ^ a11) & mask));
+    p.f[1] = p.f[0]; p.f[3] = p.f[2]; p.f[5] = p.f[4]; p.f[7] = p.f[6];
+#else
     p.f[0] = ld_row<POL>(tl + ((x0 ^ a00) & mask));
     p.f[1] = ld_row<POL>(tl + ((x1 ^ a00) & mask));
     p.f[2] = ld_row<POL>(tl + ((x0 ^ a01) & mask));
@@ -154,6 +161,7 @@ __device__ __forceinline__ void hash_issue(const float2* __restrict__ tl, float 
     p.f[5] = ld_row<POL>(tl + ((x1 ^ a10) & mask));
     p.f[6] = ld_row<POL>(tl + ((x0 ^ a11) & mask));
     p.f[7] = ld_row<POL>(tl + ((x1 ^ a11) & mask));
+#endif
 #endif
     p.wx = wx;
     p.wy = wy;
@@ -230,11 +238,16 @@ __device__ __forceinline__ void hash_issue_x(__amdgpu_buffer_rsrc_t rs, uint32_t
         sel |= (i0 & 1u) << c;
         p.q[c] = __builtin_amdgcn_raw_buffer_load_b128(rs, lvbase + ((i0 & ~1u) << 3), 0, 0);
     }
+#if ACN_DIAG_X4ONLY  // diagnostic build only: no second gather (wrong values for odd x0)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) p.r[c] = u32x2_t{0u, 0u};
+#else
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         const uint32_t i1 = (x1 ^ aa[c]) & mask;
         p.r[c] = __builtin_amdgcn_raw_buffer_load_b64(rs, (xodd || ACN_XPAIR_NOSKIP) ? lvbase + (i1 << 3) : 0xFFFFFFF0u, 0, 0);
     }
+#endif
     p.wx = wx;
     p.wy = wy;
     p.wz = wz;

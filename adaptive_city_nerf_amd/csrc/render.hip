@@ -873,6 +873,102 @@ __global__ void __launch_bounds__(256) volume_render_kernel(const float* __restr
     }
 }
 
+// Backward of volume_render (ray_rendering.py:137-165), the gradients autograd produces through
+// clamp / exp / cumprod / the three weighted sums, one wave per ray in two forward sweeps over
+// 32-sample tiles: sweep 1 rebuilds w_i = alpha_i T_i (T in double, as the forward) and the ray
+// total G = sum_k g_k w_k of g_k = dL/dw_k = G_rgb.(c_k - bg) + G_depth t_k + G_acc + G_w,k;
+// sweep 2 carries the inclusive prefix P_i of g_k w_k (double) so the suffix sum of
+//   dL/dalpha_i = g_i T_i - (1 / x_i) sum_{k>i} g_k w_k,   x_i = 1 - alpha_i + 1e-10,
+// is G - P_i.  Then alpha's clamp mask, d(1 - exp(-sigma delta))/dsigma = delta exp(-sigma delta),
+// sigma_scale and clamp_min(0)'s mask; rgb gets w_i G_rgb under clamp(0,1)'s mask; bg gets
+// (1 - acc) G_rgb.  t_vals get no gradient (stratified_t_vals runs under no_grad).
+__global__ void __launch_bounds__(256) volume_render_bwd_kernel(
+    const float* __restrict__ rs, const float* __restrict__ tv, const float* __restrict__ bgp, int64_t N, int S,
+    float sigma_scale, const float* __restrict__ g_rgb, const float* __restrict__ g_depth,
+    const float* __restrict__ g_w, const float* __restrict__ g_acc, float* __restrict__ g_rs,
+    float* __restrict__ g_bg) {
+    const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t ray = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); ray < N; ray += nw) {
+        const float* t = tv + ray * S;
+        const float gr = g_rgb ? g_rgb[3 * ray] : 0.0f, gg = g_rgb ? g_rgb[3 * ray + 1] : 0.0f,
+                    gb = g_rgb ? g_rgb[3 * ray + 2] : 0.0f;
+        const float gd = g_depth ? g_depth[ray] : 0.0f, ga = g_acc ? g_acc[ray] : 0.0f;
+        const float br = bgp ? bgp[3 * ray] : 0.0f, bgg = bgp ? bgp[3 * ray + 1] : 0.0f,
+                    bb = bgp ? bgp[3 * ray + 2] : 0.0f;
+        double G = 0.0, acc = 0.0;
+        for (int pass = 0; pass < 2; ++pass) {
+            double T = 1.0, P = 0.0;
+            for (int s0 = 0; s0 < S; s0 += 32) {
+                const int s = s0 + j;
+                const bool valid = s < S;
+                const int sc = valid ? s : S - 1;
+                const float* v = rs + (ray * S + sc) * 4;
+                const float cr = clamp_nan(v[0], 0.0f, 1.0f), cg = clamp_nan(v[1], 0.0f, 1.0f),
+                            cb = clamp_nan(v[2], 0.0f, 1.0f);
+                float sg = clamp_min_nan(v[3], 0.0f);
+                if (sigma_scale != 1.0f) sg = sg * sigma_scale;
+                float dist = (sc < S - 1) ? (t[sc + 1] - t[sc]) : (t[sc] - t[sc - 1]);
+                dist = clamp_min_nan(dist, 1e-4f);
+                const float e = expf(-sg * dist);
+                const float a = 1.0f - e;
+                const float alpha = clamp_nan(a, 0.0f, (float)(1.0 - 1e-7));
+                float x = (1.0f - alpha) + 1e-10f;
+                if (!valid) x = 1.0f;
+                double incl = (double)x;
+#pragma unroll
+                for (int off = 1; off < 32; off <<= 1) {
+                    const double y = __shfl_up(incl, off, 32);
+                    if (j >= off) incl *= y;
+                }
+                double excl = __shfl_up(incl, 1, 32);
+                if (j == 0) excl = 1.0;
+                const float Ts = (float)(T * excl);
+                const float w = valid ? alpha * Ts : 0.0f;
+                float g = gr * (cr - br) + gg * (cg - bgg) + gb * (cb - bb) + gd * t[sc] + ga;
+                if (g_w && valid) g += g_w[ray * S + s];
+                const double gw = valid ? (double)g * (double)w : 0.0;
+                if (pass == 0) {
+                    G += gw;
+                    acc += (double)w;
+                } else {
+                    double pre = gw;  // inclusive prefix of g_k w_k over the tile
+#pragma unroll
+                    for (int off = 1; off < 32; off <<= 1) {
+                        const double y = __shfl_up(pre, off, 32);
+                        if (j >= off) pre += y;
+                    }
+                    const double suffix = G - (P + pre);
+                    const float dalpha = (float)((double)g * (double)Ts - suffix / (double)x);
+                    const bool amask = (a >= 0.0f) && (a <= (float)(1.0 - 1e-7));
+                    float dsig = amask ? dalpha * dist * e : 0.0f;
+                    if (sigma_scale != 1.0f) dsig = dsig * sigma_scale;
+                    const float gsr = (v[3] >= 0.0f) ? dsig : 0.0f;
+                    if (valid && h == 0) {
+                        float* o = g_rs + (ray * S + s) * 4;
+                        o[0] = (v[0] >= 0.0f && v[0] <= 1.0f) ? w * gr : 0.0f;
+                        o[1] = (v[1] >= 0.0f && v[1] <= 1.0f) ? w * gg : 0.0f;
+                        o[2] = (v[2] >= 0.0f && v[2] <= 1.0f) ? w * gb : 0.0f;
+                        o[3] = gsr;
+                    }
+                    P += __shfl(pre, 31, 32);
+                }
+                T = T * __shfl(incl, 31, 32);
+            }
+            if (pass == 0) {
+                G = wave32_sum(G);
+                acc = wave32_sum(acc);
+            }
+        }
+        if (g_bg && lane == 0) {
+            const float om = 1.0f - (float)acc;
+            g_bg[3 * ray] = om * gr;
+            g_bg[3 * ray + 1] = om * gg;
+            g_bg[3 * ray + 2] = om * gb;
+        }
+    }
+}
+
 // MetaContainer._routing as a standalone op: W (M, K) soft weights, or hard (M) argmin
 __global__ void __launch_bounds__(256) routing_kernel(FieldCfg cfg, const float* __restrict__ pts, int64_t M, int64_t ld,
                                                       float* __restrict__ W, int32_t* __restrict__ hard) {
@@ -1058,6 +1154,21 @@ extern "C" int acn_volume_render_fwd(const float* rgb_sigma, const float* t_vals
     hipLaunchKernelGGL(volume_render_kernel, grid, block, 0, (hipStream_t)stream, rgb_sigma, t_vals, bg, N, S, raw_rgb,
                        raw_sigma, sigma_scale, rgb, depth, weights, acc);
     return acn_check_launch("acn_volume_render_fwd");
+}
+
+extern "C" int acn_volume_render_bwd(const float* rgb_sigma, const float* t_vals, const float* bg, int64_t N, int S,
+                                     float sigma_scale, const float* g_rgb, const float* g_depth,
+                                     const float* g_weights, const float* g_acc, float* g_rgb_sigma, float* g_bg,
+                                     void* stream) {
+    ACN_REQUIRE(N >= 0 && S >= 2, "acn_volume_render_bwd: need N >= 0 and S >= 2 (got S=%d)", S);
+    if (N == 0) return ACN_OK;
+    ACN_REQUIRE(rgb_sigma && t_vals && g_rgb_sigma, "acn_volume_render_bwd: NULL pointer");
+    ACN_REQUIRE(!g_bg || bg, "acn_volume_render_bwd: g_bg requested without bg");
+    const int64_t wgs = (N + 3) / 4;
+    const dim3 grid((unsigned)(wgs < 8192 ? wgs : 8192)), block(256);
+    hipLaunchKernelGGL(volume_render_bwd_kernel, grid, block, 0, (hipStream_t)stream, rgb_sigma, t_vals, bg, N, S,
+                       sigma_scale, g_rgb, g_depth, g_weights, g_acc, g_rgb_sigma, g_bg);
+    return acn_check_launch("acn_volume_render_bwd");
 }
 
 extern "C" int acn_routing_fwd(const float* pts, int64_t M, int64_t ld, const acn_routing* routing, float* weights,

@@ -252,6 +252,26 @@ def volume_render(rgb_sigma: torch.Tensor, t_vals: torch.Tensor, bg_rgb: Optiona
     return rgb, depth, w, acc
 
 
+def volume_render_bwd(rgb_sigma: torch.Tensor, t_vals: torch.Tensor, bg_rgb: Optional[torch.Tensor], sigma_scale: float,
+                      g_rgb, g_depth, g_weights, g_acc):
+    """dL/d(rgb_sigma), dL/d(bg) of volume_render (raw flags off) for the given output gradients."""
+    rs = _f32(rgb_sigma)
+    t = _f32(t_vals)
+    N, S = t.shape
+    dev = rs.device
+    bg = None if bg_rgb is None else _f32(bg_rgb.to(dev)).view(N, 3)
+    gr = None if g_rgb is None else _f32(g_rgb).view(N, 3)
+    gd = None if g_depth is None else _f32(g_depth).view(N)
+    gw = None if g_weights is None else _f32(g_weights).view(N, S)
+    ga = None if g_acc is None else _f32(g_acc).view(N)
+    g_rs = torch.empty(N, S, 4, device=dev, dtype=torch.float32)
+    g_bg = torch.empty(N, 3, device=dev, dtype=torch.float32) if bg is not None else None
+    check(_lib.lib().acn_volume_render_bwd(ptr(rs), ptr(t), ptr(bg), N, S, float(sigma_scale), ptr(gr), ptr(gd),
+                                           ptr(gw), ptr(ga), ptr(g_rs), ptr(g_bg), stream_of(rs)),
+          "acn_volume_render_bwd")
+    return g_rs, g_bg
+
+
 def get_rays_image(H: int, W: int, fx: float, fy: float, cx: float, cy: float, c2w: torch.Tensor,
                    aabb: Optional[torch.Tensor], device, center_pixels: bool = True, near: Optional[float] = None,
                    far: Optional[float] = None, near_far_override=None, apply_clamp: bool = True):

@@ -94,10 +94,32 @@ def _volume_render_autograd(rgb_sigma, t_vals, bg_rgb, raw_rgb, raw_sigma, sigma
     return rgb_map, depth_map, weights, acc_map
 
 
+class _VolumeRenderFn(torch.autograd.Function):
+    """volume_render with HIP forward (acn_volume_render_fwd) and backward (acn_volume_render_bwd):
+    two kernels instead of the ~40 elementwise/scan/reduction launches of the autograd graph."""
+
+    @staticmethod
+    def forward(ctx, rgb_sigma, t_vals, bg_rgb, sigma_scale):
+        rgb, depth, w, acc = ops.volume_render(rgb_sigma, t_vals, bg_rgb, sigma_scale=sigma_scale)
+        ctx.save_for_backward(rgb_sigma, t_vals, bg_rgb)
+        ctx.sigma_scale = sigma_scale
+        return rgb, depth, w, acc
+
+    @staticmethod
+    def backward(ctx, g_rgb, g_depth, g_w, g_acc):
+        rgb_sigma, t_vals, bg_rgb = ctx.saved_tensors
+        g_rs, g_bg = ops.volume_render_bwd(rgb_sigma, t_vals, bg_rgb, ctx.sigma_scale, g_rgb, g_depth, g_w, g_acc)
+        return (g_rs if ctx.needs_input_grad[0] else None, None,
+                g_bg if (bg_rgb is not None and ctx.needs_input_grad[2]) else None, None)
+
+
 def volume_render(rgb_sigma: Tensor, t_vals: Tensor, bg_rgb: Optional[Tensor] = None, *, raw_rgb: bool = False,
                   raw_sigma: bool = False, sigma_scale: float = 1.0, **kwargs) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
     """NeRF compositing: rgb (N,3), depth (N,), weights (N,S), acc (N,) (ray_rendering.py:114-165)."""
     if torch.is_grad_enabled() and (rgb_sigma.requires_grad or (bg_rgb is not None and bg_rgb.requires_grad)):
+        if rgb_sigma.is_cuda and not raw_rgb and not raw_sigma and rgb_sigma.dtype == torch.float32:
+            bg = None if bg_rgb is None else bg_rgb.to(rgb_sigma.device, torch.float32)
+            return _VolumeRenderFn.apply(rgb_sigma, t_vals, bg, float(sigma_scale))
         return _volume_render_autograd(rgb_sigma, t_vals, bg_rgb, raw_rgb, raw_sigma, sigma_scale)
     out = ops.volume_render(rgb_sigma, t_vals, bg_rgb, raw_rgb=raw_rgb, raw_sigma=raw_sigma, sigma_scale=sigma_scale)
     return tuple(o.to(rgb_sigma.dtype) for o in out)

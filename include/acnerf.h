@@ -123,6 +123,14 @@ int acn_volume_render_fwd(const float* rgb_sigma, const float* t_vals, const flo
                           int S, int raw_rgb, int raw_sigma, float sigma_scale, float* rgb,
                           float* depth, float* weights, float* acc, void* stream);
 
+/* Backward of volume_render (raw_rgb = raw_sigma = 0, the reference's stratified call): given the
+ * forward inputs and dL/d(rgb (N,3), depth (N), weights (N,S), acc (N)) -- any of them NULL for zero --
+ * writes dL/drgb_sigma (N,S,4) and, if g_bg != NULL, dL/dbg (N,3).  The autograd of
+ * ray_rendering.py:137-165 (clamp masks, exp, cumprod, weighted sums); t_vals get no gradient.       */
+int acn_volume_render_bwd(const float* rgb_sigma, const float* t_vals, const float* bg, int64_t N, int S,
+                          float sigma_scale, const float* g_rgb, const float* g_depth, const float* g_weights,
+                          const float* g_acc, float* g_rgb_sigma, float* g_bg, void* stream);
+
 /* Fused render_rays_stratified (ray_rendering.py:290-345 + stratified_t_vals :262-287 +
  * _get_bg_rgb :23-45 + volume_render :114-165) with the field of every expert evaluated in the
  * same kernel.  rays (N,8) [o, d, near, far]; jitter (N,S) uniforms of the training-mode draw
