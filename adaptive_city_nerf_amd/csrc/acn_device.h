@@ -168,7 +168,9 @@ __device__ __forceinline__ void hash_issue(const float2* __restrict__ tl, float 
     p.wz = wz;
 }
 
-template <int INTERP>
+// FMA: c = fma(f1, w, f0 * (1 - w)) (one rounding fewer than the reference's f0*(1-w) + f1*w; used
+// by the fused field, whose outputs are compared within tolerance)
+template <int INTERP, bool FMA = false>
 __device__ __forceinline__ void hash_finish(const HashPending& p, float& o0, float& o1) {
     if (INTERP == 0) {
         o0 = p.f[0].x;
@@ -177,24 +179,25 @@ __device__ __forceinline__ void hash_finish(const HashPending& p, float& o0, flo
     }
     const float wx = p.wx, wy = p.wy, wz = p.wz;
     const float ax = 1.0f - wx, ay = 1.0f - wy, az = 1.0f - wz;
+    auto lerp = [&](float a, float b, float w, float aw) { return FMA ? fmaf(b, w, a * aw) : a * aw + b * w; };
     // f index: bit0 = x1, bit1 = z1, bit2 = y1 (issue order above)
     {
-        const float c00 = p.f[0].x * ax + p.f[1].x * wx;
-        const float c01 = p.f[2].x * ax + p.f[3].x * wx;
-        const float c10 = p.f[4].x * ax + p.f[5].x * wx;
-        const float c11 = p.f[6].x * ax + p.f[7].x * wx;
-        const float c0 = c00 * ay + c10 * wy;
-        const float c1 = c01 * ay + c11 * wy;
-        o0 = c0 * az + c1 * wz;
+        const float c00 = lerp(p.f[0].x, p.f[1].x, wx, ax);
+        const float c01 = lerp(p.f[2].x, p.f[3].x, wx, ax);
+        const float c10 = lerp(p.f[4].x, p.f[5].x, wx, ax);
+        const float c11 = lerp(p.f[6].x, p.f[7].x, wx, ax);
+        const float c0 = lerp(c00, c10, wy, ay);
+        const float c1 = lerp(c01, c11, wy, ay);
+        o0 = lerp(c0, c1, wz, az);
     }
     {
-        const float c00 = p.f[0].y * ax + p.f[1].y * wx;
-        const float c01 = p.f[2].y * ax + p.f[3].y * wx;
-        const float c10 = p.f[4].y * ax + p.f[5].y * wx;
-        const float c11 = p.f[6].y * ax + p.f[7].y * wx;
-        const float c0 = c00 * ay + c10 * wy;
-        const float c1 = c01 * ay + c11 * wy;
-        o1 = c0 * az + c1 * wz;
+        const float c00 = lerp(p.f[0].y, p.f[1].y, wx, ax);
+        const float c01 = lerp(p.f[2].y, p.f[3].y, wx, ax);
+        const float c10 = lerp(p.f[4].y, p.f[5].y, wx, ax);
+        const float c11 = lerp(p.f[6].y, p.f[7].y, wx, ax);
+        const float c0 = lerp(c00, c10, wy, ay);
+        const float c1 = lerp(c01, c11, wy, ay);
+        o1 = lerp(c0, c1, wz, az);
     }
 }
 

@@ -51,6 +51,7 @@ struct ExpertMeta {
     const float* table;
     float amin[3];
     float ext[3];
+    float rext[3];   // 1 / ext (host)
     int32_t res[16];
 };
 

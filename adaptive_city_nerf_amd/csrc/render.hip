@@ -21,6 +21,11 @@
 
 using namespace acn;
 
+#ifndef ACN_MLP_F16X3
+#define ACN_MLP_F16X3 1  // MLP on v_mfma_f32_32x32x16_f16 with a 3-term fp16 split (hi*hi + hi*lo + lo*hi)
+#endif
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
 #ifndef ACN_LEVEL_PARITY
 #define ACN_LEVEL_PARITY 0  // 1: half h encodes levels 2i+h (instruction i = two adjacent levels)
 #endif
@@ -75,8 +80,65 @@ __device__ __forceinline__ void decode_a(int li, int NS, int& t, int& s, int& i,
     h = lane >> 5;
 }
 
+// ---- fp16x3 image (ACN_MLP_F16X3): the same layer regions [PK_W1, PK_WC3) hold, per layer, NT
+// output tiles x NK k-steps (K = 16) x {hi, lo} A fragments of v_mfma_f32_32x32x16_f16, one
+// 16-B [8 x f16] chunk per lane (lane l: row l & 31, half h = l >> 5, element e <-> k = 8h + e).
+// The B operand of a layer is its input in the accumulator layout, so element e of half h at
+// k-step s is input row xrow_acc(s, h, e) (cdna_hip_programming.md §3, "accumulator tile as the
+// next MFMA's operand"); the A image is permuted to pair with it.  hi = f16(w),
+// lo = f16(w - hi): the three products keep ~22 bits of every weight and activation.
+__device__ __forceinline__ int xrow_acc(int s, int h, int e) {
+    return 32 * (s >> 1) + 16 * (s & 1) + 8 * (e >> 2) + 4 * h + (e & 3);
+}
+// input = hash features: element e of k-step s of half h is feat[8s + e] of that half
+__device__ __forceinline__ int xcol_feat(int s, int h, int e) {
+    const int i = 8 * s + e;
+    return ACN_LEVEL_PARITY ? 4 * (i >> 1) + 2 * h + (i & 1) : 16 * h + i;
+}
+
+__device__ float xweight(const PackSrc& p, int layer, int row, int s, int h, int e) {
+    switch (layer) {
+        case 0: return p.sig_w0[row * 32 + xcol_feat(s, h, e)];                 // sigma_trunk.0 (64, 32)
+        case 1: return p.sig_w1[row * 64 + xrow_acc(s, h, e)];                  // sigma_trunk.1 (64, 64)
+        case 2: {                                                               // [sigma_head; geo; 0] x 64
+            const int k = xrow_acc(s, h, e);
+            if (row == 0) return p.sigh_w[k];
+            if (row <= kGeo) return p.geo_w[(row - 1) * 64 + k];
+            return 0.0f;
+        }
+        case 3: {                                                               // color_mlp.0 on head rows
+            const int r = xrow_acc(s, h, e);                                    // 0 sraw, 1..15 geo, 16..31 sh
+            return r == 0 ? 0.0f : p.col_w0[row * 31 + (r - 1)];
+        }
+        default: return p.col_w1[row * 64 + xrow_acc(s, h, e)];                 // color_mlp.1 (64, 64)
+    }
+}
+
+__device__ float pack_value_x3(const PackSrc& p, int idx) {
+    int base, NK, layer;
+    if (idx < PK_W2) { base = PK_W1; NK = 2; layer = 0; }
+    else if (idx < PK_WH) { base = PK_W2; NK = 4; layer = 1; }
+    else if (idx < PK_WC1) { base = PK_WH; NK = 4; layer = 2; }
+    else if (idx < PK_WC2) { base = PK_WC1; NK = 2; layer = 3; }
+    else { base = PK_WC2; NK = 4; layer = 4; }
+    const int li = idx - base;
+    const int q = li & 3, lane = (li >> 2) & 63, frag = li >> 8;
+    const int part = frag & 1, ts = frag >> 1, s = ts % NK, T = ts / NK;
+    const int row = 32 * T + (lane & 31), h = lane >> 5;
+    uint32_t bits = 0;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const float w = xweight(p, layer, row, s, h, 2 * q + u);
+        const _Float16 hi = (_Float16)w;
+        const _Float16 v = part ? (_Float16)(w - (float)hi) : hi;
+        bits |= (uint32_t)__builtin_bit_cast(uint16_t, v) << (16 * u);
+    }
+    return __uint_as_float(bits);
+}
+
 __device__ float pack_value(const PackSrc& p, int idx) {
     int t, s, i, h;
+    if (ACN_MLP_F16X3 && idx < PK_WC3) return pack_value_x3(p, idx);
     if (idx < PK_W2) {  // sigma_trunk.0 (64, 32): k = 16h + s
         decode_a(idx - PK_W1, 16, t, s, i, h);
         const int col = ACN_LEVEL_PARITY ? 4 * (s >> 1) + 2 * h + (s & 1) : 16 * h + s;
@@ -157,6 +219,56 @@ __device__ __forceinline__ f32x16 bias_frag_at(const float* cb, int tile, int h)
     return v;
 }
 
+// ---- fp16x3 MLP building blocks
+__device__ __forceinline__ f32x16 mfma16(const f16x8& a, const f16x8& b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f16x8 ldh8(const float* p) { return *reinterpret_cast<const f16x8*>(p); }
+
+// split 8 fp32 values into hi = f16(x), lo = f16(x - hi)
+__device__ __forceinline__ void split8(const float* x, f16x8& hi, f16x8& lo) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const _Float16 a = (_Float16)x[e];
+        hi[e] = a;
+        lo[e] = (_Float16)(x[e] - (float)a);
+    }
+}
+// B fragments of a 64-row input held as two accumulator tiles: k-step s = 2 * tile + half-tile
+__device__ __forceinline__ void split_acc2(const f32x16& a0, const f32x16& a1, f16x8 (&bh)[4], f16x8 (&bl)[4]) {
+    float x[8];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const f32x16& a = (s >> 1) ? a1 : a0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = a[8 * (s & 1) + e];
+        split8(x, bh[s], bl[s]);
+    }
+}
+
+// out[T] = bias + W . X over NK k-steps of 16, three fp16 products per k-step (small terms first)
+template <int NT, int NK>
+__device__ __forceinline__ void layer_x3(const float* W, int seg, const float* bias_base, int bt, int lane, int h,
+                                         const f16x8 (&bh)[NK], const f16x8 (&bl)[NK], f32x16 (&out)[NT],
+                                         int nk_used = NK) {
+#pragma unroll
+    for (int T = 0; T < NT; ++T) out[T] = bias_frag_at(bias_base, bt + T, h);
+#pragma unroll
+    for (int s = 0; s < NK; ++s) {
+        if (s >= nk_used) break;
+#pragma unroll
+        for (int T = 0; T < NT; ++T) {
+            const float* fp = W + seg + (((T * NK + s) * 2) * 64 + lane) * 4;
+            const f16x8 ahi = ldh8(fp), alo = ldh8(fp + 256);
+            out[T] = mfma16(alo, bh[s], out[T]);
+            out[T] = mfma16(ahi, bl[s], out[T]);
+            out[T] = mfma16(ahi, bh[s], out[T]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+
 // Per-ray fold of colour layer 0's SH columns (meta_ngp.py:171-190: the direction, hence its SH
 // encoding, is constant along a ray): cb[tile][h][r] = b_c0[row] + sum_m W_c0[row][15+m] sh[m]
 // for row = rho(r, h) + 32 tile, computed once per ray with the 8 SH k-steps of the packed
@@ -165,6 +277,17 @@ __device__ __forceinline__ f32x16 bias_frag_at(const float* cb, int tile, int h)
 __device__ __forceinline__ void fold_sh_bias(const float* W, const float (&shv)[8], int lane, float* cb) {
     const int h = lane >> 5;
     f32x16 q0 = bias_frag(W, BT_C1, h), q1 = bias_frag(W, BT_C1 + 1, h);
+#if ACN_MLP_F16X3
+    {   // k-step 1 of the colour-layer-0 image = head rows 16..31 = this half's SH values (shv)
+        f16x8 sh_hi, sh_lo;
+        split8(shv, sh_hi, sh_lo);
+        const float* f0 = W + PK_WC1 + (((0 * 2 + 1) * 2) * 64 + lane) * 4;
+        const float* f1 = W + PK_WC1 + (((1 * 2 + 1) * 2) * 64 + lane) * 4;
+        const f16x8 h0 = ldh8(f0), l0 = ldh8(f0 + 256), h1 = ldh8(f1), l1 = ldh8(f1 + 256);
+        q0 = mfma16(l0, sh_hi, q0); q0 = mfma16(h0, sh_lo, q0); q0 = mfma16(h0, sh_hi, q0);
+        q1 = mfma16(l1, sh_hi, q1); q1 = mfma16(h1, sh_lo, q1); q1 = mfma16(h1, sh_hi, q1);
+    }
+#else
 #pragma unroll
     for (int g = 2; g < 4; ++g) {
         const f32x4 w0 = ld4(W + PK_WC1 + ((0 * 4 + g) * 64 + lane) * 4);
@@ -175,6 +298,7 @@ __device__ __forceinline__ void fold_sh_bias(const float* W, const float (&shv)[
             q1 = mfma32(w1[q], shv[4 * (g - 2) + q], q1);
         }
     }
+#endif
     if ((lane & 31) == 0) {
         f32x4* d0 = reinterpret_cast<f32x4*>(cb + (0 * 2 + h) * 16);
         f32x4* d1 = reinterpret_cast<f32x4*>(cb + (1 * 2 + h) * 16);
@@ -189,9 +313,15 @@ __device__ __forceinline__ void fold_sh_bias(const float* W, const float (&shv)[
     }
 }
 
+#ifndef ACN_FAST_VALU
+#define ACN_FAST_VALU 0  // 1: one-instruction ReLU (v_max_f32), FMA lerps, reciprocal world->unit
+#endif
 __device__ __forceinline__ void relu16(f32x16& v) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) v[i] = v[i] < 0.0f ? 0.0f : v[i];  // NaN propagates like torch.relu
+    for (int i = 0; i < 16; ++i)
+        // ACN_FAST_VALU: v_max_f32 (NaN -> 0 inside the fused MLP; a NaN sample still renders NaN
+        // because its t / dist are NaN); else compare + select, NaN-propagating like torch.relu
+        v[i] = ACN_FAST_VALU ? fmaxf(v[i], 0.0f) : (v[i] < 0.0f ? 0.0f : v[i]);
 }
 
 // 64 -> 64 layer: out tiles (o0, o1) = bias + W . [in0; in1].  A fragments are double
@@ -279,7 +409,7 @@ __device__ __forceinline__ void hash_levels8(const ExpertMeta& em, int log2T, in
     for (int l = 0; l < 8; ++l) {
         if (l + D - 1 < 8) issue(l + D - 1, pend[(l + D - 1) % D]);
         __builtin_amdgcn_sched_barrier(0);
-        hash_finish<INTERP>(pend[l % D], feat[2 * l], feat[2 * l + 1]);
+        hash_finish<INTERP, ACN_FAST_VALU != 0>(pend[l % D], feat[2 * l], feat[2 * l + 1]);
         __builtin_amdgcn_sched_barrier(0);
     }
 }
@@ -296,9 +426,15 @@ __device__ __forceinline__ void field_tile(const float* W, const ExpertMeta& em,
     const int h = opaque_v(lane >> 5);
     // _world_to_unit (meta_ngp.py:155-158)
     const float eps = 1e-6f, hi = 1.0f - 1e-6f;
+#if ACN_FAST_VALU  // multiply by the host-computed reciprocal extent (<= 1 ulp from the division)
+    const float x0 = clamp_nan((px - em.amin[0]) * em.rext[0], eps, hi);
+    const float x1 = clamp_nan((py - em.amin[1]) * em.rext[1], eps, hi);
+    const float x2 = clamp_nan((pz - em.amin[2]) * em.rext[2], eps, hi);
+#else
     const float x0 = clamp_nan((px - em.amin[0]) / em.ext[0], eps, hi);
     const float x1 = clamp_nan((py - em.amin[1]) / em.ext[1], eps, hi);
     const float x2 = clamp_nan((pz - em.amin[2]) / em.ext[2], eps, hi);
+#endif
     float feat[16];
 #if ACN_DIAG_NOHASH  // diagnostic build only: no gathers
 #pragma unroll
@@ -321,6 +457,59 @@ __device__ __forceinline__ void field_tile(const float* W, const ExpertMeta& em,
         return;
     }
 #endif
+#if ACN_MLP_F16X3
+    f32x16 d0, d1;
+    {
+        // sigma_trunk.0: 32 -> 64 (ReLU)
+        f16x8 fh[2], fl[2];
+        split8(feat, fh[0], fl[0]);
+        split8(feat + 8, fh[1], fl[1]);
+        f32x16 a[2];
+        layer_x3<2, 2>(W, PK_W1, W + PK_B, BT_L1, lane, h, fh, fl, a);
+        relu16(a[0]);
+        relu16(a[1]);
+        // sigma_trunk.1: 64 -> 64 (ReLU)
+        f16x8 bh[4], bl[4];
+        split_acc2(a[0], a[1], bh, bl);
+        f32x16 b[2];
+        layer_x3<2, 4>(W, PK_W2, W + PK_B, BT_L2, lane, h, bh, bl, b);
+        relu16(b[0]);
+        relu16(b[1]);
+        // heads: rows 0 sigma_head, 1..15 geo_head (16..31 carry SH when not folded)
+        split_acc2(b[0], b[1], bh, bl);
+        f32x16 hd[1];
+        layer_x3<1, 4>(W, PK_WH, W + PK_B, BT_H, lane, h, bh, bl, hd);
+        if (!FOLD) {
+#pragma unroll
+            for (int r = 8; r < 16; ++r) hd[0][r] = shv[r - 8];
+        }
+        sraw = __shfl(hd[0][0], lane & 31);
+        // color_mlp.0: [geo(15), sh(16)] -> 64 (ReLU); FOLD: bias from cb, only k-step 0 (rows 0..15)
+        f16x8 ch[2], cl[2];
+        {
+            float x[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) x[e] = hd[0][e];
+            split8(x, ch[0], cl[0]);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) x[e] = hd[0][8 + e];
+            split8(x, ch[1], cl[1]);
+        }
+        f32x16 c[2];
+        if (FOLD) layer_x3<2, 2>(W, PK_WC1, cb, 0, lane, h, ch, cl, c, 1);   // per-ray folded bias
+        else layer_x3<2, 2>(W, PK_WC1, W + PK_B, BT_C1, lane, h, ch, cl, c);
+        relu16(c[0]);
+        relu16(c[1]);
+        // color_mlp.1: 64 -> 64 (ReLU)
+        split_acc2(c[0], c[1], bh, bl);
+        f32x16 dd[2];
+        layer_x3<2, 4>(W, PK_WC2, W + PK_B, BT_C2, lane, h, bh, bl, dd);
+        d0 = dd[0];
+        d1 = dd[1];
+        relu16(d0);
+        relu16(d1);
+    }
+#else
     // sigma_trunk.0: 32 -> 64 (ReLU)
     f32x16 a0 = bias_frag(W, BT_L1, h), a1 = bias_frag(W, BT_L1 + 1, h);
     {
@@ -404,6 +593,7 @@ __device__ __forceinline__ void field_tile(const float* W, const ExpertMeta& em,
     layer64x64(W, PK_WC2, BT_C2, lane, h, c0, c1, d0, d1);
     relu16(d0);
     relu16(d1);
+#endif
     // color_mlp.2: 64 -> 3 on the VALU (a 3-row MFMA tile would waste 29/32 of the pipe):
     // each half dots its 32 features, the halves are summed with a cross-half swap.
     const float* w3 = W + PK_WC3 + h * 96;
@@ -1044,7 +1234,11 @@ int prepare(const acn_expert* experts, const acn_routing* routing, int active_mo
             return acn_set_error(ACN_ERR_UNSUPPORTED, "experts must share interpolation and log2_hashmap_size");
         ExpertMeta& m = cfg.ex[i];
         m.table = e.table;
-        for (int a = 0; a < 3; ++a) { m.amin[a] = e.aabb_min[a]; m.ext[a] = e.aabb_extent[a]; }
+        for (int a = 0; a < 3; ++a) {
+            m.amin[a] = e.aabb_min[a];
+            m.ext[a] = e.aabb_extent[a];
+            m.rext[a] = 1.0f / e.aabb_extent[a];
+        }
         for (int l = 0; l < 16; ++l) m.res[l] = e.res[l];
         pa.e[i] = PackSrc{e.sig_w0, e.sig_b0, e.sig_w1, e.sig_b1, e.sigh_w, e.sigh_b, e.geo_w, e.geo_b,
                           e.col_w0, e.col_b0, e.col_w1, e.col_b1, e.col_w2, e.col_b2};

@@ -22,7 +22,7 @@ for i, l in enumerate(body):
 def n_mfma(a, b):
     return sum(1 for l in body[a:b + 1] if l.strip().startswith("v_mfma"))
 # innermost loop that still holds the MLP (the tile loop): smallest loop with >= 100 MFMAs
-n, a, b = min((x for x in loops if n_mfma(x[1], x[2]) >= 100), default=max(loops))
+n, a, b = min((x for x in loops if n_mfma(x[1], x[2]) >= 60), default=max(loops))
 c = collections.Counter()
 for l in body[a:b + 1]:
     s = l.strip()
