@@ -131,6 +131,34 @@ def cpu_baseline(model, sc, rays, S, gpu_rgb, min_seconds):
         float(np.max(np.abs(gpu_rgb - orgb)))
 
 
+def cpu_baseline_train(model, sc, rays, rgbs, S, expert, min_seconds):
+    """C5 CPU baseline: the CPU restatement of one runtime_adapt update (oracle/train_ref.py, pinned
+    by the reference's training fixture) on the host cores, same batch shape, repeated >= min_seconds."""
+    from oracle import oracle as O
+    from oracle import train_ref as TR
+    state = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    K = len(model.submodules)
+    m = TR.RefContainer(state, K, np.array(model.submodules[0].xyz_encoder._res_host), 20, sc["centroids"],
+                        model.boundary_margin, sc["mins"], [s.aabb_extent.cpu().numpy() for s in model.submodules])
+    lrs = {"encoding": 0.01, "sigma": 0.002, "color": 0.002, "background": 0.001}
+    opt = torch.optim.Adam(m.param_groups(lrs), lr=1e-4)
+    threads = O.max_threads()
+    torch.set_num_threads(threads)
+    r, g = rays.cpu(), rgbs.cpu()
+    u = torch.rand(r.shape[0], S, generator=torch.Generator().manual_seed(3))
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        TR.adapt_step(m, opt, r, g, S, u, active_module=expert)
+        reps += 1
+        if time.perf_counter() - t0 >= min_seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": r.shape[0] * S * reps / dt, "unit": "ray-samples/s", "cores": threads, "kind": "port",
+            "sample": f"{reps} runtime_adapt updates of {r.shape[0]} rays x {S} samples through expert {expert} "
+                      f"(oracle/train_ref.py: PyTorch CPU restatement, fixture-pinned; {threads} threads), "
+                      f"{dt:.1f} s"}
+
+
 def load_traffic():
     p = REPO / "profiles" / "pmc_render_r01.json"
     if p.exists():
@@ -285,6 +313,8 @@ def main():
                     "bytes_per_param": 28, "bytes_algorithmic_per_launch": int(adam_bytes)}
 
     cpu, psnr, rmse, maxerr = None, None, None, None
+    if rank == 0 and not a.no_cpu_baseline and a.workload == "c5":
+        cpu = cpu_baseline_train(model, sc, pool[0], gtp[0], S, expert, a.cpu_seconds)
     if rank == 0 and not a.no_cpu_baseline and a.workload != "c5":
         rgb_all = out[0].reshape(-1, 3)
         if a.workload == "c2":
