@@ -26,6 +26,10 @@ using namespace acn;
 #endif
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
+#ifndef ACN_SLOTS
+#define ACN_SLOTS 1  // routed K > 2: stage the two most needed experts per workgroup (render_slots_kernel)
+#endif
+
 #ifndef ACN_LEVEL_PARITY
 #define ACN_LEVEL_PARITY 0  // 1: half h encodes levels 2i+h (instruction i = two adjacent levels)
 #endif
@@ -913,6 +917,108 @@ __device__ __forceinline__ float tlin_sel(float near, float far, int i, int S, f
     return near * (1.0f - u) + far * u;
 }
 
+// One ray, front to back in 32-sample tiles: t-values -> field(px, py, pz, shv, folded, y...) ->
+// volume_render conditioning -> compositing -> background -> outputs.  `field` evaluates the
+// (routed) container for this lane's sample; it is a template callable so the single-expert, the
+// LDS-resident and the slot-staged kernels share this body.
+template <class FieldFn>
+__device__ __forceinline__ void render_ray(const RenderParams& p, const BgArgs& bg, int64_t ray, int lane, float step,
+                                           FieldFn&& field) {
+    const int j = lane & 31, h = lane >> 5;
+    const int S = p.S;
+#if ACN_DIAG_CLOCK || ACN_DIAG_PHASE
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#endif
+#if ACN_DIAG_CLOCK  // diagnostic build only: depth[ray] <- in-kernel shader clock (MHz) over the ray
+    const uint64_t diag_t0 = __builtin_amdgcn_s_memtime(), diag_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    const float* rp = p.rays + ray * 8;
+    const float ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
+    const float near = rp[6], far = rp[7];
+    const float* jit = p.jitter ? p.jitter + ray * S : nullptr;
+    float sh[16], shv[8];
+    dir_sh(dx, dy, dz, sh);
+    sh_rows_for_half(sh, h, shv);
+    uint32_t folded = 0u;
+#if ACN_DIAG_PHASE
+    uint32_t dg_hash = 0u, dg_mlp = 0u, dg_comp = 0u, dg_n = 0u;
+#endif
+    RayAcc acc{1.0, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    int s0 = 0;
+    for (; s0 < S; s0 += 32) {
+        const int s = s0 + j;
+        const bool valid = s < S;
+        const int sc = valid ? s : S - 1;
+        float t, dist;
+        if (!jit) {  // eval: dist = t[i+1] - t[i], the last one repeated (ray_rendering.py:144-145)
+            const int i0 = sc < S - 1 ? sc : S - 2;
+            const float ta = tlin_sel(near, far, i0, S, step), tb = tlin_sel(near, far, i0 + 1, S, step);
+            t = sc < S - 1 ? ta : tb;
+            dist = tb - ta;
+        } else {
+            t = tval(near, far, sc, S, jit);
+            const float tn = (sc < S - 1) ? tval(near, far, sc + 1, S, jit) : t;
+            const float tp = (sc == S - 1 && S > 1) ? tval(near, far, sc - 1, S, jit) : t;
+            dist = (sc < S - 1) ? (tn - t) : (t - tp);
+        }
+        const float px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;
+        float yr, yg, yb, ys;
+#if ACN_DIAG_PHASE
+        const uint64_t dA = __builtin_amdgcn_s_memtime();
+#endif
+        field(px, py, pz, shv, folded, yr, yg, yb, ys);
+#if ACN_DIAG_PHASE
+        const uint64_t dB = __builtin_amdgcn_s_memtime();
+        const uint32_t dS = __builtin_amdgcn_readfirstlane((uint32_t)g_diag_stamp[wave]);
+        dg_hash += dS - (uint32_t)dA;
+        dg_mlp += (uint32_t)dB - dS;
+        dg_n += 1u;
+#endif
+        // volume_render input conditioning (:140-143)
+        yr = clamp_nan(yr, 0.0f, 1.0f);
+        yg = clamp_nan(yg, 0.0f, 1.0f);
+        yb = clamp_nan(yb, 0.0f, 1.0f);
+        float sig = clamp_min_nan(ys, 0.0f);
+        if (p.sigma_scale != 1.0f) sig = sig * p.sigma_scale;
+        float wv;
+        composite_tile(acc, valid, yr, yg, yb, sig, t, dist, j, &wv);
+        if (p.weights && valid && h == 0) p.weights[ray * S + s] = wv;
+#if ACN_DIAG_PHASE
+        dg_comp += (uint32_t)__builtin_amdgcn_s_memtime() - (uint32_t)dB;
+#endif
+        const int stop = __builtin_amdgcn_readfirstlane((int)(acc.T < (double)p.tau));
+        if (stop) { s0 += 32; break; }
+    }
+    if (p.weights && h == 0)  // samples skipped by early termination carry zero weight
+        for (int s = s0 + j; s < S; s += 32) p.weights[ray * S + s] = 0.0f;
+    float bgc[3];
+    background(bg, dx, dy, dz, lane, bgc);
+    float r, g, b, dd, a;
+    finish_ray(acc, r, g, b, dd, a);
+    if (lane == 0) {
+        if (bg.mode != ACN_BG_NONE) {
+            const float om = 1.0f - a;
+            r = r + om * bgc[0];
+            g = g + om * bgc[1];
+            b = b + om * bgc[2];
+        }
+        p.rgb[ray * 3 + 0] = r;
+        p.rgb[ray * 3 + 1] = g;
+        p.rgb[ray * 3 + 2] = b;
+        p.depth[ray] = dd;
+        p.acc[ray] = a;
+#if ACN_DIAG_CLOCK
+        p.depth[ray] = (float)(__builtin_amdgcn_s_memtime() - diag_t0) * 100.0f /
+                       (float)(__builtin_amdgcn_s_memrealtime() - diag_r0);
+#endif
+#if ACN_DIAG_PHASE  // cycles per tile: depth <- hash phase, acc <- MLP phase, rgb.r <- compositing
+        p.depth[ray] = (float)dg_hash / (float)dg_n;
+        p.acc[ray] = (float)dg_mlp / (float)dg_n;
+        p.rgb[ray * 3] = (float)dg_comp / (float)dg_n;
+#endif
+    }
+}
+
 template <int INTERP, int KL, int ROUTE>
 __global__ void __launch_bounds__(1024, 4) render_kernel(FieldCfg cfg, BgArgs bg, RenderParams p) {
     constexpr bool FOLD = ACN_SHFOLD != 0;
@@ -924,100 +1030,146 @@ __global__ void __launch_bounds__(1024, 4) render_kernel(FieldCfg cfg, BgArgs bg
         stage_weights<KL>(smem, p.packed);
         W = smem;
     }
-    const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+    const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // provably uniform: ray data in SGPRs
     float* cb = FOLD ? cbuf + wave * KF * 64 : nullptr;
     const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
-    const int S = p.S;
-    const float step = 1.0f / (float)(S - 1);
-#if ACN_DIAG_CLOCK  // diagnostic build only: depth[ray] <- in-kernel shader clock (MHz) over the ray
-    const uint64_t diag_t0 = __builtin_amdgcn_s_memtime(), diag_r0 = __builtin_amdgcn_s_memrealtime();
-#endif
+    const float step = 1.0f / (float)(p.S - 1);
     for (int64_t ray = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave; ray < p.N; ray += nw) {
+        render_ray(p, bg, ray, lane, step,
+                   [&](float px, float py, float pz, const float (&shv)[8], uint32_t& folded, float& yr, float& yg,
+                       float& yb, float& ys) {
+                       container_tile<INTERP, ROUTE, FOLD>(cfg, W, px, py, pz, shv, cb, &folded, lane, yr, yg, yb, ys);
+                   });
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Routed render with more than two experts (C3 / C4).  LDS holds two expert SLOTS; per round of
+// 16 rays (one per wave) the workgroup routes every sample of its rays, counts how many waves
+// need each expert, and stages the two most needed ones into the slots (only when they change --
+// with rays sorted by owning expert, parallel.expert_sorted_plan, a workgroup's rays mostly need
+// the same one or two experts, so staging is rare).  A sample whose expert is not resident is
+// evaluated from the packed image in global memory (L2), without the SH fold.
+__device__ __forceinline__ uint32_t ray_expert_mask(const FieldCfg& cfg, int route, const RenderParams& p, int64_t ray,
+                                                    float step, int lane) {
+    uint32_t m = 0u;
+    if (ray < p.N) {
         const float* rp = p.rays + ray * 8;
         const float ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
         const float near = rp[6], far = rp[7];
-        const float* jit = p.jitter ? p.jitter + ray * S : nullptr;
-        float sh[16], shv[8];
-        dir_sh(dx, dy, dz, sh);
-        sh_rows_for_half(sh, h, shv);
-        uint32_t folded = 0u;
-#if ACN_DIAG_PHASE
-        uint32_t dg_hash = 0u, dg_mlp = 0u, dg_comp = 0u, dg_n = 0u;
-#endif
-        RayAcc acc{1.0, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-        int s0 = 0;
-        for (; s0 < S; s0 += 32) {
-            const int s = s0 + j;
-            const bool valid = s < S;
-            const int sc = valid ? s : S - 1;
-            float t, dist;
-            if (!jit) {  // eval: dist = t[i+1] - t[i], the last one repeated (ray_rendering.py:144-145)
-                const int i0 = sc < S - 1 ? sc : S - 2;
-                const float ta = tlin_sel(near, far, i0, S, step), tb = tlin_sel(near, far, i0 + 1, S, step);
-                t = sc < S - 1 ? ta : tb;
-                dist = tb - ta;
-            } else {
-                t = tval(near, far, sc, S, jit);
-                const float tn = (sc < S - 1) ? tval(near, far, sc + 1, S, jit) : t;
-                const float tp = (sc == S - 1 && S > 1) ? tval(near, far, sc - 1, S, jit) : t;
-                dist = (sc < S - 1) ? (tn - t) : (t - tp);
-            }
+        const float* jit = p.jitter ? p.jitter + ray * p.S : nullptr;
+        for (int s = lane; s < p.S; s += 64) {
+            const float t = jit ? tval(near, far, s, p.S, jit) : tlin_sel(near, far, s, p.S, step);
             const float px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;
-            float yr, yg, yb, ys;
-#if ACN_DIAG_PHASE
-            const uint64_t dA = __builtin_amdgcn_s_memtime();
-#endif
-            container_tile<INTERP, ROUTE, FOLD>(cfg, W, px, py, pz, shv, cb, &folded, lane, yr, yg, yb, ys);
-#if ACN_DIAG_PHASE
-            const uint64_t dB = __builtin_amdgcn_s_memtime();
-            const uint32_t dS = __builtin_amdgcn_readfirstlane((uint32_t)g_diag_stamp[wave]);
-            dg_hash += dS - (uint32_t)dA;
-            dg_mlp += (uint32_t)dB - dS;
-            dg_n += 1u;
-#endif
-            // volume_render input conditioning (:140-143)
-            yr = clamp_nan(yr, 0.0f, 1.0f);
-            yg = clamp_nan(yg, 0.0f, 1.0f);
-            yb = clamp_nan(yb, 0.0f, 1.0f);
-            float sig = clamp_min_nan(ys, 0.0f);
-            if (p.sigma_scale != 1.0f) sig = sig * p.sigma_scale;
-            float wv;
-            composite_tile(acc, valid, yr, yg, yb, sig, t, dist, j, &wv);
-            if (p.weights && valid && h == 0) p.weights[ray * S + s] = wv;
-#if ACN_DIAG_PHASE
-            dg_comp += (uint32_t)__builtin_amdgcn_s_memtime() - (uint32_t)dB;
-#endif
-            const int stop = __builtin_amdgcn_readfirstlane((int)(acc.T < (double)p.tau));
-            if (stop) { s0 += 32; break; }
-        }
-        if (p.weights && h == 0)  // samples skipped by early termination carry zero weight
-            for (int s = s0 + j; s < S; s += 32) p.weights[ray * S + s] = 0.0f;
-        float bgc[3];
-        background(bg, dx, dy, dz, lane, bgc);
-        float r, g, b, dd, a;
-        finish_ray(acc, r, g, b, dd, a);
-        if (lane == 0) {
-            if (bg.mode != ACN_BG_NONE) {
-                const float om = 1.0f - a;
-                r = r + om * bgc[0];
-                g = g + om * bgc[1];
-                b = b + om * bgc[2];
+            if (route == 1) {
+                const RouteState st = route_prep<1>(cfg, px, py, pz);
+                for (int k = 0; k < cfg.K; ++k)
+                    if (route_weight(cfg, st, k, px, py, pz) > 0.0f) m |= 1u << k;
+            } else {
+                m |= 1u << route_prep<2>(cfg, px, py, pz).hard;
             }
-            p.rgb[ray * 3 + 0] = r;
-            p.rgb[ray * 3 + 1] = g;
-            p.rgb[ray * 3 + 2] = b;
-            p.depth[ray] = dd;
-            p.acc[ray] = a;
-#if ACN_DIAG_CLOCK
-            p.depth[ray] = (float)(__builtin_amdgcn_s_memtime() - diag_t0) * 100.0f /
-                           (float)(__builtin_amdgcn_s_memrealtime() - diag_r0);
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) m |= __shfl_xor(m, off);
+    return m;
+}
+
+#ifndef ACN_SLOTS_THREADS
+#define ACN_SLOTS_THREADS 512  // 2 waves/SIMD, 256 VGPRs: the 1024-thread build spills and was measured wrong
 #endif
-#if ACN_DIAG_PHASE  // cycles per tile: depth <- hash phase, acc <- MLP phase, rgb.r <- compositing
-            p.depth[ray] = (float)dg_hash / (float)dg_n;
-            p.acc[ray] = (float)dg_mlp / (float)dg_n;
-            p.rgb[ray * 3] = (float)dg_comp / (float)dg_n;
+template <int INTERP, int ROUTE>
+__global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) render_slots_kernel(FieldCfg cfg, BgArgs bg, RenderParams p) {
+    constexpr bool FOLD = ACN_SHFOLD != 0;
+    __shared__ __attribute__((aligned(16))) float smem[2 * PK_FLOATS];
+    __shared__ __attribute__((aligned(16))) float cbuf[FOLD ? 16 * 2 * 64 : 4];
+    __shared__ int cnt[kMaxK];
+    __shared__ int slot_k[2], restage[2];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float* cb = FOLD ? cbuf + wave * 2 * 64 : nullptr;
+    const float step = 1.0f / (float)(p.S - 1);
+    if (threadIdx.x < kMaxK) cnt[threadIdx.x] = 0;
+    if (threadIdx.x < 2) slot_k[threadIdx.x] = -1;
+    __syncthreads();
+    const int64_t waves_per_wg = blockDim.x >> 6;
+    for (int64_t base = (int64_t)blockIdx.x * waves_per_wg; base < p.N; base += (int64_t)gridDim.x * waves_per_wg) {
+        const int64_t ray = base + wave;
+        const uint32_t m = ray_expert_mask(cfg, ROUTE, p, ray, step, lane);
+        if (lane == 0)
+            for (int k = 0; k < cfg.K; ++k)
+                if ((m >> k) & 1u) atomicAdd(&cnt[k], 1);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int b0 = -1, b1 = -1;
+            for (int k = 0; k < cfg.K; ++k) {
+                const int c = cnt[k];
+                if (c == 0) continue;
+                if (b0 < 0 || c > cnt[b0]) { b1 = b0; b0 = k; }
+                else if (b1 < 0 || c > cnt[b1]) b1 = k;
+            }
+            for (int k = 0; k < cfg.K; ++k) cnt[k] = 0;
+            // keep an expert in the slot it already occupies
+            int want[2] = {b0, b1};
+            if (want[0] == slot_k[1] || want[1] == slot_k[0]) { const int t = want[0]; want[0] = want[1]; want[1] = t; }
+            for (int sl = 0; sl < 2; ++sl) {
+                restage[sl] = (want[sl] >= 0 && want[sl] != slot_k[sl]) ? 1 : 0;
+                if (want[sl] >= 0) slot_k[sl] = want[sl];
+            }
+        }
+        __syncthreads();
+        for (int sl = 0; sl < 2; ++sl) {
+            if (restage[sl]) {
+                const f32x4* src = reinterpret_cast<const f32x4*>(p.packed + (size_t)slot_k[sl] * PK_FLOATS);
+                f32x4* dst = reinterpret_cast<f32x4*>(smem + sl * PK_FLOATS);
+                for (int i = threadIdx.x; i < PK_FLOATS / 4; i += blockDim.x) dst[i] = src[i];
+            }
+        }
+        __syncthreads();
+#if ACN_DIAG_NOSLOTS  // diagnostic build only: every expert from global memory
+        const int k0 = -1, k1 = -1;
+#else
+        const int k0 = __builtin_amdgcn_readfirstlane(slot_k[0]), k1 = __builtin_amdgcn_readfirstlane(slot_k[1]);
 #endif
+        if (ray < p.N) {
+            render_ray(p, bg, ray, lane, step,
+                       [&](float px, float py, float pz, const float (&shv)[8], uint32_t& folded, float& yr, float& yg,
+                           float& yb, float& ys) {
+                           const RouteState st = route_prep<ROUTE>(cfg, px, py, pz);
+                           yr = yg = yb = ys = 0.0f;
+                           for (int k = 0; k < cfg.K; ++k) {
+                               const float wk = (ROUTE == 1) ? route_weight(cfg, st, k, px, py, pz) : 0.0f;
+                               const bool need = (ROUTE == 1) ? (wk > 0.0f) : (st.hard == k);
+                               if (__ballot(need) == 0ull) continue;
+                               float r, g, b, sg;
+                               const int sl = (k == k0) ? 0 : ((k == k1) ? 1 : -1);
+                               if (sl >= 0) {
+                                   const float* Wk = smem + sl * PK_FLOATS;
+                                   float* cbk = FOLD ? cb + sl * 64 : nullptr;
+                                   if (FOLD && !((folded >> sl) & 1u)) {
+                                       fold_sh_bias(Wk, shv, lane, cbk);
+                                       folded |= 1u << sl;
+                                   }
+                                   field_tile<INTERP, FOLD>(Wk, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbk, lane, r, g,
+                                                            b, sg);
+                               } else {
+                                   field_tile<INTERP, false>(p.packed + (size_t)k * PK_FLOATS, cfg.ex[k], cfg.log2T,
+                                                             px, py, pz, shv, nullptr, lane, r, g, b, sg);
+                               }
+                               sg = trunc_exp(sg);
+                               if (need) {
+                                   if (ROUTE == 1) {
+                                       yr = yr + r * wk;
+                                       yg = yg + g * wk;
+                                       yb = yb + b * wk;
+                                       ys = ys + sg * wk;
+                                   } else {
+                                       yr = r; yg = g; yb = b; ys = sg;
+                                   }
+                               }
+                           }
+                       });
         }
     }
 }
@@ -1331,7 +1483,11 @@ extern "C" int acn_render_stratified_fwd(const float* rays, int64_t N, int S, co
     RenderParams p{rays, N, S, jitter, (const float*)workspace, sigma_scale, tau, rgb, depth, weights, acc};
     const int64_t wgs = (N + 15) / 16;
     const dim3 grid((unsigned)(wgs < num_cus() ? wgs : num_cus())), block(1024);
-#define ACN_RENDER_LAUNCH(I, KL, R) hipLaunchKernelGGL((render_kernel<I, KL, R>), grid, block, 0, s, cfg, b, p)
+#define ACN_RENDER_LAUNCH(I, KL, R)                                                                    \
+    do {                                                                                              \
+        if (ACN_SLOTS && KL == 0 && R != 0) hipLaunchKernelGGL((render_slots_kernel<I, (R == 0 ? 1 : R)>), grid, dim3(ACN_SLOTS_THREADS), 0, s, cfg, b, p); \
+        else hipLaunchKernelGGL((render_kernel<I, KL, R>), grid, block, 0, s, cfg, b, p);            \
+    } while (0)
     ACN_DISPATCH(ACN_RENDER_LAUNCH);
 #undef ACN_RENDER_LAUNCH
     return acn_check_launch("acn_render_stratified_fwd");
