@@ -14,8 +14,10 @@ from .encodings import FrequencyEncoder, HashGridEncoder, SHEncoder, components_
 from .meta_container import MetaContainer  # noqa: E402,F401
 from .meta_ngp import MetaNGP  # noqa: E402,F401
 from .metamodule import MetaBatchLinear, MetaLayerBlock, MetaLinear, MetaModule, MetaSequential  # noqa: E402,F401
-from .ray_rendering import (render_image, render_rays, render_rays_stratified, stratified_t_vals,  # noqa: E402,F401
-                            volume_render)
+from .ray_rendering import (render_expert_occ, render_image, render_rays, render_rays_occ,  # noqa: E402,F401
+                            render_rays_stratified, stratified_t_vals, volume_render)
+from . import nerfacc  # noqa: E402,F401
+from .nerfacc import OccGridEstimator  # noqa: E402,F401
 from .ray_sampling import clamp_rays_near_far, get_ray_directions, get_rays, pack_rays, unpack_rays  # noqa: E402,F401
 from .scene_box import SceneBox  # noqa: E402,F401
 from .trunc_exp import trunc_exp  # noqa: E402,F401

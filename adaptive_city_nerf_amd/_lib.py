@@ -89,6 +89,21 @@ SIGNATURES = {
     "acn_grad_sumsq": ([vp, vp, i64, vp, vp, vp], C.c_int),
     "acn_clip_coef": ([vp, f32, vp, vp], C.c_int),
     "acn_adam_step": ([vp, vp, i64, vp, i32, vp, vp], C.c_int),
+    "acn_occ_traverse": ([vp, i64, vp, i64, i64, vp, vp, vp, vp, i32, vp, f32, f32, vp, vp, i64, vp, vp, vp, vp, vp,
+                          vp],
+                         C.c_int),
+    "acn_occ_union": ([i32, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp], C.c_int),
+    "acn_render_packed_fwd": ([vp, i64, i64, vp, vp, vp, vp, vp, vp, i32, vp, vp, sz, vp, vp, vp, vp, vp], C.c_int),
+    "acn_packed_weights_fwd": ([vp, vp, vp, vp, vp, i64, vp, vp, vp, vp], C.c_int),
+    "acn_packed_weights_bwd": ([vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, vp, vp], C.c_int),
+    "acn_packed_accumulate_fwd": ([vp, vp, i32, vp, vp, i64, vp, vp], C.c_int),
+    "acn_packed_accumulate_bwd": ([vp, vp, i32, vp, i64, vp, vp, vp, vp], C.c_int),
+    "acn_occ_pack_bits": ([vp, i64, vp, vp], C.c_int),
+    "acn_occ_cell_points": ([vp, i64, vp, vp, vp, vp, vp], C.c_int),
+    "acn_occ_ema": ([vp, vp, vp, i64, f32, vp], C.c_int),
+    "acn_occ_binarize_workspace_bytes": ([], sz),
+    "acn_occ_binarize": ([vp, i64, f32, vp, vp, vp, vp, vp], C.c_int),
+    "acn_occ_mark_invisible": ([vp, i32, vp, i32, i32, i32, f32, vp, vp, vp, i64, vp, vp], C.c_int),
 }
 
 

@@ -1554,3 +1554,179 @@ extern "C" int acn_background_fwd(const float* dirs, int64_t N, const acn_backgr
                        b, dirs, N, out);
     return acn_check_launch("acn_background_fwd");
 }
+
+// ==========================================================================================
+// Occupancy-grid renderer over PACKED samples (render_expert_occ ray_rendering.py:467-558 and the
+// container's soft-MoE render_rays_occ :349-464, after nerfacc's marching / the boundary union):
+// per ray, samples [t0, t1) at their midpoints -> field (single expert, or every expert whose
+// routing weight exceeds 1e-8 with sigma-weighted blending BEFORE compositing) -> nerfacc
+// compositing (alpha = 1 - exp(-sigma*dt), T = exp(-exclusive_sum(sigma*dt)), w = T*alpha) ->
+// rgb / depth (at t_mid) / acc + (1 - acc) * background.  One wave per ray, 32 samples per tile,
+// the MFMA field tile and SH fold of the stratified kernels; no (M,6) / (M,4) intermediates.
+namespace {
+
+struct OccRenderParams {
+    const float* rays;
+    int64_t ld, N;
+    const int64_t *starts, *counts;
+    const float *t0, *t1;
+    const float* packed;
+    float *rgb, *depth, *weights, *acc;
+};
+
+// meta_container blend of render_rays_occ (:426-449): s = clamp_min(sum_k W_k sigma_k, 1e-12),
+// rgb = sum_k (W_k sigma_k) rgb_k / s, experts evaluated only where W_k > 1e-8.
+template <int INTERP, int ROUTE, bool FOLD>
+__device__ __forceinline__ void container_tile_occ(const FieldCfg& cfg, const float* Wbase, float px, float py,
+                                                   float pz, const float (&shv)[8], float* cb, uint32_t* folded,
+                                                   int lane, float& yr, float& yg, float& yb, float& ys) {
+    if (ROUTE == 0) {
+        container_tile<INTERP, 0, FOLD>(cfg, Wbase, px, py, pz, shv, cb, folded, lane, yr, yg, yb, ys);
+        return;
+    }
+    const RouteState st = route_prep<ROUTE>(cfg, px, py, pz);
+    float ns = 0.0f, nr = 0.0f, ng = 0.0f, nb = 0.0f;
+    for (int k = 0; k < cfg.K; ++k) {
+        const float wk = (ROUTE == 1) ? route_weight(cfg, st, k, px, py, pz) : (st.hard == k ? 1.0f : 0.0f);
+        const bool need = wk > 1e-8f;
+        if (__ballot(need) == 0ull) continue;
+        const float* Wk = Wbase + (size_t)k * PK_FLOATS;
+        float* cbk = FOLD ? cb + k * 64 : nullptr;
+        if (FOLD && !((*folded >> k) & 1u)) {
+            fold_sh_bias(Wk, shv, lane, cbk);
+            *folded |= 1u << k;
+        }
+        float r, g, b, s;
+        field_tile<INTERP, FOLD>(Wk, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbk, lane, r, g, b, s);
+        s = trunc_exp(s);
+        if (need) {
+            const float ws = wk * s;
+            ns = ns + ws;
+            nr = nr + ws * r;
+            ng = ng + ws * g;
+            nb = nb + ws * b;
+        }
+    }
+    const float sn = clamp_min_nan(ns, 1e-12f);
+    yr = nr / sn;
+    yg = ng / sn;
+    yb = nb / sn;
+    ys = sn;
+}
+
+template <class FieldFn>
+__device__ __forceinline__ void render_ray_packed(const OccRenderParams& p, const BgArgs& bg, int64_t ray, int lane,
+                                                  FieldFn&& field) {
+    const int j = lane & 31, h = lane >> 5;
+    const float* rp = p.rays + ray * p.ld;
+    const float ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
+    const int64_t b = p.starts[ray], n = p.counts[ray];
+    float sh[16], shv[8];
+    dir_sh(dx, dy, dz, sh);
+    sh_rows_for_half(sh, h, shv);
+    uint32_t folded = 0u;
+    double carry = 0.0;
+    float ar = 0.0f, ag = 0.0f, ab = 0.0f, ad = 0.0f, aa = 0.0f;
+    for (int64_t s0 = 0; s0 < n; s0 += 32) {
+        const bool valid = s0 + j < n;
+        const int64_t idx = b + (valid ? s0 + j : n - 1);
+        const float ta = p.t0[idx], tb = p.t1[idx];
+        const float tm = 0.5f * (ta + tb);
+        const float px = ox + dx * tm, py = oy + dy * tm, pz = oz + dz * tm;
+        float yr, yg, yb, ys;
+        field(px, py, pz, shv, folded, yr, yg, yb, ys);
+        const float sdt = valid ? ys * (tb - ta) : 0.0f;
+        double incl = (double)sdt;
+#pragma unroll
+        for (int off = 1; off < 32; off <<= 1) {
+            const double y = __shfl_up(incl, off, 32);
+            if (j >= off) incl += y;
+        }
+        const float excl = (float)(carry + incl - (double)sdt);
+        const float alpha = 1.0f - expf(-sdt);
+        const float w = expf(-excl) * alpha;
+        if (valid && h == 0) {
+            if (p.weights) p.weights[idx] = w;
+            ar += w * yr;
+            ag += w * yg;
+            ab += w * yb;
+            ad += w * tm;
+            aa += w;
+        }
+        carry += __shfl(incl, 31, 32);
+    }
+    float bgc[3];
+    background(bg, dx, dy, dz, lane, bgc);
+    const float r = (float)wave32_sum((double)ar), g = (float)wave32_sum((double)ag), bb = (float)wave32_sum((double)ab);
+    const float dd = (float)wave32_sum((double)ad), a = (float)wave32_sum((double)aa);
+    if (lane == 0) {
+        float orr = r, og = g, ob = bb;
+        if (bg.mode != ACN_BG_NONE) {
+            const float om = 1.0f - a;
+            orr = r + om * bgc[0];
+            og = g + om * bgc[1];
+            ob = bb + om * bgc[2];
+        }
+        p.rgb[ray * 3 + 0] = orr;
+        p.rgb[ray * 3 + 1] = og;
+        p.rgb[ray * 3 + 2] = ob;
+        p.depth[ray] = dd;
+        p.acc[ray] = a;
+    }
+}
+
+template <int INTERP, int KL, int ROUTE>
+__global__ void __launch_bounds__(1024, 4) occ_render_kernel(FieldCfg cfg, BgArgs bg, OccRenderParams p) {
+    constexpr bool FOLD = ACN_SHFOLD != 0;
+    constexpr int KF = ROUTE == 0 ? 1 : (KL == 2 ? 2 : kMaxK);
+    __shared__ __attribute__((aligned(16))) float smem[(KL > 0 ? KL : 1) * PK_FLOATS];
+    __shared__ __attribute__((aligned(16))) float cbuf[FOLD ? 16 * KF * 64 : 4];
+    const float* W = p.packed;
+    if (KL > 0) {
+        stage_weights<KL>(smem, p.packed);
+        W = smem;
+    }
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float* cb = FOLD ? cbuf + wave * KF * 64 : nullptr;
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t ray = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave; ray < p.N; ray += nw) {
+        render_ray_packed(p, bg, ray, lane,
+                          [&](float px, float py, float pz, const float (&shv)[8], uint32_t& folded, float& yr,
+                              float& yg, float& yb, float& ys) {
+                              container_tile_occ<INTERP, ROUTE, FOLD>(cfg, W, px, py, pz, shv, cb, &folded, lane, yr,
+                                                                      yg, yb, ys);
+                          });
+    }
+}
+
+}  // namespace
+
+extern "C" int acn_render_packed_fwd(const float* rays, int64_t ld, int64_t N, const int64_t* chunk_starts,
+                                     const int64_t* chunk_cnts, const float* t_starts, const float* t_ends,
+                                     const acn_expert* experts, const acn_routing* routing, int active_module,
+                                     const acn_background* bg, void* workspace, size_t workspace_bytes, float* rgb,
+                                     float* depth, float* weights, float* acc, void* stream) {
+    ACN_REQUIRE(N >= 0 && ld >= 6, "acn_render_packed_fwd: rays must be (N, >=6)");
+    if (N == 0) return ACN_OK;
+    ACN_REQUIRE(rays && chunk_starts && chunk_cnts && rgb && depth && acc, "acn_render_packed_fwd: NULL pointer");
+    ACN_REQUIRE(bg, "acn_render_packed_fwd: NULL background");
+    if (bg->mode == ACN_BG_MLP) {
+        ACN_REQUIRE(bg->w1 && bg->b1 && bg->w2 && bg->b2, "background MLP pointers are NULL");
+        ACN_REQUIRE(bg->hidden >= 1 && bg->hidden <= 64, "bg_hidden must be in [1, 64], got %d", bg->hidden);
+    }
+    hipStream_t s = (hipStream_t)stream;
+    FieldCfg cfg{};
+    int interp, K;
+    int st = prepare(experts, routing, active_module, workspace, workspace_bytes, s, cfg, interp, K, false);
+    if (st) return st;
+    BgArgs b{bg->mode, bg->hidden, {bg->color[0], bg->color[1], bg->color[2]}, bg->w1, bg->b1, bg->w2, bg->b2};
+    OccRenderParams p{rays, ld, N, chunk_starts, chunk_cnts, t_starts, t_ends, (const float*)workspace,
+                      rgb, depth, weights, acc};
+    const int64_t wgs = (N + 15) / 16;
+    const dim3 grid((unsigned)(wgs < num_cus() ? wgs : num_cus())), block(1024);
+#define ACN_OCC_LAUNCH(I, KL, R) hipLaunchKernelGGL((occ_render_kernel<I, KL, R>), grid, block, 0, s, cfg, b, p)
+    ACN_DISPATCH(ACN_OCC_LAUNCH);
+#undef ACN_OCC_LAUNCH
+    return acn_check_launch("acn_render_packed_fwd");
+}

@@ -203,7 +203,7 @@ class MetaContainer(MetaModule):
         bg, keep = self.background_spec()
         return ops.background_fwd(d.reshape(-1, 3), bg).view(*shape[:-1], 3)
 
-    # ---------------------------------------------------------------- occupancy (out of scope)
+    # ---------------------------------------------------------------- occupancy (meta_container.py:386-462)
     def maybe_update_expert_occupancies(self, step: int, params=None) -> None:
         for sub in self.submodules:
             sub.maybe_update_occ_grid(step, params)
@@ -212,8 +212,21 @@ class MetaContainer(MetaModule):
         for sub in self.submodules:
             sub.occ_frozen = flag
 
+    @torch.no_grad()
     def premark_invisible_expert_cells(self, metas, near_plane: float = 0.0, chunk: int = 32 ** 3) -> List[int]:
-        return [0] * len(self.submodules)
+        """One-time visibility pruning of every expert's grid; returns the cells marked per expert."""
+        if self.cells_premarked or not self.use_occ:
+            return [0] * len(self.submodules)
+        marked = []
+        for k, expert in enumerate(self.submodules):
+            expert.premark_invisible_cells(metas, near_plane=float(near_plane), chunk=chunk)
+            n_marked = int((expert.occ_grid.occs < 0).sum().item()) if hasattr(expert.occ_grid, "occs") else 0
+            total = expert.occ_grid.occs.numel() if hasattr(expert.occ_grid, "occs") else 0
+            marked.append(n_marked)
+            print(f"[OCC] container: expert#{k} cams={len(metas)} marked_invisible={n_marked} / {total} "
+                  f"({100.0 * n_marked / max(1, total):.2f}%)")
+        print("[OCC] container: premark complete for all experts.")
+        return marked
 
     @property
     def occ_ready(self) -> bool:

@@ -5,17 +5,21 @@ Same constructor, submodule names (state-dict keys such as ``xyz_encoder.hash_ta
 ``forward`` without autograd runs the fused HIP field kernel (hash grid -> sigma trunk -> heads ->
 SH -> colour MLP in one launch, fp32 MFMA); with autograd it composes the HIP hash-grid
 forward/backward with the fast-weight MetaLinear chain so gradients reach the table and every
-(fast) weight.  The occupancy-grid path (use_occ, nerfacc) is outside this round's scope.
+(fast) weight.  With ``occ_conf['use_occ']`` the expert owns an occupancy grid (the nerfacc
+OccGridEstimator surface of .nerfacc, HIP-marched) with the reference's premark / update /
+marching methods (meta_ngp.py:242-443).
 """
 from __future__ import annotations
 
-from typing import Dict, Literal, Optional, Union
+import math
+from typing import Dict, List, Literal, Optional, Tuple, Union
 
 import torch
 from torch import Tensor
 
 from . import ops
 from .encodings import FrequencyEncoder, HashGridEncoder, SHEncoder
+from .nerfacc import OccGridEstimator
 from .metamodule import MetaLayerBlock, MetaLinear, MetaModule, MetaSequential
 from .scene_box import SceneBox
 from .trunc_exp import trunc_exp
@@ -35,9 +39,6 @@ class MetaNGP(MetaModule):
         hash_enc_conf = hash_enc_conf or {}
         occ_conf = occ_conf or {}
         self.use_occ = bool(occ_conf.get("use_occ", False))
-        if self.use_occ:
-            raise NotImplementedError("occupancy-grid rendering (nerfacc) is not part of this build yet "
-                                      "(SURVEY §8(f) rank 1); construct with occ_conf={'use_occ': False}")
         self.geo_feat_dim = int(geo_feat_dim)
         self.use_sigmoid_rgb = bool(use_sigmoid_rgb)
         self.scene_box = scene_box
@@ -77,12 +78,46 @@ class MetaNGP(MetaModule):
         self.occ_ready = False
         self.occ_premarked = False
         self.occ_frozen = False
+        if self.use_occ:  # meta_ngp.py:100-141
+            rss = occ_conf.get("render_step_size")
+            self.render_step_size = float(rss) if rss is not None else float(scene_box.get_diagonal_length()) / 1000.0
+            self.occ_thre: float = float(occ_conf.get("occ_thre", 1e-2))
+            self.alpha_thre: float = float(occ_conf.get("alpha_thre", 1e-2))
+            self.cone_angle: float = float(occ_conf.get("cone_angle", 1.0 / 256.0))
+            self.near_plane: float = float(occ_conf.get("near_plane", 0.05))
+            self.far_plane: float = float(occ_conf.get("far_plane", 1e3))
+            self.occ_update_interval: int = int(occ_conf.get("update_interval", 16))
+            self.occ_warmup_steps: int = int(occ_conf.get("warmup_steps", 256))
+            self.occ_cosine_anneal = bool(occ_conf.get("cosine_anneal", True))
+            self.occ_alpha_thre_start: float = float(occ_conf.get("alpha_thre_start", 0.0))
+            self.occ_alpha_thre_end: float = float(occ_conf.get("alpha_thre_end", self.alpha_thre))
+            self.occ_ema_decay: float = float(occ_conf.get("ema_decay", 0.95))
+            self.occ_resolution: int = int(occ_conf.get("resolution", 128))
+            self.occ_levels: int = int(occ_conf.get("levels", 4))
+            scene_aabb = torch.cat([self.scene_box.min, self.scene_box.max]).flatten()
+            self.register_buffer("scene_aabb", scene_aabb)
+            self.occ_grid = OccGridEstimator(roi_aabb=self.scene_aabb, resolution=self.occ_resolution,
+                                             levels=self.occ_levels)
+            self._check_aabb()
+            self.occ_frozen = bool(occ_conf.get("occ_frozen", False))
+            self.occ_ready = bool(occ_conf.get("occ_ready", False))
+            self.num_occ_updates = 0
+            self.occ_premarked = False
         self._fusable = (isinstance(self.dir_encoder, SHEncoder) and self.xyz_encoder.levels == 16
                          and self.xyz_encoder.features_per_level == 2 and int(sigma_depth) == 2 and hidden == 64
                          and self.geo_feat_dim == 15 and int(color_depth) == 2 and color_hidden == 64
                          and self.use_sigmoid_rgb)
 
     # ------------------------------------------------------------------ encoding helpers
+    def _check_aabb(self) -> None:
+        aabb = self.scene_aabb
+        assert aabb.dtype == torch.float32 and aabb.isfinite().all()
+        assert aabb.numel() == 6
+        mn, mx = aabb[:3], aabb[3:]
+        if not (mn < mx).all():
+            raise ValueError(f"AABB invalid: min>=max ({mn} vs {mx})")
+        assert aabb.device == self.occ_grid.aabbs.device
+
     def _world_to_unit(self, x: Tensor) -> Tensor:
         x01 = (x - self.scene_box.min.to(x.device)) / self.aabb_extent
         return x01.clamp(self.enc_eps, 1.0 - self.enc_eps)
@@ -142,6 +177,12 @@ class MetaNGP(MetaModule):
 
     def density(self, x: Tensor, params: Optional[Dict[str, Tensor]] = None,
                 return_feats: bool = False) -> Union[Tensor, Dict[str, Tensor]]:
+        if not return_feats and x.is_cuda and self._fusable and not self.uses_grad(params):
+            # no autograd (occupancy updates / marching visibility): the fused field kernel; the
+            # direction input only feeds the colour branch, whose output is dropped
+            flat = x.reshape(-1, 3)
+            sig = self.forward(torch.cat([flat, torch.zeros_like(flat)], dim=-1), params=params)[:, 3:4]
+            return sig.reshape(*x.shape[:-1], 1)
         h = self._enc_xyz(x)
         h = self.sigma_trunk(h, params=self.get_subdict(params, "sigma_trunk"))
         sigma = self.sigma_act(self.sigma_head(h, params=self.get_subdict(params, "sigma_head")))
@@ -166,15 +207,114 @@ class MetaNGP(MetaModule):
         rgb = self.color(d, dens["geo_feat"], params=params)
         return torch.cat([rgb, dens["sigma"]], dim=-1)
 
-    # ------------------------------------------------------------------ occupancy (out of scope)
+    # ------------------------------------------------------------------ occupancy (meta_ngp.py:242-443)
+    def _anneal_alpha_thre(self, step: int) -> None:
+        """Ramp alpha threshold from start to end over warmup, then hold."""
+        if step < self.occ_warmup_steps:
+            t = step / max(1, self.occ_warmup_steps - 1)
+            if self.occ_cosine_anneal:
+                cos = 0.5 * (1 - math.cos(math.pi * t))
+                self.alpha_thre = (1 - cos) * self.occ_alpha_thre_start + cos * self.occ_alpha_thre_end
+            else:
+                self.alpha_thre = (1 - t) * self.occ_alpha_thre_start + t * self.occ_alpha_thre_end
+        else:
+            self.alpha_thre = self.occ_alpha_thre_end
+
+    @torch.no_grad()
+    def _build_intrinsics_from_metadata(self, mds: List, device: torch.device) -> Tensor:
+        """(N,3,3) K matrices from metadata intrinsics (9 values, or [fx, fy, cx, cy])."""
+        def _make_K(md) -> Tensor:
+            Kraw = torch.as_tensor(md.intrinsics, dtype=torch.float32)
+            if Kraw.numel() == 9:
+                return Kraw.view(3, 3)
+            if Kraw.numel() == 4:
+                fx, fy, cx, cy = Kraw.unbind()
+                return torch.tensor([[fx, 0.0, cx], [0.0, fy, cy], [0.0, 0.0, 1.0]], dtype=torch.float32)
+            raise ValueError(f"Unsupported intrinsics shape: {tuple(Kraw.shape)}")
+        return torch.stack([_make_K(md) for md in mds], dim=0).to(device=device, dtype=torch.float32)
+
+    @torch.no_grad()
+    def _build_c2w_rdf_from_metadata(self, mds: List, device: torch.device) -> Tensor:
+        """c2w (N,3,4) or (N,4,4) with the rotation converted from RUB to RDF."""
+        c2w = torch.stack([torch.as_tensor(md.c2w, dtype=torch.float32) for md in mds], dim=0)
+        C3 = torch.diag(torch.tensor([1.0, -1.0, -1.0], dtype=torch.float32))
+        if c2w.shape[1:] == (3, 4):
+            R_rdf = torch.einsum("nij,jk->nik", c2w[:, :3, :3], C3)
+            c2w_rdf = torch.cat([R_rdf, c2w[:, :3, 3:]], dim=2)
+        elif c2w.shape[1:] == (4, 4):
+            c2w_rdf = c2w.clone()
+            c2w_rdf[:, :3, :3] = torch.einsum("nij,jk->nik", c2w[:, :3, :3], C3)
+        else:
+            raise ValueError(f"Unsupported c2w shape: {tuple(c2w.shape)}")
+        return c2w_rdf.to(device=device, dtype=torch.float32)
+
+    @torch.no_grad()
+    def premark_invisible_cells(self, mds: List, near_plane: float = 0.05, chunk: int = 32 ** 3) -> None:
+        """One-time visibility pruning: cells no camera sees get occ < 0 (HIP projection kernel)."""
+        if not self.use_occ or self.occ_premarked:
+            return
+        mds = [md for md in mds if md is not None]
+        if len(mds) == 0:
+            print("[OCC] premark skipped: empty metadata list.")
+            self.occ_premarked = True
+            return
+        device = self.occ_grid.aabbs.device
+        K = self._build_intrinsics_from_metadata(mds, device)
+        c2w_rdf = self._build_c2w_rdf_from_metadata(mds, device)
+        H, W = int(mds[0].H), int(mds[0].W)
+        self.occ_grid.mark_invisible_cells(K=K, c2w=c2w_rdf, width=W, height=H, near_plane=float(near_plane),
+                                           chunk=chunk)
+        self.occ_premarked = True
+
+    @torch.no_grad()
     def maybe_update_occ_grid(self, step: int, params: Optional[Dict[str, Tensor]] = None) -> None:
-        return None  # use_occ is always False in this build (reference early-returns the same way)
+        """Periodic occupancy update during training (density on the fused HIP field)."""
+        if not (self.training and self.use_occ and not self.occ_frozen):
+            return
+        self.occ_ready = step >= self.occ_warmup_steps
+        self._anneal_alpha_thre(step)
 
-    def premark_invisible_cells(self, *a, **k) -> None:
-        return None
+        def occ_eval_fn(x: Tensor) -> Tensor:
+            return self.density(x, params=params).squeeze(-1) * self.render_step_size
 
-    def occupancy_marching(self, *a, **k):
-        raise NotImplementedError("occupancy marching (nerfacc) is not part of this build (SURVEY §8(f))")
+        self.occ_grid.update_every_n_steps(step=step, occ_eval_fn=occ_eval_fn, occ_thre=self.occ_thre,
+                                           ema_decay=self.occ_ema_decay, warmup_steps=self.occ_warmup_steps,
+                                           n=self.occ_update_interval)
+        self.num_occ_updates += 1
+        if step % self.occ_update_interval == 0:
+            print(f"[OCC UPDATE {self.num_occ_updates}] step={step:5d} warmup={step < self.occ_warmup_steps} "
+                  f"alpha_thre={self.alpha_thre:6.4f}")
+
+    @torch.no_grad()
+    def _occupancy_marching_packed(self, rays: Tensor, *, params: Optional[Dict[str, Tensor]] = None,
+                                   render_step_size: Optional[float] = None, alpha_thre: Optional[float] = None,
+                                   cone_angle: Optional[float] = None, prefilter_aabb=None):
+        """occupancy_marching plus the packed layout (chunk starts / counts per ray)."""
+        if getattr(self, "occ_grid", None) is None:
+            raise RuntimeError("MetaNGP: occ_grid missing")
+        rays = rays.contiguous()
+        o, d, t_min, t_max = rays[:, :3], rays[:, 3:6], rays[:, 6], rays[:, 7]
+        sigma_fn = None
+        if self.training:
+            def sigma_fn(t_starts: Tensor, t_ends: Tensor, ray_indices: Tensor) -> Tensor:
+                mids = 0.5 * (t_starts + t_ends)
+                x = o[ray_indices] + d[ray_indices] * mids[:, None]
+                return self.density(x, params=params).squeeze(-1)
+        return self.occ_grid._sampling_packed(
+            rays_o=o, rays_d=d, sigma_fn=sigma_fn, t_min=t_min, t_max=t_max,
+            render_step_size=self.render_step_size if render_step_size is None else render_step_size,
+            stratified=self.training, cone_angle=self.cone_angle if cone_angle is None else cone_angle,
+            alpha_thre=self.alpha_thre if alpha_thre is None else alpha_thre, prefilter_aabb=prefilter_aabb,
+            prefilter_near_far=rays[:, 6:8] if prefilter_aabb is not None else None)
+
+    @torch.no_grad()
+    def occupancy_marching(self, rays: Tensor, *, params: Optional[Dict[str, Tensor]] = None,
+                           render_step_size: Optional[float] = None, alpha_thre: Optional[float] = None,
+                           cone_angle: Optional[float] = None) -> Tuple[Tensor, Tensor, Tensor]:
+        """(ray_indices, t_starts, t_ends) of this expert's occupied samples (meta_ngp.py:391-443)."""
+        ri, t0, t1, _, _ = self._occupancy_marching_packed(rays, params=params, render_step_size=render_step_size,
+                                                           alpha_thre=alpha_thre, cone_angle=cone_angle)
+        return ri, t0, t1
 
     def get_param_groups(self) -> Dict[str, Dict]:
         return {

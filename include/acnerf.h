@@ -220,6 +220,85 @@ int acn_clip_coef(const double* total_sumsq, float max_norm, float* out, void* s
 int acn_adam_step(const acn_param_desc* descs, const int32_t* chunk_tensor, int64_t nchunks,
                   const acn_adam_group* groups, int ngroups, const float* grad_scale, void* stream);
 
+/* ---------------------------------------------------------------------------------------- */
+/* Occupancy-grid renderer.  The reference delegates this to nerfacc 0.5.3
+ * (third-party, not vendored): OccGridEstimator.sampling -> traverse_grids, render_weight_from_density,
+ * accumulate_along_rays, pack_info; its own glue is nerfs/ray_rendering.py:170-258, :349-558 and
+ * models/inr/meta_ngp.py:242-443.  Packed sample lists are ray-major: ray r owns samples
+ * [chunk_starts[r], chunk_starts[r] + chunk_cnts[r]) (nerfacc's packed_info columns).            */
+
+/* OccGridEstimator.sampling's traverse_grids (marching through `levels` nested grids of res[3]
+ * cells, aabbs host (levels, 6) [min3, max3]).  bits: the `binaries` buffer as one bit per cell
+ * (acn_occ_pack_bits).  near/far (N) device.  prefilter_aabb (host [min3, max3]) or NULL: rays that
+ * miss it over [near, far] = prefilter_near_far[i * ld_pf + {0, 1}] (the rays' own columns;
+ * ray_rendering.py:170-193 _intersect_rays_aabb) get no samples.  Two passes: offsets == NULL ->
+ * counts (N) per ray; else the samples of ray i are written at offsets[i].                      */
+int acn_occ_traverse(const float* rays_o, int64_t ld_o, const float* rays_d, int64_t ld_d, int64_t N,
+                     const float* near_planes, const float* far_planes, const uint32_t* bits,
+                     const float* aabbs, int levels, const int32_t* res, float step_size, float cone_angle,
+                     const float* prefilter_aabb, const float* prefilter_near_far, int64_t ld_pf,
+                     int64_t* counts, const int64_t* offsets, int64_t* ray_indices, float* t_starts,
+                     float* t_ends, void* stream);
+
+/* _merge_segments_union (ray_rendering.py:196-258): per ray, the sorted distinct boundaries of the
+ * K experts' segments; consecutive pairs become the merged segments.  starts/counts/t_starts/t_ends
+ * are HOST arrays of K device pointers (per expert: (N) chunk starts and counts over the global rays,
+ * (M_k) t values).  Two passes as acn_occ_traverse.                                             */
+int acn_occ_union(int K, int64_t N, const int64_t* const* starts, const int64_t* const* counts,
+                  const float* const* t_starts, const float* const* t_ends, int64_t* out_counts,
+                  const int64_t* offsets, int64_t* ray_indices, float* m_starts, float* m_ends, void* stream);
+
+/* Fused occupancy render over packed samples: render_expert_occ (ray_rendering.py:467-558) when
+ * active_module >= 0 or K == 1, the container's soft-MoE blend of render_rays_occ (:406-464)
+ * otherwise; nerfacc compositing; background as acn_render_stratified_fwd.  rays (N, ld>=6) [o, d].
+ * weights (M) or NULL.                                                                        */
+int acn_render_packed_fwd(const float* rays, int64_t ld, int64_t N, const int64_t* chunk_starts,
+                          const int64_t* chunk_cnts, const float* t_starts, const float* t_ends,
+                          const acn_expert* experts, const acn_routing* routing, int active_module,
+                          const acn_background* bg, void* workspace, size_t workspace_bytes, float* rgb,
+                          float* depth, float* weights, float* acc, void* stream);
+
+/* nerfacc render_weight_from_density over packed samples: weights, trans, alphas (M) (trans / alphas
+ * may be NULL).                                                                                */
+int acn_packed_weights_fwd(const float* sigmas, const float* t_starts, const float* t_ends,
+                           const int64_t* chunk_starts, const int64_t* chunk_cnts, int64_t N,
+                           float* weights, float* trans, float* alphas, void* stream);
+
+/* Backward of acn_packed_weights_fwd w.r.t. sigmas given dL/d(weights, trans, alphas) (any NULL). */
+int acn_packed_weights_bwd(const float* sigmas, const float* t_starts, const float* t_ends,
+                           const float* weights, const float* trans, const float* alphas,
+                           const float* g_weights, const float* g_trans, const float* g_alphas,
+                           const int64_t* chunk_starts, const int64_t* chunk_cnts, int64_t N,
+                           float* g_sigmas, void* stream);
+
+/* nerfacc accumulate_along_rays: out (N, C) = per-ray sum of weights * values (values (M, C) or
+ * NULL for C = 1 and values = 1).  Deterministic segmented sums.                                */
+int acn_packed_accumulate_fwd(const float* weights, const float* values, int C, const int64_t* chunk_starts,
+                              const int64_t* chunk_cnts, int64_t N, float* out, void* stream);
+
+/* Backward of acn_packed_accumulate_fwd given dL/dout (N, C): g_weights (M), g_values (M, C) (either NULL). */
+int acn_packed_accumulate_bwd(const float* weights, const float* values, int C, const int64_t* ray_indices,
+                              int64_t M, const float* g_out, float* g_weights, float* g_values, void* stream);
+
+/* OccGridEstimator maintenance.  acn_occ_pack_bits: binaries (n bytes, the bool buffer) -> one bit
+ * per cell (ceil(n/32) words).  acn_occ_cell_points: jittered cell positions of one level
+ * (nerfacc _update: aabb_min + (coords + u) / res * extent); u (n, 3) device or NULL, aabb / res
+ * host.  acn_occ_ema: occs[c] = max(occs[c] * decay, occ).  acn_occ_binarize: thre =
+ * min(mean(occs[occs >= 0]), occ_thre); binaries = occs > thre (+ bits, thre_out optional), all on
+ * device, workspace of acn_occ_binarize_workspace_bytes().  acn_occ_mark_invisible
+ * (mark_invisible_cells): Ks (nK, 3, 3), c2w (nc2w, 3, 4) device; occs_level[c] = 0 if some camera
+ * sees cell c (coords / (res - 1) in the level box) in front of near_plane, else -1.            */
+int acn_occ_pack_bits(const uint8_t* binaries, int64_t n, uint32_t* bits, void* stream);
+int acn_occ_cell_points(const int64_t* cell_indices, int64_t n, const float* u, const float* aabb,
+                        const int32_t* res, float* x, void* stream);
+int acn_occ_ema(float* occs, const int64_t* cell_ids, const float* occ, int64_t n, float decay, void* stream);
+size_t acn_occ_binarize_workspace_bytes(void);
+int acn_occ_binarize(const float* occs, int64_t n, float occ_thre, uint8_t* binaries, uint32_t* bits,
+                     float* thre_out, void* workspace, void* stream);
+int acn_occ_mark_invisible(const float* Ks, int nK, const float* c2w, int nc2w, int width, int height,
+                           float near_plane, const float* aabb, const int32_t* res,
+                           const int64_t* cell_indices, int64_t n, float* occs_level, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

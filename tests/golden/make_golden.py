@@ -85,7 +85,7 @@ def scene_json() -> dict:
     return out
 
 
-def build_container(scene: dict, mask: str, seed: int = 0, table_seed0: int = 100):
+def build_container(scene: dict, mask: str, seed: int = 0, table_seed0: int = 100, occ_conf=None):
     m = scene["masks"][mask]
     K = len(m["centroids"])
     gbox = SceneBox(aabb=torch.tensor(m["aabb_global"], dtype=torch.float32))
@@ -97,7 +97,7 @@ def build_container(scene: dict, mask: str, seed: int = 0, table_seed0: int = 10
         num_submodules=K, centroids=torch.tensor(m["centroids"], dtype=torch.float32),
         aabb=gbox.aabb, nerf_variant="instant", boundary_margin=min(max(1.0, BM_RUNTIME), m["boundary_margin"]),
         cluster_2d=m["cluster_2d"], joint_training=False, use_bg_nerf=True, bg_hidden=32,
-        bg_encoding="spherical", occ_conf={"use_occ": False}, expert_box_list=boxes, hidden=64,
+        bg_encoding="spherical", occ_conf=occ_conf or {"use_occ": False}, expert_box_list=boxes, hidden=64,
         sigma_depth=2, color_depth=2, dir_encoding="spherical", color_hidden=64,
         use_sigmoid_rgb=True, hash_enc_conf=hash_conf,
     )
@@ -404,12 +404,102 @@ def gen_train(scene: dict) -> None:
     save("train_k4", **out)
 
 
+# ----------------------------------------------------------------------------------------------
+OCC_RES, OCC_LEVELS, OCC_PCT, OCC_SEED0 = 32, 2, 50, 7
+
+
+def occ_conf_fixture() -> dict:
+    """nerf_runner.py:124-147 occupancy config at a fixture-sized grid (32^3 x 2 levels)."""
+    return {"use_occ": True, "resolution": OCC_RES, "levels": OCC_LEVELS, "render_step_size": None,
+            "occ_thre": 1e-2, "alpha_thre": 1e-2, "alpha_thre_start": 0.0, "alpha_thre_end": 1e-2,
+            "cosine_anneal": True, "warmup_steps": 256, "update_interval": 16, "ema_decay": 0.95,
+            "cone_angle": 0.004, "near_plane": 0.05, "far_plane": 1e3, "occ_frozen": False, "occ_ready": True}
+
+
+def gen_occ(scene: dict) -> None:
+    """Occupancy renderer fixtures: the reference's render_expert_occ / render_rays_occ /
+    occupancy_marching / _merge_segments_union run over the nerfacc stand-in (_refstubs.py), with
+    formula occupancy grids (oracle/occ_ref.formula_binaries, seed OCC_SEED0 + k, OCC_PCT %)."""
+    from nerfs import ray_rendering as RR
+    from oracle import occ_ref as R
+    for mask, tag in (("g11_grid_bm110_ss11", "k1"), ("g22_grid_bm110_ss11", "k4")):
+        model, gbox = build_container(scene, mask, occ_conf=occ_conf_fixture())
+        K = len(model.submodules)
+        with torch.no_grad():  # denser field (sigma ~ e^2.5): per-sample alpha ~1e-2, rays mostly opaque
+            for sub in model.submodules:
+                sub.sigma_head.bias.fill_(2.5)
+        out = {}
+        for k, sub in enumerate(model.submodules):
+            b = R.formula_binaries(OCC_LEVELS, OCC_RES, OCC_SEED0 + k, OCC_PCT)
+            with torch.no_grad():
+                sub.occ_grid.binaries.copy_(torch.from_numpy(b))
+                sub.occ_grid.occs.copy_(torch.from_numpy(b.reshape(-1).astype(np.float32) * 0.05))
+            out[f"expert{k}:render_step_size"] = np.array(sub.render_step_size, np.float64)
+            out[f"expert{k}:aabbs"] = _np(sub.occ_grid.aabbs)
+        out.update(weights_dict(model))
+        rays, valid, cam = val_rays(scene, mask, 0.25)
+        rv = rays[valid]
+        perm = torch.randperm(rv.shape[0], generator=torch.Generator().manual_seed(5))[:256]
+        r = rv[perm].contiguous()
+        out["rays"] = _np(r)
+        sub0 = model.submodules[0]
+        with torch.no_grad():
+            ri, t0, t1 = sub0.occupancy_marching(r)
+            out.update({"march0:ri": _np(ri), "march0:t0": _np(t0), "march0:t1": _np(t1)})
+            res = RR.render_rays(model, r, ray_samples=64, active_module=0, bg_color_default="white")
+            for nm, v in zip(("rgb", "depth", "weights", "acc"), res):
+                out[f"expert0:{nm}"] = _np(v)
+        # training-mode marching: stratified jitter (recorded) + density visibility filter
+        sub0.train()
+        torch.manual_seed(11)
+        with torch.no_grad():
+            ri, t0, t1 = sub0.occupancy_marching(r)
+        sub0.eval()
+        out.update({"train0:u": _np(sub0.occ_grid.last_u), "train0:ri": _np(ri), "train0:t0": _np(t0),
+                    "train0:t1": _np(t1), "train0:alpha_thre": np.array(sub0.alpha_thre, np.float64)})
+        if K > 1:
+            # per-expert prefilter + marching lists (global ray ids) and their boundary union
+            lists = ([], [], [])
+            for k, sub in enumerate(model.submodules):
+                hit = RR._intersect_rays_aabb(r, scene_box=sub.scene_box)
+                out[f"hit{k}"] = _np(hit)
+                if not hit.any():
+                    continue
+                with torch.no_grad():
+                    ri_k, t0_k, t1_k = sub.occupancy_marching(r[hit])
+                gidx = hit.nonzero(as_tuple=False).squeeze(1)[ri_k]
+                lists[0].append(gidx); lists[1].append(t0_k); lists[2].append(t1_k)
+                out.update({f"list{k}:ri": _np(gidx), f"list{k}:t0": _np(t0_k), f"list{k}:t1": _np(t1_k)})
+            mri, m0, m1 = RR._merge_segments_union(*lists)
+            out.update({"union:ri": _np(mri), "union:t0": _np(m0), "union:t1": _np(m1)})
+            # container render: the reference routes x_mid.view(1, -1, 3), which its own _routing
+            # asserts against (meta_container.py:111); the fixture routes the (M, 3) points
+            orig = type(model)._routing
+
+            def routing_flat(self, pts, _orig=orig):
+                return _orig(self, pts.reshape(-1, 3))
+            type(model)._routing = routing_flat
+            try:
+                with torch.no_grad():
+                    res = RR.render_rays(model, r, ray_samples=64, active_module=None, bg_color_default="white")
+            finally:
+                type(model)._routing = orig
+            for nm, v in zip(("rgb", "depth", "weights", "acc"), res):
+                out[f"container:{nm}"] = _np(v)
+        out["table_seeds"] = np.array([100 + k for k in range(K)], np.int64)
+        out["table_scale"] = np.array(TABLE_SCALE, np.float64)
+        out["bm"] = np.array(model.boundary_margin, np.float64)
+        out["occ"] = np.array([OCC_RES, OCC_LEVELS, OCC_PCT, OCC_SEED0], np.int64)
+        save(f"occ_{tag}", **out)
+        del model
+
+
 def main() -> None:
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     scene = scene_json()
     (HERE / "scene_drz_example.json").write_text(json.dumps(scene, indent=1))
     print("wrote scene_drz_example.json")
-    which = sys.argv[1:] or ["hashgrid", "sh", "volume_render", "routing", "rays", "render", "train"]
+    which = sys.argv[1:] or ["hashgrid", "sh", "volume_render", "routing", "rays", "render", "train", "occ"]
     if "hashgrid" in which: gen_hashgrid()
     if "sh" in which: gen_sh()
     if "volume_render" in which: gen_volume_render()
@@ -417,6 +507,7 @@ def main() -> None:
     if "rays" in which: gen_rays(scene)
     if "render" in which: gen_field_and_render(scene)
     if "train" in which: gen_train(scene)
+    if "occ" in which: gen_occ(scene)
 
 
 if __name__ == "__main__":

@@ -11,7 +11,7 @@ import torch
 import goldens as G
 
 
-def build_model(tag: str, device="cpu"):
+def build_model(tag: str, device="cpu", occ_conf=None):
     from adaptive_city_nerf_amd import MetaContainer, SceneBox
     sc = G.scene()["masks"][G.MASK[tag]]
     K = len(sc["centroids"])
@@ -23,7 +23,7 @@ def build_model(tag: str, device="cpu"):
     m = MetaContainer(num_submodules=K, centroids=torch.tensor(sc["centroids"]), aabb=gbox.aabb,
                       nerf_variant="instant", boundary_margin=min(max(1.0, 1.05), sc["boundary_margin"]),
                       cluster_2d=sc["cluster_2d"], joint_training=False, use_bg_nerf=True, bg_hidden=32,
-                      bg_encoding="spherical", occ_conf={"use_occ": False}, expert_box_list=boxes, hidden=64,
+                      bg_encoding="spherical", occ_conf=occ_conf or {"use_occ": False}, expert_box_list=boxes, hidden=64,
                       sigma_depth=2, color_depth=2, dir_encoding="spherical", color_hidden=64, use_sigmoid_rgb=True,
                       hash_enc_conf=hash_conf)
     return m.to(device), gbox
@@ -160,3 +160,22 @@ def test_autograd_path_matches_fused_forward_and_trains():
                                 allow_unused=True)
     assert all(g is not None and torch.isfinite(g).all() for g in grads[:14])
     assert grads[-1] is not None and grads[-1].abs().sum() > 0
+
+
+@pytest.mark.parametrize("tag", ["k1", "k4"])
+def test_occupancy_state_dict_matches_reference(tag):
+    """use_occ: the expert's scene_aabb buffer and the occupancy grid's nerfacc buffers (resolution,
+    aabbs, occs, binaries) appear under the reference's keys and load from its checkpoint."""
+    from test_occ_gpu import occ_conf
+    d = G.load(f"occ_{tag}")
+    m, _ = build_model(tag, occ_conf=occ_conf())
+    K = len(m.submodules)
+    sd = reference_state_dict(d, K)
+    assert set(m.state_dict().keys()) == set(sd.keys())
+    m.load_state_dict(sd)
+    for k in range(K):
+        g = m.submodules[k].occ_grid
+        assert g.binaries.shape == (2, 32, 32, 32) and g.resolution.tolist() == [32, 32, 32]
+        np.testing.assert_array_equal(g.aabbs.numpy(), d[f"expert{k}:aabbs"])
+        assert m.submodules[k].render_step_size == float(d[f"expert{k}:render_step_size"])
+    assert m.use_occ and m.occ_ready
