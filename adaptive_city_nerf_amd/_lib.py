@@ -89,9 +89,10 @@ SIGNATURES = {
     "acn_grad_sumsq": ([vp, vp, i64, vp, vp, vp], C.c_int),
     "acn_clip_coef": ([vp, f32, vp, vp], C.c_int),
     "acn_adam_step": ([vp, vp, i64, vp, i32, vp, vp], C.c_int),
-    "acn_occ_traverse": ([vp, i64, vp, i64, i64, vp, vp, vp, vp, i32, vp, f32, f32, vp, vp, i64, vp, vp, vp, vp, vp,
-                          vp],
+    "acn_occ_traverse": ([vp, i64, vp, i64, i64, vp, vp, vp, vp, i32, vp, f32, f32, vp, vp, i64, i64, vp, vp, vp, vp,
+                          vp, vp],
                          C.c_int),
+    "acn_occ_compact": ([vp, vp, i64, vp, vp, i64, vp, vp, vp, vp], C.c_int),
     "acn_occ_union": ([i32, i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp], C.c_int),
     "acn_render_packed_fwd": ([vp, i64, i64, vp, vp, vp, vp, vp, vp, i32, vp, vp, sz, vp, vp, vp, vp, vp], C.c_int),
     "acn_packed_weights_fwd": ([vp, vp, vp, vp, vp, i64, vp, vp, vp, vp], C.c_int),

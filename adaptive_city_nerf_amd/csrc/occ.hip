@@ -95,51 +95,120 @@ struct TraverseArgs {
     float* t1;
 };
 
+// Per-ray event list of traverse_grids: the 2L entry/exit times of the nested level boxes, sorted
+// (stable, ties keep index order, as torch.sort on the cat([t_mins, t_maxs]) of nerfacc).
+struct RayEvents {
+    float ts[2 * kOccMaxLevels];
+    int ti[2 * kOccMaxLevels];
+    bool hit[kOccMaxLevels];
+};
+
+__device__ __forceinline__ void ray_events(const TraverseArgs& a, const float o[3], const float d[3], RayEvents& ev) {
+    const int L = a.L;
+    for (int l = 0; l < L; ++l) {
+        float x, y;
+        ev.hit[l] = ray_aabb_slab(o, d, a.aabbs[l], -INFINITY, INFINITY, INFINITY, x, y);
+        ev.ts[l] = x;
+        ev.ts[L + l] = y;
+    }
+    for (int i = 0; i < 2 * L; ++i) ev.ti[i] = i;
+    for (int i = 1; i < 2 * L; ++i) {
+        const float v = ev.ts[i];
+        const int x = ev.ti[i];
+        int j = i - 1;
+        while (j >= 0 && ev.ts[j] > v) { ev.ts[j + 1] = ev.ts[j]; ev.ti[j + 1] = ev.ti[j]; --j; }
+        ev.ts[j + 1] = v;
+        ev.ti[j + 1] = x;
+    }
+}
+
+// Level interval of event i (the finest level containing the ray between events i and i+1) or -1.
+__device__ __forceinline__ int interval_level(const TraverseArgs& a, const RayEvents& ev, int i, float near_plane,
+                                              float far_plane, float& this_tmin, float& this_tmax) {
+    const int L = a.L;
+    const bool entering = ev.ti[i] < L;
+    int level = ev.ti[i] % L;
+    if (!ev.hit[level]) return -1;
+    if (!entering) {
+        if (ev.ti[i + 1] < L) return -1;  // leaving into the outside
+        level = ev.ti[i + 1] % L;
+        if (!ev.hit[level]) return -1;
+    }
+    this_tmin = fmaxf(ev.ts[i], near_plane);
+    this_tmax = fminf(ev.ts[i + 1], far_plane);
+    if (!(this_tmin < this_tmax)) return -1;
+    return level;
+}
+
+// 3-D DDA over one level's grid between this_tmin and this_tmax (nerfacc setup_traversal /
+// single_traversal, eps 1e-6 at both ends).
+struct Dda {
+    int cur[3], ovf[3], stp[3];
+    float tdist[3], delta[3];
+    int64_t lbase;
+};
+
+__device__ __forceinline__ void dda_setup(const TraverseArgs& a, const float o[3], const float d[3],
+                                          const float inv[3], int level, float this_tmin, float this_tmax, Dda& g) {
+    const int res[3] = {a.rx, a.ry, a.rz};
+    const float eps = 1e-6f;
+    const float* bmin = a.aabbs[level];
+    const float* bmax = bmin + 3;
+#pragma unroll
+    for (int ax = 0; ax < 3; ++ax) {
+        const float r = (float)res[ax];
+        const float vs = (bmax[ax] - bmin[ax]) / r;
+        const float ps = o[ax] + d[ax] * (this_tmin + eps);
+        const float pe = o[ax] + d[ax] * (this_tmax - eps);
+        g.cur[ax] = cell_index((ps - bmin[ax]) / (bmax[ax] - bmin[ax]) * r, res[ax]);
+        const int fin = cell_index((pe - bmin[ax]) / (bmax[ax] - bmin[ax]) * r, res[ax]);
+        const int start = g.cur[ax] + (d[ax] > 0.0f ? 1 : 0);
+        const float tm = ((bmin[ax] + ((float)start * vs)) - o[ax]) * inv[ax];
+        g.tdist[ax] = d[ax] == 0.0f ? this_tmax : tm;
+        const float sf = d[ax] == 0.0f ? 0.0f : (d[ax] > 0.0f ? 1.0f : -1.0f);
+        g.stp[ax] = (int)sf;
+        const float dtmp = vs * inv[ax] * sf;
+        g.delta[ax] = d[ax] == 0.0f ? this_tmax : dtmp;
+        g.ovf[ax] = fin + g.stp[ax];
+    }
+    g.lbase = (int64_t)level * ((int64_t)a.rx * a.ry * a.rz);
+}
+
+__device__ __forceinline__ int64_t dda_cell(const TraverseArgs& a, const Dda& g) {
+    return g.lbase + ((int64_t)g.cur[0] * a.ry + g.cur[1]) * a.rz + g.cur[2];
+}
+
+// single_traversal; false when the walk leaves the interval (overflow index, or -- a guard nerfacc
+// lacks, where it would read out of bounds -- the grid)
+__device__ __forceinline__ bool dda_step(const TraverseArgs& a, Dda& g) {
+    const int res[3] = {a.rx, a.ry, a.rz};
+    int ax;
+    if (g.tdist[0] < g.tdist[1] && g.tdist[0] < g.tdist[2]) ax = 0;
+    else if (g.tdist[1] < g.tdist[2]) ax = 1;
+    else ax = 2;
+    g.cur[ax] += g.stp[ax];
+    g.tdist[ax] += g.delta[ax];
+    if (g.cur[ax] == g.ovf[ax]) return false;
+    if (g.cur[ax] < 0 || g.cur[ax] >= res[ax]) return false;
+    return true;
+}
+
 __device__ __forceinline__ bool occupied(const uint32_t* bits, int64_t cell) {
     return (bits[cell >> 5] >> (cell & 31)) & 1u;
 }
 
-// One ray of traverse_grids (oracle/occ_oracle.c traverse_ray, same float op order).
-__device__ int64_t traverse_ray(const TraverseArgs& a, const float o[3], const float d[3], float near_plane,
-                                float far_plane, float* t0, float* t1) {
-    const int L = a.L;
-    float ts[2 * kOccMaxLevels];
-    int ti[2 * kOccMaxLevels];
-    bool hit[kOccMaxLevels];
-    for (int l = 0; l < L; ++l) {
-        float x, y;
-        hit[l] = ray_aabb_slab(o, d, a.aabbs[l], -INFINITY, INFINITY, INFINITY, x, y);
-        ts[l] = x;
-        ts[L + l] = y;
-    }
-    for (int i = 0; i < 2 * L; ++i) ti[i] = i;
-    for (int i = 1; i < 2 * L; ++i) {  // stable insertion sort by value
-        const float v = ts[i];
-        const int x = ti[i];
-        int j = i - 1;
-        while (j >= 0 && ts[j] > v) { ts[j + 1] = ts[j]; ti[j + 1] = ti[j]; --j; }
-        ts[j + 1] = v;
-        ti[j + 1] = x;
-    }
-    const int res[3] = {a.rx, a.ry, a.rz};
-    const float inv[3] = {1.0f / d[0], 1.0f / d[1], 1.0f / d[2]};
-    const float eps = 1e-6f;
-    const int64_t cells = (int64_t)a.rx * a.ry * a.rz;
+// One ray of traverse_grids (oracle/occ_oracle.c traverse_ray, same float op order).  Writes at most
+// `cap` samples to t0/t1 (if non-NULL) and returns the full sample count.
+__device__ int64_t traverse_ray(const TraverseArgs& a, const RayEvents& ev, const float o[3], const float d[3],
+                                const float inv[3], float near_plane, float far_plane, int64_t cap, float* t0,
+                                float* t1) {
     int64_t n = 0, budget = kOccMaxIters;
     float t_last = near_plane;
     bool continuous = false;
-    for (int i = 0; i < 2 * L - 1; ++i) {
-        const bool entering = ti[i] < L;
-        int level = ti[i] % L;
-        if (!hit[level]) continue;
-        if (!entering) {
-            if (ti[i + 1] < L) continue;
-            level = ti[i + 1] % L;
-            if (!hit[level]) continue;
-        }
-        const float this_tmin = fmaxf(ts[i], near_plane);
-        const float this_tmax = fminf(ts[i + 1], far_plane);
-        if (!(this_tmin < this_tmax)) continue;
+    for (int i = 0; i < 2 * a.L - 1; ++i) {
+        float this_tmin, this_tmax;
+        const int level = interval_level(a, ev, i, near_plane, far_plane, this_tmin, this_tmax);
+        if (level < 0) continue;
         if (!continuous) {
             for (;;) {
                 if (--budget < 0) return n;
@@ -148,33 +217,12 @@ __device__ int64_t traverse_ray(const TraverseArgs& a, const float o[3], const f
                 t_last += dt;
             }
         }
-        const float* bmin = a.aabbs[level];
-        const float* bmax = bmin + 3;
-        int cur[3], fin[3], stp[3];
-        float tdist[3], delta[3];
-#pragma unroll
-        for (int ax = 0; ax < 3; ++ax) {
-            const float r = (float)res[ax];
-            const float vs = (bmax[ax] - bmin[ax]) / r;
-            const float ps = o[ax] + d[ax] * (this_tmin + eps);
-            const float pe = o[ax] + d[ax] * (this_tmax - eps);
-            cur[ax] = cell_index((ps - bmin[ax]) / (bmax[ax] - bmin[ax]) * r, res[ax]);
-            fin[ax] = cell_index((pe - bmin[ax]) / (bmax[ax] - bmin[ax]) * r, res[ax]);
-            const int start = cur[ax] + (d[ax] > 0.0f ? 1 : 0);
-            const float tm = ((bmin[ax] + ((float)start * vs)) - o[ax]) * inv[ax];
-            tdist[ax] = d[ax] == 0.0f ? this_tmax : tm;
-            const float sf = d[ax] == 0.0f ? 0.0f : (d[ax] > 0.0f ? 1.0f : -1.0f);
-            stp[ax] = (int)sf;
-            const float dtmp = vs * inv[ax] * sf;
-            delta[ax] = d[ax] == 0.0f ? this_tmax : dtmp;
-        }
-        const int ovf[3] = {fin[0] + stp[0], fin[1] + stp[1], fin[2] + stp[2]};
-        const int64_t lbase = (int64_t)level * cells;
+        Dda g;
+        dda_setup(a, o, d, inv, level, this_tmin, this_tmax, g);
         for (;;) {
-            float t_trav = fminf(tdist[0], fminf(tdist[1], tdist[2]));
+            float t_trav = fminf(g.tdist[0], fminf(g.tdist[1], g.tdist[2]));
             t_trav = fminf(t_trav, this_tmax);
-            const int64_t cell = lbase + ((int64_t)cur[0] * res[1] + cur[1]) * res[2] + cur[2];
-            if (!occupied(a.bits, cell)) {
+            if (!occupied(a.bits, dda_cell(a, g))) {
                 for (;;) {
                     if (--budget < 0) return n;
                     const float dt = calc_dt(t_last, a.cone, a.step);
@@ -188,7 +236,7 @@ __device__ int64_t traverse_ray(const TraverseArgs& a, const float o[3], const f
                     const float dt = calc_dt(t_last, a.cone, a.step);
                     if (t_last + dt * 0.5f >= t_trav) break;
                     const float t_next = t_last + dt;
-                    if (t0) { t0[n] = t_last; t1[n] = t_next; }
+                    if (t0 && n < cap) { t0[n] = t_last; t1[n] = t_next; }
                     ++n;
                     continuous = true;
                     t_last = t_next;
@@ -196,20 +244,16 @@ __device__ int64_t traverse_ray(const TraverseArgs& a, const float o[3], const f
                 }
             }
             if (--budget < 0) return n;
-            int ax;
-            if (tdist[0] < tdist[1] && tdist[0] < tdist[2]) ax = 0;
-            else if (tdist[1] < tdist[2]) ax = 1;
-            else ax = 2;
-            cur[ax] += stp[ax];
-            tdist[ax] += delta[ax];
-            if (cur[ax] == ovf[ax]) break;
-            if (cur[ax] < 0 || cur[ax] >= res[ax]) break;
+            if (!dda_step(a, g)) break;
         }
     }
     return n;
 }
 
-__global__ void __launch_bounds__(256) occ_traverse_kernel(TraverseArgs a) {
+// offsets == NULL: counts[i] <- samples of ray i, and with cap > 0 its first cap samples are written
+// to the scratch rows t0/t1 + i * cap (single-pass mode, compacted by occ_compact_kernel); offsets !=
+// NULL: ray i writes all its samples at offsets[i] (second pass of the two-pass mode).
+__global__ void __launch_bounds__(64) occ_traverse_kernel(TraverseArgs a, int64_t cap) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.N) return;
     const float* po = a.rays_o + i * a.ld_o;
@@ -220,13 +264,33 @@ __global__ void __launch_bounds__(256) occ_traverse_kernel(TraverseArgs a) {
         if (!a.offsets) a.counts[i] = 0;
         return;
     }
+    RayEvents ev;
+    ray_events(a, o, d, ev);
+    const float inv[3] = {1.0f / d[0], 1.0f / d[1], 1.0f / d[2]};
     if (!a.offsets) {
-        a.counts[i] = traverse_ray(a, o, d, nr, fr, nullptr, nullptr);
+        a.counts[i] = traverse_ray(a, ev, o, d, inv, nr, fr, cap, cap > 0 ? a.t0 + i * cap : nullptr,
+                                   cap > 0 ? a.t1 + i * cap : nullptr);
         return;
     }
     const int64_t b = a.offsets[i];
-    const int64_t n = traverse_ray(a, o, d, nr, fr, a.t0 + b, a.t1 + b);
+    const int64_t n = traverse_ray(a, ev, o, d, inv, nr, fr, INT64_MAX, a.t0 + b, a.t1 + b);
     for (int64_t k = 0; k < n; ++k) a.ray_idx[b + k] = i;
+}
+
+// single-pass mode: scratch rows (cap per ray) -> packed arrays at the scanned offsets, wave per ray
+__global__ void __launch_bounds__(256) occ_compact_kernel(const float* s0, const float* s1, int64_t cap,
+                                                          const int64_t* counts, const int64_t* offsets, int64_t N,
+                                                          int64_t* ray_idx, float* t0, float* t1) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < N; r += nw) {
+        const int64_t n = counts[r], b = offsets[r];
+        for (int64_t k = lane; k < n; k += 64) {
+            t0[b + k] = s0[r * cap + k];
+            t1[b + k] = s1[r * cap + k];
+            ray_idx[b + k] = r;
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -565,12 +629,17 @@ inline unsigned blocks(int64_t n, int per = 256) { return (unsigned)((n + per - 
 }  // namespace
 
 // ==========================================================================================
+static unsigned ray_waves_grid(int64_t N) {
+    const int64_t wgs = (N + 3) / 4;  // 4 waves (rays) per 256-thread block
+    return (unsigned)(wgs < 4096 ? (wgs < 1 ? 1 : wgs) : 4096);
+}
+
 extern "C" int acn_occ_traverse(const float* rays_o, int64_t ld_o, const float* rays_d, int64_t ld_d, int64_t N,
                                 const float* near_planes, const float* far_planes, const uint32_t* bits,
                                 const float* aabbs, int levels, const int32_t* res, float step_size, float cone_angle,
                                 const float* prefilter_aabb, const float* prefilter_near_far, int64_t ld_pf,
-                                int64_t* counts, const int64_t* offsets, int64_t* ray_indices, float* t_starts,
-                                float* t_ends, void* stream) {
+                                int64_t cap, int64_t* counts, const int64_t* offsets, int64_t* ray_indices,
+                                float* t_starts, float* t_ends, void* stream) {
     ACN_REQUIRE(N >= 0, "acn_occ_traverse: N must be >= 0");
     if (N == 0) return ACN_OK;
     ACN_REQUIRE(levels >= 1 && levels <= kOccMaxLevels, "acn_occ_traverse: levels must be in [1, %d], got %d",
@@ -580,8 +649,9 @@ extern "C" int acn_occ_traverse(const float* rays_o, int64_t ld_o, const float* 
     ACN_REQUIRE(cone_angle >= 0.0f, "acn_occ_traverse: cone_angle must be >= 0");
     ACN_REQUIRE(rays_o && rays_d && near_planes && far_planes && bits && aabbs, "acn_occ_traverse: NULL pointer");
     ACN_REQUIRE(ld_o >= 3 && ld_d >= 3, "acn_occ_traverse: rays must be (N, >=3)");
+    ACN_REQUIRE(cap >= 0, "acn_occ_traverse: cap must be >= 0");
     if (offsets) ACN_REQUIRE(ray_indices && t_starts && t_ends, "acn_occ_traverse: NULL fill output");
-    else ACN_REQUIRE(counts, "acn_occ_traverse: NULL counts");
+    else ACN_REQUIRE(counts && (cap == 0 || (t_starts && t_ends)), "acn_occ_traverse: NULL count / scratch output");
     TraverseArgs a{};
     a.rays_o = rays_o; a.rays_d = rays_d; a.ld_o = ld_o; a.ld_d = ld_d; a.N = N;
     a.near = near_planes; a.far = far_planes; a.bits = bits;
@@ -597,8 +667,20 @@ extern "C" int acn_occ_traverse(const float* rays_o, int64_t ld_o, const float* 
         a.ld_pf = ld_pf;
     }
     a.counts = counts; a.offsets = offsets; a.ray_idx = ray_indices; a.t0 = t_starts; a.t1 = t_ends;
-    hipLaunchKernelGGL(occ_traverse_kernel, dim3(blocks(N)), dim3(256), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(occ_traverse_kernel, dim3(blocks(N, 64)), dim3(64), 0, (hipStream_t)stream, a,
+                       offsets ? (int64_t)0 : cap);
     return acn_check_launch("acn_occ_traverse");
+}
+
+extern "C" int acn_occ_compact(const float* scratch_t0, const float* scratch_t1, int64_t cap, const int64_t* counts,
+                               const int64_t* offsets, int64_t N, int64_t* ray_indices, float* t_starts, float* t_ends,
+                               void* stream) {
+    if (N == 0) return ACN_OK;
+    ACN_REQUIRE(scratch_t0 && scratch_t1 && counts && offsets && ray_indices && t_starts && t_ends && cap > 0,
+                "acn_occ_compact: bad arguments");
+    hipLaunchKernelGGL(occ_compact_kernel, dim3(ray_waves_grid(N)), dim3(256), 0, (hipStream_t)stream, scratch_t0,
+                       scratch_t1, cap, counts, offsets, N, ray_indices, t_starts, t_ends);
+    return acn_check_launch("acn_occ_compact");
 }
 
 extern "C" int acn_occ_union(int K, int64_t N, const int64_t* const* starts, const int64_t* const* counts,
@@ -619,11 +701,6 @@ extern "C" int acn_occ_union(int K, int64_t N, const int64_t* const* starts, con
     a.out_counts = out_counts; a.offsets = offsets; a.ray_idx = ray_indices; a.m0 = m_starts; a.m1 = m_ends;
     hipLaunchKernelGGL(occ_union_kernel, dim3(blocks(N)), dim3(256), 0, (hipStream_t)stream, a);
     return acn_check_launch("acn_occ_union");
-}
-
-static unsigned ray_waves_grid(int64_t N) {
-    const int64_t wgs = (N + 3) / 4;  // 4 waves (rays) per 256-thread block
-    return (unsigned)(wgs < 4096 ? (wgs < 1 ? 1 : wgs) : 4096);
 }
 
 extern "C" int acn_packed_weights_fwd(const float* sigmas, const float* t_starts, const float* t_ends,

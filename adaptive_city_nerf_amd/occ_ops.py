@@ -18,6 +18,10 @@ from ._lib import AcnError, check, ptr, require_hip, stream_of
 from .ops import _experts_array, _f32, pack_experts
 
 I64 = torch.int64
+# single-pass traversal: per-ray scratch rows of SINGLE_PASS_CAP samples while the scratch stays under
+# SINGLE_PASS_SCRATCH_BYTES (larger batches, or a ray with more samples, take the count + fill passes)
+SINGLE_PASS_CAP = 1024
+SINGLE_PASS_SCRATCH_BYTES = 256 << 20
 
 
 def _host_floats(vals) -> C.Array:
@@ -76,17 +80,30 @@ def traverse(rays_o: torch.Tensor, rays_d: torch.Tensor, near: torch.Tensor, far
     counts = torch.empty(N, device=dev, dtype=I64)
     lib = _lib.lib()
     s = stream_of(o)
-    check(lib.acn_occ_traverse(ptr(o), o.stride(0), ptr(d), d.stride(0), N, ptr(nr), ptr(fr), ptr(bits), ab, L, rs,
-                               float(step_size), float(cone_angle), pf, ptr(pnf), ld_pf, ptr(counts), None, None, None, None, s),
-          "acn_occ_traverse(count)")
-    starts, M = scan_counts(counts)
+    args = (ptr(o), o.stride(0), ptr(d), d.stride(0), N, ptr(nr), ptr(fr), ptr(bits), ab, L, rs, float(step_size),
+            float(cone_angle), pf, ptr(pnf), ld_pf)
+    cap = SINGLE_PASS_CAP if N * SINGLE_PASS_CAP * 8 <= SINGLE_PASS_SCRATCH_BYTES else 0
+    if cap:  # single march into per-ray scratch rows, then a wave-per-ray compaction
+        scratch = torch.empty(2, N, cap, device=dev, dtype=torch.float32)
+        check(lib.acn_occ_traverse(*args, cap, ptr(counts), None, None, ptr(scratch[0]), ptr(scratch[1]), s),
+              "acn_occ_traverse(single pass)")
+        incl = torch.cumsum(counts, 0)
+        M, cmax = [int(v) for v in torch.stack([incl[-1], counts.max()]).cpu()] if N else (0, 0)
+        starts = incl - counts
+    else:
+        check(lib.acn_occ_traverse(*args, 0, ptr(counts), None, None, None, None, s), "acn_occ_traverse(count)")
+        starts, M = scan_counts(counts)
+        cmax = None
     ri = torch.empty(M, device=dev, dtype=I64)
     t0 = torch.empty(M, device=dev, dtype=torch.float32)
     t1 = torch.empty(M, device=dev, dtype=torch.float32)
     if M > 0:
-        check(lib.acn_occ_traverse(ptr(o), o.stride(0), ptr(d), d.stride(0), N, ptr(nr), ptr(fr), ptr(bits), ab, L,
-                                   rs, float(step_size), float(cone_angle), pf, ptr(pnf), ld_pf, None, ptr(starts),
-                                   ptr(ri), ptr(t0), ptr(t1), s), "acn_occ_traverse(fill)")
+        if cap and cmax <= cap:
+            check(lib.acn_occ_compact(ptr(scratch[0]), ptr(scratch[1]), cap, ptr(counts), ptr(starts), N, ptr(ri),
+                                      ptr(t0), ptr(t1), s), "acn_occ_compact")
+        else:  # some ray overflowed its scratch row (or no scratch): march again straight into place
+            check(lib.acn_occ_traverse(*args, 0, None, ptr(starts), ptr(ri), ptr(t0), ptr(t1), s),
+                  "acn_occ_traverse(fill)")
     return ri, t0, t1, starts, counts
 
 

@@ -52,7 +52,7 @@ FP32_MFMA_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 matrix = vector pea
 HBM_PEAK_GBS = 8000.0
 
 
-def build_model(device, n_experts=1, seed=0, table_seed=100, table_scale=0.5, fill=None):
+def build_model(device, n_experts=1, seed=0, table_seed=100, table_scale=0.5, fill=None, occ_conf=None):
     from adaptive_city_nerf_amd import MetaContainer, SceneBox
     from adaptive_city_nerf_amd.synthetic import formula_table, grid_layout
     scene = json.loads((REPO / "tests" / "golden" / "scene_drz_example.json").read_text())
@@ -68,7 +68,8 @@ def build_model(device, n_experts=1, seed=0, table_seed=100, table_scale=0.5, fi
     torch.manual_seed(seed)
     m = MetaContainer(num_submodules=K, centroids=torch.tensor(sc["centroids"]), aabb=gbox.aabb,
                       nerf_variant="instant", boundary_margin=min(max(1.0, 1.05), sc["boundary_margin"]),
-                      cluster_2d=sc["cluster_2d"], use_bg_nerf=True, bg_hidden=32, occ_conf={"use_occ": False},
+                      cluster_2d=sc["cluster_2d"], use_bg_nerf=True, bg_hidden=32,
+                      occ_conf=occ_conf or {"use_occ": False},
                       expert_box_list=boxes, hidden=64, sigma_depth=2, color_depth=2, dir_encoding="spherical",
                       color_hidden=64, use_sigmoid_rgb=True,
                       hash_enc_conf={"levels": 16, "features_per_level": 2, "log2_hashmap_size": 20,
@@ -159,6 +160,35 @@ def cpu_baseline_train(model, sc, rays, rgbs, S, expert, min_seconds):
                       f"{dt:.1f} s"}
 
 
+def cpu_baseline_occ(model, rays, gpu_rgb, min_seconds):
+    """Occupancy renderer on the host cores: oracle/occ_ref.render_expert_occ (C traversal + C field +
+    numpy compositing) over the same rays and grid, repeated until >= min_seconds."""
+    from oracle import occ_ref as R
+    from oracle import oracle as O
+    sub = model.submodules[0]
+    w = {n: p.detach().cpu().numpy() for n, p in sub.meta_named_parameters()}
+    e = O.Expert(w, sub.xyz_encoder.hash_table.detach().cpu().numpy(), np.array(sub.xyz_encoder._res_host, np.int32),
+                 sub.scene_box.min.cpu().numpy(), sub.aabb_extent.cpu().numpy())
+    b = sub.occ_grid.binaries.cpu().numpy()
+    ab = sub.occ_grid.aabbs.cpu().numpy()
+    r = rays.cpu().numpy()
+    reps, n, t0 = 0, 0, time.perf_counter()
+    while True:
+        orgb, _, wts, _, smp = R.render_expert_occ(e, r, b, ab, sub.render_step_size, sub.cone_angle)
+        reps += 1
+        n += len(smp[1])
+        if time.perf_counter() - t0 >= min_seconds:
+            break
+    dt = time.perf_counter() - t0
+    mse = float(np.mean((gpu_rgb.astype(np.float64) - orgb.astype(np.float64)) ** 2))
+    psnr = float("inf") if mse == 0 else -10.0 * np.log10(mse)
+    cores = O.max_threads()
+    return {"value": n / dt, "unit": "ray-samples/s", "cores": cores, "kind": "port",
+            "sample": f"{reps} x {r.shape[0]} rays ({n // reps} marched samples) of the benchmark batch, "
+                      f"oracle/occ_ref.py (C traversal and field with OpenMP {cores} threads, numpy compositing), "
+                      f"{dt:.1f} s"}, psnr, float(np.sqrt(mse)), float(np.max(np.abs(gpu_rgb - orgb)))
+
+
 def load_traffic():
     p = REPO / "profiles" / "pmc_render_r01.json"
     if p.exists():
@@ -174,7 +204,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c2")
+    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "occ"], default="c2")
     ap.add_argument("--rays", type=int, default=4096, help="rays per GPU (c2, c3)")
     ap.add_argument("--samples", type=int, default=256)
     ap.add_argument("--frame", type=int, default=800, help="frame side (c4)")
@@ -195,8 +225,13 @@ def main():
 
     from adaptive_city_nerf_amd import ops, parallel, render_rays
     S = a.samples
-    K = {"c2": 1, "c3": 4, "c4": 8, "c5": 8}[a.workload]
-    model, gbox, scene, sc = build_model(device, K, fill=[rank % K] if a.workload == "c5" else None)
+    K = {"c2": 1, "c3": 4, "c4": 8, "c5": 8, "occ": 1}[a.workload]
+    occ_conf = None
+    if a.workload == "occ":  # nerf_runner.py:124-147 defaults: 128^3 x 4 levels, cone 0.004, step diag/1000
+        occ_conf = {"use_occ": True, "resolution": 128, "levels": 4, "render_step_size": None, "cone_angle": 0.004,
+                    "occ_thre": 1e-2, "alpha_thre": 1e-2, "warmup_steps": 256, "update_interval": 16}
+    model, gbox, scene, sc = build_model(device, K, fill=[rank % K] if a.workload == "c5" else None,
+                                         occ_conf=occ_conf)
 
     if a.workload == "c2":
         rays = make_rays(scene, gbox, device, a.rays, 1234 + rank)
@@ -205,6 +240,24 @@ def main():
         def step():
             with torch.no_grad():
                 return render_rays(model, rays, ray_samples=S, bg_color_default="white")
+        sample_rays = rays
+    elif a.workload == "occ":
+        from adaptive_city_nerf_amd import occ_ops
+        sub = model.submodules[0]
+        model.train()
+        sub.maybe_update_occ_grid(step=0)          # warmup update: every cell's density -> binaries
+        model.eval()
+        sub.occ_ready = True
+        rays = make_rays(scene, gbox, device, a.rays, 1234 + rank)
+        with torch.no_grad():
+            _, t0s, _ = sub.occupancy_marching(rays)
+        occ_samples = int(t0s.numel())
+        samples_per_step = world * occ_samples
+        occ_frac = float(sub.occ_grid.binaries.float().mean())
+
+        def step():
+            with torch.no_grad():
+                return render_rays(model, rays, bg_color_default="white", active_module=0)
         sample_rays = rays
     elif a.workload == "c3":
         # global batch (identical on every rank), sharded by owning expert; gather of rendered rays
@@ -261,6 +314,8 @@ def main():
         out = step()
     torch.cuda.synchronize()
     ops.EVENT_HOOK = []
+    if a.workload == "occ":
+        occ_ops.EVENT_HOOK = ops.EVENT_HOOK
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -298,7 +353,9 @@ def main():
     kname = {"c5": "adam_kernel (fused clip + Adam over the adapted expert + background head)",
              "c2": "render_kernel<1,1,0> (fused stratified render, 1 expert)",
              "c3": "render_kernel<1,0,1> (fused stratified render, soft routing over 4 experts)",
-             "c4": "render_kernel<1,0,1> (fused stratified render, soft routing over 8 experts)"}[a.workload]
+             "c4": "render_kernel<1,0,1> (fused stratified render, soft routing over 8 experts)",
+             "occ": "occ_render_kernel<1,1,0> (fused occupancy render over packed marched samples, 1 expert)"
+             }[a.workload]
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
                 "traffic": (tr or {}).get("hbm_bytes_per_launch"),
@@ -315,7 +372,10 @@ def main():
     cpu, psnr, rmse, maxerr = None, None, None, None
     if rank == 0 and not a.no_cpu_baseline and a.workload == "c5":
         cpu = cpu_baseline_train(model, sc, pool[0], gtp[0], S, expert, a.cpu_seconds)
-    if rank == 0 and not a.no_cpu_baseline and a.workload != "c5":
+    if rank == 0 and not a.no_cpu_baseline and a.workload == "occ":
+        idx = torch.arange(rays.shape[0], device=device)[: a.cpu_rays]
+        cpu, psnr, rmse, maxerr = cpu_baseline_occ(model, rays[idx], out[0][idx].cpu().numpy(), a.cpu_seconds)
+    if rank == 0 and not a.no_cpu_baseline and a.workload not in ("c5", "occ"):
         rgb_all = out[0].reshape(-1, 3)
         if a.workload == "c2":
             idx = torch.arange(rays.shape[0], device=device)[: a.cpu_rays]
@@ -338,7 +398,13 @@ def main():
                "c5": {"workload": f"C5: online adaptation, 8-expert container, rank r adapts expert r on 1000-ray x "
                                   f"{S}-sample batches (train render + MSE + backward + fused clip/Adam), shared "
                                   f"background grads + clip norm all-reduced", "rays_per_step_per_gpu": 1000,
-                      "experts": 8}}[a.workload]
+                      "experts": 8},
+               "occ": {"workload": f"occupancy renderer (render_expert_occ): {a.rays} rays per GPU marched through a "
+                                   f"128^3 x 4-level grid (warmup-updated from the field, "
+                                   f"{100 * occ_frac if a.workload == 'occ' else 0:.1f}% cells occupied), step "
+                                   f"diag/1000, cone 0.004; metric counts marched samples",
+                       "rays_per_gpu": a.rays, "experts": 1,
+                       "marched_samples_per_gpu": occ_samples if a.workload == "occ" else None}}[a.workload]
         cfg.update({"samples_per_ray": S, "parallelism": f"ray-sharded x{world}"})
         line = {
             "metric": "ray-samples/sec + PSNR, 4096 rays×256 samples, 1/2/4/8 MI355X",

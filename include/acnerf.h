@@ -231,14 +231,23 @@ int acn_adam_step(const acn_param_desc* descs, const int32_t* chunk_tensor, int6
  * cells, aabbs host (levels, 6) [min3, max3]).  bits: the `binaries` buffer as one bit per cell
  * (acn_occ_pack_bits).  near/far (N) device.  prefilter_aabb (host [min3, max3]) or NULL: rays that
  * miss it over [near, far] = prefilter_near_far[i * ld_pf + {0, 1}] (the rays' own columns;
- * ray_rendering.py:170-193 _intersect_rays_aabb) get no samples.  Two passes: offsets == NULL ->
- * counts (N) per ray; else the samples of ray i are written at offsets[i].                      */
+ * ray_rendering.py:170-193 _intersect_rays_aabb) get no samples.
+ * offsets == NULL: counts (N) <- samples per ray; with cap > 0 the first cap samples of ray i are also
+ *   written to the scratch rows t_starts/t_ends + i * cap (single pass; acn_occ_compact packs them
+ *   when every count <= cap).
+ * offsets != NULL: ray i writes all its samples at offsets[i] (ray_indices, t_starts, t_ends).      */
 int acn_occ_traverse(const float* rays_o, int64_t ld_o, const float* rays_d, int64_t ld_d, int64_t N,
                      const float* near_planes, const float* far_planes, const uint32_t* bits,
                      const float* aabbs, int levels, const int32_t* res, float step_size, float cone_angle,
-                     const float* prefilter_aabb, const float* prefilter_near_far, int64_t ld_pf,
+                     const float* prefilter_aabb, const float* prefilter_near_far, int64_t ld_pf, int64_t cap,
                      int64_t* counts, const int64_t* offsets, int64_t* ray_indices, float* t_starts,
                      float* t_ends, void* stream);
+
+/* Packs the scratch rows of a single-pass acn_occ_traverse (all counts <= cap) at offsets (the
+ * exclusive scan of counts): ray_indices, t_starts, t_ends (M).                                 */
+int acn_occ_compact(const float* scratch_t0, const float* scratch_t1, int64_t cap, const int64_t* counts,
+                    const int64_t* offsets, int64_t N, int64_t* ray_indices, float* t_starts, float* t_ends,
+                    void* stream);
 
 /* _merge_segments_union (ray_rendering.py:196-258): per ray, the sorted distinct boundaries of the
  * K experts' segments; consecutive pairs become the merged segments.  starts/counts/t_starts/t_ends

@@ -256,6 +256,5 @@ def test_mark_invisible_cells_vs_oracle():
     occs = est.occs.cpu().numpy().reshape(2, -1)
     for lvl in range(2):
         ref = R.mark_invisible(Ks.numpy(), c2w.numpy(), 64, 48, 0.1, est.aabbs[lvl].cpu().numpy(), [24] * 3)
-        mism = int((occs[lvl] != ref).sum())
         assert (occs[lvl] < 0).any() and (occs[lvl] == 0).any()
-        assert mism <= 2, mism  # fp32 (HIP) vs fp64 (oracle) projection at image borders
+        np.testing.assert_array_equal(occs[lvl], ref)
