@@ -1,0 +1,322 @@
+"""Offline meta-training on the HIP path.
+
+Mirrors the reference's pipelines/offline_stage/meta_core.py (``task_adapt`` :14-67, ``meta_update``
+:72-123, ``maml_meta_update`` :126-143, ``reptile_meta_update`` :146-182, ``clip_all_grads``
+:185-194, ``extract_module_params`` :200-211, ``snapshot_params`` :214-216), the ``train_step`` of
+meta_train_step.py:18-253 and the ``compute_loss`` dispatcher of nerfs/losses.py:156-166, with the
+same signatures, the same region / task / inner-loop order (so a run consumes training jitter in
+the reference's order) and the same loss reductions (sample-weighted region sums, FedAvg scaling by
+the number of regions).
+
+Every render goes through the differentiable HIP composition (hash grid forward + scatter-add
+backward, MetaLinear chain on rocBLAS, HIP compositing).  Second-order MAML (``create_graph=True``)
+runs the inner-loop forwards inside ``ray_rendering.second_order()``, which swaps the compositing to
+its twice-differentiable torch form; the hash grid's own backward is never differentiated (fast
+weights are the 14 MLP tensors), so it needs no second derivative.  Autocast is not
+used: the HIP path computes fp32; a GradScaler passed in is honoured as a scaler.
+
+Differences from the reference, all where the reference cannot run as written:
+* Reptile: the reference's train_step calls ``meta_update`` without ``fast_list``
+  (meta_train_step.py:168), so Reptile raises TypeError there; and ``reptile_meta_update`` compares
+  the expert-relative fast names with the container's meta-parameter names, so it never updates.
+  Here train_step collects the adapted fast weights and prefixes them with ``submodules.{cid}.``.
+* Expert parallelism (``group``): rank r processes the regions cid with cid % world == r; the
+  region/query counts, the shared background-head gradients and the clip norm are all-reduced, so
+  the update equals the single-process one (SURVEY §8(e) "Offline meta-training").
+"""
+from __future__ import annotations
+
+import random
+import time
+from collections import OrderedDict
+from typing import Dict, List, Mapping, Optional
+
+import torch
+import torch.distributed as dist
+
+from .optim import FusedAdam
+from .ray_rendering import second_order
+from .train import compute_mse_loss
+
+
+def psnr(mse):
+    return -10.0 * torch.log10(mse + 1e-24)
+
+
+def to_device_tree(x, device):
+    """Recursively move tensors in nested containers to device (common/utils.py:163-175)."""
+    if torch.is_tensor(x):
+        return x.to(device, non_blocking=True)
+    if isinstance(x, Mapping):
+        return {k: to_device_tree(v, device) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        ys = [to_device_tree(v, device) for v in x]
+        return tuple(ys) if isinstance(x, tuple) else ys
+    return x
+
+
+def compute_loss(P, model, data, params=None, active_module=None, **kwargs):
+    """losses.py:156-166.  With P.fim the reference's compute_fim_loss returns the plain MSE whenever
+    the model carries no Fisher store / FIM head (losses.py:78-80) -- the configuration it ships
+     -- so both branches are the MSE here."""
+    return compute_mse_loss(P, model, data, params, active_module)
+
+
+# ============================================================================ model helpers
+def extract_module_params(submodule, copy=True) -> OrderedDict:
+    """Snapshot the submodule's meta-parameters (name -> tensor); copies are fresh leaves (Reptile)."""
+    if copy:
+        return OrderedDict((n, p.detach().clone().requires_grad_(True)) for n, p in submodule.meta_named_parameters())
+    return OrderedDict((n, p) for n, p in submodule.meta_named_parameters())
+
+
+def snapshot_params(model):
+    return {n: p.detach().clone() for n, p in model.meta_named_parameters()}
+
+
+def snapshot_model_dict(model):
+    return {n: p.detach().clone() for n, p in model.state_dict().items()}
+
+
+# ============================================================================ inner loop
+def task_adapt(P, model, support, inner_lr, iterations, active_module=None):
+    """Inner-loop adaptation of the fast weights on a support set (meta_core.py:14-67)."""
+    algo = str(getattr(P, "algo", "")).lower()
+    first_order = algo in ("fomaml", "reptile")
+    base = model.submodules[active_module] if active_module is not None else model
+    fast = extract_module_params(base, copy=(algo == "reptile"))
+    inner_losses = []
+    for _ in range(int(iterations)):
+        with second_order(not first_order):
+            loss = compute_loss(P, model, support, params=fast, active_module=active_module, grad_buffer={},
+                                update_fisher=True)
+        grads = torch.autograd.grad(loss, tuple(fast.values()), create_graph=not first_order, allow_unused=True)
+        fast = OrderedDict((n, w if g is None else (w - inner_lr * g.to(w.dtype)))
+                           for (n, w), g in zip(fast.items(), grads))
+        inner_losses.append(loss.detach())
+    return fast, inner_losses
+
+
+# ============================================================================ outer update
+def clip_all_grads(optimizer, grad_clip=1.0):
+    if grad_clip is None:
+        return
+    params = [p for group in optimizer.param_groups for p in group["params"] if p.grad is not None]
+    if params:
+        torch.nn.utils.clip_grad_norm_(params, grad_clip)
+
+
+def maml_meta_update(optimizer, loss_out, scaler=None, grad_clip=1.0, group=None, shared=None):
+    """Outer MAML/FOMAML step (meta_core.py:126-143); FusedAdam folds the clip into its step."""
+    if not torch.isfinite(loss_out):
+        print(f"[WARN] Skipping meta-update: non-finite loss_out={loss_out.item()}")
+        return
+    optimizer.zero_grad(set_to_none=True)
+    use_amp = scaler is not None and getattr(scaler, "is_enabled", lambda: False)()
+    if use_amp:
+        scaler.scale(loss_out).backward()
+        scaler.unscale_(optimizer)
+        _allreduce_shared_grads(shared, group)
+        clip_all_grads(optimizer, grad_clip)
+        scaler.step(optimizer)
+        scaler.update()
+        return
+    loss_out.backward()
+    _allreduce_shared_grads(shared, group)
+    if isinstance(optimizer, FusedAdam):
+        if shared:
+            optimizer.shared_params = {id(p) for p in shared}
+        optimizer.step(max_norm=grad_clip, sumsq_group=group)
+    else:
+        clip_all_grads(optimizer, grad_clip)
+        optimizer.step()
+
+
+@torch.no_grad()
+def reptile_meta_update(P, model, fast_list):
+    """theta <- theta + lr * mean_i(W_i - theta) over the meta-parameters (meta_core.py:146-182)."""
+    if fast_list is None or len(fast_list) == 0:
+        raise ValueError("Reptile update called with empty fast_list")
+    theta = snapshot_params(model)
+    sum_delta = {k: torch.zeros_like(v) for k, v in theta.items()}
+    for fast in fast_list:
+        for k, v in fast.items():
+            if k in sum_delta:
+                sum_delta[k].add_(v.detach() - theta[k])
+    n = float(len(fast_list))
+    updated = []
+    for name, p in model.meta_named_parameters():
+        if name in sum_delta:
+            delta = sum_delta[name] / n
+            if torch.isfinite(delta).all() and delta.abs().sum() > 0:
+                p.add_(P.lr * delta)
+                updated.append(name)
+    print("Reptile meta-update: updated %d parameter tensors: %s" % (len(updated), ", ".join(updated) or "<none>"))
+
+
+def meta_update(P, model, optimizer, loss_out, scheduler=None, grad_scaler=None, fast_list=None, group=None,
+                shared=None, verbose=True):
+    """Unified outer update (meta_core.py:72-123)."""
+    algo = P.algo.lower()
+    if algo in ("maml", "fomaml"):
+        maml_meta_update(optimizer, loss_out, scaler=grad_scaler, grad_clip=getattr(P, "grad_clip", 1.0),
+                         group=group, shared=shared)
+    elif algo == "reptile":
+        reptile_meta_update(P, model, fast_list=fast_list)
+    else:
+        raise ValueError(f"Unsupported algo {algo!r}")
+    if verbose:
+        with torch.no_grad():  # per-region outer gradient norms, one device->host copy
+            norms = []
+            for expert in model.submodules:
+                sq = [p.grad.double().pow(2).sum() for p in expert.parameters() if p.grad is not None]
+                norms.append(torch.stack(sq).sum() if sq else torch.zeros((), dtype=torch.float64,
+                                                                           device=loss_out.device))
+            for cid, v in enumerate(torch.stack(norms).sqrt().tolist()):
+                print(f"debug/outer_grad_norm_region_{cid}: ", v)
+    if scheduler is not None:
+        scheduler.step()
+    if verbose:
+        print(f"group LRs = {[g['lr'] for g in optimizer.param_groups]}")
+
+
+def _allreduce_shared_grads(shared, group):
+    """Sum the shared (background-head) gradients over the expert-parallel group."""
+    if group is None or not dist.is_initialized() or dist.get_world_size(group) <= 1 or not shared:
+        return
+    grads = [p.grad for p in shared if p.grad is not None]
+    if not grads:
+        return
+    flat = torch.cat([g.reshape(-1) for g in grads])
+    dist.all_reduce(flat, group=group)
+    off = 0
+    for g in grads:
+        g.copy_(flat[off: off + g.numel()].view_as(g))
+        off += g.numel()
+
+
+@torch.no_grad()
+def broadcast_experts(model, group=None):
+    """Expert parallelism: copy every expert's parameters and buffers from its owner rank
+    (cid % world) to all ranks (e.g. before evaluation or a checkpoint)."""
+    if not dist.is_initialized() or dist.get_world_size(group) <= 1:
+        return
+    world = dist.get_world_size(group)
+    for cid, expert in enumerate(model.submodules):
+        src = dist.get_global_rank(group, cid % world) if group is not None else cid % world
+        for t in list(expert.parameters()) + list(expert.buffers()):
+            dist.broadcast(t.data, src=src, group=group)
+
+
+# ============================================================================ one meta step
+def train_step(P, step, model, optimizer, task_data, metric_logger=None, logger=None, scheduler=None,
+               grad_scaler=None, group=None):
+    """One offline meta-training step over tasks grouped by region (meta_train_step.py:18-253).
+
+    ``task_data``: {cid: [task, ...]} with task.support / task.query (or dict keys) holding
+    {"rays": (n, 8), "rgbs": (n, 3)}.  Returns a dict of the step's losses and timings."""
+    t_step_start = time.perf_counter()
+    model.train()
+    device = next(model.parameters()).device
+    time_setup = time_data = time_inner = time_outer = 0.0
+    t0 = time.perf_counter()
+    total_tasks = sum(len(v) for v in task_data.values())
+    cids = list(task_data.keys())
+    rnd = random.Random(getattr(P, "seed", 0) + step)
+    rnd.shuffle(cids)
+    num_regions = len(cids)
+    world, rank = 1, 0
+    if group is not None and dist.is_initialized():
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+    mine = [cid for cid in cids if cid % world == rank]
+    region_inner_sum = {cid: torch.tensor(0.0, device=device) for cid in cids}
+    region_inner_count = {cid: 0 for cid in cids}
+    region_query_sum = {cid: torch.tensor(0.0, device=device) for cid in cids}
+    region_query_count = {cid: 0 for cid in cids}
+    algo = str(getattr(P, "algo", "")).lower()
+    fast_list: List[Dict[str, torch.Tensor]] = []
+    time_setup += time.perf_counter() - t0
+
+    for cid in mine:
+        for task in task_data[cid]:
+            t1 = time.perf_counter()
+            if hasattr(task, "support") and hasattr(task, "query"):
+                sup_i, qry_i = task.support, task.query
+            else:
+                sup_i, qry_i = task["support"], task["query"]
+            sup_i = to_device_tree(sup_i, device)
+            qry_i = to_device_tree(qry_i, device)
+            time_data += time.perf_counter() - t1
+            n_sup, n_q = int(sup_i["rays"].shape[0]), int(qry_i["rays"].shape[0])
+            if n_sup == 0 or n_q == 0:
+                if logger is not None:
+                    logger.log(f"[WARN] Empty task in region {cid}; skipping.")
+                continue
+            t2 = time.perf_counter()
+            fast_i, inner_losses = task_adapt(P, model, sup_i, P.inner_lr, P.inner_iter, active_module=cid)
+            time_inner += time.perf_counter() - t2
+            last_inner = inner_losses[-1] if inner_losses else torch.tensor(0.0, device=device)
+            region_inner_sum[cid] += last_inner.detach() * n_sup
+            region_inner_count[cid] += n_sup
+            if algo == "reptile":
+                fast_list.append({f"submodules.{cid}.{n}": v for n, v in fast_i.items()})
+            t3 = time.perf_counter()
+            loss_q = compute_loss(P, model, qry_i, params=fast_i, active_module=cid)
+            time_outer += time.perf_counter() - t3
+            region_query_sum[cid] += loss_q * n_q
+            region_query_count[cid] += n_q
+
+    total_sup = sum(region_inner_count.values())
+    total_q = sum(region_query_count.values())
+    if world > 1:  # global sample counts
+        c = torch.tensor([float(total_sup), float(total_q)], device=device, dtype=torch.float64)
+        dist.all_reduce(c, group=group)
+        total_sup, total_q = int(c[0]), int(c[1])
+    if total_q == 0:
+        if logger is not None:
+            logger.log("[WARN] train_step_ray: no query samples in any region; skipping step")
+        return None
+    loss_in_local = sum(region_inner_sum[cid] for cid in cids) / max(total_sup, 1)
+    loss_out_local = sum(region_query_sum[cid] for cid in cids) / total_q
+    loss_out_meta = num_regions * loss_out_local  # FedAvg scaled by regions (meta_train_step.py:157-159)
+
+    t4 = time.perf_counter()
+    shared = list(model.bg_mlp.parameters()) if getattr(model, "use_bg_nerf", False) else None
+    meta_update(P, model, optimizer, loss_out_meta, scheduler=scheduler, grad_scaler=grad_scaler,
+                fast_list=fast_list if algo == "reptile" else None, group=group if world > 1 else None,
+                shared=shared)
+    time_outer += time.perf_counter() - t4
+    if getattr(model, "use_occ", False):
+        model.maybe_update_expert_occupancies(step, params=None)
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+    loss_in, loss_out = loss_in_local.detach(), loss_out_local.detach()
+    if world > 1:
+        s = torch.stack([loss_in.double(), loss_out.double()])
+        dist.all_reduce(s, group=group)
+        loss_in, loss_out = s[0].float(), s[1].float()
+    t_total = time.perf_counter() - t_step_start
+    t_misc = max(0.0, t_total - (time_setup + time_data + time_inner + time_outer))
+    out = {"loss_in": float(loss_in), "loss_out": float(loss_out), "psnr_in": float(psnr(loss_in)),
+           "psnr_out": float(psnr(loss_out)), "tasks": total_tasks, "rays_in": total_sup, "rays_out": total_q,
+           "time_setup": time_setup, "time_data": time_data, "time_inner": time_inner, "time_outer": time_outer,
+           "time_misc": t_misc, "time_total_step": t_total}
+    if metric_logger is not None:
+        metric_logger.meters["batch_time"].update(t_total, n=1)
+        metric_logger.meters["tasks"].update(total_tasks, n=1)
+        metric_logger.meters["loss_in"].update(out["loss_in"], n=total_sup)
+        metric_logger.meters["psnr_in"].update(out["psnr_in"], n=total_sup)
+        metric_logger.meters["loss_out"].update(out["loss_out"], n=total_q)
+        metric_logger.meters["psnr_out"].update(out["psnr_out"], n=total_q)
+        if hasattr(metric_logger, "synchronize_between_processes"):
+            metric_logger.synchronize_between_processes()
+    if logger is not None and step % getattr(P, "print_step", 1) == 0:
+        logger.log_dirname(f"Step {step}")
+        for k in ("loss_in", "loss_out", "psnr_in", "psnr_out"):
+            logger.scalar_summary(f"train/{k}", out[k], step)
+        for k in ("time_setup", "time_data", "time_inner", "time_outer", "time_misc", "time_total_step"):
+            logger.scalar_summary(f"train/{k}", out[k], step)
+        logger.log("[TRAIN] [Step %d] [LossIn %.6f] [LossOut %.6f] [PSNRIn %.2f] [PSNROut %.2f] [InnerLR %.6f]"
+                   % (step, out["loss_in"], out["loss_out"], out["psnr_in"], out["psnr_out"], float(P.inner_lr)))
+    return out

@@ -16,12 +16,13 @@ with torch.rand_like, ray_rendering.py:286) so a training step can be reproduced
 """
 from __future__ import annotations
 
+import threading
+import warnings
+from contextlib import contextmanager
 from typing import Optional, Tuple
 
 import torch
 from torch import Tensor
-
-import warnings
 
 from . import nerfacc, occ_ops, ops
 from ._lib import acn_routing
@@ -31,6 +32,24 @@ from .ray_sampling import clamp_rays_near_far, get_ray_directions, get_rays  # n
 from .trunc_exp import trunc_exp
 
 _LINSPACE_CACHE = {}
+_GRAPH_MODE = threading.local()
+
+
+@contextmanager
+def second_order(enabled: bool = True):
+    """Within this context, differentiable renders build twice-differentiable graphs (second-order
+    MAML: meta_core.py:57 takes ``autograd.grad(create_graph=True)`` of the inner loss): the
+    compositing runs as torch ops instead of the HIP forward/backward pair.  Thread-local."""
+    prev = getattr(_GRAPH_MODE, "second_order", False)
+    _GRAPH_MODE.second_order = bool(enabled)
+    try:
+        yield
+    finally:
+        _GRAPH_MODE.second_order = prev
+
+
+def _second_order() -> bool:
+    return getattr(_GRAPH_MODE, "second_order", False)
 
 
 # ============================== BG helpers ===============================
@@ -119,7 +138,8 @@ def volume_render(rgb_sigma: Tensor, t_vals: Tensor, bg_rgb: Optional[Tensor] = 
                   raw_sigma: bool = False, sigma_scale: float = 1.0, **kwargs) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
     """NeRF compositing: rgb (N,3), depth (N,), weights (N,S), acc (N,) (ray_rendering.py:114-165)."""
     if torch.is_grad_enabled() and (rgb_sigma.requires_grad or (bg_rgb is not None and bg_rgb.requires_grad)):
-        if rgb_sigma.is_cuda and not raw_rgb and not raw_sigma and rgb_sigma.dtype == torch.float32:
+        if rgb_sigma.is_cuda and not raw_rgb and not raw_sigma and rgb_sigma.dtype == torch.float32 \
+                and not _second_order():
             bg = None if bg_rgb is None else bg_rgb.to(rgb_sigma.device, torch.float32)
             return _VolumeRenderFn.apply(rgb_sigma, t_vals, bg, float(sigma_scale))
         return _volume_render_autograd(rgb_sigma, t_vals, bg_rgb, raw_rgb, raw_sigma, sigma_scale)
@@ -280,6 +300,9 @@ def _empty_occ_result(model, rays, d, params, N, bg_color_default):
 
 def _composite_packed(model, rays, d, params, ri, t0, t1, starts, counts, sigma, rgb, t_mid, N, bg_color_default):
     """nerfacc compositing of packed samples under autograd (training path)."""
+    if _second_order():
+        raise ops.AcnError("second-order (create_graph) gradients through the occupancy renderer are not "
+                           "supported (nerfacc's scan backward is first order too)")
     packed = torch.stack([starts, counts], -1)
     weights = nerfacc.render_weight_from_density(t_starts=t0, t_ends=t1, sigmas=sigma, packed_info=packed)[0][..., None]
     w1 = weights.squeeze(-1)

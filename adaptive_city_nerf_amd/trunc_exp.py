@@ -20,6 +20,10 @@ def _clamp(x: torch.Tensor) -> torch.Tensor:
 
 
 class TruncExp(torch.autograd.Function):
+    """Forward exp(clamp(x)); backward g * exp(xc) with xc saved from the forward (models/trunc_exp.py:
+    43-57).  Under create_graph the backward is differentiable in g only -- xc is a constant of the
+    saved forward, exactly as in the reference, so second-order MAML matches it term for term."""
+
     @staticmethod
     def forward(ctx, x):
         xc = _clamp(x)

@@ -494,12 +494,124 @@ def gen_occ(scene: dict) -> None:
         del model
 
 
+# ----------------------------------------------------------------------------------------------
+class _StubLogger:
+    """Logger surface train_step calls (utils.Logger writes tensorboard/files; not needed here)."""
+
+    def log(self, *a, **k):
+        pass
+
+    def log_dirname(self, *a, **k):
+        pass
+
+    def scalar_summary(self, *a, **k):
+        pass
+
+
+META_S, META_RAYS, META_REGIONS = 16, 64, (0, 2)
+
+
+def gen_meta(scene: dict) -> None:
+    """SURVEY §8(f) rank 2 fixture: one offline meta-training step (pipelines/offline_stage/
+    meta_train_step.py:18-253 train_step -> meta_core.task_adapt / meta_update) of the K=4
+    container for FOMAML, second-order MAML and Reptile: 2 regions x 1 task, 64 support + 64 query
+    rays x 16 samples, 2 inner steps; the training-mode jitter of every render call is recorded in
+    call order (ray_rendering.py:286 draws it with torch.rand_like).  Also task_adapt alone (fast
+    weights after the inner loop)."""
+    import random
+    from types import SimpleNamespace
+    from common.utils import get_optimizer
+    from pipelines.offline_stage import meta_core as MC
+    from pipelines.offline_stage.meta_train_step import train_step
+    from utils import MetricLogger
+    mask = "g22_grid_bm110_ss11"
+    rays, valid, _ = val_rays(scene, mask, 0.25)
+    rv = rays[valid]
+    S = META_S
+    rows_g = torch.Generator().manual_seed(22)
+    sample_rows = torch.randint(0, 16 << 20, (4, 2048), generator=rows_g)
+    for algo in ("fomaml", "maml", "reptile"):
+        model, gbox = build_container(scene, mask)
+        out = dict(weights_dict(model))
+        out["rows"] = _np(sample_rows)
+        P = SimpleNamespace(algo=algo, ray_samples=S, chunk_points=1 << 20, color_space="linear", optimizer="adam",
+                            lr=1e-4, encoding_lr=0.01, sigma_lr=0.002, color_lr=0.002, bg_lr=0.001, weight_decay=0.0,
+                            inner_lr=0.05, inner_iter=2, fim=False, use_amp=False, grad_clip=1.0, seed=0,
+                            mixed_precision=False, print_step=10 ** 9)
+        opt = get_optimizer(P, model)
+        g = torch.Generator().manual_seed(21)
+        task_data = {}
+        for cid in META_REGIONS:
+            task = {}
+            for part in ("support", "query"):
+                perm = torch.randperm(rv.shape[0], generator=g)[:META_RAYS]
+                task[part] = {"rays": rv[perm].contiguous(), "rgbs": torch.rand(META_RAYS, 3, generator=g)}
+                out[f"task{cid}:{part}:rays"] = _np(task[part]["rays"])
+                out[f"task{cid}:{part}:rgbs"] = _np(task[part]["rgbs"])
+            task_data[cid] = [task]
+        gu = torch.Generator().manual_seed(23)
+        us = []
+        real = torch.rand_like
+
+        def fake(t, *a, **k):
+            if t.dim() == 2 and t.shape[1] == S:
+                u = torch.rand(tuple(t.shape), generator=gu)
+                us.append(u)
+                return u.clone()
+            return real(t, *a, **k)
+        model.train()
+        torch.rand_like = fake
+        try:
+            if algo == "maml":  # the inner loop alone: fast weights after 2 create_graph steps
+                fast, inner = MC.task_adapt(P, model, task_data[0][0]["support"], P.inner_lr, P.inner_iter,
+                                            active_module=0)
+                for name, v in fast.items():
+                    out["adapt_fast:" + name] = _np(v)
+                out["adapt_inner_losses"] = np.array([float(x) for x in inner], np.float64)
+                out["adapt_n_u"] = np.array(len(us), np.int64)
+            if algo != "reptile":
+                train_step(P, 1, model, opt, task_data, MetricLogger(delimiter="  "), _StubLogger())
+            else:
+                # the reference's train_step calls meta_update without fast_list (meta_train_step.py:168),
+                # so Reptile raises there; its update rule (meta_core.py:145-182) is pinned directly, with
+                # the expert-relative fast names prefixed to the container's meta-parameter names
+                # (unprefixed, `name in sum_delta` never matches and the update is a no-op)
+                order = list(META_REGIONS)
+                random.Random(P.seed + 1).shuffle(order)
+                fast_list = []
+                for cid in order:
+                    fast, _ = MC.task_adapt(P, model, task_data[cid][0]["support"], P.inner_lr, P.inner_iter,
+                                            active_module=cid)
+                    fast_list.append({f"submodules.{cid}.{n}": v for n, v in fast.items()})
+                MC.reptile_meta_update(P, model, fast_list)
+        finally:
+            torch.rand_like = real
+        out["u"] = _np(torch.stack(us, 0))
+        order = list(META_REGIONS)
+        random.Random(P.seed + 1).shuffle(order)
+        out["region_order"] = np.array(order, np.int64)
+        for name, prm in model.named_parameters():
+            if name.endswith("hash_table"):
+                k = int(name.split(".")[1])
+                out[f"after_table_rows:{k}"] = _np(prm.detach()[sample_rows[k]])
+                if prm.grad is not None:
+                    out[f"grad_table_rows:{k}"] = _np(prm.grad[sample_rows[k]])
+            else:
+                out["after:" + name] = _np(prm)
+                if prm.grad is not None:
+                    out["grad:" + name] = _np(prm.grad)
+        out["table_seeds"] = np.array([100 + k for k in range(4)], np.int64)
+        out["table_scale"] = np.array(TABLE_SCALE, np.float64)
+        save(f"meta_{algo}", **out)
+        del model
+
+
 def main() -> None:
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     scene = scene_json()
     (HERE / "scene_drz_example.json").write_text(json.dumps(scene, indent=1))
     print("wrote scene_drz_example.json")
-    which = sys.argv[1:] or ["hashgrid", "sh", "volume_render", "routing", "rays", "render", "train", "occ"]
+    which = sys.argv[1:] or ["hashgrid", "sh", "volume_render", "routing", "rays", "render", "train", "occ", "meta"]
     if "hashgrid" in which: gen_hashgrid()
     if "sh" in which: gen_sh()
     if "volume_render" in which: gen_volume_render()
@@ -508,6 +620,7 @@ def main() -> None:
     if "render" in which: gen_field_and_render(scene)
     if "train" in which: gen_train(scene)
     if "occ" in which: gen_occ(scene)
+    if "meta" in which: gen_meta(scene)
 
 
 if __name__ == "__main__":

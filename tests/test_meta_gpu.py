@@ -1,0 +1,104 @@
+"""GPU parity of the offline meta-training loop (adaptive_city_nerf_amd.meta_train, SURVEY §8(f)
+rank 2) against the reference's own step (tests/golden/meta_*.npz): FOMAML and second-order MAML
+train_step, the MAML inner loop alone, and the Reptile update rule, with the reference's recorded
+training jitter replayed in call order."""
+import contextlib
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+
+import goldens as G
+from test_module_api import build_model, reference_state_dict
+
+pytestmark = pytest.mark.gpu
+LRS = {"encoding": 0.01, "sigma": 0.002, "color": 0.002, "background": 0.001}
+
+
+def _P(algo):
+    return SimpleNamespace(algo=algo, ray_samples=16, chunk_points=1 << 20, color_space="linear", optimizer="adam",
+                           lr=1e-4, encoding_lr=0.01, sigma_lr=0.002, color_lr=0.002, bg_lr=0.001, weight_decay=0.0,
+                           inner_lr=0.05, inner_iter=2, fim=False, use_amp=False, grad_clip=1.0, seed=0,
+                           mixed_precision=False, print_step=10 ** 9)
+
+
+@contextlib.contextmanager
+def replay_jitter(us):
+    """torch.rand_like of the (N, 16) training jitter returns the recorded draws in order."""
+    real = torch.rand_like
+    it = iter(us)
+
+    def fake(t, *a, **k):
+        if t.dim() == 2 and t.shape[1] == 16:
+            return next(it).to(t.device, t.dtype).clone()
+        return real(t, *a, **k)
+    torch.rand_like = fake
+    try:
+        yield it
+    finally:
+        torch.rand_like = real
+
+
+def _model_and_tasks(d):
+    m, _ = build_model("k4")
+    m.load_state_dict(reference_state_dict(d, 4))
+    m = m.cuda().train()
+    tasks = {cid: [{part: {"rays": torch.from_numpy(d[f"task{cid}:{part}:rays"]).cuda(),
+                           "rgbs": torch.from_numpy(d[f"task{cid}:{part}:rgbs"]).cuda()}
+                    for part in ("support", "query")}] for cid in (0, 2)}
+    return m, tasks
+
+
+def _close_frac(a, b, atol, rtol):
+    a = np.asarray(a, np.float64); b = np.asarray(b, np.float64)
+    return float(np.mean(np.abs(a - b) <= atol + rtol * np.abs(b)))
+
+
+def _group(name):
+    return "encoding" if name.endswith("hash_table") else "background" if name.startswith("bg_mlp") else \
+        "color" if ".color_mlp." in name else "sigma"
+
+
+def test_maml_inner_loop_matches_reference():
+    from adaptive_city_nerf_amd import meta_train as MT
+    d = G.load("meta_maml")
+    m, tasks = _model_and_tasks(d)
+    with replay_jitter(torch.from_numpy(d["u"])):
+        fast, losses = MT.task_adapt(_P("maml"), m, tasks[0][0]["support"], 0.05, 2, active_module=0)
+    np.testing.assert_allclose([float(x) for x in losses], d["adapt_inner_losses"], rtol=1e-5)
+    for n, v in fast.items():
+        ref = d["adapt_fast:" + n]
+        np.testing.assert_allclose(v.detach().cpu().numpy(), ref, rtol=0, atol=1e-5 * max(1.0, np.abs(ref).max()),
+                                   err_msg=n)
+
+
+@pytest.mark.parametrize("algo", ["fomaml", "maml", "reptile"])
+def test_train_step_matches_reference(algo):
+    from adaptive_city_nerf_amd import meta_train as MT
+    from adaptive_city_nerf_amd.optim import build_optimizer
+    d = G.load(f"meta_{algo}")
+    m, tasks = _model_and_tasks(d)
+    P = _P(algo)
+    opt = build_optimizer(P, m)
+    us = torch.from_numpy(d["u"])
+    with replay_jitter(us[2:] if algo == "maml" else us):
+        MT.train_step(P, 1, m, opt, tasks)
+    rows = torch.from_numpy(d["rows"]).cuda()
+    for name, p in m.named_parameters():
+        lr = LRS[_group(name)]
+        if name.endswith("hash_table"):
+            k = int(name.split(".")[1])
+            got, ref = p.detach()[rows[k]].cpu().numpy(), d[f"after_table_rows:{k}"]
+            if algo != "reptile" and f"grad_table_rows:{k}" in d:
+                g = p.grad[rows[k]].cpu().numpy()
+                gr = d[f"grad_table_rows:{k}"]
+                np.testing.assert_allclose(g, gr, rtol=1e-3, atol=1e-4 * max(1e-12, np.abs(gr).max()), err_msg=name)
+        else:
+            got, ref = p.detach().cpu().numpy(), d["after:" + name]
+            if algo != "reptile" and "grad:" + name in d:
+                gr = d["grad:" + name]
+                np.testing.assert_allclose(p.grad.cpu().numpy(), gr, rtol=0, atol=2e-4 * max(1e-12, np.abs(gr).max()),
+                                           err_msg=name)
+        # Adam's first step moves a parameter by ~lr * sign(g): a few near-zero gradients may flip
+        assert _close_frac(got, ref, 1e-3 * lr, 1e-6) >= 0.998, name
