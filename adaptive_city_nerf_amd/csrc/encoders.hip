@@ -161,6 +161,62 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_f2(const float* __restrict__
     unsafeAtomicAdd(gtable + (((int64_t)l << log2T) + h) * 2 + f, gv);
 }
 
+// Run-length-aggregated variant: lane = (sub-group s = lane >> 4, corner, feature) walks PPL
+// consecutive points (a stretch of one ray: the training path lays samples out ray-major) at one
+// level, summing gradients in a register while the target row repeats and issuing one atomic per
+// run.  Coarse levels see long runs (several samples per cell), which is where the per-row atomic
+// contention was; waves interleave levels (l = wave % L) so concurrent waves spread over all levels
+// instead of all hammering level 0's few thousand rows at once.  Sum order within a run is the
+// sample order; across runs it is the (unordered) atomic order, as before.
+template <int INTERP, int PPL>
+__global__ void __launch_bounds__(256) hashgrid_bwd_rle(const float* __restrict__ x01, int64_t M,
+                                                        const float* __restrict__ gout, Res32 res, int L,
+                                                        int log2T, float* __restrict__ gtable) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int l = (int)(wave % L);
+    const int64_t chunk = wave / L;
+    const int64_t m0 = (chunk * 4 + (lane >> 4)) * PPL;
+    if (m0 >= M) return;
+    const int f = lane & 1, bx = (lane >> 1) & 1, by = (lane >> 3) & 1, bz = (lane >> 2) & 1;
+    const float r = (float)res.v[l];
+    const uint32_t mask = (uint32_t)((1ull << log2T) - 1ull);
+    const int64_t base = ((int64_t)l << log2T) * 2 + f;
+    int64_t cur = -1;
+    float acc = 0.0f;
+#pragma unroll 4
+    for (int i = 0; i < PPL; ++i) {
+        const int64_t m = m0 + i;
+        if (m >= M) break;
+        const float sx = x01[3 * m] * r, sy = x01[3 * m + 1] * r, sz = x01[3 * m + 2] * r;
+        const float fx = floorf(sx), fy = floorf(sy), fz = floorf(sz);
+        float wx = sx - fx, wy = sy - fy, wz = sz - fz;
+        if (INTERP == 2) {
+            wx = (wx * wx) * (3.0f - 2.0f * wx);
+            wy = (wy * wy) * (3.0f - 2.0f * wy);
+            wz = (wz * wz) * (3.0f - 2.0f * wz);
+        }
+        const uint32_t xi = (uint32_t)(int)fx + (uint32_t)bx;
+        const uint32_t yi = (uint32_t)(int)fy * acn::kP1 + (by ? acn::kP1 : 0u);
+        const uint32_t zi = (uint32_t)(int)fz * acn::kP2 + (bz ? acn::kP2 : 0u);
+        const int64_t a = base + (int64_t)((xi ^ yi ^ zi) & mask) * 2;
+        const float gv = ((gout[(m * L + l) * 2 + f] * (bz ? wz : 1.0f - wz)) * (by ? wy : 1.0f - wy)) *
+                         (bx ? wx : 1.0f - wx);
+        if (a == cur) {
+            acc += gv;
+        } else {
+            if (cur >= 0) unsafeAtomicAdd(gtable + cur, acc);
+            cur = a;
+            acc = gv;
+        }
+    }
+    if (cur >= 0) unsafeAtomicAdd(gtable + cur, acc);
+}
+
+#ifndef ACN_HASH_BWD_PPL
+#define ACN_HASH_BWD_PPL 16  // consecutive points per lane in hashgrid_bwd_rle (0: the per-point kernel)
+#endif
+
 template <int DEGREE>
 __global__ void __launch_bounds__(256) sh_fwd_kernel(const float* __restrict__ d, int64_t M,
                                                      float* __restrict__ out) {
@@ -215,6 +271,14 @@ extern "C" int acn_hashgrid_bwd(const float* x01, int64_t M, const float* grad_o
     Res32 r{};
     for (int i = 0; i < L; ++i) r.v[i] = res[i];
     hipStream_t s = (hipStream_t)stream;
+    if (F == 2 && interp != 0 && ACN_HASH_BWD_PPL > 0) {
+        constexpr int PPL = ACN_HASH_BWD_PPL > 0 ? ACN_HASH_BWD_PPL : 1;
+        const int64_t waves = ((M + 4 * PPL - 1) / (4 * PPL)) * L;
+        const dim3 grid((unsigned)((waves + 3) / 4)), block(256);
+        if (interp == 1) hipLaunchKernelGGL((hashgrid_bwd_rle<1, PPL>), grid, block, 0, s, x01, M, grad_out, r, L, log2T, grad_table);
+        else hipLaunchKernelGGL((hashgrid_bwd_rle<2, PPL>), grid, block, 0, s, x01, M, grad_out, r, L, log2T, grad_table);
+        return acn_check_launch("acn_hashgrid_bwd");
+    }
     if (F == 2 && interp != 0) {
         const int64_t waves = ((M + 3) / 4) * L;
         const dim3 grid((unsigned)((waves + 3) / 4)), block(256);

@@ -88,6 +88,18 @@ def _wgrad_splitk(g: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     return gw
 
 
+def _bias_grad(g: torch.Tensor) -> torch.Tensor:
+    """Column sums of the tall (M x out) output gradient.  torch's dim-0 reduction is fast for 64
+    columns but 5-15x slower for the 15-, 3- and 1-wide heads (490 us vs 37 us at M = 384k, measured
+    with tools/micro/bias_sum.py); reducing 2048-row slices first is uniform across widths."""
+    M, C = g.shape
+    if M < _SPLITK_MIN_ROWS or C % 64 == 0:
+        return g.sum(0)
+    main = (M // _SPLITK_ROWS) * _SPLITK_ROWS
+    gb = g[:main].view(-1, _SPLITK_ROWS, C).sum(1).sum(0)
+    return gb + g[main:].sum(0) if main < M else gb
+
+
 class _LinearFn(torch.autograd.Function):
     """y = x W^T + b (one addmm) with a split-K weight gradient; the backward is written with
     differentiable ops, so second-order MAML (create_graph=True) still works through it."""
@@ -103,7 +115,7 @@ class _LinearFn(torch.autograd.Function):
         x, w = ctx.saved_tensors
         gx = g @ w if ctx.needs_input_grad[0] else None
         gw = _wgrad_splitk(g, x) if ctx.needs_input_grad[1] else None
-        gb = g.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        gb = _bias_grad(g) if ctx.has_bias and ctx.needs_input_grad[2] else None
         return gx, gw, gb
 
 

@@ -189,6 +189,40 @@ def cpu_baseline_occ(model, rays, gpu_rgb, min_seconds):
                       f"{dt:.1f} s"}, psnr, float(np.sqrt(mse)), float(np.max(np.abs(gpu_rgb - orgb)))
 
 
+def cpu_baseline_meta(model, sc, task_data, S, min_seconds):
+    """Meta-training on the host cores: oracle/meta_ref.py (the fixture-pinned PyTorch CPU restatement
+    of train_step) on a bounded sample: one region, one task cut to 500 support + 250 query rays, the
+    configured inner steps; repeated until >= min_seconds; samples counted like the GPU line."""
+    from oracle import meta_ref as MR
+    from oracle import oracle as O
+    from oracle import train_ref as TR
+    state = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    K = len(model.submodules)
+    m = TR.RefContainer(state, K, np.array(model.submodules[0].xyz_encoder._res_host), 20, sc["centroids"],
+                        model.boundary_margin, sc["mins"], [s.aabb_extent.cpu().numpy() for s in model.submodules])
+    lrs = {"encoding": 0.01, "sigma": 0.002, "color": 0.002, "background": 0.001}
+    opt = torch.optim.Adam(m.param_groups(lrs), lr=1e-4)
+    threads = O.max_threads()
+    torch.set_num_threads(threads)
+    t = task_data[0][0]
+    ns, nq, iters = 500, 250, 8
+    task = {0: {"support": {k: v[:ns].cpu() for k, v in t["support"].items()},
+                "query": {k: v[:nq].cpu() for k, v in t["query"].items()}}}
+    g = torch.Generator().manual_seed(3)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        us = iter([torch.rand(ns, S, generator=g) for _ in range(iters)] + [torch.rand(nq, S, generator=g)])
+        MR.meta_step(m, opt, task, [0], S, us, "fomaml", 0.015, iters, 1e-4)
+        reps += 1
+        if time.perf_counter() - t0 >= min_seconds:
+            break
+    dt = time.perf_counter() - t0
+    n = reps * (iters * ns + nq) * S
+    return {"value": n / dt, "unit": "ray-samples/s", "cores": threads, "kind": "port",
+            "sample": f"{reps} meta steps of 1 region x 1 task ({ns} support x {iters} inner + {nq} query rays, "
+                      f"{S} samples; oracle/meta_ref.py PyTorch CPU restatement, {threads} threads), {dt:.1f} s"}
+
+
 def load_traffic():
     p = REPO / "profiles" / "pmc_render_r01.json"
     if p.exists():
@@ -204,13 +238,16 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "occ"], default="c2")
+    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "occ", "meta"], default="c2")
     ap.add_argument("--rays", type=int, default=4096, help="rays per GPU (c2, c3)")
     ap.add_argument("--samples", type=int, default=256)
     ap.add_argument("--frame", type=int, default=800, help="frame side (c4)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-rays", type=int, default=4096, help="rays in the CPU-baseline / PSNR sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--inner-iter", type=int, default=8, help="meta: inner steps (configs/train.json)")
+    ap.add_argument("--support-rays", type=int, default=4000, help="meta: support rays per task")
+    ap.add_argument("--query-rays", type=int, default=2000, help="meta: query rays per task")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -225,7 +262,7 @@ def main():
 
     from adaptive_city_nerf_amd import ops, parallel, render_rays
     S = a.samples
-    K = {"c2": 1, "c3": 4, "c4": 8, "c5": 8, "occ": 1}[a.workload]
+    K = {"c2": 1, "c3": 4, "c4": 8, "c5": 8, "occ": 1, "meta": 4}[a.workload]
     occ_conf = None
     if a.workload == "occ":  # nerf_runner.py:124-147 defaults: 128^3 x 4 levels, cone 0.004, step diag/1000
         occ_conf = {"use_occ": True, "resolution": 128, "levels": 4, "render_step_size": None, "cone_angle": 0.004,
@@ -273,6 +310,42 @@ def main():
             with torch.no_grad():
                 return parallel.render_rays_sharded(grays, render_fn, plan)
         sample_rays = grays
+    elif a.workload == "meta":
+        # offline meta-training (configs/train.json): 4 regions x batch_size 3 tasks, 4000 support +
+        # 2000 query rays, 96 samples, 8 inner steps, FOMAML, Adam param groups; expert parallel
+        from types import SimpleNamespace
+        from adaptive_city_nerf_amd import meta_train as MT
+        from adaptive_city_nerf_amd import optim as aoptim
+        S = 96 if a.samples == 256 else a.samples
+        P = SimpleNamespace(algo="fomaml", ray_samples=S, chunk_points=4000000, color_space="linear",
+                            optimizer="adam", lr=1e-4, encoding_lr=0.01, sigma_lr=0.002, color_lr=0.002, bg_lr=0.001,
+                            weight_decay=0.0, inner_lr=0.015, inner_iter=a.inner_iter, fim=False, use_amp=False,
+                            grad_clip=1.0, seed=0, mixed_precision=False, print_step=10 ** 9)
+        nsup, nqry, ntask = a.support_rays, a.query_rays, 3
+        pool = make_rays(scene, gbox, device, 60000, 4321)
+        gen = torch.Generator(device).manual_seed(9)
+        task_data = {}
+        for cid in range(4):
+            task_data[cid] = []
+            for t in range(ntask):
+                sel = torch.randint(0, pool.shape[0], (nsup + nqry,), device=device, generator=gen)
+                rg = torch.rand(nsup + nqry, 3, device=device, generator=gen)
+                task_data[cid].append({"support": {"rays": pool[sel[:nsup]], "rgbs": rg[:nsup]},
+                                       "query": {"rays": pool[sel[nsup:]], "rgbs": rg[nsup:]}})
+        model.train()
+        opt = aoptim.build_optimizer(P, model)
+        pg = dist.group.WORLD if world > 1 else None
+        my_regions = [c for c in range(4) if c % world == rank]
+        samples_per_step = sum(len(task_data[c]) * (P.inner_iter * nsup + nqry) for c in range(4)) * S
+        it = [0]
+
+        def step():
+            it[0] += 1
+            import contextlib, io
+            with contextlib.redirect_stdout(io.StringIO()):  # meta_update's per-region debug prints
+                return MT.train_step(P, it[0], model, opt, task_data, group=pg)
+        sample_rays = pool[:1]
+        aoptim.EVENT_HOOK = []
     elif a.workload == "c5":
         from types import SimpleNamespace
         from adaptive_city_nerf_amd import optim as aoptim
@@ -326,7 +399,7 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    if a.workload == "c5":
+    if a.workload in ("c5", "meta"):
         from adaptive_city_nerf_amd import optim as aoptim
         hook = aoptim.EVENT_HOOK[-a.steps:]
         aoptim.EVENT_HOOK = None
@@ -346,6 +419,11 @@ def main():
         nparam = sum(p.numel() for p in model.submodules[expert].parameters()) + sum(p.numel() for p in shared)
         adam_bytes = 28 * nparam            # read p, g, m, v + write p, m, v (fp32)
         achieved_gbs = adam_bytes / (kernel_ms * 1e-3) / 1e9
+    if a.workload == "meta":  # the outer Adam updates the experts of this rank's regions + the shared head
+        nparam = sum(p.numel() for c in my_regions for p in model.submodules[c].parameters()) + \
+            sum(p.numel() for p in model.bg_mlp.parameters())
+        adam_bytes = 28 * nparam
+        achieved_gbs = adam_bytes / (kernel_ms * 1e-3) / 1e9
     # samples one launch of the dominant kernel processes on this rank
     launch_samples = samples_per_step // world // max(kernel_launches, 1)
     achieved = FLOP_PER_SAMPLE * launch_samples / (kernel_ms * 1e-3) / 1e12
@@ -354,7 +432,8 @@ def main():
              "c2": "render_kernel<1,1,0> (fused stratified render, 1 expert)",
              "c3": "render_kernel<1,0,1> (fused stratified render, soft routing over 4 experts)",
              "c4": "render_kernel<1,0,1> (fused stratified render, soft routing over 8 experts)",
-             "occ": "occ_render_kernel<1,1,0> (fused occupancy render over packed marched samples, 1 expert)"
+             "occ": "occ_render_kernel<1,1,0> (fused occupancy render over packed marched samples, 1 expert)",
+             "meta": "adam_kernel (fused clip + Adam of the outer meta-update over the region experts + shared head)"
              }[a.workload]
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
@@ -362,8 +441,10 @@ def main():
                 "kernel": kname, "kernel_ms": round(kernel_ms, 4), "samples_per_launch": int(launch_samples),
                 "flop_per_sample": FLOP_PER_SAMPLE,
                 "hash_bytes_algorithmic_per_launch": int(BYTES_PER_SAMPLE * launch_samples),
-                "hash_gbs_algorithmic": round(BYTES_PER_SAMPLE * launch_samples / (kernel_ms * 1e-3) / 1e9, 1)}
-    if a.workload == "c5":
+                "hash_gbs_algorithmic": round(BYTES_PER_SAMPLE * launch_samples / (kernel_ms * 1e-3) / 1e9, 1),
+                "mlp_arith": "fp32-accurate 3-term fp16 split (hi*hi + hi*lo + lo*hi) on v_mfma_f32_32x32x16_f16, "
+                             "fp32 accumulate (DESIGN.md 4)"}
+    if a.workload in ("c5", "meta"):
         roofline = {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kname,
                     "kernel_ms": round(kernel_ms, 4), "params_per_launch": int(nparam),
@@ -375,7 +456,9 @@ def main():
     if rank == 0 and not a.no_cpu_baseline and a.workload == "occ":
         idx = torch.arange(rays.shape[0], device=device)[: a.cpu_rays]
         cpu, psnr, rmse, maxerr = cpu_baseline_occ(model, rays[idx], out[0][idx].cpu().numpy(), a.cpu_seconds)
-    if rank == 0 and not a.no_cpu_baseline and a.workload not in ("c5", "occ"):
+    if rank == 0 and not a.no_cpu_baseline and a.workload == "meta":
+        cpu = cpu_baseline_meta(model, sc, task_data, S, a.cpu_seconds)
+    if rank == 0 and not a.no_cpu_baseline and a.workload not in ("c5", "occ", "meta"):
         rgb_all = out[0].reshape(-1, 3)
         if a.workload == "c2":
             idx = torch.arange(rays.shape[0], device=device)[: a.cpu_rays]
@@ -404,7 +487,12 @@ def main():
                                    f"{100 * occ_frac if a.workload == 'occ' else 0:.1f}% cells occupied), step "
                                    f"diag/1000, cone 0.004; metric counts marched samples",
                        "rays_per_gpu": a.rays, "experts": 1,
-                       "marched_samples_per_gpu": occ_samples if a.workload == "occ" else None}}[a.workload]
+                       "marched_samples_per_gpu": occ_samples if a.workload == "occ" else None},
+               "meta": {"workload": "offline meta-training step (meta_train_step.train_step, configs/train.json): 4 "
+                                    "regions x 3 tasks, 4000 support + 2000 query rays x 96 samples, 8 inner FOMAML "
+                                    "steps, outer clip + Adam; metric = trained ray-samples (fwd+bwd) per second",
+                        "experts": 4, "regions": 4, "tasks_per_region": 3,
+                        "inner_iter": a.inner_iter if a.workload == "meta" else None}}[a.workload]
         cfg.update({"samples_per_ray": S, "parallelism": f"ray-sharded x{world}"})
         line = {
             "metric": "ray-samples/sec + PSNR, 4096 rays×256 samples, 1/2/4/8 MI355X",

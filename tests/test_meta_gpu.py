@@ -82,7 +82,12 @@ def test_train_step_matches_reference(algo):
     P = _P(algo)
     opt = build_optimizer(P, m)
     us = torch.from_numpy(d["u"])
-    with replay_jitter(us[2:] if algo == "maml" else us):
+    if algo == "maml":
+        us = us[2:]  # the fixture ran the inner loop alone first
+    elif algo == "reptile":  # the fixture pinned the update rule without the query renders train_step adds
+        q = torch.rand_like(us[0])
+        us = torch.stack([us[0], us[1], q, us[2], us[3], q])
+    with replay_jitter(us):
         MT.train_step(P, 1, m, opt, tasks)
     rows = torch.from_numpy(d["rows"]).cuda()
     for name, p in m.named_parameters():
