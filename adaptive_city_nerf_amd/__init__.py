@@ -21,3 +21,5 @@ from .nerfacc import OccGridEstimator  # noqa: E402,F401
 from .ray_sampling import clamp_rays_near_far, get_ray_directions, get_rays, pack_rays, unpack_rays  # noqa: E402,F401
 from .scene_box import SceneBox  # noqa: E402,F401
 from .trunc_exp import trunc_exp  # noqa: E402,F401
+from .data import (DeviceRaysDataset, ImageMetadata, Task, TaskDataset, get_dataset,  # noqa: E402,F401
+                   get_image_metadata)

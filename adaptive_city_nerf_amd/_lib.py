@@ -105,6 +105,10 @@ SIGNATURES = {
     "acn_occ_binarize_workspace_bytes": ([], sz),
     "acn_occ_binarize": ([vp, i64, f32, vp, vp, vp, vp, vp], C.c_int),
     "acn_occ_mark_invisible": ([vp, i32, vp, i32, i32, i32, f32, vp, vp, vp, i64, vp, vp], C.c_int),
+    # data.hip
+    "acn_route_rays": ([vp, i64, vp, vp, vp, vp, f32, f32, i32, i32, vp, vp, vp], C.c_int),
+    "acn_bin_rays_workspace_bytes": ([i64, i32], C.c_size_t),
+    "acn_bin_rays": ([vp, vp, i64, i32, vp, vp, vp, C.c_size_t, vp], C.c_int),
 }
 
 

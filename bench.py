@@ -189,6 +189,29 @@ def cpu_baseline_occ(model, rays, gpu_rgb, min_seconds):
                       f"{dt:.1f} s"}, psnr, float(np.sqrt(mse)), float(np.max(np.abs(gpu_rgb - orgb)))
 
 
+def cpu_baseline_data(td, rays, gpu_bins, min_seconds):
+    """_route_and_bin on the host cores: oracle/data_ref.route (float32 numpy restatement of the
+    reference's torch CPU routing) + the reference's argsort binning, on a bounded prefix of the
+    region's rays; its bins are checked against the GPU's for that prefix."""
+    from oracle import data_ref as DR
+    n = min(rays.shape[0], 1 << 19)
+    r = rays[:n].cpu().numpy()
+    aabb = td.aabb.numpy()
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        cid, flags = DR.route(r, aabb, td.cells, td.assignment_checkpoint, td.routing_policy)
+        bins = DR.bins(cid, flags, int(np.prod(td.cells)))
+        reps += 1
+        if time.perf_counter() - t0 >= min_seconds:
+            break
+    dt = time.perf_counter() - t0
+    full = [b.cpu().numpy() for b in gpu_bins]
+    same = all(np.array_equal(np.sort(b[b < n]), np.sort(c)) for b, c in zip(full, bins))
+    return {"value": reps * n / dt, "unit": "rays/s", "cores": 1, "kind": "port",
+            "sample": f"{reps} x {n} rays (prefix of the region table), oracle/data_ref.py route+bins (numpy, "
+                      f"single thread), {dt:.1f} s; per-cell membership equal to the GPU bins: {same}"}
+
+
 def cpu_baseline_meta(model, sc, task_data, S, min_seconds):
     """Meta-training on the host cores: oracle/meta_ref.py (the fixture-pinned PyTorch CPU restatement
     of train_step) on a bounded sample: one region, one task cut to 500 support + 250 query rays, the
@@ -238,7 +261,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "occ", "meta"], default="c2")
+    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "occ", "meta", "data"], default="c2")
     ap.add_argument("--rays", type=int, default=4096, help="rays per GPU (c2, c3)")
     ap.add_argument("--samples", type=int, default=256)
     ap.add_argument("--frame", type=int, default=800, help="frame side (c4)")
@@ -248,6 +271,7 @@ def main():
     ap.add_argument("--inner-iter", type=int, default=8, help="meta: inner steps (configs/train.json)")
     ap.add_argument("--support-rays", type=int, default=4000, help="meta: support rays per task")
     ap.add_argument("--query-rays", type=int, default=2000, help="meta: query rays per task")
+    ap.add_argument("--data-rays", type=int, default=1 << 22, help="data: rays in the region table")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -262,7 +286,7 @@ def main():
 
     from adaptive_city_nerf_amd import ops, parallel, render_rays
     S = a.samples
-    K = {"c2": 1, "c3": 4, "c4": 8, "c5": 8, "occ": 1, "meta": 4}[a.workload]
+    K = {"c2": 1, "c3": 4, "c4": 8, "c5": 8, "occ": 1, "meta": 4, "data": 1}[a.workload]
     occ_conf = None
     if a.workload == "occ":  # nerf_runner.py:124-147 defaults: 128^3 x 4 levels, cone 0.004, step diag/1000
         occ_conf = {"use_occ": True, "resolution": 128, "levels": 4, "render_step_size": None, "cone_angle": 0.004,
@@ -346,6 +370,36 @@ def main():
                 return MT.train_step(P, it[0], model, opt, task_data, group=pg)
         sample_rays = pool[:1]
         aoptim.EVENT_HOOK = []
+    elif a.workload == "data":
+        # TaskDataset construction over one region's device ray table (nerf_runner.py:193-201: DDA
+        # routing, 1 x 5 x 5 micro-cells, image cap 0.4): HIP routing + device sort + per-cell bins
+        from types import SimpleNamespace
+        from adaptive_city_nerf_amd import data as adata
+        # the table a DeviceRaysDataset holds: image after image, valid pixels row-major; images are the
+        # validation camera at downscale 0.25 with the origin shifted per image
+        H, W, intr, c2w = frame_camera(scene)
+        psf = scene["pose_scale_factor"]
+        n = a.data_rays
+        g = torch.Generator(device).manual_seed(31 + rank)
+        frames, ids, total = [], [], 0
+        while total < n:
+            fr, fv = ops.get_rays_image(H, W, *intr, c2w, gbox.aabb, device, near_far_override=(0.0, 100000 / psf))
+            fr = fr[fv]
+            fr[:, :3] += 0.05 * (torch.rand(1, 3, device=device, generator=g) - 0.5)
+            ids.append(torch.full((fr.shape[0],), len(frames), dtype=torch.int32, device=device))
+            frames.append(fr)
+            total += fr.shape[0]
+        rays = torch.cat(frames)[:n].contiguous()
+        table = SimpleNamespace(_rays=rays, _rgbs=torch.rand(n, 3, device=device, generator=g),
+                                _img_indices=torch.cat(ids)[:n])
+        td = adata.TaskDataset(table, cell_id=rank, S_target=4000, Q_target=2000, min_rays_cell=3000,
+                               image_cap=0.4, routing_policy="dda", cells=(1, 5, 5))
+        samples_per_step = world * n
+
+        def step():
+            return td._route_and_bin()
+        sample_rays = rays
+        data_n = n
     elif a.workload == "c5":
         from types import SimpleNamespace
         from adaptive_city_nerf_amd import optim as aoptim
@@ -406,6 +460,16 @@ def main():
     else:
         hook = ops.EVENT_HOOK
     kernel_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in hook]))
+    if a.workload == "data":
+        # route_kernel (~0.1 ms) is shorter than the host gap between a per-call event and its launch
+        # (the step syncs for the bin counts, so the queue is empty): time it back to back instead
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record()
+        for _ in range(a.steps):
+            adata.route_rays(rays, td.aabb, td.cells, td.assignment_checkpoint, td.routing_policy)
+        ev[1].record()
+        torch.cuda.synchronize()
+        kernel_ms_gapped, kernel_ms = kernel_ms, ev[0].elapsed_time(ev[1]) / a.steps
     kernel_launches = len(hook) // max(a.steps, 1)
     ops.EVENT_HOOK = None
     if world > 1:
@@ -419,6 +483,9 @@ def main():
         nparam = sum(p.numel() for p in model.submodules[expert].parameters()) + sum(p.numel() for p in shared)
         adam_bytes = 28 * nparam            # read p, g, m, v + write p, m, v (fp32)
         achieved_gbs = adam_bytes / (kernel_ms * 1e-3) / 1e9
+    if a.workload == "data":  # route_kernel: read a ray (32 B), write cell id (8 B) + flags (1 B)
+        route_bytes = 41 * data_n
+        achieved_gbs = route_bytes / (kernel_ms * 1e-3) / 1e9
     if a.workload == "meta":  # the outer Adam updates the experts of this rank's regions + the shared head
         nparam = sum(p.numel() for c in my_regions for p in model.submodules[c].parameters()) + \
             sum(p.numel() for p in model.bg_mlp.parameters())
@@ -433,7 +500,8 @@ def main():
              "c3": "render_kernel<1,0,1> (fused stratified render, soft routing over 4 experts)",
              "c4": "render_kernel<1,0,1> (fused stratified render, soft routing over 8 experts)",
              "occ": "occ_render_kernel<1,1,0> (fused occupancy render over packed marched samples, 1 expert)",
-             "meta": "adam_kernel (fused clip + Adam of the outer meta-update over the region experts + shared head)"
+             "meta": "adam_kernel (fused clip + Adam of the outer meta-update over the region experts + shared head)",
+             "data": "route_kernel (TaskDataset region clip + DDA max-overlap micro-cell routing + keep tolerance)"
              }[a.workload]
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
@@ -449,6 +517,12 @@ def main():
                     "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kname,
                     "kernel_ms": round(kernel_ms, 4), "params_per_launch": int(nparam),
                     "bytes_per_param": 28, "bytes_algorithmic_per_launch": int(adam_bytes)}
+    if a.workload == "data":
+        roofline = {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kname,
+                    "kernel_ms": round(kernel_ms, 4), "kernel_ms_in_step_events": round(kernel_ms_gapped, 4),
+                    "rays_per_launch": int(data_n), "bytes_per_ray": 41,
+                    "bytes_algorithmic_per_launch": int(route_bytes)}
 
     cpu, psnr, rmse, maxerr = None, None, None, None
     if rank == 0 and not a.no_cpu_baseline and a.workload == "c5":
@@ -458,7 +532,9 @@ def main():
         cpu, psnr, rmse, maxerr = cpu_baseline_occ(model, rays[idx], out[0][idx].cpu().numpy(), a.cpu_seconds)
     if rank == 0 and not a.no_cpu_baseline and a.workload == "meta":
         cpu = cpu_baseline_meta(model, sc, task_data, S, a.cpu_seconds)
-    if rank == 0 and not a.no_cpu_baseline and a.workload not in ("c5", "occ", "meta"):
+    if rank == 0 and not a.no_cpu_baseline and a.workload == "data":
+        cpu = cpu_baseline_data(td, rays, out, a.cpu_seconds)
+    if rank == 0 and not a.no_cpu_baseline and a.workload not in ("c5", "occ", "meta", "data"):
         rgb_all = out[0].reshape(-1, 3)
         if a.workload == "c2":
             idx = torch.arange(rays.shape[0], device=device)[: a.cpu_rays]
@@ -492,11 +568,16 @@ def main():
                                     "regions x 3 tasks, 4000 support + 2000 query rays x 96 samples, 8 inner FOMAML "
                                     "steps, outer clip + Adam; metric = trained ray-samples (fwd+bwd) per second",
                         "experts": 4, "regions": 4, "tasks_per_region": 3,
-                        "inner_iter": a.inner_iter if a.workload == "meta" else None}}[a.workload]
+                        "inner_iter": a.inner_iter if a.workload == "meta" else None},
+               "data": {"workload": f"TaskDataset construction (task_dataset.py _route_and_bin, nerf_runner.py "
+                                    f"configuration: DDA routing, 1x5x5 cells): {a.data_rays} device-resident rays of "
+                                    f"one region (images of the validation camera at downscale 0.25, pixel order) "
+                                    f"routed, keep-filtered, stably binned per cell and copied to the host per step; "
+                                    f"metric counts routed rays", "rays_per_gpu": a.data_rays}}[a.workload]
         cfg.update({"samples_per_ray": S, "parallelism": f"ray-sharded x{world}"})
         line = {
             "metric": "ray-samples/sec + PSNR, 4096 rays×256 samples, 1/2/4/8 MI355X",
-            "value": round(value, 1), "unit": "ray-samples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "value": round(value, 1), "unit": "rays/s" if a.workload == "data" else "ray-samples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "strong" if a.workload == "c4" else "weak", "vs_baseline": None,
             "dtype": "f32", "data": "synthetic (formula-filled hash table, seeded MLP init; rays from the "

@@ -308,6 +308,29 @@ int acn_occ_mark_invisible(const float* Ks, int nK, const float* c2w, int nc2w, 
                            float near_plane, const float* aabb, const int32_t* res,
                            const int64_t* cell_indices, int64_t n, float* occs_level, void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Episodic task routing (data.hip).  Replaces TaskDataset's region clip + micro-cell assignment
+ * (data/task_dataset.py:130-172 _aabb_intersect/_region_segment, :229-352 DDA max overlap,
+ * :354-418 alpha point + 6-neighbour max overlap, :544-598 selected-cell overlap >= tolerance).
+ * rays (N, 8) device; region_aabb[6], cells[3] (nx, ny, nz) host; cell_bounds (C, 2, 3) and
+ * tol_cell (C) device (C = nx*ny*nz, x-major); alpha = assignment_checkpoint; tol_abs =
+ * max(1e-6 * median cell diagonal, 1e-9); policy 0 alpha / 1 dda (max_steps DDA steps).
+ * Out: cell_ids (N) int64 (-1 when the ray misses the region segment), flags (N) u8: bit0 the ray
+ * has a positive segment in the region, bit1 its overlap with the selected cell passes tol_cell.  */
+int acn_route_rays(const float* rays, int64_t N, const float* region_aabb, const int32_t* cells,
+                   const float* cell_bounds, const float* tol_cell, float alpha, float tol_abs, int policy,
+                   int max_steps, int64_t* cell_ids, uint8_t* flags, void* stream);
+
+/* Per-cell ray lists of _route_and_bin (data/task_dataset.py:575-628: sort the region-valid rays by
+ * cell, keep relative order, drop rays failing the keep tolerance): a stable counting sort of the
+ * rays with flags bit1 set by cell_ids.  ray_index (>= kept rays) int32 device receives the ray
+ * indices cell after cell, ascending inside a cell; counts (n_cells + 1) int64 device receives
+ * the kept rays per cell and, last, the number of region-valid rays (flags bit0).  N < 2^31,
+ * n_cells <= 4096; workspace of acn_bin_rays_workspace_bytes(N, n_cells) device bytes.          */
+size_t acn_bin_rays_workspace_bytes(int64_t N, int n_cells);
+int acn_bin_rays(const int64_t* cell_ids, const uint8_t* flags, int64_t N, int n_cells, int32_t* ray_index,
+                 int64_t* counts, void* workspace, size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

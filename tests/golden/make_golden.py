@@ -605,13 +605,105 @@ def gen_meta(scene: dict) -> None:
         save(f"meta_{algo}", **out)
         del model
 
+DATA_STEMS = ["000006", "000007", "000009", "000010"]
+DATA_SCALE = 0.125
+DATA_MASKS = "g22_grid_bm110_ss11"
+TASK_CASES = {
+    # name: (region, TaskDataset kwargs) -- "runner" is nerf_runner.py:193-201's configuration
+    "runner": (0, dict(S_target=512, Q_target=256, min_rays_cell=384, image_cap=0.4, assignment_checkpoint=0.7,
+                       routing_policy="dda", cells=(1, 5, 5), seed=0)),
+    "alpha_box": (0, dict(S_target=400, Q_target=200, min_rays_cell=600, image_cap=None, routing_policy="alpha",
+                          max_images_support=2, max_images_query=1,
+                          cells=(1, 6, 6), seed=3, region_box=True)),
+    "small_alpha": (2, dict(S_target=300, Q_target=150, min_rays_cell=200, image_cap=0.4, routing_policy="alpha",
+                            cells=(2, 3, 3), seed=7, max_images_query=1, min_images_support=3)),
+}
+TASK_EPISODES = 4
+
+
+def _digest(t: torch.Tensor) -> str:
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(_np(t)).tobytes()).hexdigest()
+
+
+def gen_data(scene: dict) -> None:
+    """RamRaysDataset (per-region masks, expert box, near/far override) over 4 train images, then
+    TaskDataset bins + episodes for three configurations (data/ram_rays_dataset.py, task_dataset.py)."""
+    from zipfile import ZipFile
+    from data.dataset import get_image_metadata as ref_get_image_metadata
+    from data.ram_rays_dataset import RamRaysDataset
+    from data.task_dataset import TaskDataset
+
+    m = scene["masks"][DATA_MASKS] if DATA_MASKS in scene["masks"] else None
+    b = torch.load(DATA / "masks" / DATA_MASKS / "scene_boxes.pt", map_location="cpu", weights_only=True)
+    boxes = [SceneBox(aabb=torch.stack([b["mins"][k].float(), b["maxs"][k].float()])) for k in range(len(b["mins"]))]
+    out = {"stems": np.array(DATA_STEMS), "scale": np.array(DATA_SCALE, np.float64),
+           "box_aabbs": np.stack([_np(bx.aabb) for bx in boxes])}
+    overrides = {0: (0.0, 100000.0), 2: (0.05, 1.2)}
+    datasets = {}
+    for region in (0, 2):
+        tr, _ = ref_get_image_metadata(DATA, DATA_SCALE, DATA / "masks" / DATA_MASKS / str(region))
+        items = [md for md in tr if md is not None and md.image_path.stem in DATA_STEMS]
+        items.sort(key=lambda md: md.image_path.stem)
+        assert len(items) == len(DATA_STEMS)
+        if region == 0:
+            out["images"] = np.stack([md.load_image().numpy() for md in items])
+            out["c2w"] = np.stack([_np(md.c2w.float()) for md in items])
+            out["intrinsics"] = np.stack([_np(md.intrinsics.float()) for md in items])
+            out["image_index"] = np.array([md.image_index for md in items], np.int64)
+            out["HW"] = np.array([items[0].H, items[0].W], np.int64)
+        masks = []
+        for md in items:
+            with ZipFile(md.mask_path, "r") as zf, zf.open(zf.namelist()[0]) as f:
+                mk = torch.load(f, map_location="cpu", weights_only=True)
+            masks.append(np.packbits(_np(mk.bool()).reshape(-1)))
+        out[f"r{region}_mask_shape"] = np.array(mk.shape, np.int64)
+        out[f"r{region}_masks"] = np.stack(masks)
+        ds = RamRaysDataset(items, center_pixels=True,
+                            ray_gen_kwargs={"scene_box": boxes[region], "near_far_override": overrides[region]},
+                            num_workers=1)
+        out[f"r{region}_override"] = np.array(overrides[region], np.float64)
+        out[f"r{region}_n"] = np.array(len(ds), np.int64)
+        for key, t in (("rays", ds._rays), ("rgbs", ds._rgbs), ("img", ds._img_indices)):
+            out[f"r{region}_{key}_sha"] = np.array(_digest(t))
+        out[f"r{region}_rays_sample"] = _np(ds._rays[::61])
+        out[f"r{region}_rgbs_sample"] = _np(ds._rgbs[::61])
+        out[f"r{region}_img"] = _np(ds._img_indices)
+        datasets[region] = ds
+    for name, (region, kw) in TASK_CASES.items():
+        kw = dict(kw)
+        if kw.pop("region_box", False):
+            kw["region_bounds"] = tuple(tuple(float(v) for v in row) for row in boxes[region].aabb.tolist())
+        ds = datasets[region]
+        td = TaskDataset(ds, cell_id=region, **kw)
+        nv = int(td._region_segment(ds._rays, td.aabb)[0].sum())
+        counts = np.array([int(x.numel()) for x in td._cell_flat_idx], np.int64)
+        # bins in routing order = the flat pools un-permuted is not recoverable; store the pools
+        out[f"t_{name}_n_valid"] = np.array(nv, np.int64)
+        out[f"t_{name}_aabb"] = _np(td.aabb)
+        out[f"t_{name}_counts"] = counts
+        out[f"t_{name}_flat_idx"] = np.concatenate([_np(x) for x in td._cell_flat_idx]).astype(np.int64)
+        out[f"t_{name}_eligible"] = np.array(td.eligible_cells, np.int64)
+        it = iter(td)
+        ep_s, ep_q, ep_meta = [], [], []
+        for _ in range(TASK_EPISODES):
+            task = next(it)
+            ep_s.append(_np(task.support["idx"])); ep_q.append(_np(task.query["idx"]))
+            ep_meta.append([task.block_id, len(ep_s[-1]), len(ep_q[-1]), int(task.metrics["image_disjoint_ok"]),
+                            len(task.warnings)])
+        out[f"t_{name}_support"] = np.concatenate(ep_s).astype(np.int64)
+        out[f"t_{name}_query"] = np.concatenate(ep_q).astype(np.int64)
+        out[f"t_{name}_episodes"] = np.array(ep_meta, np.int64)
+        print(name, "valid", nv, "cells", counts.tolist(), "episodes", ep_meta)
+    save("data_tasks", **out)
+
 
 def main() -> None:
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     scene = scene_json()
     (HERE / "scene_drz_example.json").write_text(json.dumps(scene, indent=1))
     print("wrote scene_drz_example.json")
-    which = sys.argv[1:] or ["hashgrid", "sh", "volume_render", "routing", "rays", "render", "train", "occ", "meta"]
+    which = sys.argv[1:] or ["hashgrid", "sh", "volume_render", "routing", "rays", "render", "train", "occ", "meta", "data"]
     if "hashgrid" in which: gen_hashgrid()
     if "sh" in which: gen_sh()
     if "volume_render" in which: gen_volume_render()
@@ -621,6 +713,7 @@ def main() -> None:
     if "train" in which: gen_train(scene)
     if "occ" in which: gen_occ(scene)
     if "meta" in which: gen_meta(scene)
+    if "data" in which: gen_data(scene)
 
 
 if __name__ == "__main__":
