@@ -611,3 +611,6 @@ class TaskDataset(IterableDataset):
 
     def __len__(self):
         return len(self.eligible_cells)
+
+
+RamRaysDataset = DeviceRaysDataset  # the reference's name (data/ram_rays_dataset.py:127)
