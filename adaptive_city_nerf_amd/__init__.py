@@ -23,3 +23,4 @@ from .scene_box import SceneBox  # noqa: E402,F401
 from .trunc_exp import trunc_exp  # noqa: E402,F401
 from .data import (DeviceRaysDataset, ImageMetadata, Task, TaskDataset, get_dataset,  # noqa: E402,F401
                    get_image_metadata)
+from . import clusters  # noqa: E402,F401

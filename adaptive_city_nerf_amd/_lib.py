@@ -109,6 +109,8 @@ SIGNATURES = {
     "acn_route_rays": ([vp, i64, vp, vp, vp, vp, f32, f32, i32, i32, vp, vp, vp], C.c_int),
     "acn_bin_rays_workspace_bytes": ([i64, i32], C.c_size_t),
     "acn_bin_rays": ([vp, vp, i64, i32, vp, vp, vp, C.c_size_t, vp], C.c_int),
+    # clusters.hip
+    "acn_voronoi_route": ([vp, i64, i32, vp, i32, i32, C.c_double, i32, i32, vp, vp, vp, vp, vp, vp], C.c_int),
 }
 
 

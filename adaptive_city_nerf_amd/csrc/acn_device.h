@@ -35,6 +35,50 @@ __device__ __forceinline__ float clamp_nan(float v, float lo, float hi) {
     return v > hi ? hi : v;
 }
 
+// get_ray_directions (nerfs/ray_sampling.py:122-136) for pixel (i, j)
+__device__ __forceinline__ void pixel_dir(int i, int j, float fx, float fy, float cx, float cy, int center,
+                                          float& dx, float& dy, float& dz) {
+    float fi = (float)i, fj = (float)j;
+    if (center) { fi = fi + 0.5f; fj = fj + 0.5f; }
+    dx = (fi - cx) / fx;
+    dy = -((fj - cy) / fy);
+    dz = -1.0f;
+    const float n = clamp_min_nan(norm3(dx, dy, dz), 1e-12f);
+    dx = dx / n; dy = dy / n; dz = dz / n;
+}
+
+// SceneBox.ray_aabb_intersect (scene_box.py:81-107): slab test with eps-signed inverse,
+// clamp to [0, max_bound], misses (tmax <= tmin) tagged with invalid_value
+__device__ __forceinline__ void slab(const float* o, const float* d, const float* aabb, float eps, float max_bound,
+                                     float invalid_value, float& tmin, float& tmax) {
+    float t0m = -INFINITY, t1m = INFINITY;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        float rd = d[r];
+        if (fabsf(rd) < eps) rd = (rd >= 0.0f) ? eps : -eps;
+        const float inv = 1.0f / rd;
+        const float t0 = (aabb[r] - o[r]) * inv, t1 = (aabb[3 + r] - o[r]) * inv;
+        t0m = fmaxf(t0m, fminf(t0, t1));
+        t1m = fminf(t1m, fmaxf(t0, t1));
+    }
+    tmin = fminf(fmaxf(t0m, 0.0f), max_bound);
+    tmax = fminf(fmaxf(t1m, 0.0f), max_bound);
+    if (tmax <= tmin) { tmin = invalid_value; tmax = invalid_value; }
+}
+
+// torch.linspace(0, 1, S)[i] (CPU and GPU kernels: start + step*i below the middle, end - step*(S-1-i)
+// above, each evaluated as one fma)
+__device__ __forceinline__ float linspace01(int i, int S) {
+    if (S == 1) return 0.0f;
+    const float step = 1.0f / (float)(S - 1);
+    return i < S / 2 ? fmaf(step, (float)i, 0.0f) : fmaf(-step, (float)(S - 1 - i), 1.0f);
+}
+
+// torch.lerp(start, end, w) (ATen Lerp.h; the CPU vector kernel and the GPU kernel both end in one fma)
+__device__ __forceinline__ float lerp_t(float start, float end, float w) {
+    return fabsf(w) < 0.5f ? fmaf(w, end - start, start) : fmaf(w - 1.0f, end - start, end);
+}
+
 // models/encodings.py:27-81 components_from_spherical_harmonics, float32 op order of the torch
 // expressions (scalar * tensor evaluated left to right).
 template <int DEGREE>

@@ -7,36 +7,8 @@
 
 namespace {
 
-// get_ray_directions (ray_sampling.py:122-136) for pixel (i, j)
-__device__ __forceinline__ void pixel_dir(int i, int j, float fx, float fy, float cx, float cy, int center,
-                                          float& dx, float& dy, float& dz) {
-    float fi = (float)i, fj = (float)j;
-    if (center) { fi = fi + 0.5f; fj = fj + 0.5f; }
-    dx = (fi - cx) / fx;
-    dy = -((fj - cy) / fy);
-    dz = -1.0f;
-    const float n = acn::clamp_min_nan(acn::norm3(dx, dy, dz), 1e-12f);
-    dx = dx / n; dy = dy / n; dz = dz / n;
-}
-
-// SceneBox.ray_aabb_intersect (scene_box.py:81-107): slab test with eps-signed inverse,
-// clamp to [0, max_bound], misses (tmax <= tmin) tagged with invalid_value
-__device__ __forceinline__ void slab(const float* o, const float* d, const float* aabb, float eps, float max_bound,
-                                     float invalid_value, float& tmin, float& tmax) {
-    float t0m = -INFINITY, t1m = INFINITY;
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-        float rd = d[r];
-        if (fabsf(rd) < eps) rd = (rd >= 0.0f) ? eps : -eps;
-        const float inv = 1.0f / rd;
-        const float t0 = (aabb[r] - o[r]) * inv, t1 = (aabb[3 + r] - o[r]) * inv;
-        t0m = fmaxf(t0m, fminf(t0, t1));
-        t1m = fminf(t1m, fmaxf(t0, t1));
-    }
-    tmin = fminf(fmaxf(t0m, 0.0f), max_bound);
-    tmax = fminf(fmaxf(t1m, 0.0f), max_bound);
-    if (tmax <= tmin) { tmin = invalid_value; tmax = invalid_value; }
-}
+using acn::pixel_dir;
+using acn::slab;
 
 __global__ void __launch_bounds__(256) dirs_kernel(int H, int W, float fx, float fy, float cx, float cy, int center,
                                                    float* __restrict__ dirs) {

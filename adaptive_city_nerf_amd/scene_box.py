@@ -73,3 +73,34 @@ class SceneBox:
     def from_camera_poses(poses: Tensor, scale_factor: float) -> "SceneBox":
         xyzs = poses[..., :3, -1]
         return SceneBox(aabb=torch.stack([torch.min(xyzs, dim=0)[0], torch.max(xyzs, dim=0)[0]]) * scale_factor)
+
+    @staticmethod
+    def from_bound(aabb: Tensor) -> "SceneBox":
+        """An explicit (2, 3) AABB (scene_box.py:148-160)."""
+        assert isinstance(aabb, torch.Tensor), "aabb must be a torch.Tensor"
+        assert aabb.shape == (2, 3), f"Expected (2,3) AABB, got {tuple(aabb.shape)}"
+        return SceneBox(aabb=aabb)
+
+    def expand(self, pad) -> "SceneBox":
+        """Absolute padding (scene_box.py:162-205): scalar, per-axis (3,)/(1,3), or (2,3) [min side, max side]."""
+        p = torch.as_tensor(pad, dtype=self.aabb.dtype, device=self.aabb.device)
+        if p.ndim == 0:
+            lo = hi = p.expand(3)
+        elif tuple(p.shape) in ((3,), (1, 3)):
+            lo = hi = p.view(-1, 3)[-1]
+        elif tuple(p.shape) == (2, 3):
+            lo, hi = p[0], p[1]
+        else:
+            raise ValueError(f"pad must be scalar, (3,), (1,3), or (2,3); got shape {tuple(p.shape)}")
+        mn, mx = self.aabb[0] - lo, self.aabb[1] + hi
+        if not torch.all(mn < mx):
+            raise ValueError(f"expand produced invalid AABB: min {mn} not < max {mx}")
+        return SceneBox(aabb=torch.stack([mn, mx], dim=0))
+
+    def union(self, other: "SceneBox") -> "SceneBox":
+        return SceneBox(aabb=torch.stack([torch.minimum(self.aabb[0], other.aabb[0]),
+                                          torch.maximum(self.aabb[1], other.aabb[1])], dim=0))
+
+    @staticmethod
+    def reduce_union(aabbs: Tensor) -> "SceneBox":
+        return SceneBox(aabb=torch.stack([aabbs[:, 0, :].min(dim=0).values, aabbs[:, 1, :].max(dim=0).values], dim=0))

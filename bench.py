@@ -212,6 +212,26 @@ def cpu_baseline_data(td, rays, gpu_bins, min_seconds):
                       f"single thread), {dt:.1f} s; per-cell membership equal to the GPU bins: {same}"}
 
 
+def cpu_baseline_clusters(out, cents, S, min_seconds):
+    """create_clusters routing on the host cores: oracle/cluster_ref.voronoi (C, one thread) over a
+    bounded prefix of the same frame's rays; its bits are checked against the GPU's for that prefix."""
+    from oracle import cluster_ref as CR
+    bits, _, rays = out
+    n = 1 << 14
+    r = rays[:n].cpu().numpy()
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        got, _ = CR.voronoi(r, S, cents.numpy(), True, 1.1, update=True)
+        reps += 1
+        if time.perf_counter() - t0 >= min_seconds:
+            break
+    dt = time.perf_counter() - t0
+    same = bool(np.array_equal(got, bits[:n].cpu().numpy().view(np.uint64)))
+    return {"value": reps * n * S / dt, "unit": "ray-samples/s", "cores": 1, "kind": "port",
+            "sample": f"{reps} x {n} rays x {S} samples of the benchmark frame, oracle/cluster_oracle.c "
+                      f"(single thread), {dt:.1f} s; bits equal to the GPU's: {same}"}
+
+
 def cpu_baseline_meta(model, sc, task_data, S, min_seconds):
     """Meta-training on the host cores: oracle/meta_ref.py (the fixture-pinned PyTorch CPU restatement
     of train_step) on a bounded sample: one region, one task cut to 500 support + 250 query rays, the
@@ -261,7 +281,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "occ", "meta", "data"], default="c2")
+    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "occ", "meta", "data", "clusters"], default="c2")
     ap.add_argument("--rays", type=int, default=4096, help="rays per GPU (c2, c3)")
     ap.add_argument("--samples", type=int, default=256)
     ap.add_argument("--frame", type=int, default=800, help="frame side (c4)")
@@ -286,7 +306,7 @@ def main():
 
     from adaptive_city_nerf_amd import ops, parallel, render_rays
     S = a.samples
-    K = {"c2": 1, "c3": 4, "c4": 8, "c5": 8, "occ": 1, "meta": 4, "data": 1}[a.workload]
+    K = {"c2": 1, "c3": 4, "c4": 8, "c5": 8, "occ": 1, "meta": 4, "data": 1, "clusters": 1}[a.workload]
     occ_conf = None
     if a.workload == "occ":  # nerf_runner.py:124-147 defaults: 128^3 x 4 levels, cone 0.004, step diag/1000
         occ_conf = {"use_occ": True, "resolution": 128, "levels": 4, "render_step_size": None, "cone_angle": 0.004,
@@ -400,6 +420,32 @@ def main():
             return td._route_and_bin()
         sample_rays = rays
         data_n = n
+    elif a.workload == "clusters":
+        # create_clusters.py per-image step at the example dataset's g22 configuration (grid 2x2, YZ
+        # routing, margin 1.1, 256 samples, centred pixels, full 1536 x 2048 frames): ray generation +
+        # Voronoi routing with AABB streaming; rank r routes its own images (rank-strided, no exchange
+        # until the final box all-reduce)
+        from adaptive_city_nerf_amd import clusters as CL
+        from adaptive_city_nerf_amd.scene_box import SceneBox
+        msc = scene["masks"]["g22_grid_bm110_ss11"]
+        cl_cents = torch.tensor(msc["centroids"], dtype=torch.float32)
+        cl_box = SceneBox(aabb=torch.tensor(msc["aabb_global"], dtype=torch.float32).to(device))
+        cam = scene["val_cam0"]
+        cl_md = {"H": cam["H"], "W": cam["W"], "intrinsics": torch.tensor(cam["intrinsics"], dtype=torch.float32),
+                 "c2w": torch.tensor(cam["c2w"], dtype=torch.float32)}
+        S = 256
+        Cn = cl_cents.shape[0]
+        cl_state = [torch.full((Cn, 3), float("inf"), device=device), torch.full((Cn, 3), float("-inf"), device=device),
+                    torch.zeros(Cn, dtype=torch.int64, device=device), torch.zeros(Cn, dtype=torch.int32, device=device)]
+        data_n = cam["H"] * cam["W"]
+        samples_per_step = world * data_n * S
+
+        def step():
+            rays, valid = CL.image_rays(cl_md, True, cl_box, (None, None), device)
+            bits = CL.voronoi_route(rays, S, cl_cents, True, 1.1, update_aabbs=True, mins_out=cl_state[0],
+                                    maxs_out=cl_state[1], counts_out=cl_state[2], nan_out=cl_state[3])
+            return bits, valid, rays
+        sample_rays = None
     elif a.workload == "c5":
         from types import SimpleNamespace
         from adaptive_city_nerf_amd import optim as aoptim
@@ -483,6 +529,9 @@ def main():
         nparam = sum(p.numel() for p in model.submodules[expert].parameters()) + sum(p.numel() for p in shared)
         adam_bytes = 28 * nparam            # read p, g, m, v + write p, m, v (fp32)
         achieved_gbs = adam_bytes / (kernel_ms * 1e-3) / 1e9
+    if a.workload == "clusters":  # fp32 VALU arithmetic per sample: t, x, |x|^2 (10) + per centroid dot + d2 (7)
+        cl_flop = 10 + Cn * 7
+        cl_achieved = cl_flop * data_n * S / (kernel_ms * 1e-3) / 1e12
     if a.workload == "data":  # route_kernel: read a ray (32 B), write cell id (8 B) + flags (1 B)
         route_bytes = 41 * data_n
         achieved_gbs = route_bytes / (kernel_ms * 1e-3) / 1e9
@@ -501,7 +550,9 @@ def main():
              "c4": "render_kernel<1,0,1> (fused stratified render, soft routing over 8 experts)",
              "occ": "occ_render_kernel<1,1,0> (fused occupancy render over packed marched samples, 1 expert)",
              "meta": "adam_kernel (fused clip + Adam of the outer meta-update over the region experts + shared head)",
-             "data": "route_kernel (TaskDataset region clip + DDA max-overlap micro-cell routing + keep tolerance)"
+             "data": "route_kernel (TaskDataset region clip + DDA max-overlap micro-cell routing + keep tolerance)",
+             "clusters": "voronoi_kernel<4,2> (create_clusters Voronoi routing, 256 samples x 4 centroids per ray, "
+                         "AABB streaming)"
              }[a.workload]
     roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
@@ -517,6 +568,12 @@ def main():
                     "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kname,
                     "kernel_ms": round(kernel_ms, 4), "params_per_launch": int(nparam),
                     "bytes_per_param": 28, "bytes_algorithmic_per_launch": int(adam_bytes)}
+    if a.workload == "clusters":
+        roofline = {"bound": "mfma", "achieved": round(cl_achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(cl_achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                    "kernel": kname, "kernel_ms": round(kernel_ms, 4), "rays_per_launch": int(data_n),
+                    "flop_per_sample": cl_flop, "note": "fp32 VALU (no matrix shape: K = 2); MI355X's FP32 vector "
+                                                        "peak equals its FP32 matrix peak"}
     if a.workload == "data":
         roofline = {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kname,
@@ -532,9 +589,11 @@ def main():
         cpu, psnr, rmse, maxerr = cpu_baseline_occ(model, rays[idx], out[0][idx].cpu().numpy(), a.cpu_seconds)
     if rank == 0 and not a.no_cpu_baseline and a.workload == "meta":
         cpu = cpu_baseline_meta(model, sc, task_data, S, a.cpu_seconds)
+    if rank == 0 and not a.no_cpu_baseline and a.workload == "clusters":
+        cpu = cpu_baseline_clusters(out, cl_cents, S, a.cpu_seconds)
     if rank == 0 and not a.no_cpu_baseline and a.workload == "data":
         cpu = cpu_baseline_data(td, rays, out, a.cpu_seconds)
-    if rank == 0 and not a.no_cpu_baseline and a.workload not in ("c5", "occ", "meta", "data"):
+    if rank == 0 and not a.no_cpu_baseline and a.workload not in ("c5", "occ", "meta", "data", "clusters"):
         rgb_all = out[0].reshape(-1, 3)
         if a.workload == "c2":
             idx = torch.arange(rays.shape[0], device=device)[: a.cpu_rays]
@@ -569,6 +628,11 @@ def main():
                                     "steps, outer clip + Adam; metric = trained ray-samples (fwd+bwd) per second",
                         "experts": 4, "regions": 4, "tasks_per_region": 3,
                         "inner_iter": a.inner_iter if a.workload == "meta" else None},
+               "clusters": {"workload": "cluster creation (create_clusters.py, example dataset g22 configuration): "
+                                        "one 1536x2048 frame per step -- ray generation + Voronoi routing of "
+                                        "256 samples x 4 centroids per ray (YZ, margin 1.1) + per-expert AABB "
+                                        "streaming; metric counts routed ray-samples", "frame": [1536, 2048],
+                            "centroids": 4},
                "data": {"workload": f"TaskDataset construction (task_dataset.py _route_and_bin, nerf_runner.py "
                                     f"configuration: DDA routing, 1x5x5 cells): {a.data_rays} device-resident rays of "
                                     f"one region (images of the validation camera at downscale 0.25, pixel order) "

@@ -331,6 +331,20 @@ size_t acn_bin_rays_workspace_bytes(int64_t N, int n_cells);
 int acn_bin_rays(const int64_t* cell_ids, const uint8_t* flags, int64_t N, int n_cells, int32_t* ray_index,
                  int64_t* counts, void* workspace, size_t workspace_bytes, void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Cluster creation (clusters.hip).  Replaces scripts/create_clusters.py's per-image routing:
+ * compute_voronoi_opt (:386-556) and, with orig != 0, compute_voronoi_orig (:559-634).
+ * rays (N, 8) device (16-B aligned); centroids (C, 3) host, C <= 63; routing in YZ when cluster_2d.
+ * bits (N) uint64 device: bit c = ray belongs to centroid c (ray_samples samples on
+ * lerp(near, far, linspace(0, 1, S)); strict argmin when boundary_margin == 1, else
+ * d2 <= margin^2 * min d2; orig: min over samples of dist / (nearest + 1e-8) <= margin).
+ * update_aabbs (ignored with orig, as the reference): mins / maxs (C, 3) device lowered / raised in
+ * place by the assigned samples, counts (C) int64 += assigned samples, nan_flag (C) int32 set when
+ * an assigned sample is NaN.                                                                     */
+int acn_voronoi_route(const float* rays, int64_t N, int ray_samples, const float* centroids, int n_centroids,
+                      int cluster_2d, double boundary_margin, int orig, int update_aabbs, uint64_t* bits,
+                      float* mins, float* maxs, int64_t* counts, int32_t* nan_flag, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

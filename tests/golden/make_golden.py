@@ -698,12 +698,150 @@ def gen_data(scene: dict) -> None:
     save("data_tasks", **out)
 
 
+CLUSTER_ROUTE_CASES = {
+    # name: (image index in train+val metadata order, centroid set, cluster_2d, boundary_margin, samples)
+    "c2d_bm105": (0, "cent_grid22_2d", True, 1.05, 48),
+    "c2d_strict": (7, "cent_grid42_2d", True, 1.0, 32),
+    "c3d_bm110": (5, "cent_grid222_3d", False, 1.1, 40),
+}
+CLUSTER_MAIN_CASES = {
+    "grid_orig": dict(centroid_mode="grid", grid_dim=[2, 2], cluster_2d=True, boundary_margin=1.05, ray_samples=32,
+                      near=None, far=None, box_margin=0.0),
+    "kmeans_near_far": dict(centroid_mode="kmeans", grid_dim=[2, 2], cluster_2d=True, boundary_margin=1.0,
+                            ray_samples=24, near=1.0, far=200.0, box_margin=3.0, kmeans_weight_by_pixels=True),
+    "grid3d": dict(centroid_mode="grid", grid_dim=[2, 1, 2], cluster_2d=False, boundary_margin=1.1, ray_samples=16,
+                   near=None, far=150.0, box_margin=0.0),
+}
+CLUSTER_MAIN_STEMS = {"train": ["000001", "000005", "000009"], "val": ["000000"]}
+CLUSTER_MAIN_SCALE = 1.0 / 32.0
+
+
+def _cluster_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("ref_create_clusters", REF / "scripts" / "create_clusters.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def gen_clusters(scene: dict) -> None:
+    """scripts/create_clusters.py on the CPU: centroid generators, compute_voronoi_orig on three images,
+    main() end to end (--orig; the CPU path) on a 4-image dataset at 1/32 resolution, plus the
+    reference's own GPU-made outputs that ship with the example dataset (scene boxes, two images'
+    masks) for the full-scale check on the GPU."""
+    import types
+    import zipfile
+    from nerfs.ray_sampling import clamp_rays_near_far, get_ray_directions, get_rays
+    cc = _cluster_module()
+    coord = torch.load(DATA / "coordinates.pt", map_location="cpu", weights_only=True)
+    metas = sorted((DATA / "train" / "metadata").glob("*.pt")) + sorted((DATA / "val" / "metadata").glob("*.pt"))
+    mds = [torch.load(p, map_location="cpu", weights_only=True) for p in metas]
+    out = {"meta_split": np.array([p.parent.parent.name for p in metas]), "meta_stem": np.array([p.stem for p in metas]),
+           "meta_c2w": np.stack([_np(m["c2w"]) for m in mds]).astype(np.float32),
+           "meta_intr": np.stack([_np(m["intrinsics"]) for m in mds]).astype(np.float64),
+           "meta_HW": np.array([[int(m["H"]), int(m["W"])] for m in mds], np.int64),
+           "pose_scale": np.array(float(coord["pose_scale_factor"]), np.float64),
+           "origin_drb": _np(coord["origin_drb"]).astype(np.float32),
+           "altitude_range_enu": _np(torch.as_tensor(coord["altitude_range_enu"])).astype(np.float64)}
+    assert all(m["c2w"].dtype == torch.float32 for m in mds)
+    cams = torch.stack([m["c2w"] for m in mds]).float()[..., :3, 3]
+    out["cent_grid22_2d"] = _np(cc._grid_centroids(cams, 1, 2, 2, True))
+    out["cent_grid42_2d"] = _np(cc._grid_centroids(cams, 1, 4, 2, True))
+    out["cent_grid222_3d"] = _np(cc._grid_centroids(cams, 2, 2, 2, False))
+    out["cent_km4_pp"] = _np(cc._run_kmeans(cams[:, 1:].cpu(), 4, 50, "kmeans++", 0, None))
+    w = cc._cam_weights(metas)
+    out["cent_km4_pp_w"] = _np(cc._run_kmeans(cams[:, 1:].cpu(), 4, 50, "kmeans++", 0, w))
+    out["cent_km3_rand_3d"] = _np(cc._run_kmeans(cams.cpu(), 3, 20, "random", 5, None))
+    # the global box of main() (create_clusters.py:650-700) with scene_scale 1.1, pad 10 m
+    ps, ox = float(coord["pose_scale_factor"]), float(coord["origin_drb"][0])
+    lo_m, hi_m = map(float, coord["altitude_range_enu"])
+    gbox = SceneBox.from_bound(torch.tensor([[(-hi_m - ox) / ps, -1.1, -1.1], [(-lo_m - ox) / ps, 1.1, 1.1]],
+                                            dtype=torch.float32)).expand(torch.tensor([[10.0 / ps, 0, 0]]))
+    out["route_gbox"] = _np(gbox.aabb)
+    for name, (idx, cset, c2d, bm, S) in CLUSTER_ROUTE_CASES.items():
+        md = mds[idx]
+        H, W = int(md["H"]) // 16, int(md["W"]) // 16
+        fx, fy, cx, cy = [float(v) for v in (md["intrinsics"].float() / 16)]
+        dirs = get_ray_directions(H, W, fx, fy, cx, cy, True, torch.device("cpu"))
+        rays = get_rays(dirs, md["c2w"], scene_box=gbox, aabb_max_bound=1e10, aabb_invalid_value=float("inf")).view(-1, 8)
+        rays, valid = clamp_rays_near_far(rays, (None, None))
+        mask = cc.compute_voronoi_orig(rays, ray_samples=S, ray_chunk_size=4096, sample_chunk_size=S * 1000,
+                                       centroids=torch.from_numpy(out[cset]), cluster_2d=c2d,
+                                       device=torch.device("cpu"), boundary_margin=bm)
+        out[f"route_{name}_rays_sha"] = np.array(__import__("hashlib").sha256(_np(rays).tobytes()).hexdigest())
+        out[f"route_{name}_hw_intr"] = np.array([H, W, fx, fy, cx, cy], np.float64)
+        out[f"route_{name}_valid"] = _np(valid)
+        out[f"route_{name}_mask"] = np.packbits(_np(mask).reshape(-1))
+        print(name, H, W, "valid", int(valid.sum()), "mask per centroid", _np(mask).sum(0).tolist())
+    # main() end to end on a small dataset
+    import shutil
+    import tempfile
+    root = Path(tempfile.mkdtemp(prefix="acn_cc_"))
+    try:
+        torch.save(dict(coord), root / "coordinates.pt")
+        for split, stems in CLUSTER_MAIN_STEMS.items():
+            (root / split / "metadata").mkdir(parents=True)
+            for stem in stems:
+                md = dict(torch.load(DATA / split / "metadata" / f"{stem}.pt", map_location="cpu", weights_only=True))
+                md["H"], md["W"] = int(md["H"] * CLUSTER_MAIN_SCALE), int(md["W"] * CLUSTER_MAIN_SCALE)
+                md["intrinsics"] = md["intrinsics"] * CLUSTER_MAIN_SCALE
+                torch.save(md, root / split / "metadata" / f"{stem}.pt")
+        out["main_stems"] = np.array([f"{sp}/{s}" for sp, ss in CLUSTER_MAIN_STEMS.items() for s in ss])
+        for case, kw in CLUSTER_MAIN_CASES.items():
+            h = types.SimpleNamespace(data_path=root, output=Path(case), segmentation_path=None, resume=False,
+                                      kmeans_iters=50, kmeans_init="kmeans++", kmeans_seed=0,
+                                      kmeans_weight_by_pixels=False, center_pixels=True, orig=True,
+                                      ray_chunk_size=8192, sample_chunk_size=1 << 20, fp16=False, scene_scale=1.1,
+                                      altitude_range=None, altitude_pad=10.0)
+            for k_, v_ in kw.items():
+                setattr(h, k_, v_)
+            cc.main(h)
+            od = root / "masks" / case
+            params = torch.load(od / "params.pt", map_location="cpu", weights_only=True)
+            boxes = torch.load(od / "scene_boxes.pt", map_location="cpu", weights_only=True)
+            out[f"main_{case}_centroids"] = _np(params["centroids"])
+            out[f"main_{case}_aabb_global"] = _np(boxes["aabb_global"])
+            out[f"main_{case}_mins"] = _np(boxes["mins"])
+            out[f"main_{case}_maxs"] = _np(boxes["maxs"])
+            out[f"main_{case}_counts"] = _np(boxes["counts"])
+            out[f"main_{case}_params_json"] = np.array(json.dumps(
+                {k_: (list(v_) if isinstance(v_, tuple) else v_) for k_, v_ in params.items()
+                 if not isinstance(v_, torch.Tensor)}))
+            C_ = params["centroids"].shape[0]
+            masks = []
+            for sp_stem in out["main_stems"]:
+                stem = str(sp_stem).split("/")[1]
+                for c in range(C_):
+                    with zipfile.ZipFile(od / str(c) / f"{stem}.pt") as zf, zf.open(zf.namelist()[0]) as f:
+                        m = torch.load(f, map_location="cpu", weights_only=True)
+                    masks.append(np.packbits(_np(m).reshape(-1)))
+            out[f"main_{case}_masks"] = np.stack(masks)
+            print(case, "boxes", _np(boxes["mins"]).round(4).tolist(), "counts", _np(boxes["counts"]).tolist())
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+    # the reference's GPU-made mask sets that ship with the example dataset
+    for mset in ("g22_grid_bm110_ss11", "g32_grid_bm110_ss11", "g12_grid_bm110_ss11", "g11_grid_bm110_ss11"):
+        b = torch.load(DATA / "masks" / mset / "scene_boxes.pt", map_location="cpu", weights_only=True)
+        p = torch.load(DATA / "masks" / mset / "params.pt", map_location="cpu", weights_only=True)
+        for key in ("mins", "maxs", "counts", "centroids", "aabb_global"):
+            out[f"ship_{mset}_{key}"] = _np(b[key])
+        out[f"ship_{mset}_params_json"] = np.array(json.dumps(
+            {k_: (list(v_) if isinstance(v_, tuple) else v_) for k_, v_ in p.items() if not isinstance(v_, torch.Tensor)}))
+    for stem in ("000000", "000007"):
+        for c in range(4):
+            with zipfile.ZipFile(DATA / "masks" / "g22_grid_bm110_ss11" / str(c) / f"{stem}.pt") as zf, \
+                    zf.open(zf.namelist()[0]) as f:
+                m = torch.load(f, map_location="cpu", weights_only=True)
+            out[f"ship_mask_{stem}_{c}"] = np.packbits(_np(m.bool()).reshape(-1))
+    save("clusters", **out)
+
+
 def main() -> None:
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     scene = scene_json()
     (HERE / "scene_drz_example.json").write_text(json.dumps(scene, indent=1))
     print("wrote scene_drz_example.json")
-    which = sys.argv[1:] or ["hashgrid", "sh", "volume_render", "routing", "rays", "render", "train", "occ", "meta", "data"]
+    which = sys.argv[1:] or ["hashgrid", "sh", "volume_render", "routing", "rays", "render", "train", "occ", "meta", "data", "clusters"]
     if "hashgrid" in which: gen_hashgrid()
     if "sh" in which: gen_sh()
     if "volume_render" in which: gen_volume_render()
@@ -714,6 +852,7 @@ def main() -> None:
     if "occ" in which: gen_occ(scene)
     if "meta" in which: gen_meta(scene)
     if "data" in which: gen_data(scene)
+    if "clusters" in which: gen_clusters(scene)
 
 
 if __name__ == "__main__":
