@@ -56,6 +56,11 @@ ACN_OPTIM_CHUNK = 65536
 ACN_OPTIM_MAX_GROUPS = 8
 
 
+class acn_param_desc(C.Structure):
+    _fields_ = [("param", C.c_void_p), ("grad", C.c_void_p), ("exp_avg", C.c_void_p), ("exp_avg_sq", C.c_void_p),
+                ("numel", C.c_int64), ("group", C.c_int32), ("first_chunk", C.c_int32)]
+
+
 class acn_adam_group(C.Structure):
     _fields_ = [("lr", C.c_double), ("beta1", C.c_double), ("beta2", C.c_double), ("eps", C.c_double),
                 ("weight_decay", C.c_double), ("step", C.c_int32), ("pad", C.c_int32)]
@@ -89,6 +94,10 @@ SIGNATURES = {
     "acn_grad_sumsq": ([vp, vp, i64, vp, vp, vp], C.c_int),
     "acn_clip_coef": ([vp, f32, vp, vp], C.c_int),
     "acn_adam_step": ([vp, vp, i64, vp, i32, vp, vp], C.c_int),
+    "acn_optim_plan_device": ([vp, i32, vp, vp, i64, vp], C.c_int),
+    "acn_adam_table_bytes": ([i32, i32], C.c_size_t),
+    "acn_adam_table_fill": ([vp, i32, i32, i32, vp, C.c_size_t], C.c_int),
+    "acn_adam_step_table": ([vp, vp, i64, vp, i32, vp, i32, i32, vp, vp], C.c_int),
     "acn_occ_traverse": ([vp, i64, vp, i64, i64, vp, vp, vp, vp, i32, vp, f32, f32, vp, vp, i64, i64, vp, vp, vp, vp,
                           vp, vp],
                          C.c_int),

@@ -139,7 +139,141 @@ __global__ void __launch_bounds__(kThreads) adam_kernel(const acn_param_desc* __
     }
 }
 
+// graph-replayable variant: the per-group constants come from a device table indexed by a device
+// step counter that bump_kernel advances once per replay (before adam_table_kernel runs)
+__global__ void bump_kernel(int32_t* __restrict__ step_dev) { step_dev[0] += 1; }
+
+__global__ void __launch_bounds__(kThreads) adam_table_kernel(const acn_param_desc* __restrict__ descs,
+                                                              const int32_t* __restrict__ chunk_tensor,
+                                                              const GroupK* __restrict__ table, int ngroups,
+                                                              const int32_t* __restrict__ step_dev, int first_step,
+                                                              int table_steps, const float* __restrict__ grad_scale) {
+    const int row = step_dev[0] - first_step;
+    if (row < 0 || row >= table_steps) return;  // out of the uploaded range: the host re-uploads first
+    const acn_param_desc d = descs[chunk_tensor[blockIdx.x]];
+    if (d.grad == nullptr) return;
+    const GroupK k = table[(int64_t)row * ngroups + d.group];
+    const float scale = grad_scale ? grad_scale[1] : 1.0f;
+    const int64_t base = (int64_t)(blockIdx.x - d.first_chunk) * ACN_OPTIM_CHUNK;
+    const int64_t n = d.numel - base < ACN_OPTIM_CHUNK ? d.numel - base : ACN_OPTIM_CHUNK;
+    float* p = d.param + base;
+    const float* g = d.grad + base;
+    float* m = d.exp_avg + base;
+    float* v = d.exp_avg_sq + base;
+    const uintptr_t align = reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) |
+                            reinterpret_cast<uintptr_t>(m) | reinterpret_cast<uintptr_t>(v);
+    int64_t done = 0;
+    if ((align & 15) == 0) {
+        const int64_t n4 = n >> 2;
+        f4* p4 = reinterpret_cast<f4*>(p);
+        const f4* g4 = reinterpret_cast<const f4*>(g);
+        f4* m4 = reinterpret_cast<f4*>(m);
+        f4* v4 = reinterpret_cast<f4*>(v);
+        for (int64_t i = threadIdx.x; i < n4; i += kThreads) {
+            f4 pp = p4[i], mm = m4[i], vv = v4[i];
+            const f4 gg = g4[i];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                float a = pp[c], b = mm[c], e = vv[c];
+                adam_elem(a, gg[c], b, e, scale, k);
+                pp[c] = a; mm[c] = b; vv[c] = e;
+            }
+            p4[i] = pp;
+            m4[i] = mm;
+            v4[i] = vv;
+        }
+        done = n4 << 2;
+    }
+    for (int64_t i = done + threadIdx.x; i < n; i += kThreads) {
+        float a = p[i], b = m[i], e = v[i];
+        adam_elem(a, g[i], b, e, scale, k);
+        p[i] = a; m[i] = b; v[i] = e;
+    }
+}
+
+// python-float (double) scalars of _single_tensor_adam for one group at one step, cast to fp32 where
+// they meet tensors
+void group_consts(const acn_adam_group& g, GroupK& k) {
+    const double b1 = g.beta1, b2 = g.beta2;
+    const double bc1 = 1.0 - pow(b1, (double)g.step);
+    const double bc2 = 1.0 - pow(b2, (double)g.step);
+    const double step_size = (double)g.lr / bc1;
+    k.lr_neg_step = (float)(-step_size);
+    k.w1 = (float)(1.0 - b1);
+    k.beta2 = (float)b2;
+    k.one_m_beta2 = (float)(1.0 - b2);
+    k.bc2s = (float)sqrt(bc2);
+    k.eps = (float)g.eps;
+    k.wd = (float)g.weight_decay;
+}
+
+// descriptors as kernel arguments -> device memory + the chunk -> tensor map (graph capture: the
+// addresses are baked into the captured node, no host-to-device copy)
+constexpr int kPlanMax = 64;
+struct PlanArg {
+    acn_param_desc d[kPlanMax];
+};
+
+__global__ void __launch_bounds__(kThreads) plan_kernel(PlanArg pa, int n, acn_param_desc* __restrict__ out,
+                                                        int32_t* __restrict__ chunk_tensor, int64_t nchunks) {
+    for (int i = threadIdx.x; i < n; i += kThreads) out[i] = pa.d[i];
+    for (int64_t c = (int64_t)blockIdx.x * kThreads + threadIdx.x; c < nchunks; c += (int64_t)gridDim.x * kThreads) {
+        int t = 0;
+        while (t + 1 < n && pa.d[t + 1].first_chunk <= c) ++t;
+        chunk_tensor[c] = t;
+    }
+}
+
 }  // namespace
+
+extern "C" int acn_optim_plan_device(const acn_param_desc* host_descs, int n, acn_param_desc* descs,
+                                     int32_t* chunk_tensor, int64_t nchunks, void* stream) {
+    ACN_REQUIRE(n >= 1 && n <= kPlanMax, "acn_optim_plan_device: 1 <= n <= %d tensors", kPlanMax);
+    ACN_REQUIRE(host_descs && descs && chunk_tensor && nchunks >= 1, "acn_optim_plan_device: bad arguments");
+    PlanArg pa{};
+    for (int i = 0; i < n; ++i) pa.d[i] = host_descs[i];
+    const unsigned blocks = (unsigned)((nchunks + kThreads - 1) / kThreads);
+    hipLaunchKernelGGL(plan_kernel, dim3(blocks < 1 ? 1 : blocks), dim3(kThreads), 0, (hipStream_t)stream, pa, n,
+                       descs, chunk_tensor, nchunks);
+    return acn_check_launch("acn_optim_plan_device");
+}
+
+extern "C" size_t acn_adam_table_bytes(int ngroups, int steps) {
+    return (size_t)ngroups * (size_t)steps * sizeof(GroupK);
+}
+
+extern "C" int acn_adam_table_fill(const acn_adam_group* groups, int ngroups, int first_step, int steps, void* out,
+                                   size_t bytes) {
+    ACN_REQUIRE(groups && out, "acn_adam_table_fill: NULL pointer");
+    ACN_REQUIRE(ngroups >= 1 && ngroups <= ACN_OPTIM_MAX_GROUPS && steps >= 1 && first_step >= 1,
+                "acn_adam_table_fill: bad ngroups / steps / first_step");
+    ACN_REQUIRE(bytes >= acn_adam_table_bytes(ngroups, steps), "acn_adam_table_fill: buffer too small");
+    GroupK* t = reinterpret_cast<GroupK*>(out);
+    for (int s = 0; s < steps; ++s)
+        for (int i = 0; i < ngroups; ++i) {
+            acn_adam_group g = groups[i];
+            g.step = first_step + s;
+            group_consts(g, t[(size_t)s * ngroups + i]);
+        }
+    return ACN_OK;
+}
+
+extern "C" int acn_adam_step_table(const acn_param_desc* descs, const int32_t* chunk_tensor, int64_t nchunks,
+                                   const void* table, int ngroups, int32_t* step_dev, int first_step, int table_steps,
+                                   const float* grad_scale, void* stream) {
+    ACN_REQUIRE(nchunks >= 0 && nchunks <= 0x7fffffff, "acn_adam_step_table: bad nchunks");
+    ACN_REQUIRE(table && step_dev && ngroups >= 1 && ngroups <= ACN_OPTIM_MAX_GROUPS && table_steps >= 1,
+                "acn_adam_step_table: bad arguments");
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(bump_kernel, dim3(1), dim3(1), 0, s, step_dev);
+    if (nchunks > 0) {
+        ACN_REQUIRE(descs && chunk_tensor, "acn_adam_step_table: NULL pointer");
+        hipLaunchKernelGGL(adam_table_kernel, dim3((unsigned)nchunks), dim3(kThreads), 0, s, descs, chunk_tensor,
+                           reinterpret_cast<const GroupK*>(table), ngroups, step_dev, first_step, table_steps,
+                           grad_scale);
+    }
+    return acn_check_launch("acn_adam_step_table");
+}
 
 extern "C" int acn_grad_sumsq(const acn_param_desc* descs, const int32_t* chunk_tensor, int64_t nchunks,
                               double* partials, double* total, void* stream) {
@@ -172,21 +306,9 @@ extern "C" int acn_adam_step(const acn_param_desc* descs, const int32_t* chunk_t
                 ACN_OPTIM_MAX_GROUPS);
     GroupsArg ga{};
     for (int i = 0; i < ngroups; ++i) {
-        const acn_adam_group& g = groups[i];
-        ACN_REQUIRE(g.step >= 1, "acn_adam_step: group %d step must be >= 1 (incremented before the update)", i);
-        // python-float (double) scalars of _single_tensor_adam, cast to fp32 where they meet tensors
-        const double b1 = g.beta1, b2 = g.beta2;
-        const double bc1 = 1.0 - pow(b1, (double)g.step);
-        const double bc2 = 1.0 - pow(b2, (double)g.step);
-        const double step_size = (double)g.lr / bc1;
-        GroupK& k = ga.g[i];
-        k.lr_neg_step = (float)(-step_size);
-        k.w1 = (float)(1.0 - b1);
-        k.beta2 = (float)b2;
-        k.one_m_beta2 = (float)(1.0 - b2);
-        k.bc2s = (float)sqrt(bc2);
-        k.eps = (float)g.eps;
-        k.wd = (float)g.weight_decay;
+        ACN_REQUIRE(groups[i].step >= 1, "acn_adam_step: group %d step must be >= 1 (incremented before the update)",
+                    i);
+        group_consts(groups[i], ga.g[i]);
     }
     hipLaunchKernelGGL(adam_kernel, dim3((unsigned)nchunks), dim3(kThreads), 0, (hipStream_t)stream, descs,
                        chunk_tensor, ga, grad_scale);

@@ -118,8 +118,20 @@ class MetaNGP(MetaModule):
             raise ValueError(f"AABB invalid: min>=max ({mn} vs {mx})")
         assert aabb.device == self.occ_grid.aabbs.device
 
+    def _box_min_on(self, device) -> Tensor:
+        """scene_box.min on ``device``, cached on the tensor's identity / version (no per-call host copy,
+        so the training step stays capturable in a HIP graph)."""
+        mn = self.scene_box.min
+        if mn.device == device:
+            return mn
+        key = (mn.data_ptr(), mn._version, str(device))
+        if getattr(self, "_min_dev_key", None) != key:
+            self._min_dev = mn.to(device)
+            self._min_dev_key = key
+        return self._min_dev
+
     def _world_to_unit(self, x: Tensor) -> Tensor:
-        x01 = (x - self.scene_box.min.to(x.device)) / self.aabb_extent
+        x01 = (x - self._box_min_on(x.device)) / self.aabb_extent
         return x01.clamp(self.enc_eps, 1.0 - self.enc_eps)
 
     def _enc_xyz(self, x_world: Tensor) -> Tensor:

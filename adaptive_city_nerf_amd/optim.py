@@ -22,9 +22,13 @@ from ._lib import ACN_OPTIM_CHUNK, ACN_OPTIM_MAX_GROUPS, AcnError, acn_adam_grou
 
 
 class _Plan:
-    """Device descriptors (acn_param_desc) + chunk -> tensor map for a list of (p, g, m, v, key)."""
+    """Device descriptors (acn_param_desc) + chunk -> tensor map for a list of (p, g, m, v, key).
+    Under stream capture the descriptors travel as kernel arguments (acn_optim_plan_device)."""
 
     def __init__(self, rows, device):
+        if torch.cuda.is_current_stream_capturing() and rows:
+            self._init_captured(rows, device)
+            return
         self.key = tuple((p.data_ptr(), 0 if g is None else g.data_ptr(), m.data_ptr(), v.data_ptr(), k)
                          for p, g, m, v, k in rows)
         descs, owners, first = [], [], 0
@@ -42,6 +46,23 @@ class _Plan:
         self.chunk_tensor = own.pin_memory().to(device, non_blocking=True) if own.numel() else own.to(device)
         self.partials = torch.empty(max(first, 1), dtype=torch.float64, device=device)
         self._keep = (host, own)
+
+    def _init_captured(self, rows, device):
+        self.key = tuple((p.data_ptr(), 0 if g is None else g.data_ptr(), m.data_ptr(), v.data_ptr(), k)
+                         for p, g, m, v, k in rows)
+        arr = (_lib.acn_param_desc * len(rows))()
+        first = 0
+        for t, (p, g, m, v, k) in enumerate(rows):
+            arr[t] = _lib.acn_param_desc(p.data_ptr(), 0 if g is None else g.data_ptr(), m.data_ptr(), v.data_ptr(),
+                                         p.numel(), k, first)
+            first += (p.numel() + ACN_OPTIM_CHUNK - 1) // ACN_OPTIM_CHUNK
+        self.nchunks = first
+        self.descs = torch.empty(len(rows) * C.sizeof(_lib.acn_param_desc), dtype=torch.uint8, device=device)
+        self.chunk_tensor = torch.empty(max(first, 1), dtype=torch.int32, device=device)
+        self.partials = torch.empty(max(first, 1), dtype=torch.float64, device=device)
+        check(_lib.lib().acn_optim_plan_device(arr, len(rows), self.descs.data_ptr(), self.chunk_tensor.data_ptr(),
+                                               first, _stream(device)), "acn_optim_plan_device")
+        self._keep = (arr,)
 
 
 # Optional timing hook (bench.py): when set to a list, FusedAdam.step appends a pair of recorded
@@ -108,6 +129,46 @@ class FusedAdam(torch.optim.Optimizer):
         # parameters replicated across an expert-parallel group (e.g. the shared background head):
         # their squared norm is added once, after the all-reduce of everyone else's
         self.shared_params = set()
+        self._graph = None   # graph-replay state (GraphedAdaptStep): device step counter + constant table
+
+    # ------------------------------------------------------------------ graph replay
+    def graph_begin(self, max_steps: int = 1 << 16) -> None:
+        """Prepare a capture: the Adam constants of the next ``max_steps`` steps go to a device table and
+        the step count to a device counter, so the captured update is right on every replay
+        (acn_adam_step_table).  The captured step must find every gradient-carrying parameter at the
+        step after the highest one recorded now (run the warmup steps first)."""
+        cur = 0
+        for group in self.param_groups:
+            for p in group["params"]:
+                st = self.state.get(p)
+                if st and "step" in st:
+                    cur = max(cur, int(st["step"].item()))
+        ng = len(self.param_groups)
+        L = _lib.lib()
+        nbytes = int(L.acn_adam_table_bytes(ng, int(max_steps)))
+        host = torch.empty(nbytes, dtype=torch.uint8)
+        groups = (acn_adam_group * ng)()
+        for i, g in enumerate(self.param_groups):
+            b1, b2 = g["betas"]
+            groups[i] = acn_adam_group(float(g["lr"]), float(b1), float(b2), float(g["eps"]), float(g["weight_decay"]),
+                                       cur + 1, 0)
+        check(L.acn_adam_table_fill(groups, ng, cur + 1, int(max_steps), host.data_ptr(), nbytes),
+              "acn_adam_table_fill")
+        device = next(p for g in self.param_groups for p in g["params"]).device
+        self._graph = {"table": host.to(device), "step_dev": torch.tensor([cur], dtype=torch.int32, device=device),
+                       "first": cur + 1, "steps": int(max_steps), "params": []}
+
+    def graph_end_capture(self) -> None:
+        """After the capture: undo the host-side step increments the capture pass made."""
+        self.graph_sync_steps(0)
+
+    def graph_sync_steps(self, replays: int) -> None:
+        """Host-side state['step'] of the captured parameters after ``replays`` replays (state_dict)."""
+        gs = self._graph
+        for p in gs["params"]:
+            self.state[p]["step"].fill_(float(gs["first"] - 1 + replays))
+        if replays >= gs["steps"]:
+            raise AcnError("FusedAdam: graph replays exceeded the precomputed Adam table; capture again")
 
     def _rows(self):
         """(p, grad, exp_avg, exp_avg_sq, kind) rows; kind indexes distinct (group, step) pairs."""
@@ -173,6 +234,18 @@ class FusedAdam(torch.optim.Optimizer):
                     dist.all_reduce(total, group=sumsq_group)
             scale = clip_coef(total, max_norm)
             self.last_norm = scale
+        if self._graph is not None:
+            gs = self._graph
+            if len(kinds) != len(self.param_groups) or any(k != (i, gs["first"]) for i, k in enumerate(kinds)):
+                raise AcnError("FusedAdam graph mode: every parameter group needs gradients, all at the step "
+                               f"after graph_begin ({gs['first']}); got {kinds}")
+            gs["params"] = [r[0] for r in rows]
+            check(_lib.lib().acn_adam_step_table(plan.descs.data_ptr(), plan.chunk_tensor.data_ptr(), plan.nchunks,
+                                                 gs["table"].data_ptr(), len(self.param_groups),
+                                                 gs["step_dev"].data_ptr(), gs["first"], gs["steps"],
+                                                 None if scale is None else scale.data_ptr(), _stream(device)),
+                  "acn_adam_step_table")
+            return loss
         groups = (acn_adam_group * len(kinds))()
         for i, (gi, step) in enumerate(kinds):
             g = self.param_groups[gi]

@@ -67,6 +67,61 @@ def adapt_step(P, base, rays, rgbs, optimizer, active_module=None, grad_clip: Op
     return loss.detach()
 
 
+class GraphedAdaptStep:
+    """adapt_step captured once into a HIP graph and replayed per batch (the launch-bound inner loop
+    of runtime_adapt: ~165 kernels per 1000-ray step).  Same arithmetic as the eager step -- the Adam
+    constants come from FusedAdam's device table, the jitter from the graph-safe generator -- with
+    the batch copied into static buffers before each replay.  ``warmup`` eager steps run first (they
+    are real updates on the first batch).  Only fixed-shape steps are capturable: one expert
+    (``active_module``, the C5 / meta-training placement) or a bare MetaNGP -- the routed container's
+    per-expert index selection is data-dependent.  Expert-parallel groups are not captured (use
+    adapt_step)."""
+
+    def __init__(self, P, base, rays, rgbs, optimizer, active_module=None, grad_clip: Optional[float] = 1.0,
+                 warmup: int = 2, max_steps: int = 1 << 16, **render_kwargs):
+        from .meta_container import MetaContainer
+        if not isinstance(optimizer, FusedAdam):
+            raise TypeError("GraphedAdaptStep needs FusedAdam")
+        if isinstance(base, MetaContainer) and active_module is None:
+            raise ValueError("GraphedAdaptStep: the routed container step is data-dependent; pass active_module")
+        self.static_rays = rays.detach().clone()
+        self.static_rgbs = rgbs.detach().clone()
+        self.static_u = None
+        if render_kwargs.get("jitter_u") is not None:  # caller-supplied jitter: a static input too
+            self.static_u = render_kwargs["jitter_u"].detach().clone()
+            render_kwargs = dict(render_kwargs, jitter_u=self.static_u)
+        self.args = (P, base, optimizer, active_module, grad_clip, render_kwargs)
+        side = torch.cuda.Stream(rays.device)
+        side.wait_stream(torch.cuda.current_stream(rays.device))
+        with torch.cuda.stream(side):
+            for _ in range(max(1, int(warmup))):
+                adapt_step(P, base, self.static_rays, self.static_rgbs, optimizer, active_module=active_module,
+                           grad_clip=grad_clip, **render_kwargs)
+        torch.cuda.current_stream(rays.device).wait_stream(side)
+        torch.cuda.synchronize(rays.device)
+        optimizer.graph_begin(max_steps)
+        optimizer.zero_grad(set_to_none=True)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.static_loss = adapt_step(P, base, self.static_rays, self.static_rgbs, optimizer,
+                                          active_module=active_module, grad_clip=grad_clip, **render_kwargs)
+        optimizer.graph_end_capture()
+        self.replays = 0
+
+    def __call__(self, rays: torch.Tensor, rgbs: torch.Tensor, jitter_u: Optional[torch.Tensor] = None) -> torch.Tensor:
+        self.static_rays.copy_(rays, non_blocking=True)
+        self.static_rgbs.copy_(rgbs, non_blocking=True)
+        if jitter_u is not None:
+            self.static_u.copy_(jitter_u, non_blocking=True)
+        self.graph.replay()
+        self.replays += 1
+        return self.static_loss
+
+    def sync_state(self) -> None:
+        """Write the replay count into the optimizer's host state['step'] entries."""
+        self.args[2].graph_sync_steps(self.replays)
+
+
 def runtime_adapt(*, P, model, data_loader: Iterable, optimizer, steps: Optional[int] = None,
                   active_module: Optional[int] = None, grad_clip: Optional[float] = 1.0) -> Dict[str, float]:
     """runtime_adapt.py:213-315: adapt in place; one pass over the loader (steps=None) or exactly

@@ -292,6 +292,7 @@ def main():
     ap.add_argument("--support-rays", type=int, default=4000, help="meta: support rays per task")
     ap.add_argument("--query-rays", type=int, default=2000, help="meta: query rays per task")
     ap.add_argument("--data-rays", type=int, default=1 << 22, help="data: rays in the region table")
+    ap.add_argument("--no-graph", action="store_true", help="c5: eager steps instead of the HIP-graph replay")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -464,9 +465,17 @@ def main():
         samples_per_step = world * bsz * S
         it = [0]
 
+        graphed = None
+        if world == 1 and not a.no_graph:  # the launch-bound step replayed as one HIP graph
+            from adaptive_city_nerf_amd.train import GraphedAdaptStep
+            graphed = GraphedAdaptStep(P, model, pool[0], gtp[0], opt, active_module=expert, grad_clip=1.0,
+                                       warmup=2)
+
         def step():
             i = it[0] % nb
             it[0] += 1
+            if graphed is not None:
+                return graphed(pool[i], gtp[i])
             return adapt_step(P, model, pool[i], gtp[i], opt, active_module=expert, grad_clip=1.0, group=pg,
                               shared=shared)
         sample_rays = pool[0]
@@ -499,6 +508,14 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    if a.workload == "c5" and graphed is not None:
+        # graph replays run no Python, so the Adam launch is timed by one eager step afterwards
+        from adaptive_city_nerf_amd import optim as aoptim
+        graphed.sync_state()
+        opt._graph = None
+        aoptim.EVENT_HOOK = []
+        adapt_step(P, model, pool[0], gtp[0], opt, active_module=expert, grad_clip=1.0)
+        torch.cuda.synchronize()
     if a.workload in ("c5", "meta"):
         from adaptive_city_nerf_amd import optim as aoptim
         hook = aoptim.EVENT_HOOK[-a.steps:]
@@ -615,7 +632,8 @@ def main():
                       "frame": [a.frame, a.frame], "experts": 8},
                "c5": {"workload": f"C5: online adaptation, 8-expert container, rank r adapts expert r on 1000-ray x "
                                   f"{S}-sample batches (train render + MSE + backward + fused clip/Adam), shared "
-                                  f"background grads + clip norm all-reduced", "rays_per_step_per_gpu": 1000,
+                                  f"background grads + clip norm all-reduced; 1 GPU: the step replayed as one HIP graph"
+                                  f"{' (disabled)' if a.no_graph else ''}", "rays_per_step_per_gpu": 1000,
                       "experts": 8},
                "occ": {"workload": f"occupancy renderer (render_expert_occ): {a.rays} rays per GPU marched through a "
                                    f"128^3 x 4-level grid (warmup-updated from the field, "

@@ -220,6 +220,21 @@ int acn_clip_coef(const double* total_sumsq, float max_norm, float* out, void* s
 int acn_adam_step(const acn_param_desc* descs, const int32_t* chunk_tensor, int64_t nchunks,
                   const acn_adam_group* groups, int ngroups, const float* grad_scale, void* stream);
 
+/* The same update, replayable inside a captured hipGraph: the per-group constants of steps
+ * first_step .. first_step + table_steps - 1 are precomputed on the host (acn_adam_table_fill into
+ * acn_adam_table_bytes of host memory, then copied to the device by the caller); each call first
+ * advances the device step counter *step_dev by one, then updates with the table row of that step
+ * (a step outside the table leaves the parameters untouched -- the caller refills in time).      */
+/* Descriptors given in host memory (n <= 64) written to device memory together with the chunk ->
+ * tensor map by one kernel whose arguments carry them (capturable: no host-to-device copy).     */
+int acn_optim_plan_device(const acn_param_desc* host_descs, int n, acn_param_desc* descs, int32_t* chunk_tensor,
+                          int64_t nchunks, void* stream);
+size_t acn_adam_table_bytes(int ngroups, int steps);
+int acn_adam_table_fill(const acn_adam_group* groups, int ngroups, int first_step, int steps, void* out, size_t bytes);
+int acn_adam_step_table(const acn_param_desc* descs, const int32_t* chunk_tensor, int64_t nchunks, const void* table,
+                        int ngroups, int32_t* step_dev, int first_step, int table_steps, const float* grad_scale,
+                        void* stream);
+
 /* ---------------------------------------------------------------------------------------- */
 /* Occupancy-grid renderer.  The reference delegates this to nerfacc 0.5.3
  * (third-party, not vendored): OccGridEstimator.sampling -> traverse_grids, render_weight_from_density,
