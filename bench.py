@@ -266,8 +266,10 @@ def cpu_baseline_meta(model, sc, task_data, S, min_seconds):
                       f"{S} samples; oracle/meta_ref.py PyTorch CPU restatement, {threads} threads), {dt:.1f} s"}
 
 
-def load_traffic():
-    p = REPO / "profiles" / "pmc_render_r01.json"
+def load_traffic(name: str = "render"):
+    """Committed per-launch HBM bytes of a workload's dominant kernel (profiles/pmc_<name>_r01.json,
+    from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes: tools/pmc_kernel.sh + pmc_fold.py)."""
+    p = REPO / "profiles" / f"pmc_{name}_r01.json"
     if p.exists():
         try:
             return json.loads(p.read_text())
@@ -587,13 +589,15 @@ def main():
                     "bytes_per_param": 28, "bytes_algorithmic_per_launch": int(adam_bytes)}
     if a.workload == "clusters":
         roofline = {"bound": "mfma", "achieved": round(cl_achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
-                    "unit": "TFLOP/s", "frac": round(cl_achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                    "unit": "TFLOP/s", "frac": round(cl_achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+                    "traffic": (load_traffic("clusters") or {}).get("hbm_bytes_per_launch"),
                     "kernel": kname, "kernel_ms": round(kernel_ms, 4), "rays_per_launch": int(data_n),
                     "flop_per_sample": cl_flop, "note": "fp32 VALU (no matrix shape: K = 2); MI355X's FP32 vector "
                                                         "peak equals its FP32 matrix peak"}
     if a.workload == "data":
         roofline = {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kname,
+                    "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
+                    "traffic": (load_traffic("data") or {}).get("hbm_bytes_per_launch"), "kernel": kname,
                     "kernel_ms": round(kernel_ms, 4), "kernel_ms_in_step_events": round(kernel_ms_gapped, 4),
                     "rays_per_launch": int(data_n), "bytes_per_ray": 41,
                     "bytes_algorithmic_per_launch": int(route_bytes)}
