@@ -61,6 +61,11 @@ class acn_param_desc(C.Structure):
                 ("numel", C.c_int64), ("group", C.c_int32), ("first_chunk", C.c_int32)]
 
 
+class acn_mlp(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("w0", "b0", "w1", "b1", "wsh", "bsh", "wg", "bg", "wc0", "bc0", "wc1",
+                                          "bc1", "wc2", "bc2")]
+
+
 class acn_adam_group(C.Structure):
     _fields_ = [("lr", C.c_double), ("beta1", C.c_double), ("beta2", C.c_double), ("eps", C.c_double),
                 ("weight_decay", C.c_double), ("step", C.c_int32), ("pad", C.c_int32)]
@@ -118,6 +123,10 @@ SIGNATURES = {
     "acn_route_rays": ([vp, i64, vp, vp, vp, vp, f32, f32, i32, i32, vp, vp, vp], C.c_int),
     "acn_bin_rays_workspace_bytes": ([i64, i32], C.c_size_t),
     "acn_bin_rays": ([vp, vp, i64, i32, vp, vp, vp, C.c_size_t, vp], C.c_int),
+    # mlp_train.hip
+    "acn_mlp_workspace_bytes": ([], C.c_size_t),
+    "acn_mlp_train_fwd": ([vp, vp, i64, vp, vp, vp, vp, vp], C.c_int),
+    "acn_mlp_train_bwd": ([vp, vp, vp, i64, vp, vp, vp, vp, vp], C.c_int),
     # clusters.hip
     "acn_voronoi_route": ([vp, i64, i32, vp, i32, i32, C.c_double, i32, i32, vp, vp, vp, vp, vp, vp], C.c_int),
 }

@@ -15,6 +15,7 @@
 namespace {
 
 constexpr int kThreads = 256;
+constexpr int kUnroll = 4;  // 16-B vectors in flight per lane and array: 2 blocks per CU need them to cover HBM latency
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
@@ -44,7 +45,17 @@ __global__ void __launch_bounds__(kThreads) sumsq_kernel(const acn_param_desc* _
         if (vec) {
             const int64_t n4 = n >> 2;
             const f4* g4 = reinterpret_cast<const f4*>(g);
-            for (int64_t i = threadIdx.x; i < n4; i += kThreads) {
+            int64_t i = threadIdx.x;
+            for (; i + (kUnroll - 1) * kThreads < n4; i += kUnroll * kThreads) {  // kUnroll loads in flight
+                f4 v[kUnroll];
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u) v[u] = g4[i + u * kThreads];
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u)
+                    acc += (double)v[u][0] * v[u][0] + (double)v[u][1] * v[u][1] + (double)v[u][2] * v[u][2] +
+                           (double)v[u][3] * v[u][3];
+            }
+            for (; i < n4; i += kThreads) {
                 const f4 v = g4[i];
                 acc += (double)v[0] * v[0] + (double)v[1] * v[1] + (double)v[2] * v[2] + (double)v[3] * v[3];
             }
@@ -95,6 +106,62 @@ __device__ __forceinline__ void adam_elem(float& p, float gr, float& m, float& v
     p = p + (k.lr_neg_step * m) / denom;         // addcdiv_(m, denom, value = -step_size)
 }
 
+__device__ __forceinline__ void adam_vec(f4& pp, const f4& gg, f4& mm, f4& vv, float scale, const GroupK& k) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        float a = pp[c], b = mm[c], e = vv[c];
+        adam_elem(a, gg[c], b, e, scale, k);
+        pp[c] = a; mm[c] = b; vv[c] = e;
+    }
+}
+
+// one chunk of one tensor: 16-B vectors, kUnroll of each array loaded before any is updated
+__device__ __forceinline__ void adam_chunk(float* p, const float* g, float* m, float* v, int64_t n, float scale,
+                                           const GroupK& k) {
+    const uintptr_t align = reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) |
+                            reinterpret_cast<uintptr_t>(m) | reinterpret_cast<uintptr_t>(v);
+    int64_t done = 0;
+    if ((align & 15) == 0) {
+        const int64_t n4 = n >> 2;
+        f4* p4 = reinterpret_cast<f4*>(p);
+        const f4* g4 = reinterpret_cast<const f4*>(g);
+        f4* m4 = reinterpret_cast<f4*>(m);
+        f4* v4 = reinterpret_cast<f4*>(v);
+        int64_t i = threadIdx.x;
+        for (; i + (kUnroll - 1) * kThreads < n4; i += kUnroll * kThreads) {
+            f4 pp[kUnroll], gg[kUnroll], mm[kUnroll], vv[kUnroll];
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                pp[u] = p4[i + u * kThreads];
+                gg[u] = g4[i + u * kThreads];
+                mm[u] = m4[i + u * kThreads];
+                vv[u] = v4[i + u * kThreads];
+            }
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                adam_vec(pp[u], gg[u], mm[u], vv[u], scale, k);
+                p4[i + u * kThreads] = pp[u];
+                m4[i + u * kThreads] = mm[u];
+                v4[i + u * kThreads] = vv[u];
+            }
+        }
+        for (; i < n4; i += kThreads) {
+            f4 pp = p4[i], mm = m4[i], vv = v4[i];
+            const f4 gg = g4[i];
+            adam_vec(pp, gg, mm, vv, scale, k);
+            p4[i] = pp;
+            m4[i] = mm;
+            v4[i] = vv;
+        }
+        done = n4 << 2;
+    }
+    for (int64_t i = done + threadIdx.x; i < n; i += kThreads) {
+        float a = p[i], b = m[i], e = v[i];
+        adam_elem(a, g[i], b, e, scale, k);
+        p[i] = a; m[i] = b; v[i] = e;
+    }
+}
+
 __global__ void __launch_bounds__(kThreads) adam_kernel(const acn_param_desc* __restrict__ descs,
                                                         const int32_t* __restrict__ chunk_tensor, GroupsArg ga,
                                                         const float* __restrict__ grad_scale) {
@@ -108,35 +175,7 @@ __global__ void __launch_bounds__(kThreads) adam_kernel(const acn_param_desc* __
     const float* g = d.grad + base;
     float* m = d.exp_avg + base;
     float* v = d.exp_avg_sq + base;
-    const uintptr_t align = reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) |
-                            reinterpret_cast<uintptr_t>(m) | reinterpret_cast<uintptr_t>(v);
-    int64_t done = 0;
-    if ((align & 15) == 0) {
-        const int64_t n4 = n >> 2;
-        f4* p4 = reinterpret_cast<f4*>(p);
-        const f4* g4 = reinterpret_cast<const f4*>(g);
-        f4* m4 = reinterpret_cast<f4*>(m);
-        f4* v4 = reinterpret_cast<f4*>(v);
-        for (int64_t i = threadIdx.x; i < n4; i += kThreads) {
-            f4 pp = p4[i], mm = m4[i], vv = v4[i];
-            const f4 gg = g4[i];
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                float a = pp[c], b = mm[c], e = vv[c];
-                adam_elem(a, gg[c], b, e, scale, k);
-                pp[c] = a; mm[c] = b; vv[c] = e;
-            }
-            p4[i] = pp;
-            m4[i] = mm;
-            v4[i] = vv;
-        }
-        done = n4 << 2;
-    }
-    for (int64_t i = done + threadIdx.x; i < n; i += kThreads) {
-        float a = p[i], b = m[i], e = v[i];
-        adam_elem(a, g[i], b, e, scale, k);
-        p[i] = a; m[i] = b; v[i] = e;
-    }
+    adam_chunk(p, g, m, v, n, scale, k);
 }
 
 // graph-replayable variant: the per-group constants come from a device table indexed by a device
@@ -160,35 +199,7 @@ __global__ void __launch_bounds__(kThreads) adam_table_kernel(const acn_param_de
     const float* g = d.grad + base;
     float* m = d.exp_avg + base;
     float* v = d.exp_avg_sq + base;
-    const uintptr_t align = reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) |
-                            reinterpret_cast<uintptr_t>(m) | reinterpret_cast<uintptr_t>(v);
-    int64_t done = 0;
-    if ((align & 15) == 0) {
-        const int64_t n4 = n >> 2;
-        f4* p4 = reinterpret_cast<f4*>(p);
-        const f4* g4 = reinterpret_cast<const f4*>(g);
-        f4* m4 = reinterpret_cast<f4*>(m);
-        f4* v4 = reinterpret_cast<f4*>(v);
-        for (int64_t i = threadIdx.x; i < n4; i += kThreads) {
-            f4 pp = p4[i], mm = m4[i], vv = v4[i];
-            const f4 gg = g4[i];
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                float a = pp[c], b = mm[c], e = vv[c];
-                adam_elem(a, gg[c], b, e, scale, k);
-                pp[c] = a; mm[c] = b; vv[c] = e;
-            }
-            p4[i] = pp;
-            m4[i] = mm;
-            v4[i] = vv;
-        }
-        done = n4 << 2;
-    }
-    for (int64_t i = done + threadIdx.x; i < n; i += kThreads) {
-        float a = p[i], b = m[i], e = v[i];
-        adam_elem(a, g[i], b, e, scale, k);
-        p[i] = a; m[i] = b; v[i] = e;
-    }
+    adam_chunk(p, g, m, v, n, scale, k);
 }
 
 // python-float (double) scalars of _single_tensor_adam for one group at one step, cast to fp32 where

@@ -203,6 +203,10 @@ class MetaNGP(MetaModule):
         geo = self.geo_head(h, params=self.get_subdict(params, "geo_head"))
         return {"sigma": sigma, "geo_feat": geo}
 
+    def _fused_train_ok(self, x: Tensor) -> bool:
+        from .ray_rendering import _second_order
+        return x.is_cuda and self._fusable and x.dtype == torch.float32 and not _second_order()
+
     def forward(self, x_d: Tensor, params=None) -> Tensor:
         """[xyz(3), dir(3)] -> [rgb(3), sigma(1)] (meta_ngp.py:226-241)."""
         assert x_d.shape[-1] == 6, f"Expected (...,6) [xyz,dir], got {x_d.shape}"
@@ -215,6 +219,15 @@ class MetaNGP(MetaModule):
             return ops.field_fwd(flat, [spec], r, active_module=0,
                                  packed=self.packed_weights(spec, r, params)).view(*x_d.shape[:-1], 4)
         x, d = x_d[..., :3], x_d[..., 3:6]
+        if self._fused_train_ok(x_d):
+            # training: hash grid (HIP, autograd to the table) + the whole MLP fwd/bwd on MFMA
+            flat = x_d.reshape(-1, 6)
+            h0 = self._enc_xyz(flat[:, :3])
+            with torch.no_grad():
+                sh = self._enc_dir(flat[:, 3:6])
+            ws = [t.contiguous() for t in self._mlp_tensors(params).values()]
+            out = _FusedMLPFn.apply(h0.contiguous(), sh.contiguous(), *ws)
+            return out.view(*x_d.shape[:-1], 4)
         dens = self.density(x, params=params, return_feats=True)
         rgb = self.color(d, dens["geo_feat"], params=params)
         return torch.cat([rgb, dens["sigma"]], dim=-1)
@@ -335,3 +348,50 @@ class MetaNGP(MetaModule):
                       + list(self.geo_head.parameters())},
             "color": {"params": list(self.color_mlp.parameters())},
         }
+
+
+class _FusedMLPFn(torch.autograd.Function):
+    """The expert MLP on the MFMA kernels of mlp_train.hip: forward -> [sigmoid(rgb), trunc_exp(sigma)];
+    backward -> dL/d(hash features) from the kernel and each layer's [dW | db] as one GEMM over the
+    batch, dY^T . [X | 1] (the kernel saves X with a ones column).  First-order only: second-order
+    MAML renders inside ray_rendering.second_order(), which keeps the composed torch chain."""
+
+    @staticmethod
+    def forward(ctx, h0, sh, *ws):
+        need_save = any(ctx.needs_input_grad)
+        out, save = ops.mlp_train_fwd(h0, sh, ws, save=need_save)
+        if need_save:
+            ctx.save_for_backward(save, out, *ws)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        save, out, *ws = ctx.saved_tensors
+        gs, gh = ops.mlp_train_bwd(save, out, g.contiguous(), ws, want_h0=ctx.needs_input_grad[0])
+        need = ctx.needs_input_grad[2:]
+
+        def mm(go, gn, xo, xn):  # [dW | db] of one layer: batched over the 2048-sample groups, then summed
+            return torch.bmm(gs[:, go:go + gn, :], save[:, xo:xo + xn, :].transpose(1, 2)).sum(0)
+
+        grads = [None] * 14
+        if need[0] or need[1]:
+            d = mm(0, 64, 0, 33)
+            grads[0], grads[1] = d[:, :32], d[:, 32]
+        if need[2] or need[3]:
+            d = mm(64, 64, 33, 65)
+            grads[2], grads[3] = d[:, :64], d[:, 64]
+        if any(need[4:8]):
+            d = mm(128, 16, 98, 65)
+            grads[4], grads[5] = d[15:16, :64], d[15, 64:65]
+            grads[6], grads[7] = d[:15, :64], d[:15, 64]
+        if need[8] or need[9]:
+            d = mm(144, 64, 163, 32)
+            grads[8], grads[9] = d[:, :31], d[:, 31]
+        if need[10] or need[11]:
+            d = mm(208, 64, 195, 65)
+            grads[10], grads[11] = d[:, :64], d[:, 64]
+        if need[12] or need[13]:
+            d = mm(272, 3, 260, 65)
+            grads[12], grads[13] = d[:, :64], d[:, 64]
+        grads = [gr if n else None for gr, n in zip(grads, need)]
+        return (gh, None, *grads)

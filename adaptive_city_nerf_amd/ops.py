@@ -375,3 +375,58 @@ def background_fwd(dirs: torch.Tensor, background) -> torch.Tensor:
     check(_lib.lib().acn_background_fwd(ptr(d), d.shape[0], C.byref(background), ptr(out), stream_of(d)),
           "acn_background_fwd")
     return out
+
+
+# ------------------------------------------------------------------------------------------
+# expert MLP of the training path (mlp_train.hip)
+MLP_SAVE_COLS, MLP_GRAD_COLS = 325, 275
+
+
+def _mlp_struct(ws: Sequence[torch.Tensor]):
+    from ._lib import acn_mlp
+    w = acn_mlp()
+    for name, t in zip(("w0", "b0", "w1", "b1", "wsh", "bsh", "wg", "bg", "wc0", "bc0", "wc1", "bc1", "wc2", "bc2"), ws):
+        if not (t.is_contiguous() and t.dtype == torch.float32):
+            raise AcnError(f"mlp_train: {name} must be a contiguous fp32 tensor")
+        setattr(w, name, t.data_ptr())
+    return w
+
+
+MLP_GROUP = 2048
+
+
+def _mlp_ws(device):
+    return torch.empty(int(_lib.lib().acn_mlp_workspace_bytes()), dtype=torch.uint8, device=device)
+
+
+def _fm_zeros(M: int, cols: int, device) -> torch.Tensor:
+    """(groups, cols, 2048) feature-major buffer; only the last group's tail needs zeros."""
+    G = (M + MLP_GROUP - 1) // MLP_GROUP
+    t = torch.empty(G, cols, MLP_GROUP, device=device, dtype=torch.float32)
+    if M % MLP_GROUP:
+        t[-1, :, M % MLP_GROUP:].zero_()
+    return t
+
+
+def mlp_train_fwd(h0: torch.Tensor, sh: torch.Tensor, ws: Sequence[torch.Tensor], save: bool = True):
+    """(M,32) hash features + (M,16) SH -> out (M,4) and the feature-major saved layer inputs (or None)."""
+    require_hip(h0, "MetaNGP MLP (training)")
+    M = h0.shape[0]
+    out = torch.empty(M, 4, device=h0.device, dtype=torch.float32)
+    sv = _fm_zeros(M, MLP_SAVE_COLS, h0.device) if save else None
+    w = _mlp_struct(ws)
+    check(_lib.lib().acn_mlp_train_fwd(ptr(h0), ptr(sh), M, C.byref(w), ptr(out), ptr(sv) if save else None,
+                                       ptr(_mlp_ws(h0.device)), stream_of(h0)), "acn_mlp_train_fwd")
+    return out, sv
+
+
+def mlp_train_bwd(save: torch.Tensor, out: torch.Tensor, gout: torch.Tensor, ws: Sequence[torch.Tensor],
+                  want_h0: bool = True):
+    M = out.shape[0]
+    gs = _fm_zeros(M, MLP_GRAD_COLS, out.device)
+    gh = torch.empty(M, 32, device=out.device, dtype=torch.float32) if want_h0 else None
+    w = _mlp_struct(ws)
+    check(_lib.lib().acn_mlp_train_bwd(ptr(save), ptr(out), ptr(gout), M, C.byref(w), ptr(gs),
+                                       ptr(gh) if want_h0 else None, ptr(_mlp_ws(out.device)), stream_of(out)),
+          "acn_mlp_train_bwd")
+    return gs, gh

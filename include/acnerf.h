@@ -324,6 +324,37 @@ int acn_occ_mark_invisible(const float* Ks, int nK, const float* c2w, int nc2w, 
                            const int64_t* cell_indices, int64_t n, float* occs_level, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * The expert MLP of the training path (mlp_train.hip).  Replaces the differentiable MetaLinear chain
+ * of MetaNGP.density / color (models/inr/meta_ngp.py:171-241) and its autograd backward for the
+ * reference configuration (hash features 32 -> 64 -> 64 ReLU -> geo 15 + sigma 1; [geo, SH 16] ->
+ * 64 -> 64 ReLU -> 3 sigmoid).  Pointers: device weights in the reference's nn.Linear layout (out, in)
+ * -- module parameters or fast weights.                                                          */
+typedef struct acn_mlp {
+    const float *w0, *b0;          /* sigma_trunk.0.linear (64, 32), (64) */
+    const float *w1, *b1;          /* sigma_trunk.1.linear (64, 64), (64) */
+    const float *wsh, *bsh;        /* sigma_head (1, 64), (1)             */
+    const float *wg, *bg;          /* geo_head (15, 64), (15)             */
+    const float *wc0, *bc0;        /* color_mlp.0.linear (64, 31), (64)   */
+    const float *wc1, *bc1;        /* color_mlp.1.linear (64, 64), (64)   */
+    const float *wc2, *bc2;        /* color_mlp.2 (3, 64), (3)            */
+} acn_mlp;
+
+/* h0 (M, 32) hash features, sh (M, 16) SH of the directions -> out (M, 4) = [sigmoid(rgb), trunc_exp(
+ * sigma)]; save or NULL: the layer inputs with ones columns, features [h0|1][a1|1][a2|1][cin|1][c1|1]
+ * [c2|1] (widths 33, 65, 65, 32, 65, 65 = 325), stored feature-major per group of 2048 samples:
+ * (ceil(M / 2048), 325, 2048), samples past M zero (caller-initialised).  workspace:
+ * acn_mlp_workspace_bytes() device bytes (the padded weight image).                              */
+size_t acn_mlp_workspace_bytes(void);
+int acn_mlp_train_fwd(const float* h0, const float* sh, int64_t M, const acn_mlp* w, float* out, float* save,
+                      void* workspace, void* stream);
+/* Backward from dL/dout (M, 4): gsave (ceil(M / 2048), 275, 2048) = per-layer output gradients [da1 64]
+ * [da2 64][dhead 16: geo 0..14, sigma 15][dc1 64][dc2 64][drgb 3] (after the ReLU / trunc_exp / sigmoid
+ * derivatives; samples past M zero, caller-initialised), and gh0 (M, 32) = dL/dh0 (NULL: skipped).
+ * [dW | db] of a layer = sum over groups of gsave_block . save_block^T.                          */
+int acn_mlp_train_bwd(const float* save, const float* out, const float* gout, int64_t M, const acn_mlp* w,
+                      float* gsave, float* gh0, void* workspace, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
  * Episodic task routing (data.hip).  Replaces TaskDataset's region clip + micro-cell assignment
  * (data/task_dataset.py:130-172 _aabb_intersect/_region_segment, :229-352 DDA max overlap,
  * :354-418 alpha point + 6-neighbour max overlap, :544-598 selected-cell overlap >= tolerance).
