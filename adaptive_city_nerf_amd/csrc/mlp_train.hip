@@ -34,11 +34,14 @@ constexpr int O_H0 = 0, O_A1 = 33, O_A2 = 98, O_CIN = 163, O_C1 = 195, O_C2 = 26
 constexpr int DS = 275;                 // gradient row: [da1 64][da2 64][dhead 16][dc1 64][dc2 64][drgb 3]
 constexpr int G_A1 = 0, G_A2 = 64, G_HD = 128, G_C1 = 144, G_C2 = 208, G_RGB = 272;
 
-// LDS weight image: row-major, stride = cols + 1 (odd): W0 64x32, W1 64x64, Whead 16x64 (geo rows 0..14,
-// sigma row 15), Wc0 64x31 (col 31 = 0), Wc1 64x64, Wc2 3x64, then the biases
-constexpr int L_W0 = 0, L_W1 = L_W0 + 64 * 33, L_WH = L_W1 + 64 * 65, L_WC0 = L_WH + 16 * 65, L_WC1 = L_WC0 + 64 * 33,
-              L_WC2 = L_WC1 + 64 * 65, L_B0 = L_WC2 + 3 * 65, L_B1 = L_B0 + 64, L_BH = L_B1 + 64, L_BC0 = L_BH + 16,
-              L_BC1 = L_BC0 + 64, L_BC2 = L_BC1 + 64, L_FLOATS = (L_BC2 + 4 + 3) / 4 * 4;
+// LDS weight image: row-major, stride = cols + 1 (odd): W0 64x32, W1 64x64, Whead 32x64 (geo rows 0..14,
+// sigma row 15, rows 16..31 zero), Wc0 64x31 (col 31 = 0), Wc1 64x64, Wc2 32x64 (rows 3..31 zero), then
+// the biases (zero-padded to 32 rows likewise).  Padding every layer to whole 32-row tiles lets the
+// kernels read operands unconditionally (no exec-masked LDS loads).
+constexpr int L_W0 = 0, L_W1 = L_W0 + 64 * 33, L_WH = L_W1 + 64 * 65, L_WC0 = L_WH + 32 * 65, L_WC1 = L_WC0 + 64 * 33,
+              L_WC2 = L_WC1 + 64 * 65, L_B0 = L_WC2 + 32 * 65, L_B1 = L_B0 + 64, L_BH = L_B1 + 64, L_BC0 = L_BH + 32,
+              L_BC1 = L_BC0 + 64, L_BC2 = L_BC1 + 64, L_FLOATS = L_BC2 + 32;
+static_assert(L_FLOATS % 4 == 0, "16-B staging");
 
 struct MlpPtrs {
     const float *w0, *b0, *w1, *b1, *wsh, *bsh, *wg, *bg, *wc0, *bc0, *wc1, *bc1, *wc2, *bc2;
@@ -48,6 +51,16 @@ __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 __device__ __forceinline__ int rho(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+// values the compiler must treat as unknown per loop iteration, so loop-invariant LDS weight reads and
+// lane-address arithmetic are not hoisted out of the tile loop (and then spilled)
+__device__ __forceinline__ int opaque_s(int v) {
+    asm volatile("" : "+s"(v));
+    return v;
+}
+__device__ __forceinline__ int opaque_v(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
 
 __device__ __forceinline__ int64_t fm_index(int64_t m, int nfeat, int f) {
     return (m / GS) * ((int64_t)nfeat * GS) + (int64_t)f * GS + (m % GS);
@@ -64,14 +77,17 @@ __global__ void __launch_bounds__(256) mlp_pack_kernel(MlpPtrs p, float* __restr
         else if (e < L_WH) { const int q = e - L_W1, r = q / 65, c = q % 65; v = c < 64 ? p.w1[r * 64 + c] : 0.0f; }
         else if (e < L_WC0) {
             const int q = e - L_WH, r = q / 65, c = q % 65;
-            v = c < 64 ? (r < 15 ? p.wg[r * 64 + c] : p.wsh[c]) : 0.0f;
+            v = c < 64 && r < 16 ? (r < 15 ? p.wg[r * 64 + c] : p.wsh[c]) : 0.0f;
         }
         else if (e < L_WC1) { const int q = e - L_WC0, r = q / 33, c = q % 33; v = c < 31 ? p.wc0[r * 31 + c] : 0.0f; }
         else if (e < L_WC2) { const int q = e - L_WC1, r = q / 65, c = q % 65; v = c < 64 ? p.wc1[r * 64 + c] : 0.0f; }
-        else if (e < L_B0) { const int q = e - L_WC2, r = q / 65, c = q % 65; v = c < 64 ? p.wc2[r * 64 + c] : 0.0f; }
+        else if (e < L_B0) {
+            const int q = e - L_WC2, r = q / 65, c = q % 65;
+            v = c < 64 && r < 3 ? p.wc2[r * 64 + c] : 0.0f;
+        }
         else if (e < L_B1) v = p.b0[e - L_B0];
         else if (e < L_BH) v = p.b1[e - L_B1];
-        else if (e < L_BC0) { const int q = e - L_BH; v = q < 15 ? p.bg[q] : p.bsh[0]; }
+        else if (e < L_BC0) { const int q = e - L_BH; v = q < 15 ? p.bg[q] : (q == 15 ? p.bsh[0] : 0.0f); }
         else if (e < L_BC1) v = p.bc0[e - L_BC0];
         else if (e < L_BC2) v = p.bc1[e - L_BC1];
         else { const int q = e - L_BC2; v = q < 3 ? p.bc2[q] : 0.0f; }
@@ -85,43 +101,49 @@ __device__ __forceinline__ void stage_weights(const float* __restrict__ img, flo
     for (int e = threadIdx.x; e < L_FLOATS / 4; e += blockDim.x) dst[e] = src[e];
 }
 
-// Y[to] (rows 32to..) = b + W . X  (W rows < nrow, ld = stride; X: KT input tiles)
+// Y[to] (rows 32to..) = b + W . X  (W: 32*NT padded rows, ld = stride; X: KT input tiles).  The A operands
+// of an output tile are read into registers before its MFMA chain.
 template <int NT, int KT>
-__device__ __forceinline__ void fwd_layer(const float* W, int ld, int nrow, const float* b, const f32x16 (&X)[KT],
+__device__ __forceinline__ void fwd_layer(const float* W, int ld, const float* b, const f32x16 (&X)[KT],
                                           f32x16 (&Y)[NT], int lane) {
     const int i = lane & 31, h = lane >> 5;
 #pragma unroll
     for (int to = 0; to < NT; ++to) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int row = 32 * to + rho(r, h);
-            Y[to][r] = row < nrow ? b[row] : 0.0f;
-        }
-        const int wrow = 32 * to + i;
-        const float* wr = W + (wrow < nrow ? wrow : 0) * ld;
-        const bool live = wrow < nrow;
+        const float* wr = W + (32 * to + i) * ld;
+        float a[KT][16];
 #pragma unroll
         for (int t = 0; t < KT; ++t)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) Y[to] = mfma32(live ? wr[32 * t + rho(r, h)] : 0.0f, X[t][r], Y[to]);
+            for (int r = 0; r < 16; ++r) a[t][r] = wr[32 * t + rho(r, h)];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) Y[to][r] = b[32 * to + rho(r, h)];
+#pragma unroll
+        for (int t = 0; t < KT; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) Y[to] = mfma32(a[t][r], X[t][r], Y[to]);
     }
 }
 
-// dX[ti] (input features 32ti..) = W^T . dY  (W rows = output features < nrow)
-template <int NT, int KT>
-__device__ __forceinline__ void bwd_layer(const float* W, int ld, int nrow, const f32x16 (&dY)[KT], f32x16 (&dX)[NT],
+// dX[ti] (input features 32ti..) = W^T . dY  (W rows = output features; k-steps whose rows are all
+// >= NROW are skipped at compile time, the other lane half reads zero padding rows)
+template <int NT, int KT, int NROW>
+__device__ __forceinline__ void bwd_layer(const float* W, int ld, const f32x16 (&dY)[KT], f32x16 (&dX)[NT],
                                           int lane) {
     const int i = lane & 31, h = lane >> 5;
 #pragma unroll
     for (int ti = 0; ti < NT; ++ti) {
+        float a[KT][16];
+#pragma unroll
+        for (int t = 0; t < KT; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if (32 * t + rho(r, 0) < NROW) a[t][r] = W[(32 * t + rho(r, h)) * ld + 32 * ti + i];
         dX[ti] = 0.0f;
 #pragma unroll
         for (int t = 0; t < KT; ++t)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int orow = 32 * t + rho(r, h);
-                dX[ti] = mfma32(orow < nrow ? W[orow * ld + 32 * ti + i] : 0.0f, dY[t][r], dX[ti]);
-            }
+            for (int r = 0; r < 16; ++r)
+                if (32 * t + rho(r, 0) < NROW) dX[ti] = mfma32(a[t][r], dY[t][r], dX[ti]);
     }
 }
 
@@ -186,26 +208,26 @@ __device__ __forceinline__ void store_tiles(float* dst, int64_t stride, int off,
 // forward of one tile: everything the backward needs is recomputable from h0 + sh, but the weight
 // gradients need the layer inputs in memory anyway, so they are saved here
 __device__ __forceinline__ void tile_forward(const float* Wl, const float* h0, const float* sh, int64_t m, bool ok,
-                                             int lane, f32x16 (&A1)[2], f32x16 (&A2)[2], f32x16 (&Hd)[1],
-                                             f32x16 (&Cin)[1], f32x16 (&C1)[2], f32x16 (&C2)[2], f32x16 (&Rg)[1]) {
+                                             int lane, f32x16 (&X0)[1], f32x16 (&A1)[2], f32x16 (&A2)[2],
+                                             f32x16 (&Hd)[1], f32x16 (&Cin)[1], f32x16 (&C1)[2], f32x16 (&C2)[2],
+                                             f32x16 (&Rg)[1]) {
     const int h = lane >> 5;
-    f32x16 X0[1];
     load_tiles<1>(h0, 32, 0, 32, m, ok, h, X0);
-    fwd_layer<2, 1>(Wl + L_W0, 33, 64, Wl + L_B0, X0, A1, lane);
+    fwd_layer<2, 1>(Wl + L_W0, 33, Wl + L_B0, X0, A1, lane);
     relu<2>(A1);
-    fwd_layer<2, 2>(Wl + L_W1, 65, 64, Wl + L_B1, A1, A2, lane);
+    fwd_layer<2, 2>(Wl + L_W1, 65, Wl + L_B1, A1, A2, lane);
     relu<2>(A2);
-    fwd_layer<1, 2>(Wl + L_WH, 65, 16, Wl + L_BH, A2, Hd, lane);
+    fwd_layer<1, 2>(Wl + L_WH, 65, Wl + L_BH, A2, Hd, lane);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int f = rho(r, h);
         Cin[0][r] = f < 15 ? Hd[0][r] : ((ok && f < 31) ? sh[m * 16 + (f - 15)] : 0.0f);
     }
-    fwd_layer<2, 1>(Wl + L_WC0, 33, 64, Wl + L_BC0, Cin, C1, lane);
+    fwd_layer<2, 1>(Wl + L_WC0, 33, Wl + L_BC0, Cin, C1, lane);
     relu<2>(C1);
-    fwd_layer<2, 2>(Wl + L_WC1, 65, 64, Wl + L_BC1, C1, C2, lane);
+    fwd_layer<2, 2>(Wl + L_WC1, 65, Wl + L_BC1, C1, C2, lane);
     relu<2>(C2);
-    fwd_layer<1, 2>(Wl + L_WC2, 65, 3, Wl + L_BC2, C2, Rg, lane);
+    fwd_layer<1, 2>(Wl + L_WC2, 65, Wl + L_BC2, C2, Rg, lane);
 }
 
 __global__ void __launch_bounds__(256) mlp_fwd_kernel(const float* __restrict__ img, const float* __restrict__ h0,
@@ -221,8 +243,8 @@ __global__ void __launch_bounds__(256) mlp_fwd_kernel(const float* __restrict__ 
     for (int64_t tile = wave; tile < ntiles; tile += nwaves) {
         const int64_t m = tile * 32 + j;
         const bool ok = m < M;
-        f32x16 A1[2], A2[2], Hd[1], Cin[1], C1[2], C2[2], Rg[1];
-        tile_forward(Wl, h0, sh, m, ok, lane, A1, A2, Hd, Cin, C1, C2, Rg);
+        f32x16 X0[1], A1[2], A2[2], Hd[1], Cin[1], C1[2], C2[2], Rg[1];
+        tile_forward(Wl, h0, sh, m, ok, lane, X0, A1, A2, Hd, Cin, C1, C2, Rg);
         if (ok) {
             if (h == 0) {
 #pragma unroll
@@ -287,21 +309,21 @@ __global__ void __launch_bounds__(256) mlp_bwd_kernel(const float* __restrict__ 
         }
         store_fm<1>(gsave, DS, G_RGB, 3, m, ok, h, dRg);
         f32x16 G2[2], G1[2], Gc[1], mask[2];
-        bwd_layer<2, 1>(Wl + L_WC2, 65, 3, dRg, G2, lane);
+        bwd_layer<2, 1, 3>(Wl + L_WC2, 65, dRg, G2, lane);
         load_fm<2>(save, SS, O_C2, 64, m, ok, h, mask);
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
             for (int r = 0; r < 16; ++r) G2[t][r] = mask[t][r] > 0.0f ? G2[t][r] : 0.0f;
         store_fm<2>(gsave, DS, G_C2, 64, m, ok, h, G2);
-        bwd_layer<2, 2>(Wl + L_WC1, 65, 64, G2, G1, lane);
+        bwd_layer<2, 2, 64>(Wl + L_WC1, 65, G2, G1, lane);
         load_fm<2>(save, SS, O_C1, 64, m, ok, h, mask);
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
             for (int r = 0; r < 16; ++r) G1[t][r] = mask[t][r] > 0.0f ? G1[t][r] : 0.0f;
         store_fm<2>(gsave, DS, G_C1, 64, m, ok, h, G1);
-        bwd_layer<1, 2>(Wl + L_WC0, 33, 64, G1, Gc, lane);  // d cin: rows 0..14 = d geo (SH rows dropped)
+        bwd_layer<1, 2, 64>(Wl + L_WC0, 33, G1, Gc, lane);  // d cin: rows 0..14 = d geo (SH rows dropped)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int f = rho(r, h);
@@ -309,22 +331,244 @@ __global__ void __launch_bounds__(256) mlp_bwd_kernel(const float* __restrict__ 
         }
         store_fm<1>(gsave, DS, G_HD, 16, m, ok, h, dHd);
         f32x16 GA2[2], GA1[2], GH[1];
-        bwd_layer<2, 1>(Wl + L_WH, 65, 16, dHd, GA2, lane);
+        bwd_layer<2, 1, 16>(Wl + L_WH, 65, dHd, GA2, lane);
         load_fm<2>(save, SS, O_A2, 64, m, ok, h, mask);
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
             for (int r = 0; r < 16; ++r) GA2[t][r] = mask[t][r] > 0.0f ? GA2[t][r] : 0.0f;
         store_fm<2>(gsave, DS, G_A2, 64, m, ok, h, GA2);
-        bwd_layer<2, 2>(Wl + L_W1, 65, 64, GA2, GA1, lane);
+        bwd_layer<2, 2, 64>(Wl + L_W1, 65, GA2, GA1, lane);
         load_fm<2>(save, SS, O_A1, 64, m, ok, h, mask);
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
             for (int r = 0; r < 16; ++r) GA1[t][r] = mask[t][r] > 0.0f ? GA1[t][r] : 0.0f;
         store_fm<2>(gsave, DS, G_A1, 64, m, ok, h, GA1);
-        bwd_layer<1, 2>(Wl + L_W0, 33, 64, GA1, GH, lane);
+        bwd_layer<1, 2, 64>(Wl + L_W0, 33, GA1, GH, lane);
         if (gh0) store_tiles<1>(gh0, 32, 0, 32, m, ok, h, GH);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused backward with the weight gradients (acn_mlp_train_bwd_dw).  A workgroup of 4 waves takes 4 tiles
+// (128 samples) per round; each wave re-runs the forward of its tile from h0 / sh (the same tile_forward
+// as mlp_fwd_kernel, so the activations are bit-identical) instead of reading saved activations, and runs
+// the backward chain layer by layer.  At each layer the 4 waves put dY and X of their tiles into one
+// shared LDS stage [feature][128 samples]; after a barrier, wave w forms its share of that layer's
+// [dW | db] over all 128 samples on v_mfma_f32_16x16x4_f32 (row block w of the 64-row layers, column
+// block w of the sigma / colour heads), accumulating in registers that live for the whole kernel:
+// every gradient element has exactly one owner wave, so there are no atomics, and a workgroup writes
+// its 13,715 partial sums once at the end (mlp_dw_reduce_kernel adds the workgroups' copies).
+// Nothing per sample is written except dL/dh0.
+constexpr int D_W0 = 0, D_B0 = 2048, D_W1 = 2112, D_B1 = 6208, D_WSH = 6272, D_BSH = 6336, D_WG = 6337,
+              D_BG = 7297, D_WC0 = 7312, D_BC0 = 9296, D_WC1 = 9360, D_BC1 = 13456, D_WC2 = 13520, D_BC2 = 13712,
+              NDW = 13715;
+constexpr int SW = 132;                  // stage row stride (floats): 128 samples + 4, 16-B aligned rows
+constexpr int X_ROW = 64;                // stage rows 0..63 = dY, 64..127 = X
+constexpr int MAX_DW_BLOCKS = 256;       // partial copies (workgroups) of the fused backward
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// rows of accumulator-layout tiles -> stage[row0 + feature][32 * w + sample] (all 32 * NT rows; rows past a
+// layer's width hold zeros in the tiles)
+template <int NT>
+__device__ __forceinline__ void stage_put(float* st, int row0, const f32x16 (&T)[NT], int w, int lane) {
+    const int j = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) st[(row0 + 32 * t + rho(r, h)) * SW + 32 * w + j] = T[t][r];
+}
+
+// acc[n] += dY[16 rows from arow] . X[16 features from xrow + 16 n]^T over the 128 staged samples;
+// lane (i = l & 15, q = l >> 4) supplies k = sample 32 q + kk (4 k-steps per 16-B read).  bsum += this
+// lane's share of the bias row sum (the A operand is dY itself).
+template <int NCB>
+__device__ __forceinline__ void dw_blocks(const float* st, int arow, int xrow, f32x4 (&acc)[NCB], float& bsum,
+                                          int lane) {
+    const int i = lane & 15, q = lane >> 4;
+    const float* pa = st + (arow + i) * SW + 32 * q;
+    const float* pb = st + (xrow + i) * SW + 32 * q;
+#pragma unroll
+    for (int k4 = 0; k4 < 8; ++k4) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(pa + 4 * k4);
+        bsum += (a[0] + a[1]) + (a[2] + a[3]);
+#pragma unroll
+        for (int n = 0; n < NCB; ++n) {
+            const f32x4 b = *reinterpret_cast<const f32x4*>(pb + 16 * n * SW + 4 * k4);
+            acc[n] = mfma16(a[0], b[0], acc[n]);
+            acc[n] = mfma16(a[1], b[1], acc[n]);
+            acc[n] = mfma16(a[2], b[2], acc[n]);
+            acc[n] = mfma16(a[3], b[3], acc[n]);
+        }
+    }
+}
+
+template <int NT>
+__device__ __forceinline__ void relu_mask(f32x16 (&G)[NT], const f32x16 (&Y)[NT]) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) G[t][r] = Y[t][r] > 0.0f ? G[t][r] : 0.0f;
+}
+
+// one layer's stage round: barrier (previous readers done), put dY / X, barrier
+template <int NO, int NI>
+__device__ __forceinline__ void stage_layer(float* st, const f32x16 (&dY)[NO], const f32x16 (&X)[NI], int w,
+                                            int lane) {
+    __syncthreads();
+    stage_put<NO>(st, 0, dY, w, lane);
+    stage_put<NI>(st, X_ROW, X, w, lane);
+    __syncthreads();
+}
+
+// D (16x16x4 layout: lane l, reg r = row 4 (l >> 4) + r, col l & 15) of one block -> dst rows / cols
+template <typename Put>
+__device__ __forceinline__ void flush_block(const f32x4& d, int lane, Put put) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) put(4 * (lane >> 4) + r, lane & 15, d[r]);
+}
+
+__global__ void __launch_bounds__(256) mlp_bwd_dw_kernel(const float* __restrict__ img, const float* __restrict__ h0,
+                                                         const float* __restrict__ sh, const float* __restrict__ out,
+                                                         const float* __restrict__ gout, int64_t M,
+                                                         float* __restrict__ gh0, float* __restrict__ partial) {
+    __shared__ __attribute__((aligned(16))) float Wl[L_FLOATS];
+    __shared__ __attribute__((aligned(16))) float st_base[128 * SW];
+    stage_weights(img, Wl);
+    __syncthreads();
+    const int lane0 = threadIdx.x & 63, h = lane0 >> 5, j = lane0 & 31, w = threadIdx.x >> 6;
+    const int64_t ntiles = (M + 31) / 32;
+    f32x4 aWC2[1], aWC1[4], aWC0[2], aHD[1], aW1[4], aW0[2];
+    float bWC2 = 0.0f, bWC1 = 0.0f, bWC0 = 0.0f, bHD = 0.0f, bW1 = 0.0f, bW0 = 0.0f;
+    aWC2[0] = 0.0f; aHD[0] = 0.0f;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) { aWC1[n] = 0.0f; aW1[n] = 0.0f; }
+#pragma unroll
+    for (int n = 0; n < 2; ++n) { aWC0[n] = 0.0f; aW0[n] = 0.0f; }
+    // rounds are uniform over the workgroup (barriers inside): tiles past the end have zero gradients
+    for (int64_t base = (int64_t)blockIdx.x * 4; base < ntiles; base += (int64_t)gridDim.x * 4) {
+        const float* W = Wl + opaque_s(0);
+        float* st = st_base + opaque_s(0);
+        const int lane = opaque_v(lane0);
+        const int64_t m = (base + w) * 32 + j;
+        const bool ok = m < M;
+        f32x16 A1[2], A2[2], Hd[1], Cin[1], C1[2], C2[2], Rg[1];
+        {
+            f32x16 X0[1];
+            tile_forward(W, h0, sh, m, ok, lane, X0, A1, A2, Hd, Cin, C1, C2, Rg);
+        }
+        f32x16 dRg[1], dHd[1];
+        dRg[0] = 0.0f;
+        float dsig = 0.0f;
+        if (ok) {
+            if (h == 0) {
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    const float y = out[m * 4 + c];
+                    dRg[0][c] = (gout[m * 4 + c] * (1.0f - y)) * y;
+                }
+            } else {
+                dsig = gout[m * 4 + 3] * out[m * 4 + 3];
+            }
+        }
+        // colour head 3 x 64: column block w, rows 0..15 (0..2 live)
+        stage_layer<1, 2>(st, dRg, C2, w, lane);
+        dw_blocks<1>(st, 0, X_ROW + 16 * w, aWC2, bWC2, lane);
+        f32x16 G2[2], G1[2], Gc[1];
+        bwd_layer<2, 1, 3>(W + L_WC2, 65, dRg, G2, lane);
+        relu_mask<2>(G2, C2);
+        // colour layer 1, 64 x 64: row block w
+        stage_layer<2, 2>(st, G2, C1, w, lane);
+        dw_blocks<4>(st, 16 * w, X_ROW, aWC1, bWC1, lane);
+        bwd_layer<2, 2, 64>(W + L_WC1, 65, G2, G1, lane);
+        relu_mask<2>(G1, C1);
+        // colour layer 0, 64 x 31 (input 31 = zero column): row block w
+        stage_layer<2, 1>(st, G1, Cin, w, lane);
+        dw_blocks<2>(st, 16 * w, X_ROW, aWC0, bWC0, lane);
+        bwd_layer<1, 2, 64>(W + L_WC0, 33, G1, Gc, lane);  // d cin: rows 0..14 = d geo (SH rows dropped)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int f = rho(r, h);
+            dHd[0][r] = f < 15 ? Gc[0][r] : (f == 15 ? dsig : 0.0f);
+        }
+        // heads [geo 15 | sigma 1] x 64: column block w
+        stage_layer<1, 2>(st, dHd, A2, w, lane);
+        dw_blocks<1>(st, 0, X_ROW + 16 * w, aHD, bHD, lane);
+        f32x16 GA2[2], GA1[2], GH[1];
+        bwd_layer<2, 1, 16>(W + L_WH, 65, dHd, GA2, lane);
+        relu_mask<2>(GA2, A2);
+        // sigma trunk 1, 64 x 64: row block w
+        stage_layer<2, 2>(st, GA2, A1, w, lane);
+        dw_blocks<4>(st, 16 * w, X_ROW, aW1, bW1, lane);
+        bwd_layer<2, 2, 64>(W + L_W1, 65, GA2, GA1, lane);
+        relu_mask<2>(GA1, A1);
+        // sigma trunk 0, 64 x 32: row block w
+        f32x16 X0[1];
+        load_tiles<1>(h0, 32, 0, 32, m, ok, h, X0);  // reloaded (L2-hot) rather than kept live
+        stage_layer<2, 1>(st, GA1, X0, w, lane);
+        dw_blocks<2>(st, 16 * w, X_ROW, aW0, bW0, lane);
+        if (gh0) {
+            bwd_layer<1, 2, 64>(W + L_W0, 33, GA1, GH, lane);
+            store_tiles<1>(gh0, 32, 0, 32, m, ok, h, GH);
+        }
+    }
+    // flush: every element of the workgroup's copy has exactly one owner
+    float* dst = partial + (int64_t)blockIdx.x * NDW;
+    const int cw = 16 * w;
+    flush_block(aWC2[0], lane0, [&](int o, int c, float v) { if (o < 3) dst[D_WC2 + 64 * o + cw + c] = v; });
+    flush_block(aHD[0], lane0, [&](int o, int c, float v) {
+        dst[o < 15 ? D_WG + 64 * o + cw + c : D_WSH + cw + c] = v;
+    });
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+        flush_block(aWC1[n], lane0, [&](int o, int c, float v) { dst[D_WC1 + 64 * (cw + o) + 16 * n + c] = v; });
+        flush_block(aW1[n], lane0, [&](int o, int c, float v) { dst[D_W1 + 64 * (cw + o) + 16 * n + c] = v; });
+    }
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+        flush_block(aWC0[n], lane0, [&](int o, int c, float v) {
+            if (16 * n + c < 31) dst[D_WC0 + 31 * (cw + o) + 16 * n + c] = v;
+        });
+        flush_block(aW0[n], lane0, [&](int o, int c, float v) { dst[D_W0 + 32 * (cw + o) + 16 * n + c] = v; });
+    }
+    // bias rows: lane (i, q) holds the sum over samples 32 q .. 32 q + 31 of row i of its row block
+    auto red = [](float v) { v += __shfl_xor(v, 16); return v + __shfl_xor(v, 32); };
+    bWC2 = red(bWC2); bHD = red(bHD); bWC1 = red(bWC1); bWC0 = red(bWC0); bW1 = red(bW1); bW0 = red(bW0);
+    if (lane0 < 16) {
+        const int i = lane0;
+        if (w == 0) {
+            if (i < 3) dst[D_BC2 + i] = bWC2;
+            dst[i < 15 ? D_BG + i : D_BSH] = bHD;
+        }
+        dst[D_BC1 + cw + i] = bWC1;
+        dst[D_BC0 + cw + i] = bWC0;
+        dst[D_B1 + cw + i] = bW1;
+        dst[D_B0 + cw + i] = bW0;
+    }
+}
+
+// dw[e] = sum over the nblk partial copies: a block sums 32 consecutive elements, its 8 thread rows
+// stride over the copies (128-B coalesced rows), then the rows are added in LDS
+__global__ void __launch_bounds__(256) mlp_dw_reduce_kernel(const float* __restrict__ partial, int nblk,
+                                                            float* __restrict__ dw) {
+    __shared__ float red[8][32];
+    const int c = threadIdx.x & 31, row = threadIdx.x >> 5;
+    const int e = blockIdx.x * 32 + c;
+    float s = 0.0f;
+    if (e < NDW)
+        for (int b = row; b < nblk; b += 8) s += partial[(int64_t)b * NDW + e];
+    red[row][c] = s;
+    __syncthreads();
+    if (row == 0 && e < NDW) {
+        float t = red[0][c];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) t += red[k][c];
+        dw[e] = t;
     }
 }
 
@@ -364,4 +608,29 @@ extern "C" int acn_mlp_train_bwd(const float* save, const float* out, const floa
     hipLaunchKernelGGL(mlp_bwd_kernel, dim3(grid_for(M)), dim3(256), 0, s, (const float*)workspace, save, out, gout,
                        M, gsave, gh0);
     return acn_check_launch("acn_mlp_train_bwd");
+}
+
+extern "C" size_t acn_mlp_dw_workspace_bytes(void) {
+    return ((size_t)L_FLOATS + (size_t)MAX_DW_BLOCKS * NDW) * sizeof(float);
+}
+
+extern "C" int acn_mlp_train_bwd_dw(const float* h0, const float* sh, const float* out, const float* gout, int64_t M,
+                                    const acn_mlp* w, float* dw, float* gh0, void* workspace, void* stream) {
+    ACN_REQUIRE(M >= 0 && w && workspace && dw, "acn_mlp_train_bwd_dw: bad arguments");
+    hipStream_t s = (hipStream_t)stream;
+    if (M == 0) {
+        const hipError_t e = hipMemsetAsync(dw, 0, (size_t)NDW * sizeof(float), s);
+        return e == hipSuccess ? ACN_OK : acn_set_error((int)e, "acn_mlp_train_bwd_dw: memset failed");
+    }
+    ACN_REQUIRE(h0 && sh && out && gout, "acn_mlp_train_bwd_dw: NULL pointer");
+    float* img = (float*)workspace;
+    float* partial = img + L_FLOATS;  // L_FLOATS is a multiple of 4: 16-B aligned
+    const int64_t tiles = (M + 31) / 32, want = (tiles + 3) / 4;
+    const int nblk = (int)(want < MAX_DW_BLOCKS ? want : MAX_DW_BLOCKS);
+    hipLaunchKernelGGL(mlp_pack_kernel, dim3((L_FLOATS + 255) / 256), dim3(256), 0, s, ptrs(w), img);
+    hipLaunchKernelGGL(mlp_bwd_dw_kernel, dim3(nblk), dim3(256), 0, s, (const float*)img, h0, sh, out, gout, M, gh0,
+                       partial);
+    hipLaunchKernelGGL(mlp_dw_reduce_kernel, dim3((NDW + 31) / 32), dim3(256), 0, s, (const float*)partial, nblk,
+                       dw);
+    return acn_check_launch("acn_mlp_train_bwd_dw");
 }

@@ -352,23 +352,36 @@ class MetaNGP(MetaModule):
 
 class _FusedMLPFn(torch.autograd.Function):
     """The expert MLP on the MFMA kernels of mlp_train.hip: forward -> [sigmoid(rgb), trunc_exp(sigma)];
-    backward -> dL/d(hash features) from the kernel and each layer's [dW | db] as one GEMM over the
-    batch, dY^T . [X | 1] (the kernel saves X with a ones column).  First-order only: second-order
+    backward -> one fused kernel (acn_mlp_train_bwd_dw) that re-runs the forward of each 32-sample tile in
+    registers and returns dL/d(hash features) and all 14 [dW | db] (no per-sample activations are saved).
+    With DW_FUSED off, the previous split path: the forward saves the layer inputs feature-major and each
+    layer's [dW | db] is one batched GEMM dY^T . [X | 1] over the batch.  First-order only: second-order
     MAML renders inside ray_rendering.second_order(), which keeps the composed torch chain."""
+
+    DW_FUSED = True
 
     @staticmethod
     def forward(ctx, h0, sh, *ws):
-        need_save = any(ctx.needs_input_grad)
-        out, save = ops.mlp_train_fwd(h0, sh, ws, save=need_save)
-        if need_save:
-            ctx.save_for_backward(save, out, *ws)
+        need = any(ctx.needs_input_grad)
+        fused = _FusedMLPFn.DW_FUSED
+        out, save = ops.mlp_train_fwd(h0, sh, ws, save=need and not fused)
+        ctx.fused = fused
+        if need:
+            if fused:
+                ctx.save_for_backward(h0, sh, out, *ws)
+            else:
+                ctx.save_for_backward(save, out, *ws)
         return out
 
     @staticmethod
     def backward(ctx, g):
+        need = ctx.needs_input_grad[2:]
+        if ctx.fused:
+            h0, sh, out, *ws = ctx.saved_tensors
+            grads, gh = ops.mlp_train_bwd_dw(h0, sh, out, g.contiguous(), ws, want_h0=ctx.needs_input_grad[0])
+            return (gh, None, *[gr if n else None for gr, n in zip(grads, need)])
         save, out, *ws = ctx.saved_tensors
         gs, gh = ops.mlp_train_bwd(save, out, g.contiguous(), ws, want_h0=ctx.needs_input_grad[0])
-        need = ctx.needs_input_grad[2:]
 
         def mm(go, gn, xo, xn):  # [dW | db] of one layer: batched over the 2048-sample groups, then summed
             return torch.bmm(gs[:, go:go + gn, :], save[:, xo:xo + xn, :].transpose(1, 2)).sum(0)

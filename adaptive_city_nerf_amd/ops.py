@@ -430,3 +430,32 @@ def mlp_train_bwd(save: torch.Tensor, out: torch.Tensor, gout: torch.Tensor, ws:
                                        ptr(gh) if want_h0 else None, ptr(_mlp_ws(out.device)), stream_of(out)),
           "acn_mlp_train_bwd")
     return gs, gh
+
+
+# [dW | db] layout of acn_mlp_train_bwd_dw (include/acnerf.h): the 14 gradients, acn_mlp order
+MLP_DW_SHAPES = ((64, 32), (64,), (64, 64), (64,), (1, 64), (1,), (15, 64), (15,), (64, 31), (64,), (64, 64), (64,),
+                 (3, 64), (3,))
+MLP_DW_FLOATS = 13715
+
+
+def mlp_train_bwd_dw(h0: torch.Tensor, sh: torch.Tensor, out: torch.Tensor, gout: torch.Tensor,
+                     ws: Sequence[torch.Tensor], want_h0: bool = True):
+    """Fused backward: the 14 weight / bias gradients (views of one flat buffer, nn.Linear shapes) and
+    dL/dh0 (M, 32) or None, from h0 / sh (the forward is re-run in registers) and dL/dout."""
+    require_hip(h0, "MetaNGP MLP (training)")
+    M = out.shape[0]
+    dw = torch.empty(MLP_DW_FLOATS, device=out.device, dtype=torch.float32)
+    gh = torch.empty(M, 32, device=out.device, dtype=torch.float32) if want_h0 else None
+    wsp = torch.empty(int(_lib.lib().acn_mlp_dw_workspace_bytes()), dtype=torch.uint8, device=out.device)
+    w = _mlp_struct(ws)
+    check(_lib.lib().acn_mlp_train_bwd_dw(ptr(h0), ptr(sh), ptr(out), ptr(gout), M, C.byref(w), ptr(dw),
+                                          ptr(gh) if want_h0 else None, ptr(wsp), stream_of(out)),
+          "acn_mlp_train_bwd_dw")
+    grads, o = [], 0
+    for shp in MLP_DW_SHAPES:
+        n = 1
+        for d in shp:
+            n *= d
+        grads.append(dw[o:o + n].view(shp))
+        o += n
+    return grads, gh

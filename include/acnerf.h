@@ -353,6 +353,19 @@ int acn_mlp_train_fwd(const float* h0, const float* sh, int64_t M, const acn_mlp
  * [dW | db] of a layer = sum over groups of gsave_block . save_block^T.                          */
 int acn_mlp_train_bwd(const float* save, const float* out, const float* gout, int64_t M, const acn_mlp* w,
                       float* gsave, float* gh0, void* workspace, void* stream);
+/* Fused backward with the weight gradients (no saved activations): re-runs the forward from h0 / sh,
+ * back-propagates dL/dout (M, 4) (out = the forward's output) and writes
+ *   dw (13715 floats) = the 14 gradients concatenated in acn_mlp order, each in the nn.Linear layout:
+ *     w0 64x32 @0, b0 @2048, w1 64x64 @2112, b1 @6208, wsh 1x64 @6272, bsh @6336, wg 15x64 @6337,
+ *     bg @7297, wc0 64x31 @7312, bc0 @9296, wc1 64x64 @9360, bc1 @13456, wc2 3x64 @13520, bc2 @13712;
+ *   gh0 (M, 32) = dL/dh0 (NULL: skipped).
+ * Replaces the autograd backward of the MetaLinear chain incl. its weight-gradient GEMMs
+ * (torch.autograd over models/inr/meta_ngp.py:171-241).  Sums run in a different order than torch's
+ * (fp32 MFMA + workgroup partials); not bitwise reproducible run to run (LDS float atomics).
+ * workspace: acn_mlp_dw_workspace_bytes() device bytes.                                           */
+size_t acn_mlp_dw_workspace_bytes(void);
+int acn_mlp_train_bwd_dw(const float* h0, const float* sh, const float* out, const float* gout, int64_t M,
+                         const acn_mlp* w, float* dw, float* gh0, void* workspace, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Episodic task routing (data.hip).  Replaces TaskDataset's region clip + micro-cell assignment

@@ -57,3 +57,60 @@ def test_fused_mlp_fast_weights():
     out = sub(xd, params=fast)
     g = torch.autograd.grad(out.square().sum(), list(fast.values()))
     assert all(t is not None and torch.isfinite(t).all() for t in g)
+
+
+@pytest.mark.parametrize("n", [1, 4113, 300_007])
+def test_fused_dw_matches_split_path(n):
+    """acn_mlp_train_bwd_dw (forward re-run in registers, [dW | db] on MFMA, workgroup partials) against
+    the split path (saved activations + batched GEMMs): dL/dh0 and all 14 gradients.  n = 300k fills
+    every partial slot (256 workgroups x 4 waves x > 1 tile)."""
+    from adaptive_city_nerf_amd import ops
+    g = torch.Generator(device="cuda").manual_seed(n)
+    sub = _expert()
+    ws = [t.detach().contiguous() for t in (
+        sub.sigma_trunk[0].linear.weight, sub.sigma_trunk[0].linear.bias, sub.sigma_trunk[1].linear.weight,
+        sub.sigma_trunk[1].linear.bias, sub.sigma_head.weight, sub.sigma_head.bias, sub.geo_head.weight,
+        sub.geo_head.bias, sub.color_mlp[0].linear.weight, sub.color_mlp[0].linear.bias,
+        sub.color_mlp[1].linear.weight, sub.color_mlp[1].linear.bias, sub.color_mlp[2].weight,
+        sub.color_mlp[2].bias)]
+    h0 = (torch.rand(n, 32, device="cuda", generator=g) - 0.5) * 2
+    sh = (torch.rand(n, 16, device="cuda", generator=g) - 0.5) * 2
+    gout = torch.randn(n, 4, device="cuda", generator=g)
+    out, save = ops.mlp_train_fwd(h0, sh, ws, save=True)
+    out2, _ = ops.mlp_train_fwd(h0, sh, ws, save=False)
+    assert torch.equal(out, out2)
+    fused, gh_f = ops.mlp_train_bwd_dw(h0, sh, out, gout, ws, want_h0=True)
+    gs, gh_s = ops.mlp_train_bwd(save, out, gout, ws, want_h0=True)
+    # split path: layer GEMMs over the saved feature-major blocks
+    mm = lambda go, gn, xo, xn: torch.bmm(gs[:, go:go + gn, :].double(),  # noqa: E731
+                                          save[:, xo:xo + xn, :].double().transpose(1, 2)).sum(0)
+    d0, d1, dh, dc0, dc1, dc2 = mm(0, 64, 0, 33), mm(64, 64, 33, 65), mm(128, 16, 98, 65), mm(144, 64, 163, 32), \
+        mm(208, 64, 195, 65), mm(272, 3, 260, 65)
+    split = [d0[:, :32], d0[:, 32], d1[:, :64], d1[:, 64], dh[15:16, :64], dh[15, 64:65], dh[:15, :64], dh[:15, 64],
+             dc0[:, :31], dc0[:, 31], dc1[:, :64], dc1[:, 64], dc2[:, :64], dc2[:, 64]]
+    assert torch.equal(gh_f, gh_s)  # same chain, same order: bit-identical
+    for k, (a, b) in enumerate(zip(fused, split)):
+        assert a.shape == b.shape, (k, a.shape, b.shape)
+        a, b = a.double().cpu().numpy(), b.cpu().numpy()
+        scale = max(np.abs(b).max(), 1e-12)
+        assert np.abs(a - b).max() <= 2e-5 * scale + 1e-9, (k, np.abs(a - b).max(), scale)
+
+
+def test_fused_dw_empty_batch():
+    from adaptive_city_nerf_amd import ops
+    z = torch.zeros(0, 32, device="cuda")
+    out = torch.zeros(0, 4, device="cuda")
+    ws14 = [torch.zeros(s, device="cuda") for s in ops.MLP_DW_SHAPES]
+    grads, gh = ops.mlp_train_bwd_dw(z, torch.zeros(0, 16, device="cuda"), out, out, ws14, want_h0=True)
+    assert gh.shape == (0, 32) and all(float(g.abs().max()) == 0.0 for g in grads)
+
+
+def test_split_path_still_matches_composed():
+    """The previous split backward stays selectable (_FusedMLPFn.DW_FUSED = False) and correct."""
+    from adaptive_city_nerf_amd.meta_ngp import _FusedMLPFn
+    old = _FusedMLPFn.DW_FUSED
+    _FusedMLPFn.DW_FUSED = False
+    try:
+        test_fused_mlp_matches_composed(1000)
+    finally:
+        _FusedMLPFn.DW_FUSED = old
