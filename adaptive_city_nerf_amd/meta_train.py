@@ -91,8 +91,17 @@ def task_adapt(P, model, support, inner_lr, iterations, active_module=None):
             loss = compute_loss(P, model, support, params=fast, active_module=active_module, grad_buffer={},
                                 update_fisher=True)
         grads = torch.autograd.grad(loss, tuple(fast.values()), create_graph=not first_order, allow_unused=True)
-        fast = OrderedDict((n, w if g is None else (w - inner_lr * g.to(w.dtype)))
-                           for (n, w), g in zip(fast.items(), grads))
+        live = [k for k, g in enumerate(grads) if g is not None]
+        if first_order and live:
+            # the same w - lr * g (mul, then sub: bitwise equal) as two multi-tensor launches instead of
+            # two kernels per tensor; differentiable w.r.t. w for the outer gradient
+            names, ws = list(fast.keys()), list(fast.values())
+            step = torch._foreach_mul([grads[k].to(ws[k].dtype) for k in live], inner_lr)
+            upd = dict(zip(live, torch._foreach_sub([ws[k] for k in live], step)))
+            fast = OrderedDict((n, upd.get(k, ws[k])) for k, n in enumerate(names))
+        else:
+            fast = OrderedDict((n, w if g is None else (w - inner_lr * g.to(w.dtype)))
+                               for (n, w), g in zip(fast.items(), grads))
         inner_losses.append(loss.detach())
     return fast, inner_losses
 
