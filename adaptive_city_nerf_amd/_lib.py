@@ -128,6 +128,7 @@ SIGNATURES = {
     "acn_mlp_train_fwd": ([vp, vp, i64, vp, vp, vp, vp, vp], C.c_int),
     "acn_mlp_train_bwd": ([vp, vp, vp, i64, vp, vp, vp, vp, vp], C.c_int),
     "acn_mlp_dw_workspace_bytes": ([], C.c_size_t),
+    "acn_sample_stratified": ([vp, i64, C.c_int, vp, vp, vp, C.c_float, C.c_float, vp, vp, vp, vp], C.c_int),
     "acn_mlp_train_bwd_dw": ([vp, vp, vp, vp, i64, vp, vp, vp, vp, vp], C.c_int),
     # clusters.hip
     "acn_voronoi_route": ([vp, i64, i32, vp, i32, i32, C.c_double, i32, i32, vp, vp, vp, vp, vp, vp], C.c_int),

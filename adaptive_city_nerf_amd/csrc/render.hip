@@ -1429,6 +1429,33 @@ int prepare(const acn_expert* experts, const acn_routing* routing, int active_mo
         else ACN_DISPATCH_I(L, 2);                                     \
     } while (0)
 
+// Training-path sampler: stratified_t_vals (ray_rendering.py:262-287, jitter from caller uniforms), the
+// sample points o + d t (:318-320), MetaNGP._world_to_unit (meta_ngp.py:155-158) of the expert's box and
+// the colour-branch SH of the ray direction (meta_ngp.py:165-168, encodings.py:144-151), one lane per
+// sample, the same roundings as those torch ops (bitwise).  Replaces ~20 elementwise launches per call.
+__global__ void __launch_bounds__(256) sample_train_kernel(const float* __restrict__ rays, int64_t N, int S,
+                                                           const float* __restrict__ jit, float3 amin, float3 ext,
+                                                           float lo, float hi, float* __restrict__ t_out,
+                                                           float* __restrict__ x01, float* __restrict__ sh_out) {
+    const int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (m >= N * (int64_t)S) return;
+    const int64_t ray = m / S;
+    const int s = (int)(m - ray * S);
+    const float* rp = rays + ray * 8;
+    const float ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
+    const float t = tval(rp[6], rp[7], s, S, jit ? jit + ray * S : nullptr);
+    t_out[m] = t;
+    const float px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;
+    x01[m * 3 + 0] = clamp_nan((px - amin.x) / ext.x, lo, hi);
+    x01[m * 3 + 1] = clamp_nan((py - amin.y) / ext.y, lo, hi);
+    x01[m * 3 + 2] = clamp_nan((pz - amin.z) / ext.z, lo, hi);
+    float sh[16];
+    dir_sh(dx, dy, dz, sh);
+    float4* o4 = reinterpret_cast<float4*>(sh_out + m * 16);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o4[q] = make_float4(sh[4 * q], sh[4 * q + 1], sh[4 * q + 2], sh[4 * q + 3]);
+}
+
 extern "C" size_t acn_workspace_bytes(int K) { return (size_t)(K < 1 ? 1 : K) * PK_BYTES; }
 
 extern "C" int acn_pack_experts(const acn_expert* experts, const acn_routing* routing, int active_module,
@@ -1729,4 +1756,18 @@ extern "C" int acn_render_packed_fwd(const float* rays, int64_t ld, int64_t N, c
     ACN_DISPATCH(ACN_OCC_LAUNCH);
 #undef ACN_OCC_LAUNCH
     return acn_check_launch("acn_render_packed_fwd");
+}
+
+extern "C" int acn_sample_stratified(const float* rays, int64_t N, int S, const float* jitter, const float* aabb_min,
+                                     const float* aabb_extent, float lo, float hi, float* t_vals, float* x01,
+                                     float* sh, void* stream) {
+    ACN_REQUIRE(N >= 0 && S >= 1 && aabb_min && aabb_extent, "acn_sample_stratified: bad arguments");
+    if (N == 0) return ACN_OK;
+    ACN_REQUIRE(rays && t_vals && x01 && sh, "acn_sample_stratified: NULL pointer");
+    const int64_t M = N * (int64_t)S;
+    const float3 mn = make_float3(aabb_min[0], aabb_min[1], aabb_min[2]);
+    const float3 ex = make_float3(aabb_extent[0], aabb_extent[1], aabb_extent[2]);
+    hipLaunchKernelGGL(sample_train_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       rays, N, S, jitter, mn, ex, lo, hi, t_vals, x01, sh);
+    return acn_check_launch("acn_sample_stratified");
 }

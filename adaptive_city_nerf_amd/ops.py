@@ -459,3 +459,30 @@ def mlp_train_bwd_dw(h0: torch.Tensor, sh: torch.Tensor, out: torch.Tensor, gout
         grads.append(dw[o:o + n].view(shp))
         o += n
     return grads, gh
+
+
+def sample_stratified(rays: torch.Tensor, S: int, jitter: Optional[torch.Tensor], aabb_min, aabb_extent,
+                      eps: float):
+    """Training-path sampler (acn_sample_stratified): t_vals (N,S), x01 (N*S,3) in the expert's unit box
+    clamped to [eps, 1 - eps] with eps the fp32 enc_eps buffer (1 - eps evaluated in fp32, as
+    MetaNGP._world_to_unit's tensor arithmetic does), SH (N*S,16)."""
+    require_hip(rays, "render_rays_stratified sampler")
+    rays = rays.contiguous()
+    N = rays.shape[0]
+    dev = rays.device
+    t = torch.empty(N, S, device=dev, dtype=torch.float32)
+    x01 = torch.empty(N * S, 3, device=dev, dtype=torch.float32)
+    sh = torch.empty(N * S, 16, device=dev, dtype=torch.float32)
+    jit = None
+    if jitter is not None:
+        jitter = jitter.to(dev, torch.float32).contiguous()
+        jit = ptr(jitter)
+    mn = (C.c_float * 3)(*aabb_min)
+    ex = (C.c_float * 3)(*aabb_extent)
+    import numpy as np
+    lo = np.float32(eps)
+    hi = np.float32(1.0) - lo
+    check(_lib.lib().acn_sample_stratified(ptr(rays), N, int(S), jit, C.cast(mn, C.c_void_p), C.cast(ex, C.c_void_p),
+                                           C.c_float(lo), C.c_float(hi),
+                                           ptr(t), ptr(x01), ptr(sh), stream_of(rays)), "acn_sample_stratified")
+    return t, x01, sh

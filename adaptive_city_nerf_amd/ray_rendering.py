@@ -171,6 +171,18 @@ def stratified_t_vals(near: Tensor, far: Tensor, ray_samples: int, randomized: b
     return t_vals
 
 
+FUSED_TRAIN_SAMPLER = True  # tests switch it off to compare with the composed chain
+ENC_EPS = 1e-6  # MetaNGP.enc_eps (a constant fp32 buffer, meta_ngp.py:155-158), known on the host
+
+
+def _train_expert(model, active_module):
+    """The single MetaNGP a differentiable render evaluates (container + active_module, or a bare
+    MetaNGP), when it is the fused configuration; else None."""
+    sub = model.submodules[active_module] if isinstance(model, MetaContainer) and active_module is not None else (
+        model if isinstance(model, MetaNGP) else None)
+    return sub if sub is not None and sub._fusable else None
+
+
 def _fused_experts(model, params, active_module):
     """(specs, routing) for the fused kernels, or None if the model/config is not fusable."""
     if isinstance(model, MetaContainer):
@@ -236,6 +248,24 @@ def render_rays_stratified(model, rays: Tensor, ray_samples: int, params=None, a
                                                        packed=packed, want_weights=want_weights)
             return (rgb.to(rays.dtype), depth.to(rays.dtype), None if w is None else w.to(rays.dtype),
                     acc.to(rays.dtype))
+    sub = _train_expert(model, active_module) if FUSED_TRAIN_SAMPLER else None
+    if sub is not None and rays.is_cuda and rays.dtype == torch.float32 and sub._fused_train_ok(rays):
+        # differentiable single-expert path (training, inner loops): one sampler launch (t-values,
+        # unit-box points, SH), the HIP hash grid under autograd and the fused MLP -- the same values
+        # as the composed chain below
+        from .meta_ngp import _FusedMLPFn
+        u = kwargs.get("jitter_u")
+        if model.training and u is None:
+            u = torch.rand_like(rays.new_empty(N, ray_samples))  # the reference's rand_like(low) draw
+        mn, ext = sub._host_box()
+        t_vals, x01, sh = ops.sample_stratified(rays, ray_samples, u if model.training else None, mn, ext,
+                                                ENC_EPS)
+        h0 = sub.xyz_encoder(x01)
+        ws = [t.contiguous() for t in sub._mlp_tensors(params).values()]
+        rgb_sigma = _FusedMLPFn.apply(h0.contiguous(), sh, *ws).view(N, ray_samples, 4)
+        bg_rgb = _get_bg_rgb(model, rays[:, 3:6], params, rgb_sigma, N=N, bg_color_default=bg_color_default)
+        return volume_render(rgb_sigma, t_vals, bg_rgb=bg_rgb, raw_rgb=False, raw_sigma=False,
+                             sigma_scale=sigma_scale)
     # composed (differentiable) path -- same structure as the reference
     o, d = rays[:, :3], rays[:, 3:6]
     near, far = rays[:, 6], rays[:, 7]

@@ -131,6 +131,15 @@ int acn_volume_render_bwd(const float* rgb_sigma, const float* t_vals, const flo
                           float sigma_scale, const float* g_rgb, const float* g_depth, const float* g_weights,
                           const float* g_acc, float* g_rgb_sigma, float* g_bg, void* stream);
 
+/* Training-path sampler (the differentiable render_rays_stratified's non-differentiable front):
+ * stratified_t_vals (ray_rendering.py:262-287; jitter (N,S) uniforms or NULL), points o + d t
+ * (:318-320), MetaNGP._world_to_unit (meta_ngp.py:155-158) with HOST aabb_min / aabb_extent (3 floats
+ * each) and clamp [lo, hi], and the colour-branch SH-4 of the ray direction (meta_ngp.py:165-168).
+ * Outputs t_vals (N,S), x01 (N*S,3), sh (N*S,16); bitwise equal to those torch ops.               */
+int acn_sample_stratified(const float* rays, int64_t N, int S, const float* jitter, const float* aabb_min,
+                          const float* aabb_extent, float lo, float hi, float* t_vals, float* x01, float* sh,
+                          void* stream);
+
 /* Fused render_rays_stratified (ray_rendering.py:290-345 + stratified_t_vals :262-287 +
  * _get_bg_rgb :23-45 + volume_render :114-165) with the field of every expert evaluated in the
  * same kernel.  rays (N,8) [o, d, near, far]; jitter (N,S) uniforms of the training-mode draw
