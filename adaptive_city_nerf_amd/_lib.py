@@ -87,6 +87,9 @@ SIGNATURES = {
     "acn_volume_render_fwd": ([vp, vp, vp, i64, i32, i32, i32, f32, vp, vp, vp, vp, vp], C.c_int),
     "acn_render_stratified_fwd": ([vp, i64, i32, vp, vp, vp, i32, vp, f32, f32, vp, sz, vp, vp, vp, vp, vp],
                                   C.c_int),
+    "acn_render_order_bytes": ([i64], sz),
+    "acn_render_stratified_fwd_ordered": ([vp, i64, i32, vp, vp, vp, i32, vp, f32, f32, vp, sz, vp, vp, vp, vp,
+                                           vp, sz, vp], C.c_int),
     "acn_get_rays": ([i32, i32, f32, f32, f32, f32, i32, vp, vp, f32, f32, i32, f32, i32, f32, i32, vp, vp, vp],
                      C.c_int),
     "acn_ray_directions": ([i32, i32, f32, f32, f32, f32, i32, vp, vp], C.c_int),

@@ -903,6 +903,7 @@ struct RenderParams {
     const float* packed;
     float sigma_scale, tau;
     float *rgb, *depth, *weights, *acc;
+    const int32_t* order;  // optional visiting order (ray_order_kernel); NULL = rays in the given order
 };
 
 #ifndef ACN_SHFOLD
@@ -1033,9 +1034,26 @@ __global__ void __launch_bounds__(1024, 4) render_kernel(FieldCfg cfg, BgArgs bg
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // provably uniform: ray data in SGPRs
     float* cb = FOLD ? cbuf + wave * KF * 64 : nullptr;
-    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
     const float step = 1.0f / (float)(p.S - 1);
-    for (int64_t ray = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave; ray < p.N; ray += nw) {
+    // XCD bands: workgroups are dispatched round-robin over the 8 XCDs (block b -> XCD b % 8), so
+    // when the grid is a multiple of 8, XCD x walks the x-th contiguous eighth of the visiting order.
+    // With a spatially coherent order (ray_order_kernel, or pixel-ordered full frames) each XCD's
+    // 4 MB L2 then serves the hash cells of one image region instead of the whole frame.
+    const int64_t wpb = blockDim.x >> 6;
+    int64_t pos, hi, stride;
+    if ((gridDim.x & 7) == 0) {
+        const int64_t chunk = (p.N + 7) >> 3;
+        const int64_t lo = min(p.N, (int64_t)(blockIdx.x & 7) * chunk);
+        hi = min(p.N, lo + chunk);
+        pos = lo + (int64_t)(blockIdx.x >> 3) * wpb + wave;
+        stride = (int64_t)(gridDim.x >> 3) * wpb;
+    } else {
+        hi = p.N;
+        pos = (int64_t)blockIdx.x * wpb + wave;
+        stride = (int64_t)gridDim.x * wpb;
+    }
+    for (; pos < hi; pos += stride) {
+        const int64_t ray = p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[pos]) : pos;
         render_ray(p, bg, ray, lane, step,
                    [&](float px, float py, float pz, const float (&shv)[8], uint32_t& folded, float& yr, float& yg,
                        float& yb, float& ys) {
@@ -1456,7 +1474,154 @@ __global__ void __launch_bounds__(256) sample_train_kernel(const float* __restri
     for (int q = 0; q < 4; ++q) o4[q] = make_float4(sh[4 * q], sh[4 * q + 1], sh[4 * q + 2], sh[4 * q + 3]);
 }
 
+// Visiting order of a small batch (N <= ACN_ORDER_MAX): rays grouped by direction, so that the XCD
+// bands of render_kernel become compact image regions (a random pixel batch otherwise spreads every
+// XCD's samples over the whole frame and its 4 MB L2 serves the hash cells of all of it).  One
+// workgroup: the batch's mean direction m and an orthonormal pair (e1, e2) perpendicular to it; every
+// ray's gnomonic coordinates (d.e1 / d.m, d.e2 / d.m) (for one camera: its image-plane position),
+// quantised to a 64 x 64 grid over the batch's bounding box and Z-ordered; a counting sort over the
+// 4096 cells with LDS atomics (the order inside a cell is arbitrary -- it does not matter, see below).
+// Only the order changes: each ray is still rendered alone and its outputs written at its own index,
+// so results are bit-identical to the given order.  Rays with a non-finite direction or d.m <= 0
+// go to the last cell.
+#define ACN_ORDER_MAX 8192
+#define ACN_ORDER_BINS 4096
+__device__ __forceinline__ uint32_t spread6(uint32_t v) {
+    v &= 63u;
+    v = (v | (v << 4)) & 0x30Fu;
+    v = (v | (v << 2)) & 0x333u;
+    v = (v | (v << 1)) & 0x555u;
+    return v;
+}
+// workgroup-wide reductions (1024 threads = 16 waves) of 3 sums / 4 maxima; every thread gets the result
+template <int OP>
+__device__ __forceinline__ float wave_reduce(float v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const float o = __shfl_xor(v, off);
+        v = OP == 0 ? v + o : fmaxf(v, o);
+    }
+    return v;
+}
+template <int OP>
+__device__ __forceinline__ void block_reduce3(float& a, float& b, float& c, float* red) {
+    a = wave_reduce<OP>(a), b = wave_reduce<OP>(b), c = wave_reduce<OP>(c);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) red[w] = a, red[16 + w] = b, red[32 + w] = c;
+    __syncthreads();
+    a = red[0], b = red[16], c = red[32];
+    for (int k = 1; k < 16; ++k) a += red[k], b += red[16 + k], c += red[32 + k];
+    __syncthreads();  // red[] reuse
+}
+__device__ __forceinline__ void block_reduce4max(float& a, float& b, float& c, float& d, float* red) {
+    a = wave_reduce<1>(a), b = wave_reduce<1>(b), c = wave_reduce<1>(c), d = wave_reduce<1>(d);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) red[w] = a, red[16 + w] = b, red[32 + w] = c, red[48 + w] = d;
+    __syncthreads();
+    for (int k = 0; k < 16; ++k)
+        a = fmaxf(a, red[k]), b = fmaxf(b, red[16 + k]), c = fmaxf(c, red[32 + k]), d = fmaxf(d, red[48 + k]);
+    __syncthreads();
+}
+__device__ __forceinline__ bool dir_ok(float x, float y, float z) {
+    const float n2 = x * x + y * y + z * z;
+    return n2 > 0.0f && n2 < 3.0e38f;  // finite, non-zero
+}
+__global__ void __launch_bounds__(1024) ray_order_kernel(const float* __restrict__ rays, int N,
+                                                         int32_t* __restrict__ order) {
+    constexpr int PER = ACN_ORDER_MAX / 1024;
+    __shared__ int hist[ACN_ORDER_BINS];
+    __shared__ float dir[3][ACN_ORDER_MAX];
+    __shared__ uint16_t cell_of[ACN_ORDER_MAX], rank_of[ACN_ORDER_MAX];
+    __shared__ int wsum[16];
+    __shared__ float red[16 * 4];
+    const int tid = threadIdx.x;
+    for (int c = tid; c < ACN_ORDER_BINS; c += 1024) hist[c] = 0;
+    // one pass over global memory, every load of the thread in flight at once
+    float sx = 0.0f, sy = 0.0f, sz = 0.0f;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int i = tid + q * 1024;
+        if (i < N) {
+            const float* rp = rays + (int64_t)i * 8;
+            const float x = rp[3], y = rp[4], z = rp[5];
+            dir[0][i] = x, dir[1][i] = y, dir[2][i] = z;
+            if (dir_ok(x, y, z)) {
+                const float r = rsqrtf(x * x + y * y + z * z);
+                sx += x * r, sy += y * r, sz += z * r;
+            }
+        }
+    }
+    block_reduce3<0>(sx, sy, sz, red);
+    const float mn = sqrtf(sx * sx + sy * sy + sz * sz);
+    float mx = 0.0f, my = 0.0f, mz = 1.0f;
+    if (mn > 0.0f && mn < 3.0e38f) mx = sx / mn, my = sy / mn, mz = sz / mn;
+    // e1 = normalize(m x a) with a the axis least aligned with m; e2 = m x e1
+    float ax = 0.0f, ay = 0.0f, az = 0.0f;
+    if (fabsf(mx) <= fabsf(my) && fabsf(mx) <= fabsf(mz)) ax = 1.0f;
+    else if (fabsf(my) <= fabsf(mz)) ay = 1.0f;
+    else az = 1.0f;
+    float e1x = my * az - mz * ay, e1y = mz * ax - mx * az, e1z = mx * ay - my * ax;
+    const float e1n = rsqrtf(e1x * e1x + e1y * e1y + e1z * e1z);
+    e1x *= e1n, e1y *= e1n, e1z *= e1n;
+    const float e2x = my * e1z - mz * e1y, e2y = mz * e1x - mx * e1z, e2z = mx * e1y - my * e1x;
+    auto coords = [&](int i, float& u, float& v) -> bool {
+        const float x = dir[0][i], y = dir[1][i], z = dir[2][i];
+        if (!dir_ok(x, y, z)) return false;
+        const float dm = x * mx + y * my + z * mz;
+        if (!(dm > 0.0f)) return false;
+        u = (x * e1x + y * e1y + z * e1z) / dm;
+        v = (x * e2x + y * e2y + z * e2z) / dm;
+        return fabsf(u) < 1.0e30f && fabsf(v) < 1.0e30f;
+    };
+    float umin = 3.0e38f, vmin = 3.0e38f, umax = -3.0e38f, vmax = -3.0e38f;
+    for (int i = tid; i < N; i += 1024) {
+        float u, v;
+        if (coords(i, u, v)) umin = fminf(umin, u), umax = fmaxf(umax, u), vmin = fminf(vmin, v), vmax = fmaxf(vmax, v);
+    }
+    umin = -umin, vmin = -vmin;  // one max-reduction for all four
+    block_reduce4max(umin, vmin, umax, vmax, red);
+    umin = -umin, vmin = -vmin;
+    const float su = umax > umin ? 63.999f / (umax - umin) : 0.0f;
+    const float sv = vmax > vmin ? 63.999f / (vmax - vmin) : 0.0f;
+    for (int i = tid; i < N; i += 1024) {
+        float u, v;
+        int c = ACN_ORDER_BINS - 1;
+        if (coords(i, u, v)) {
+            const uint32_t qu = (uint32_t)fminf(fmaxf((u - umin) * su, 0.0f), 63.0f);
+            const uint32_t qv = (uint32_t)fminf(fmaxf((v - vmin) * sv, 0.0f), 63.0f);
+            c = (int)(spread6(qu) | (spread6(qv) << 1));
+        }
+        cell_of[i] = (uint16_t)c;
+        rank_of[i] = (uint16_t)atomicAdd(&hist[c], 1);
+    }
+    __syncthreads();
+    // exclusive scan of hist: 4 cells per thread, wave scan of the thread sums, then the wave totals
+    constexpr int CPT = ACN_ORDER_BINS / 1024;
+    int h[CPT], run = 0;
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) h[c] = hist[tid * CPT + c], run += h[c];
+    const int lane = tid & 63;
+    int incl = run;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(incl, off);
+        if (lane >= off) incl += o;
+    }
+    if (lane == 63) wsum[tid >> 6] = incl;
+    __syncthreads();
+    int base = incl - run;
+    for (int w = 0; w < (tid >> 6); ++w) base += wsum[w];
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) hist[tid * CPT + c] = base, base += h[c];
+    __syncthreads();
+    for (int i = tid; i < N; i += 1024) order[hist[cell_of[i]] + rank_of[i]] = i;
+}
+
 extern "C" size_t acn_workspace_bytes(int K) { return (size_t)(K < 1 ? 1 : K) * PK_BYTES; }
+
+extern "C" size_t acn_render_order_bytes(int64_t N) {
+    return N >= 1 && N <= ACN_ORDER_MAX ? (size_t)N * sizeof(int32_t) : 0;
+}
 
 extern "C" int acn_pack_experts(const acn_expert* experts, const acn_routing* routing, int active_module,
                                 void* workspace, size_t workspace_bytes, void* stream) {
@@ -1492,6 +1657,16 @@ extern "C" int acn_render_stratified_fwd(const float* rays, int64_t N, int S, co
                                          const acn_background* bg, float sigma_scale, float tau, void* workspace,
                                          size_t workspace_bytes, float* rgb, float* depth, float* weights, float* acc,
                                          void* stream) {
+    return acn_render_stratified_fwd_ordered(rays, N, S, jitter, experts, routing, active_module, bg, sigma_scale, tau,
+                                             workspace, workspace_bytes, rgb, depth, weights, acc, nullptr, 0, stream);
+}
+
+extern "C" int acn_render_stratified_fwd_ordered(const float* rays, int64_t N, int S, const float* jitter,
+                                                 const acn_expert* experts, const acn_routing* routing,
+                                                 int active_module, const acn_background* bg, float sigma_scale,
+                                                 float tau, void* workspace, size_t workspace_bytes, float* rgb,
+                                                 float* depth, float* weights, float* acc, void* order_scratch,
+                                                 size_t order_bytes, void* stream) {
     ACN_REQUIRE(N >= 0, "acn_render_stratified_fwd: N must be >= 0");
     ACN_REQUIRE(S >= 2, "acn_render_stratified_fwd: ray_samples must be >= 2, got %d", S);
     if (N == 0) return ACN_OK;
@@ -1507,9 +1682,15 @@ extern "C" int acn_render_stratified_fwd(const float* rays, int64_t N, int S, co
     int st = prepare(experts, routing, active_module, workspace, workspace_bytes, s, cfg, interp, K, false);
     if (st) return st;
     BgArgs b{bg->mode, bg->hidden, {bg->color[0], bg->color[1], bg->color[2]}, bg->w1, bg->b1, bg->w2, bg->b2};
-    RenderParams p{rays, N, S, jitter, (const float*)workspace, sigma_scale, tau, rgb, depth, weights, acc};
-    const int64_t wgs = (N + 15) / 16;
+    RenderParams p{rays, N, S, jitter, (const float*)workspace, sigma_scale, tau, rgb, depth, weights, acc, nullptr};
+    int64_t wgs = (N + 15) / 16;
+    if ((num_cus() & 7) == 0) wgs = (wgs + 7) & ~(int64_t)7;  // whole XCD bands (render_kernel)
     const dim3 grid((unsigned)(wgs < num_cus() ? wgs : num_cus())), block(1024);
+    const bool slots = ACN_SLOTS && cfg.routing != 0 && K != 2;  // render_slots_kernel keeps its own order
+    if (order_scratch && !slots && N <= ACN_ORDER_MAX && order_bytes >= (size_t)N * sizeof(int32_t)) {
+        hipLaunchKernelGGL(ray_order_kernel, dim3(1), dim3(1024), 0, s, rays, (int)N, (int32_t*)order_scratch);
+        p.order = (const int32_t*)order_scratch;
+    }
 #define ACN_RENDER_LAUNCH(I, KL, R)                                                                    \
     do {                                                                                              \
         if (ACN_SLOTS && KL == 0 && R != 0) hipLaunchKernelGGL((render_slots_kernel<I, (R == 0 ? 1 : R)>), grid, dim3(ACN_SLOTS_THREADS), 0, s, cfg, b, p); \

@@ -199,11 +199,15 @@ def field_fwd(x: torch.Tensor, experts: Sequence[ExpertSpec], routing: acn_routi
 # recorded HIP events bracketing exactly the fused render kernel on the launch stream.
 EVENT_HOOK = None
 
+# Default of render_stratified(reorder=None): direction-sorted visiting order for small batches
+# (acn_render_stratified_fwd_ordered; outputs are identical either way, only the speed changes).
+REORDER = True
+
 
 def render_stratified(rays: torch.Tensor, S: int, experts: Sequence[ExpertSpec], routing: acn_routing,
                       active_module: Optional[int], background, sigma_scale: float = 1.0, tau: float = 0.0,
                       jitter: Optional[torch.Tensor] = None, want_weights: bool = True,
-                      packed: Optional[torch.Tensor] = None):
+                      packed: Optional[torch.Tensor] = None, reorder: Optional[bool] = None):
     require_hip(rays, "render_rays")
     assert rays.dim() == 2 and rays.shape[-1] == 8, "rays must be (N,8)"
     r = _f32(rays)
@@ -218,14 +222,17 @@ def render_stratified(rays: torch.Tensor, S: int, experts: Sequence[ExpertSpec],
     ws = packed if packed is not None else pack_experts(experts, routing, active_module)
     arr = _experts_array(experts)
     jit = None if jitter is None else _f32(jitter)
+    # scratch for the ray visiting order (small batches; the outputs do not depend on it)
+    obytes = int(_lib.lib().acn_render_order_bytes(N)) if (REORDER if reorder is None else reorder) else 0
+    order = torch.empty(obytes // 4, device=dev, dtype=torch.int32) if obytes else None
     hook = EVENT_HOOK
     if hook is not None:
         e0 = torch.cuda.Event(enable_timing=True)
         e0.record()
-    check(_lib.lib().acn_render_stratified_fwd(
+    check(_lib.lib().acn_render_stratified_fwd_ordered(
         ptr(r), N, int(S), ptr(jit), arr, C.byref(routing), -1 if active_module is None else int(active_module),
         C.byref(background), float(sigma_scale), float(tau), ptr(ws), ws.numel() * 4, ptr(rgb), ptr(depth),
-        ptr(weights), ptr(acc), stream_of(r)), "acn_render_stratified_fwd")
+        ptr(weights), ptr(acc), ptr(order), obytes, stream_of(r)), "acn_render_stratified_fwd_ordered")
     if hook is not None:
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()

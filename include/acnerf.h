@@ -152,6 +152,22 @@ int acn_render_stratified_fwd(const float* rays, int64_t N, int S, const float* 
                               float tau, void* workspace, size_t workspace_bytes, float* rgb,
                               float* depth, float* weights, float* acc, void* stream);
 
+/* Bytes of caller scratch acn_render_stratified_fwd_ordered uses to re-order a batch of N rays
+ * (0 when N is outside the re-ordered range 1..8192: the call then renders in the given order). */
+size_t acn_render_order_bytes(int64_t N);
+
+/* acn_render_stratified_fwd with a caller-owned scratch of acn_render_order_bytes(N) bytes (NULL /
+ * too small = no re-ordering).  Small batches are first sorted by ray direction (Z-order) so that
+ * each XCD renders one compact image region and its L2 serves that region's hash cells; every ray
+ * is still rendered alone and written at its own index, so the outputs are bit-identical to
+ * acn_render_stratified_fwd.  Same reference function (ray_rendering.py:290-345).              */
+int acn_render_stratified_fwd_ordered(const float* rays, int64_t N, int S, const float* jitter,
+                                      const acn_expert* experts, const acn_routing* routing,
+                                      int active_module, const acn_background* bg, float sigma_scale,
+                                      float tau, void* workspace, size_t workspace_bytes, float* rgb,
+                                      float* depth, float* weights, float* acc, void* order_scratch,
+                                      size_t order_bytes, void* stream);
+
 /* get_ray_directions + get_rays + clamp_rays_near_far (nerfs/ray_sampling.py:111-136, :50-108,
  * :139-176) with SceneBox.ray_aabb_intersect (nerfs/scene_box.py:45-107).  c2w: host (3,4)
  * row-major; aabb: host (2,3) or NULL (then near/far constants are used); the override flags

@@ -30,6 +30,8 @@ def test_library_loads_and_exports_every_declared_symbol():
     assert L.acn_version() == 1
     assert set(_lib.exported_symbols()) == set(declared_symbols())
     assert L.acn_workspace_bytes(1) > 50_000 and L.acn_workspace_bytes(4) == 4 * L.acn_workspace_bytes(1)
+    # ray-order scratch: 4 B per ray for the re-ordered batch sizes (1..8192), none otherwise
+    assert [L.acn_render_order_bytes(n) for n in (0, 1, 4096, 8192, 8193)] == [0, 4, 16384, 32768, 0]
 
 
 def test_argument_errors_are_reported_without_a_gpu():
@@ -45,3 +47,5 @@ def test_argument_errors_are_reported_without_a_gpu():
     assert L.acn_sh_fwd(None, 4, 7, None, None) == -1
     assert L.acn_render_stratified_fwd(None, 4, 1, None, None, None, -1, None, 1.0, 0.0, None, 0, None, None,
                                        None, None, None) == -1
+    assert L.acn_render_stratified_fwd_ordered(None, 4, 1, None, None, None, -1, None, 1.0, 0.0, None, 0, None,
+                                               None, None, None, None, 0, None) == -1

@@ -213,3 +213,33 @@ def test_invalid_rays_give_nan_like_reference():
     rgb, depth, w, acc = ops.render_stratified(_t(rays), 64, specs, routing, None, bg)
     rgb = rgb.cpu().numpy()
     assert np.all(np.isnan(rgb[::2])) and np.all(np.isfinite(rgb[1::2]))
+
+
+@pytest.mark.parametrize("n", [1, 17, 777, 4096, 8192, 8193])
+@pytest.mark.parametrize("jitter", [False, True])
+def test_render_ray_order_bit_identical(n, jitter):
+    """acn_render_stratified_fwd_ordered sorts small batches by direction (Z-order) and walks them
+    in XCD bands; every output must equal the given-order render bit for bit -- including NaN
+    rays (inf near/far), a zero and a NaN direction -- on both sides of the re-ordered size cap."""
+    ops = _ops()
+    d = G.load("render_k1")
+    mask = G.MASK["k1"]
+    sc = G.scene()["masks"][mask]
+    base = d["render:rays"]
+    rng = np.random.default_rng(n)
+    rays = base[rng.integers(0, base.shape[0], n)].copy()
+    if n > 4:
+        rays[1, 6:] = np.inf
+        rays[2, 3:6] = 0.0
+        rays[3, 3:6] = np.nan
+    specs = [_spec(d, 0, mask, prefix="hiw:")]
+    routing = ops.make_routing(torch.tensor(sc["centroids"]), 1, True, float(d["bm"]))
+    bgw = {k[len("bg_mlp."):]: _t(v) for k, v in G.bg_weights(d, "hiw:").items()}
+    bg, keep = ops.make_background("mlp", mlp=bgw)
+    S = 64
+    jit = _t(rng.random((n, S), dtype=np.float32)) if jitter else None
+    a = ops.render_stratified(_t(rays), S, specs, routing, None, bg, jitter=jit, reorder=True)
+    b = ops.render_stratified(_t(rays), S, specs, routing, None, bg, jitter=jit, reorder=False)
+    for x, y in zip(a, b):
+        assert np.array_equal(x.cpu().numpy(), y.cpu().numpy(), equal_nan=True)
+    assert (_ops()._lib.lib().acn_render_order_bytes(n) > 0) == (n <= 8192)
