@@ -564,7 +564,8 @@ def main():
     achieved = FLOP_PER_SAMPLE * launch_samples / (kernel_ms * 1e-3) / 1e12
     tr = load_traffic() if a.workload == "c2" else None
     kname = {"c5": "adam_kernel (fused clip + Adam over the adapted expert + background head)",
-             "c2": "render_kernel<1,1,0> (fused stratified render, 1 expert)",
+             "c2": "ray_order_kernel + render_kernel<1,1,0> (one acn_render_stratified_fwd_ordered call: direction "
+                   "grouping of the batch, then the fused stratified render, 1 expert; events bracket both)",
              "c3": "render_kernel<1,0,1> (fused stratified render, soft routing over 4 experts)",
              "c4": "render_kernel<1,0,1> (fused stratified render, soft routing over 8 experts)",
              "occ": "occ_render_kernel<1,1,0> (fused occupancy render over packed marched samples, 1 expert)",
