@@ -70,6 +70,14 @@ class _Plan:
 EVENT_HOOK = None
 
 
+def bump_versions(params) -> None:
+    """The kernels write parameters through raw pointers, which torch does not see: bump the
+    version counters so caches keyed on them (ops.PackCache, the packed MLP image of the fused
+    render) notice the update, as torch.optim.Adam's in-place ops would."""
+    if params:
+        torch.autograd.graph.increment_version(list(params))
+
+
 def _stream(device) -> int:
     return int(torch.cuda.current_stream(device).cuda_stream)
 
@@ -245,6 +253,7 @@ class FusedAdam(torch.optim.Optimizer):
                                                  gs["step_dev"].data_ptr(), gs["first"], gs["steps"],
                                                  None if scale is None else scale.data_ptr(), _stream(device)),
                   "acn_adam_step_table")
+            bump_versions(gs["params"])
             return loss
         groups = (acn_adam_group * len(kinds))()
         for i, (gi, step) in enumerate(kinds):
@@ -259,6 +268,7 @@ class FusedAdam(torch.optim.Optimizer):
         check(_lib.lib().acn_adam_step(plan.descs.data_ptr(), plan.chunk_tensor.data_ptr(), plan.nchunks, groups,
                                        len(kinds), None if scale is None else scale.data_ptr(), _stream(device)),
               "acn_adam_step")
+        bump_versions([r[0] for r in rows])
         if hook is not None:
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record()

@@ -107,14 +107,21 @@ class GraphedAdaptStep:
                                           active_module=active_module, grad_clip=grad_clip, **render_kwargs)
         optimizer.graph_end_capture()
         self.replays = 0
+        self.max_steps = int(max_steps)
 
     def __call__(self, rays: torch.Tensor, rgbs: torch.Tensor, jitter_u: Optional[torch.Tensor] = None) -> torch.Tensor:
+        if self.replays >= self.max_steps:
+            # past the precomputed Adam table the captured update would silently stop
+            raise RuntimeError(f"GraphedAdaptStep: {self.max_steps} replays exhausted the Adam constant table; "
+                               f"capture a new GraphedAdaptStep (max_steps=...)")
         self.static_rays.copy_(rays, non_blocking=True)
         self.static_rgbs.copy_(rgbs, non_blocking=True)
         if jitter_u is not None:
             self.static_u.copy_(jitter_u, non_blocking=True)
         self.graph.replay()
         self.replays += 1
+        from .optim import bump_versions
+        bump_versions(self.args[2]._graph["params"])  # the replayed Adam wrote them: packed images are stale
         return self.static_loss
 
     def sync_state(self) -> None:

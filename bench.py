@@ -38,6 +38,7 @@ import os
 import sys
 import time
 from pathlib import Path
+from typing import Optional
 
 import numpy as np
 import torch
@@ -278,6 +279,32 @@ def load_traffic(name: str = "render"):
     return None
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_command(argv, n_gpus: int, port: int):
+    """torch.distributed.run command that starts ``n_gpus`` ranks of this script with the same
+    arguments (one process per GPU, rendezvous on 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n_gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve()), *argv]
+
+
+def maybe_launch(argv, n_gpus: int) -> Optional[int]:
+    """``bench.py --gpus N`` run directly (no WORLD_SIZE in the environment) with N > 1: start the N
+    ranks as a child torch.distributed.run and return its exit code.  Runs before anything touches
+    the GPU (the parent never initialises HIP, so nothing is re-exec'd from a GPU process)."""
+    if n_gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(launch_command(argv, n_gpus, free_port()), env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -295,9 +322,28 @@ def main():
     ap.add_argument("--query-rays", type=int, default=2000, help="meta: query rays per task")
     ap.add_argument("--data-rays", type=int, default=1 << 22, help="data: rays in the region table")
     ap.add_argument("--no-graph", action="store_true", help="c5: eager steps instead of the HIP-graph replay")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check: every rank reports (rank, world) over gloo and exits before any GPU call")
     a = ap.parse_args()
+    rc = maybe_launch(sys.argv[1:], a.gpus)
+    if rc is not None:
+        sys.exit(rc)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    if a.dry_run:
+        if world > 1:
+            dist.init_process_group("gloo")
+            t = torch.tensor([1.0])
+            dist.all_reduce(t)
+            world_seen = int(t.item())
+            dist.destroy_process_group()
+        else:
+            world_seen = 1
+        print(json.dumps({"dry_run": True, "rank": int(os.environ.get("RANK", "0")), "world": world,
+                          "world_seen": world_seen}), flush=True)
+        return
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
