@@ -22,7 +22,7 @@ def scene() -> dict:
     return json.loads((GOLDEN / "scene_drz_example.json").read_text())
 
 
-MASK = {"k1": "g11_grid_bm110_ss11", "k4": "g22_grid_bm110_ss11"}
+MASK = {"k1": "g11_grid_bm110_ss11", "k4": "g22_grid_bm110_ss11", "k8": "g42_synthetic"}
 
 
 def expert_weights(d: dict, k: int, prefix: str = "w:") -> dict:

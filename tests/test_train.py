@@ -103,25 +103,30 @@ def _close_frac(a, b, atol, rtol):
     return float(np.mean(np.abs(a - b) <= atol + rtol * np.abs(b)))
 
 
-@pytest.mark.gpu
-def test_adapt_steps_match_reference_fixture():
+LRS = {"encoding": 0.01, "sigma": 0.002, "color": 0.002, "background": 0.001}
+FIXTURES = {"k4": ("train_k4", 32, 2), "k8": ("train_k8", 96, 3)}   # tag: (fixture, samples, steps)
+
+
+def check_adapt_fixture(tag, step_fn, make_opt=None):
+    """Replay the reference's runtime_adapt steps of fixture ``tag`` through ``step_fn(P, model, rays,
+    rgbs, opt, u) -> loss`` and compare loss, clip norm, gradients and parameters after every step."""
     from test_module_api import build_model, reference_state_dict
     from adaptive_city_nerf_amd.optim import build_optimizer
-    from adaptive_city_nerf_amd.train import adapt_step
-    d = G.load("train_k4")
-    m, _ = build_model("k4")
+    name_, S, nsteps = FIXTURES[tag]
+    d = G.load(name_)
+    Pk = SimpleNamespace(**{**vars(P), "ray_samples": S, "chunk_points": 4_000_000})
+    m, _ = build_model(tag)
     K = len(m.submodules)
     m.load_state_dict(reference_state_dict(d, K, "w:"))
     m = m.cuda().train()
-    opt = build_optimizer(P, m)
+    opt = (make_opt or build_optimizer)(Pk, m)
     rows = d["train:rows"]
-    lrs = {"encoding": 0.01, "sigma": 0.002, "color": 0.002, "background": 0.001}
-    for step in range(2):
+    for step in range(nsteps):
         pre = f"train{step}:"
         rays = torch.from_numpy(d[pre + "rays"]).cuda()
         rgbs = torch.from_numpy(d[pre + "rgbs"]).cuda()
         u = torch.from_numpy(d[pre + "u"]).cuda()
-        loss = adapt_step(P, m, rays, rgbs, opt, grad_clip=1.0, jitter_u=u)
+        loss = step_fn(Pk, m, rays, rgbs, opt, u)
         torch.cuda.synchronize()
         ref_loss = float(d[pre + "loss"])
         assert abs(float(loss) - ref_loss) <= 1e-5 * ref_loss, (float(loss), ref_loss)
@@ -147,19 +152,38 @@ def test_adapt_steps_match_reference_fixture():
                 ref = d[gkey]
                 scale = float(np.abs(ref).max()) + 1e-12
                 np.testing.assert_allclose(p.grad.detach().cpu().numpy(), ref, rtol=0, atol=1e-4 * scale)
+            else:
+                assert p.grad is None or float(p.grad.abs().max()) == 0.0, name
         for name, p in named.items():
             group = "encoding" if name.endswith("hash_table") else \
                 "background" if name.startswith("bg_mlp") else \
                 "color" if ".color_mlp." in name else "sigma"
-            lr = lrs[group]
+            lr = LRS[group]
             if name.endswith("hash_table"):
                 k = int(name.split(".")[1])
                 got = p.detach()[torch.from_numpy(rows[k]).cuda()].cpu().numpy()
                 ref = d[pre + f"table_rows:{k}"]
+                if (pre + f"table_level_sum:{k}") in d:   # every row moves: compare the level sums too
+                    np.testing.assert_allclose(p.detach().view(16, -1).double().sum(1).cpu().numpy(),
+                                               d[pre + f"table_level_sum:{k}"], rtol=1e-6, atol=1e-3 * lr)
             else:
                 got = p.detach().cpu().numpy()
                 ref = d[pre + "param:" + name]
             assert _close_frac(got, ref, 1e-3 * lr, 1e-6) >= 0.999, name
+    return m, opt
+
+
+def _eager_step(Pk, m, rays, rgbs, opt, u):
+    from adaptive_city_nerf_amd.train import adapt_step
+    return adapt_step(Pk, m, rays, rgbs, opt, grad_clip=1.0, jitter_u=u)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tag", ["k4", "k8"])
+def test_adapt_steps_match_reference_fixture(tag):
+    """runtime_adapt on the routed container (no active_module): K=4 (2 steps, 256 rays x 32) and
+    BASELINE C5's K=8 (3 steps, 1000 rays x 96 samples)."""
+    check_adapt_fixture(tag, _eager_step)
 
 
 @pytest.mark.gpu
@@ -194,3 +218,45 @@ def test_volume_render_backward_matches_autograd(with_bg, scale):
         np.testing.assert_allclose(got[..., c], ref[..., c], rtol=0, atol=2e-5 * sc)
     if with_bg:
         np.testing.assert_allclose(bg_g.grad.cpu().numpy(), bg_c.grad.numpy(), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graphed", [False, True])
+def test_render_after_fused_adam_sees_updated_weights(graphed):
+    """The fused Adam writes parameters through raw pointers; the packed MLP image the fused render
+    caches must be rebuilt after every update (eager step and graph replay), so a render after
+    adaptation equals the render of a fresh model holding the updated weights."""
+    from test_module_api import build_model, reference_state_dict
+    from adaptive_city_nerf_amd import render_rays
+    from adaptive_city_nerf_amd.optim import build_optimizer
+    from adaptive_city_nerf_amd.train import GraphedAdaptStep, adapt_step
+    d = G.load("train_k4")
+    m, _ = build_model("k4")
+    m.load_state_dict(reference_state_dict(d, 4, "w:"))
+    m = m.cuda()
+    rays = torch.from_numpy(d["train0:rays"]).cuda()
+    rgbs = torch.from_numpy(d["train0:rgbs"]).cuda()
+    am = 0 if graphed else None
+
+    def render(model):
+        model.eval()
+        with torch.no_grad():
+            out = render_rays(model, rays, ray_samples=32, active_module=am)[0].clone()
+        model.train()
+        return out
+    before = render(m)                              # fills the packed-weight cache
+    opt = build_optimizer(P, m)
+    if graphed:
+        g = GraphedAdaptStep(P, m, rays, rgbs, opt, active_module=0, grad_clip=1.0, warmup=1)
+        for _ in range(2):
+            g(rays, rgbs)
+    else:
+        for _ in range(2):
+            adapt_step(P, m, rays, rgbs, opt, grad_clip=1.0)
+    torch.cuda.synchronize()
+    after = render(m)
+    fresh, _ = build_model("k4")
+    fresh.load_state_dict(m.state_dict())
+    ref = render(fresh.cuda())
+    assert not torch.equal(before, after)
+    assert torch.equal(after, ref)
