@@ -133,6 +133,12 @@ SIGNATURES = {
     "acn_mlp_dw_workspace_bytes": ([], C.c_size_t),
     "acn_sample_stratified": ([vp, i64, C.c_int, vp, vp, vp, C.c_float, C.c_float, vp, vp, vp, vp], C.c_int),
     "acn_mlp_train_bwd_dw": ([vp, vp, vp, vp, i64, vp, vp, vp, vp, vp], C.c_int),
+    # routed.hip
+    "acn_routed_workspace_bytes": ([i64, i32], C.c_size_t),
+    "acn_routed_count": ([vp, i64, i32, vp, vp, vp, vp, vp, sz, vp], C.c_int),
+    "acn_routed_scatter": ([vp, i64, i32, i32, vp, vp, vp, vp, f32, f32, vp, vp, vp, vp, vp, vp, vp], C.c_int),
+    "acn_routed_blend_fwd": ([vp, vp, vp, i64, i32, vp, vp], C.c_int),
+    "acn_routed_blend_bwd": ([vp, vp, vp, i64, vp, vp], C.c_int),
     # clusters.hip
     "acn_voronoi_route": ([vp, i64, i32, vp, i32, i32, C.c_double, i32, i32, vp, vp, vp, vp, vp, vp], C.c_int),
 }

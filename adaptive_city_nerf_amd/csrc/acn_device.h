@@ -374,4 +374,97 @@ __device__ __forceinline__ void hash_level_f2(const float2* __restrict__ tl, flo
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// shared by the fused render (render.hip) and the routed training sampler (routed.hip); Cfg is any
+// struct with K, cluster_2d, bm, cent[k][3]
+// Routing (meta_container.py:97-134), cdist mm-path restated exactly as in the oracle.
+// Computed without per-expert arrays (runtime-indexed arrays would live in scratch): a first
+// pass gives min distance / denominator (soft) or argmin (hard), then w_k is recomputed per k.
+template <typename Cfg>
+__device__ __forceinline__ float route_dist(const Cfg& cfg, int k, float px, float py, float pz) {
+    float s = 0.0f, xn, cn;
+    if (cfg.cluster_2d) {
+        const float cy = cfg.cent[k][1], cz = cfg.cent[k][2];
+        xn = py * py + pz * pz;
+        cn = cy * cy + cz * cz;
+        s = fmaf(-2.0f * py, cy, s);
+        s = fmaf(-2.0f * pz, cz, s);
+    } else {
+        const float cx = cfg.cent[k][0], cy = cfg.cent[k][1], cz = cfg.cent[k][2];
+        xn = (px * px + py * py) + pz * pz;
+        cn = (cx * cx + cy * cy) + cz * cz;
+        s = fmaf(-2.0f * px, cx, s);
+        s = fmaf(-2.0f * py, cy, s);
+        s = fmaf(-2.0f * pz, cz, s);
+    }
+    s = s + xn;
+    s = s + cn;
+    return sqrtf(s > 0.0f ? s : 0.0f);
+}
+
+struct RouteState {
+    float thr, den;  // soft: bm * min dist, sum of masked inverse distances
+    int hard;        // hard: argmin
+};
+
+template <int ROUTE, typename Cfg>
+__device__ __forceinline__ RouteState route_prep(const Cfg& cfg, float px, float py, float pz) {
+    RouteState st{0.0f, 0.0f, 0};
+    if (ROUTE == 1) {
+        float mind = INFINITY;
+        for (int k = 0; k < cfg.K; ++k) {
+            float d = route_dist(cfg, k, px, py, pz);
+            d = d < 1e-6f ? 1e-6f : d;
+            mind = fminf(mind, d);
+        }
+        st.thr = cfg.bm * mind;
+        float den = 0.0f;
+        for (int k = 0; k < cfg.K; ++k) {
+            float d = route_dist(cfg, k, px, py, pz);
+            d = d < 1e-6f ? 1e-6f : d;
+            den = den + ((d <= st.thr) ? 1.0f / d : 0.0f);
+        }
+        st.den = den < 1e-6f ? 1e-6f : den;
+    } else if (ROUTE == 2) {
+        float best = INFINITY;
+        for (int k = 0; k < cfg.K; ++k) {
+            const float d = route_dist(cfg, k, px, py, pz);
+            if (d < best || k == 0) { best = d; st.hard = k; }
+        }
+    }
+    return st;
+}
+
+template <typename Cfg>
+__device__ __forceinline__ float route_weight(const Cfg& cfg, const RouteState& st, int k, float px, float py,
+                                              float pz) {
+    float d = route_dist(cfg, k, px, py, pz);
+    d = d < 1e-6f ? 1e-6f : d;
+    return ((d <= st.thr) ? 1.0f / d : 0.0f) / st.den;
+}
+
+// colour-branch direction encoding (meta_ngp.py:165-168 then encodings.py:144-151)
+__device__ __forceinline__ void dir_sh(float dx, float dy, float dz, float (&sh)[16]) {
+    const float n = clamp_min_nan(norm3(dx, dy, dz), 1e-9f);
+    sh_encode<3>(dx / n, dy / n, dz / n, sh);
+}
+
+// t value of sample s (stratified_t_vals, ray_rendering.py:278-287); linspace as torch CPU
+__device__ __forceinline__ float lin01(int i, int S) {
+    if (S == 1) return 0.0f;
+    const float step = 1.0f / (float)(S - 1);
+    return i < S / 2 ? fmaf(step, (float)i, 0.0f) : fmaf(-step, (float)(S - 1 - i), 1.0f);
+}
+__device__ __forceinline__ float tlin(float near, float far, int i, int S) {
+    const float u = lin01(i, S);
+    return near * (1.0f - u) + far * u;
+}
+__device__ __forceinline__ float tval(float near, float far, int s, int S, const float* jit) {
+    const float ts = tlin(near, far, s, S);
+    if (!jit) return ts;
+    const float lo = s == 0 ? ts : 0.5f * (tlin(near, far, s - 1, S) + ts);
+    const float hi = s == S - 1 ? ts : 0.5f * (ts + tlin(near, far, s + 1, S));
+    return lo + (hi - lo) * jit[s];
+}
+
 }  // namespace acn

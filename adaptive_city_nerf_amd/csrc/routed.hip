@@ -1,0 +1,294 @@
+// routed.hip -- (sample, expert) pair lists of the routed container (gfx950).
+//
+// Replaces the front end of the differentiable container render and its expert dispatch
+// (nerfs/ray_rendering.py:262-345 stratified_t_vals / points / id6, models/inr/meta_container.py:
+// 97-134 _routing, :300-343 the per-expert nonzero -> index_select -> expert -> index_add_ loop,
+// meta_ngp.py:155-168 _world_to_unit / _enc_dir):
+//
+//   acn_routed_count   : one lane per sample -> t (N,S), routing weights W (M,K) in the reference's
+//                        cdist-mm arithmetic, per-256-sample block counts of routed samples per expert,
+//                        then one workgroup scans them -> pair segment of every expert (starts[K+1]).
+//   acn_routed_scatter : one lane per sample -> for every expert k with w_k > 0, pair record at
+//                        starts[k] + (rank of the sample among expert k's samples, in sample order):
+//                        sample index, weight, x in expert k's unit box (clamped), SH-4 of the ray
+//                        direction; pmap (M,K) = pair index or -1.  Pairs of expert k are therefore
+//                        exactly the rows the reference's index_select(nonzero(w[:,k] > 0)) gathers,
+//                        in the same order.
+//   acn_routed_blend_fwd / _bwd : y_m = sum_k y_pk * w_pk accumulated in expert order from zero
+//                        (index_add_); backward dY_p = dY_m * w_p (mul + index_add_ backward).
+//
+// Pairs are the currency of the expert-parallel layouts too: the pairs of expert k are what an
+// all-to-all sends to the GPU that owns expert k (parallel.py).
+#include "acn_device.h"
+#include "acn_internal.h"
+
+using namespace acn;
+
+namespace {
+
+constexpr int kBlk = 256;  // samples per count / scatter block (4 waves)
+
+struct RouteCfg {
+    int32_t K, cluster_2d, routing;  // routing: 1 soft (bm > 1), 2 hard (argmin)
+    float bm;
+    float cent[kMaxK][3];
+};
+
+// weight of expert k for a sample at p (the reference's rule; hard routing as weight 1 of the argmin:
+// 0 + y * 1 == y, identical to index_copy_)
+__device__ __forceinline__ void route_row(const RouteCfg& cfg, float px, float py, float pz, float (&w)[kMaxK]) {
+    if (cfg.routing == 1) {
+        const RouteState st = route_prep<1>(cfg, px, py, pz);
+#pragma unroll
+        for (int k = 0; k < kMaxK; ++k) w[k] = k < cfg.K ? route_weight(cfg, st, k, px, py, pz) : 0.0f;
+    } else {
+        const RouteState st = route_prep<2>(cfg, px, py, pz);
+#pragma unroll
+        for (int k = 0; k < kMaxK; ++k) w[k] = (k < cfg.K && st.hard == k) ? 1.0f : 0.0f;
+    }
+}
+
+__global__ void __launch_bounds__(kBlk) routed_count_kernel(const float* __restrict__ rays, int64_t N, int S,
+                                                            const float* __restrict__ jit, RouteCfg cfg,
+                                                            float* __restrict__ t_out, float* __restrict__ W,
+                                                            int32_t* __restrict__ blk_cnt) {
+    __shared__ int wcnt[kBlk / 64][kMaxK];
+    const int64_t M = N * (int64_t)S;
+    const int64_t m = (int64_t)blockIdx.x * kBlk + threadIdx.x;
+    float w[kMaxK];
+#pragma unroll
+    for (int k = 0; k < kMaxK; ++k) w[k] = 0.0f;
+    if (m < M) {
+        const int64_t ray = m / S;
+        const int s = (int)(m - ray * S);
+        const float* rp = rays + ray * 8;
+        const float t = tval(rp[6], rp[7], s, S, jit ? jit + ray * S : nullptr);
+        t_out[m] = t;
+        const float px = rp[0] + rp[3] * t, py = rp[1] + rp[4] * t, pz = rp[2] + rp[5] * t;
+        route_row(cfg, px, py, pz, w);
+#pragma unroll
+        for (int k = 0; k < kMaxK; ++k)
+            if (k < cfg.K) W[m * cfg.K + k] = w[k];
+    }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < kMaxK; ++k) {
+        if (k >= cfg.K) break;
+        const uint64_t b = __ballot(w[k] > 0.0f);
+        if (lane == 0) wcnt[wave][k] = __popcll(b);
+    }
+    __syncthreads();
+    if (threadIdx.x < cfg.K) {
+        int c = 0;
+#pragma unroll
+        for (int q = 0; q < kBlk / 64; ++q) c += wcnt[q][threadIdx.x];
+        blk_cnt[(int64_t)blockIdx.x * cfg.K + threadIdx.x] = c;
+    }
+}
+
+// one workgroup: per expert, exclusive scan of the block counts (in place) and the segment starts
+__global__ void __launch_bounds__(1024) routed_scan_kernel(int32_t* __restrict__ blk_cnt, int64_t nblk, int K,
+                                                           int64_t* __restrict__ starts) {
+    __shared__ int64_t part[1024];
+    __shared__ int64_t base;
+    const int tid = threadIdx.x;
+    const int64_t per = (nblk + 1023) / 1024;
+    const int64_t b0 = tid * per, b1 = b0 + per < nblk ? b0 + per : nblk;
+    if (tid == 0) base = 0;
+    for (int k = 0; k < K; ++k) {
+        int64_t s = 0;
+        for (int64_t b = b0; b < b1; ++b) s += blk_cnt[b * K + k];
+        part[tid] = s;
+        __syncthreads();
+        for (int off = 1; off < 1024; off <<= 1) {  // inclusive Hillis-Steele scan
+            const int64_t v = tid >= off ? part[tid - off] : 0;
+            __syncthreads();
+            part[tid] += v;
+            __syncthreads();
+        }
+        int64_t run = part[tid] - s;  // exclusive prefix of this thread's chunk
+        for (int64_t b = b0; b < b1; ++b) {
+            const int32_t c = blk_cnt[b * K + k];
+            blk_cnt[b * K + k] = (int32_t)run;
+            run += c;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            starts[k] = base;
+            base += part[1023];
+        }
+        __syncthreads();
+    }
+    if (tid == 0) starts[K] = base;
+}
+
+struct BoxCfg {
+    float amin[kMaxK][3], ext[kMaxK][3];
+    float lo, hi;
+};
+
+__global__ void __launch_bounds__(kBlk) routed_scatter_kernel(const float* __restrict__ rays, int64_t N, int S,
+                                                              int K, const float* __restrict__ t_vals,
+                                                              const float* __restrict__ W,
+                                                              const int32_t* __restrict__ blk_off,
+                                                              const int64_t* __restrict__ starts, BoxCfg box,
+                                                              int32_t* __restrict__ pidx, float* __restrict__ pw,
+                                                              float* __restrict__ x01, float* __restrict__ sh_out,
+                                                              int32_t* __restrict__ pmap) {
+    __shared__ int wcnt[kBlk / 64][kMaxK];
+    const int64_t M = N * (int64_t)S;
+    const int64_t m = (int64_t)blockIdx.x * kBlk + threadIdx.x;
+    const bool live = m < M;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float px = 0.0f, py = 0.0f, pz = 0.0f, sh[16];
+    if (live) {
+        const int64_t ray = m / S;
+        const float* rp = rays + ray * 8;
+        const float t = t_vals[m];
+        px = rp[0] + rp[3] * t;
+        py = rp[1] + rp[4] * t;
+        pz = rp[2] + rp[5] * t;
+        dir_sh(rp[3], rp[4], rp[5], sh);
+    }
+    const uint64_t below = (1ull << lane) - 1ull;
+    for (int k = 0; k < K; ++k) {
+        const float wk = live ? W[m * K + k] : 0.0f;
+        const uint64_t b = __ballot(wk > 0.0f);
+        if (lane == 0) wcnt[wave][k] = __popcll(b);
+    }
+    __syncthreads();
+    for (int k = 0; k < K; ++k) {
+        const float wk = live ? W[m * K + k] : 0.0f;
+        const uint64_t b = __ballot(wk > 0.0f);  // recomputed (a runtime-indexed array would go to scratch)
+        if (!live) continue;
+        if (!(wk > 0.0f)) {
+            pmap[m * K + k] = -1;
+            continue;
+        }
+        int64_t pos = starts[k] + blk_off[(int64_t)blockIdx.x * K + k] + __popcll(b & below);
+        for (int q = 0; q < wave; ++q) pos += wcnt[q][k];
+        pmap[m * K + k] = (int32_t)pos;
+        pidx[pos] = (int32_t)m;
+        pw[pos] = wk;
+        x01[pos * 3 + 0] = clamp_nan((px - box.amin[k][0]) / box.ext[k][0], box.lo, box.hi);
+        x01[pos * 3 + 1] = clamp_nan((py - box.amin[k][1]) / box.ext[k][1], box.lo, box.hi);
+        x01[pos * 3 + 2] = clamp_nan((pz - box.amin[k][2]) / box.ext[k][2], box.lo, box.hi);
+        float4* o4 = reinterpret_cast<float4*>(sh_out + pos * 16);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o4[q] = make_float4(sh[4 * q], sh[4 * q + 1], sh[4 * q + 2], sh[4 * q + 3]);
+    }
+}
+
+__global__ void __launch_bounds__(256) blend_fwd_kernel(const float4* __restrict__ y, const float* __restrict__ pw,
+                                                        const int32_t* __restrict__ pmap, int64_t M, int K,
+                                                        float4* __restrict__ out) {
+    const int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (m >= M) return;
+    float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    for (int k = 0; k < K; ++k) {
+        const int32_t p = pmap[m * K + k];
+        if (p < 0) continue;
+        const float4 v = y[p];
+        const float w = pw[p];
+        acc.x = acc.x + v.x * w;
+        acc.y = acc.y + v.y * w;
+        acc.z = acc.z + v.z * w;
+        acc.w = acc.w + v.w * w;
+    }
+    out[m] = acc;
+}
+
+__global__ void __launch_bounds__(256) blend_bwd_kernel(const float4* __restrict__ g, const int32_t* __restrict__ pidx,
+                                                        const float* __restrict__ pw, int64_t P,
+                                                        float4* __restrict__ gy) {
+    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= P) return;
+    const float4 v = g[pidx[p]];
+    const float w = pw[p];
+    gy[p] = make_float4(v.x * w, v.y * w, v.z * w, v.w * w);
+}
+
+unsigned blocks_for(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
+
+}  // namespace
+
+extern "C" size_t acn_routed_workspace_bytes(int64_t M, int K) {
+    const int64_t nblk = (M + kBlk - 1) / kBlk;
+    return (size_t)(M * K) * sizeof(float) + (size_t)(nblk * K) * sizeof(int32_t) + 16;
+}
+
+extern "C" int acn_routed_count(const float* rays, int64_t N, int S, const float* jitter, const acn_routing* routing,
+                                float* t_vals, int64_t* starts, void* workspace, size_t workspace_bytes,
+                                void* stream) {
+    ACN_REQUIRE(N >= 0 && S >= 1 && routing && starts, "acn_routed_count: bad arguments");
+    const int K = routing->K;
+    ACN_REQUIRE(K >= 1 && K <= kMaxK, "acn_routed_count: K = %d outside [1, %d]", K, kMaxK);
+    const int64_t M = N * (int64_t)S;
+    ACN_REQUIRE(workspace && workspace_bytes >= acn_routed_workspace_bytes(M, K),
+                "acn_routed_count: workspace too small");
+    hipStream_t s = (hipStream_t)stream;
+    if (M == 0) {
+        const hipError_t e = hipMemsetAsync(starts, 0, (size_t)(K + 1) * sizeof(int64_t), s);
+        return e == hipSuccess ? ACN_OK : acn_set_error((int)e, "acn_routed_count: memset failed");
+    }
+    ACN_REQUIRE(rays && t_vals, "acn_routed_count: NULL pointer");
+    RouteCfg cfg{};
+    cfg.K = K;
+    cfg.cluster_2d = routing->cluster_2d;
+    cfg.bm = routing->boundary_margin;
+    cfg.routing = routing->boundary_margin > 1.0f ? 1 : 2;
+    for (int k = 0; k < K; ++k)
+        for (int a = 0; a < 3; ++a) cfg.cent[k][a] = routing->centroids[k][a];
+    float* W = (float*)workspace;
+    int32_t* blk = (int32_t*)(W + M * K);
+    const int64_t nblk = (M + kBlk - 1) / kBlk;
+    hipLaunchKernelGGL(routed_count_kernel, dim3(blocks_for(M, kBlk)), dim3(kBlk), 0, s, rays, N, S, jitter, cfg, t_vals,
+                       W, blk);
+    hipLaunchKernelGGL(routed_scan_kernel, dim3(1), dim3(1024), 0, s, blk, nblk, K, starts);
+    return acn_check_launch("acn_routed_count");
+}
+
+extern "C" int acn_routed_scatter(const float* rays, int64_t N, int S, int K, const float* t_vals,
+                                  const int64_t* starts, const float* aabb_min, const float* aabb_extent, float lo,
+                                  float hi, const void* workspace, int32_t* pidx, float* pw, float* x01, float* sh,
+                                  int32_t* pmap, void* stream) {
+    ACN_REQUIRE(N >= 0 && S >= 1 && K >= 1 && K <= kMaxK && aabb_min && aabb_extent,
+                "acn_routed_scatter: bad arguments");
+    const int64_t M = N * (int64_t)S;
+    if (M == 0) return ACN_OK;
+    ACN_REQUIRE(rays && t_vals && starts && workspace && pidx && pw && x01 && sh && pmap,
+                "acn_routed_scatter: NULL pointer");
+    BoxCfg box{};
+    for (int k = 0; k < K; ++k)
+        for (int a = 0; a < 3; ++a) {
+            box.amin[k][a] = aabb_min[3 * k + a];
+            box.ext[k][a] = aabb_extent[3 * k + a];
+        }
+    box.lo = lo;
+    box.hi = hi;
+    const float* W = (const float*)workspace;
+    const int32_t* blk = (const int32_t*)(W + M * K);
+    hipLaunchKernelGGL(routed_scatter_kernel, dim3(blocks_for(M, kBlk)), dim3(kBlk), 0, (hipStream_t)stream, rays, N,
+                       S, K, t_vals, W, blk, starts, box, pidx, pw, x01, sh, pmap);
+    return acn_check_launch("acn_routed_scatter");
+}
+
+extern "C" int acn_routed_blend_fwd(const float* y, const float* pw, const int32_t* pmap, int64_t M, int K, float* out,
+                                    void* stream) {
+    ACN_REQUIRE(M >= 0 && K >= 1 && K <= kMaxK, "acn_routed_blend_fwd: bad arguments");
+    if (M == 0) return ACN_OK;
+    ACN_REQUIRE(pw && pmap && out, "acn_routed_blend_fwd: NULL pointer");
+    hipLaunchKernelGGL(blend_fwd_kernel, dim3(blocks_for(M, 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const float4*)y, pw, pmap, M, K, (float4*)out);
+    return acn_check_launch("acn_routed_blend_fwd");
+}
+
+extern "C" int acn_routed_blend_bwd(const float* g, const int32_t* pidx, const float* pw, int64_t P, float* gy,
+                                    void* stream) {
+    ACN_REQUIRE(P >= 0, "acn_routed_blend_bwd: bad arguments");
+    if (P == 0) return ACN_OK;
+    ACN_REQUIRE(g && pidx && pw && gy, "acn_routed_blend_bwd: NULL pointer");
+    hipLaunchKernelGGL(blend_bwd_kernel, dim3(blocks_for(P, 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const float4*)g, pidx, pw, P, (float4*)gy);
+    return acn_check_launch("acn_routed_blend_bwd");
+}

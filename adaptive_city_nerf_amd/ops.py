@@ -493,3 +493,58 @@ def sample_stratified(rays: torch.Tensor, S: int, jitter: Optional[torch.Tensor]
                                            C.c_float(lo), C.c_float(hi),
                                            ptr(t), ptr(x01), ptr(sh), stream_of(rays)), "acn_sample_stratified")
     return t, x01, sh
+
+
+# ------------------------------------------------------------------------------------------
+# routed container, differentiable path (routed.hip)
+def routed_pairs(rays: torch.Tensor, S: int, jitter: Optional[torch.Tensor], routing: acn_routing, aabb_mins,
+                 aabb_exts, eps: float):
+    """t_vals (N,S) and the (sample, expert) pairs of the routed container: returns (t_vals, starts (K+1
+    host ints), pidx (P,) int32, pw (P,), x01 (P,3), sh (P,16), pmap (M,K) int32).  One host
+    synchronisation (the segment sizes) sits between the count and the scatter launches."""
+    require_hip(rays, "render_rays (routed container)")
+    r = _f32(rays)
+    N = r.shape[0]
+    M = N * int(S)
+    K = int(routing.K)
+    dev = r.device
+    L = _lib.lib()
+    ws = torch.empty(int(L.acn_routed_workspace_bytes(M, K)), dtype=torch.uint8, device=dev)
+    t = torch.empty(N, int(S), device=dev, dtype=torch.float32)
+    starts = torch.empty(K + 1, device=dev, dtype=torch.int64)
+    jit = None if jitter is None else _f32(jitter.to(dev))
+    check(L.acn_routed_count(ptr(r), N, int(S), ptr(jit), C.byref(routing), ptr(t), ptr(starts), ptr(ws),
+                             ws.numel(), stream_of(r)), "acn_routed_count")
+    st = [int(v) for v in starts.cpu().tolist()]
+    P = st[K]
+    pidx = torch.empty(P, device=dev, dtype=torch.int32)
+    pw = torch.empty(P, device=dev, dtype=torch.float32)
+    x01 = torch.empty(P, 3, device=dev, dtype=torch.float32)
+    sh = torch.empty(P, 16, device=dev, dtype=torch.float32)
+    pmap = torch.empty(M, K, device=dev, dtype=torch.int32)
+    mins = (C.c_float * (3 * K))(*[float(v) for row in aabb_mins for v in row])
+    exts = (C.c_float * (3 * K))(*[float(v) for row in aabb_exts for v in row])
+    import numpy as np
+    lo = np.float32(eps)
+    hi = np.float32(1.0) - lo
+    check(L.acn_routed_scatter(ptr(r), N, int(S), K, ptr(t), ptr(starts), C.cast(mins, C.c_void_p),
+                               C.cast(exts, C.c_void_p), C.c_float(lo), C.c_float(hi), ptr(ws), ptr(pidx), ptr(pw),
+                               ptr(x01), ptr(sh), ptr(pmap), stream_of(r)), "acn_routed_scatter")
+    return t, st, pidx, pw, x01, sh, pmap
+
+
+def routed_blend_fwd(y: torch.Tensor, pw: torch.Tensor, pmap: torch.Tensor) -> torch.Tensor:
+    M, K = pmap.shape
+    out = torch.empty(M, 4, device=pmap.device, dtype=torch.float32)
+    yy = _f32(y).view(-1, 4) if y.numel() else None
+    check(_lib.lib().acn_routed_blend_fwd(ptr(yy), ptr(pw), ptr(pmap), M, K, ptr(out), stream_of(pmap)),
+          "acn_routed_blend_fwd")
+    return out
+
+
+def routed_blend_bwd(g: torch.Tensor, pidx: torch.Tensor, pw: torch.Tensor) -> torch.Tensor:
+    P = pidx.shape[0]
+    gy = torch.empty(P, 4, device=pidx.device, dtype=torch.float32)
+    check(_lib.lib().acn_routed_blend_bwd(ptr(_f32(g)), ptr(pidx), ptr(pw), P, ptr(gy), stream_of(pidx)),
+          "acn_routed_blend_bwd")
+    return gy

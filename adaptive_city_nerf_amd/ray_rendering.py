@@ -172,6 +172,7 @@ def stratified_t_vals(near: Tensor, far: Tensor, ray_samples: int, randomized: b
 
 
 FUSED_TRAIN_SAMPLER = True  # tests switch it off to compare with the composed chain
+ROUTED_TRAIN = True         # differentiable routed-container renders on the pair kernels (routed.hip)
 ENC_EPS = 1e-6  # MetaNGP.enc_eps (a constant fp32 buffer, meta_ngp.py:155-158), known on the host
 
 
@@ -181,6 +182,55 @@ def _train_expert(model, active_module):
     sub = model.submodules[active_module] if isinstance(model, MetaContainer) and active_module is not None else (
         model if isinstance(model, MetaNGP) else None)
     return sub if sub is not None and sub._fusable else None
+
+
+class _BlendFn(torch.autograd.Function):
+    """MetaContainer.forward's weighted index_add_ over experts (meta_container.py:300-337) on the
+    (sample, expert) pairs: y (P,4) -> (M,4); backward dY_p = dY_m * w_p."""
+
+    @staticmethod
+    def forward(ctx, y, pw, pmap, pidx):
+        ctx.save_for_backward(pw, pidx)
+        return ops.routed_blend_fwd(y, pw, pmap)
+
+    @staticmethod
+    def backward(ctx, g):
+        pw, pidx = ctx.saved_tensors
+        return ops.routed_blend_bwd(g.contiguous(), pidx, pw), None, None, None
+
+
+def _routed_train_ok(model, rays, active_module) -> bool:
+    return (ROUTED_TRAIN and isinstance(model, MetaContainer) and active_module is None and rays.is_cuda
+            and rays.dtype == torch.float32 and all(s._fusable for s in model.submodules) and not _second_order())
+
+
+def _render_routed(model, rays: Tensor, S: int, params, u: Optional[Tensor], bg_color_default: str, sigma_scale):
+    """Differentiable render of the routed container (training / runtime_adapt, ray_rendering.py:290-345
+    over MetaContainer.forward :275-343): routing + per-expert pair lists on the GPU (routed.hip, one
+    host sync for the segment sizes), per expert the HIP hash grid (autograd to its table) and the fused
+    MLP, the weighted blend in expert order, HIP compositing.  Experts no sample reaches get no
+    gradient at all (grad None), as in the reference's loop."""
+    N = rays.shape[0]
+    if model.training and u is None:
+        u = torch.rand_like(rays.new_empty(N, S))  # the reference's rand_like(low) draw
+    boxes = [sub._host_box() for sub in model.submodules]
+    t_vals, starts, pidx, pw, x01, sh, pmap = ops.routed_pairs(
+        rays.contiguous(), S, u if model.training else None, model.routing_spec(), [b[0] for b in boxes],
+        [b[1] for b in boxes], ENC_EPS)
+    from .meta_ngp import _FusedMLPFn
+    sub_params = model._sub_params(params)
+    outs = []
+    for k, sub in enumerate(model.submodules):
+        a, b = starts[k], starts[k + 1]
+        if b == a:
+            continue
+        h0 = sub.xyz_encoder(x01[a:b])
+        ws = [t.contiguous() for t in sub._mlp_tensors(sub_params[k]).values()]
+        outs.append(_FusedMLPFn.apply(h0.contiguous(), sh[a:b], *ws))
+    y = torch.cat(outs, 0) if len(outs) > 1 else (outs[0] if outs else rays.new_zeros(0, 4))
+    rgb_sigma = _BlendFn.apply(y, pw, pmap, pidx).view(N, S, 4)
+    bg_rgb = _get_bg_rgb(model, rays[:, 3:6], params, rgb_sigma, N=N, bg_color_default=bg_color_default)
+    return volume_render(rgb_sigma, t_vals, bg_rgb=bg_rgb, raw_rgb=False, raw_sigma=False, sigma_scale=sigma_scale)
 
 
 def _fused_experts(model, params, active_module):
@@ -266,6 +316,9 @@ def render_rays_stratified(model, rays: Tensor, ray_samples: int, params=None, a
         bg_rgb = _get_bg_rgb(model, rays[:, 3:6], params, rgb_sigma, N=N, bg_color_default=bg_color_default)
         return volume_render(rgb_sigma, t_vals, bg_rgb=bg_rgb, raw_rgb=False, raw_sigma=False,
                              sigma_scale=sigma_scale)
+    if _routed_train_ok(model, rays, active_module):
+        return _render_routed(model, rays, ray_samples, params, kwargs.get("jitter_u"), bg_color_default,
+                              sigma_scale)
     # composed (differentiable) path -- same structure as the reference
     o, d = rays[:, :3], rays[:, 3:6]
     near, far = rays[:, 6], rays[:, 7]

