@@ -217,6 +217,86 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_rle(const float* __restrict_
 #define ACN_HASH_BWD_PPL 16  // consecutive points per lane in hashgrid_bwd_rle (0: the per-point kernel)
 #endif
 
+// ---------------------------------------------------------------------------------------------
+// (sample, expert) pair lists of the routed container (routed.hip): slot p belongs to expert pk[p],
+// the live slot count is seg[K] on the device (graph-replayable: grids are fixed, loops stride to it).
+struct Tables {
+    const float2* t[acn::kMaxK];
+};
+struct GradTables {
+    float* t[acn::kMaxK];
+};
+
+template <int INTERP>
+__global__ void __launch_bounds__(256) hashgrid_fwd_pairs(const float* __restrict__ x01, const int32_t* __restrict__ pk,
+                                                          const int64_t* __restrict__ seg, int K, Tables tabs,
+                                                          Res32 res, int L, int log2T, float2* __restrict__ out) {
+    const int64_t n = seg[K] * L;
+    const uint32_t mask = (uint32_t)((1ull << log2T) - 1ull);
+    for (int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; gid < n; gid += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t m = gid / L;
+        const int l = (int)(gid - m * L);
+        const float r = (float)res.v[l];
+        const float sx = x01[3 * m] * r, sy = x01[3 * m + 1] * r, sz = x01[3 * m + 2] * r;
+        const float2* tl = tabs.t[pk[m]] + ((int64_t)l << log2T);
+        float o0, o1;
+        acn::hash_level_f2<INTERP>(tl, sx, sy, sz, mask, o0, o1);
+        out[m * L + l] = make_float2(o0, o1);
+    }
+}
+
+// hashgrid_bwd_rle over pair slots: the run key is the target address, so a stretch may cross an
+// expert boundary; padding slots (pidx < 0) add nothing
+template <int INTERP, int PPL>
+__global__ void __launch_bounds__(256) hashgrid_bwd_pairs(const float* __restrict__ x01, const int32_t* __restrict__ pk,
+                                                          const int32_t* __restrict__ pidx,
+                                                          const int64_t* __restrict__ seg, int K,
+                                                          const float* __restrict__ gout, GradTables gt, Res32 res,
+                                                          int L, int log2T) {
+    const int lane = threadIdx.x & 63;
+    const int64_t M = seg[K];
+    const int64_t nwaves = ((M + 4 * PPL - 1) / (4 * PPL)) * L;
+    const int f = lane & 1, bx = (lane >> 1) & 1, by = (lane >> 3) & 1, bz = (lane >> 2) & 1;
+    const uint32_t mask = (uint32_t)((1ull << log2T) - 1ull);
+    for (int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; wave < nwaves;
+         wave += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+        const int l = (int)(wave % L);
+        const int64_t chunk = wave / L;
+        const int64_t m0 = (chunk * 4 + (lane >> 4)) * PPL;
+        const float r = (float)res.v[l];
+        const int64_t base = ((int64_t)l << log2T) * 2 + f;
+        float* cur = nullptr;
+        float acc = 0.0f;
+        for (int i = 0; i < PPL; ++i) {
+            const int64_t m = m0 + i;
+            if (m >= M) break;
+            if (pidx[m] < 0) continue;
+            const float sx = x01[3 * m] * r, sy = x01[3 * m + 1] * r, sz = x01[3 * m + 2] * r;
+            const float fx = floorf(sx), fy = floorf(sy), fz = floorf(sz);
+            float wx = sx - fx, wy = sy - fy, wz = sz - fz;
+            if (INTERP == 2) {
+                wx = (wx * wx) * (3.0f - 2.0f * wx);
+                wy = (wy * wy) * (3.0f - 2.0f * wy);
+                wz = (wz * wz) * (3.0f - 2.0f * wz);
+            }
+            const uint32_t xi = (uint32_t)(int)fx + (uint32_t)bx;
+            const uint32_t yi = (uint32_t)(int)fy * acn::kP1 + (by ? acn::kP1 : 0u);
+            const uint32_t zi = (uint32_t)(int)fz * acn::kP2 + (bz ? acn::kP2 : 0u);
+            float* a = gt.t[pk[m]] + base + (int64_t)((xi ^ yi ^ zi) & mask) * 2;
+            const float gv = ((gout[(m * L + l) * 2 + f] * (bz ? wz : 1.0f - wz)) * (by ? wy : 1.0f - wy)) *
+                             (bx ? wx : 1.0f - wx);
+            if (a == cur) {
+                acc += gv;
+            } else {
+                if (cur) unsafeAtomicAdd(cur, acc);
+                cur = a;
+                acc = gv;
+            }
+        }
+        if (cur) unsafeAtomicAdd(cur, acc);
+    }
+}
+
 template <int DEGREE>
 __global__ void __launch_bounds__(256) sh_fwd_kernel(const float* __restrict__ d, int64_t M,
                                                      float* __restrict__ out) {
@@ -309,4 +389,41 @@ extern "C" int acn_sh_fwd(const float* d, int64_t M, int levels, float* out, voi
         default: hipLaunchKernelGGL(sh_fwd_kernel<4>, grid, block, 0, s, d, M, out); break;
     }
     return acn_check_launch("acn_sh_fwd");
+}
+
+extern "C" int acn_hashgrid_fwd_pairs(const float* x01, const int32_t* pk, const int64_t* seg, int K,
+                                      const float* const* tables, const int32_t* res, int L, int log2T, int interp,
+                                      float* out, void* stream) {
+    ACN_REQUIRE(K >= 1 && K <= acn::kMaxK && tables && res && seg && x01 && pk && out,
+                "acn_hashgrid_fwd_pairs: bad arguments");
+    ACN_REQUIRE(L >= 1 && L <= ACN_MAX_LEVELS && log2T >= 1 && log2T <= 30 && interp >= 0 && interp <= 2,
+                "acn_hashgrid_fwd_pairs: bad grid configuration");
+    Res32 r{};
+    for (int i = 0; i < L; ++i) r.v[i] = res[i];
+    Tables t{};
+    for (int k = 0; k < K; ++k) t.t[k] = (const float2*)tables[k];
+    const dim3 grid(2048), block(256);  // grid-stride to the device slot count
+    hipStream_t s = (hipStream_t)stream;
+    if (interp == 0) hipLaunchKernelGGL(hashgrid_fwd_pairs<0>, grid, block, 0, s, x01, pk, seg, K, t, r, L, log2T, (float2*)out);
+    else if (interp == 1) hipLaunchKernelGGL(hashgrid_fwd_pairs<1>, grid, block, 0, s, x01, pk, seg, K, t, r, L, log2T, (float2*)out);
+    else hipLaunchKernelGGL(hashgrid_fwd_pairs<2>, grid, block, 0, s, x01, pk, seg, K, t, r, L, log2T, (float2*)out);
+    return acn_check_launch("acn_hashgrid_fwd_pairs");
+}
+
+extern "C" int acn_hashgrid_bwd_pairs(const float* x01, const int32_t* pk, const int32_t* pidx, const int64_t* seg,
+                                      int K, const float* grad_out, float* const* grad_tables, const int32_t* res,
+                                      int L, int log2T, int interp, void* stream) {
+    ACN_REQUIRE(K >= 1 && K <= acn::kMaxK && grad_tables && res && seg && x01 && pk && pidx && grad_out,
+                "acn_hashgrid_bwd_pairs: bad arguments");
+    ACN_REQUIRE(L >= 1 && L <= ACN_MAX_LEVELS && log2T >= 1 && log2T <= 30 && (interp == 1 || interp == 2),
+                "acn_hashgrid_bwd_pairs: Linear / Smoothstep interpolation only");
+    Res32 r{};
+    for (int i = 0; i < L; ++i) r.v[i] = res[i];
+    GradTables t{};
+    for (int k = 0; k < K; ++k) t.t[k] = grad_tables[k];
+    const dim3 grid(2048), block(256);
+    hipStream_t s = (hipStream_t)stream;
+    if (interp == 1) hipLaunchKernelGGL((hashgrid_bwd_pairs<1, 16>), grid, block, 0, s, x01, pk, pidx, seg, K, grad_out, t, r, L, log2T);
+    else hipLaunchKernelGGL((hashgrid_bwd_pairs<2, 16>), grid, block, 0, s, x01, pk, pidx, seg, K, grad_out, t, r, L, log2T);
+    return acn_check_launch("acn_hashgrid_bwd_pairs");
 }

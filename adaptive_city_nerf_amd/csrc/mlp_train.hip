@@ -68,31 +68,41 @@ __device__ __forceinline__ int64_t fm_index(int64_t m, int nfeat, int f) {
 
 // the padded LDS image, built once per call (one element per thread), then copied by every block of
 // the MLP kernels with 16-B loads
-__global__ void __launch_bounds__(256) mlp_pack_kernel(MlpPtrs p, float* __restrict__ img) {
-    {
-        const int e = blockIdx.x * 256 + threadIdx.x;
-        if (e >= L_FLOATS) return;
-        float v = 0.0f;
-        if (e < L_W1) { const int r = e / 33, c = e % 33; v = c < 32 ? p.w0[r * 32 + c] : 0.0f; }
-        else if (e < L_WH) { const int q = e - L_W1, r = q / 65, c = q % 65; v = c < 64 ? p.w1[r * 64 + c] : 0.0f; }
-        else if (e < L_WC0) {
-            const int q = e - L_WH, r = q / 65, c = q % 65;
-            v = c < 64 && r < 16 ? (r < 15 ? p.wg[r * 64 + c] : p.wsh[c]) : 0.0f;
-        }
-        else if (e < L_WC1) { const int q = e - L_WC0, r = q / 33, c = q % 33; v = c < 31 ? p.wc0[r * 31 + c] : 0.0f; }
-        else if (e < L_WC2) { const int q = e - L_WC1, r = q / 65, c = q % 65; v = c < 64 ? p.wc1[r * 64 + c] : 0.0f; }
-        else if (e < L_B0) {
-            const int q = e - L_WC2, r = q / 65, c = q % 65;
-            v = c < 64 && r < 3 ? p.wc2[r * 64 + c] : 0.0f;
-        }
-        else if (e < L_B1) v = p.b0[e - L_B0];
-        else if (e < L_BH) v = p.b1[e - L_B1];
-        else if (e < L_BC0) { const int q = e - L_BH; v = q < 15 ? p.bg[q] : (q == 15 ? p.bsh[0] : 0.0f); }
-        else if (e < L_BC1) v = p.bc0[e - L_BC0];
-        else if (e < L_BC2) v = p.bc1[e - L_BC1];
-        else { const int q = e - L_BC2; v = q < 3 ? p.bc2[q] : 0.0f; }
-        img[e] = v;
+__device__ __forceinline__ float pack_elem(const MlpPtrs& p, int e) {
+    float v = 0.0f;
+    if (e < L_W1) { const int r = e / 33, c = e % 33; v = c < 32 ? p.w0[r * 32 + c] : 0.0f; }
+    else if (e < L_WH) { const int q = e - L_W1, r = q / 65, c = q % 65; v = c < 64 ? p.w1[r * 64 + c] : 0.0f; }
+    else if (e < L_WC0) {
+        const int q = e - L_WH, r = q / 65, c = q % 65;
+        v = c < 64 && r < 16 ? (r < 15 ? p.wg[r * 64 + c] : p.wsh[c]) : 0.0f;
     }
+    else if (e < L_WC1) { const int q = e - L_WC0, r = q / 33, c = q % 33; v = c < 31 ? p.wc0[r * 31 + c] : 0.0f; }
+    else if (e < L_WC2) { const int q = e - L_WC1, r = q / 65, c = q % 65; v = c < 64 ? p.wc1[r * 64 + c] : 0.0f; }
+    else if (e < L_B0) {
+        const int q = e - L_WC2, r = q / 65, c = q % 65;
+        v = c < 64 && r < 3 ? p.wc2[r * 64 + c] : 0.0f;
+    }
+    else if (e < L_B1) v = p.b0[e - L_B0];
+    else if (e < L_BH) v = p.b1[e - L_B1];
+    else if (e < L_BC0) { const int q = e - L_BH; v = q < 15 ? p.bg[q] : (q == 15 ? p.bsh[0] : 0.0f); }
+    else if (e < L_BC1) v = p.bc0[e - L_BC0];
+    else if (e < L_BC2) v = p.bc1[e - L_BC1];
+    else { const int q = e - L_BC2; v = q < 3 ? p.bc2[q] : 0.0f; }
+    return v;
+}
+
+__global__ void __launch_bounds__(256) mlp_pack_kernel(MlpPtrs p, float* __restrict__ img) {
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e < L_FLOATS) img[e] = pack_elem(p, e);
+}
+
+// the images of K experts at once (routed pair lists): blockIdx.y = expert
+struct MlpPtrsK {
+    MlpPtrs e[acn::kMaxK];
+};
+__global__ void __launch_bounds__(256) mlp_pack_multi_kernel(MlpPtrsK p, float* __restrict__ imgs) {
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e < L_FLOATS) imgs[(int64_t)blockIdx.y * L_FLOATS + e] = pack_elem(p.e[blockIdx.y], e);
 }
 
 __device__ __forceinline__ void stage_weights(const float* __restrict__ img, float* s) {
@@ -433,112 +443,119 @@ __device__ __forceinline__ void flush_block(const f32x4& d, int lane, Put put) {
     for (int r = 0; r < 4; ++r) put(4 * (lane >> 4) + r, lane & 15, d[r]);
 }
 
-__global__ void __launch_bounds__(256) mlp_bwd_dw_kernel(const float* __restrict__ img, const float* __restrict__ h0,
-                                                         const float* __restrict__ sh, const float* __restrict__ out,
-                                                         const float* __restrict__ gout, int64_t M,
-                                                         float* __restrict__ gh0, float* __restrict__ partial) {
-    __shared__ __attribute__((aligned(16))) float Wl[L_FLOATS];
-    __shared__ __attribute__((aligned(16))) float st_base[128 * SW];
-    stage_weights(img, Wl);
-    __syncthreads();
-    const int lane0 = threadIdx.x & 63, h = lane0 >> 5, j = lane0 & 31, w = threadIdx.x >> 6;
-    const int64_t ntiles = (M + 31) / 32;
+// expert of pair slot p (segment starts seg[0..K], routed.hip)
+__device__ __forceinline__ int seg_expert(const int64_t* seg, int K, int64_t p) {
+    int k = 0;
+    while (k + 1 < K && seg[k + 1] <= p) ++k;
+    return k;
+}
+
+// the 14 weight-gradient blocks of one wave (56 accumulator registers) and its bias partial sums
+struct DwAcc {
     f32x4 aWC2[1], aWC1[4], aWC0[2], aHD[1], aW1[4], aW0[2];
-    float bWC2 = 0.0f, bWC1 = 0.0f, bWC0 = 0.0f, bHD = 0.0f, bW1 = 0.0f, bW0 = 0.0f;
-    aWC2[0] = 0.0f; aHD[0] = 0.0f;
+    float bWC2, bWC1, bWC0, bHD, bW1, bW0;
+};
+
+__device__ __forceinline__ void dw_zero(DwAcc& a) {
+    a.aWC2[0] = 0.0f; a.aHD[0] = 0.0f;
 #pragma unroll
-    for (int n = 0; n < 4; ++n) { aWC1[n] = 0.0f; aW1[n] = 0.0f; }
+    for (int n = 0; n < 4; ++n) { a.aWC1[n] = 0.0f; a.aW1[n] = 0.0f; }
 #pragma unroll
-    for (int n = 0; n < 2; ++n) { aWC0[n] = 0.0f; aW0[n] = 0.0f; }
-    // rounds are uniform over the workgroup (barriers inside): tiles past the end have zero gradients
-    for (int64_t base = (int64_t)blockIdx.x * 4; base < ntiles; base += (int64_t)gridDim.x * 4) {
-        const float* W = Wl + opaque_s(0);
-        float* st = st_base + opaque_s(0);
-        const int lane = opaque_v(lane0);
-        const int64_t m = (base + w) * 32 + j;
-        const bool ok = m < M;
-        f32x16 A1[2], A2[2], Hd[1], Cin[1], C1[2], C2[2], Rg[1];
-        {
-            f32x16 X0[1];
-            tile_forward(W, h0, sh, m, ok, lane, X0, A1, A2, Hd, Cin, C1, C2, Rg);
-        }
-        f32x16 dRg[1], dHd[1];
-        dRg[0] = 0.0f;
-        float dsig = 0.0f;
-        if (ok) {
-            if (h == 0) {
-#pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    const float y = out[m * 4 + c];
-                    dRg[0][c] = (gout[m * 4 + c] * (1.0f - y)) * y;
-                }
-            } else {
-                dsig = gout[m * 4 + 3] * out[m * 4 + 3];
-            }
-        }
-        // colour head 3 x 64: column block w, rows 0..15 (0..2 live)
-        stage_layer<1, 2>(st, dRg, C2, w, lane);
-        dw_blocks<1>(st, 0, X_ROW + 16 * w, aWC2, bWC2, lane);
-        f32x16 G2[2], G1[2], Gc[1];
-        bwd_layer<2, 1, 3>(W + L_WC2, 65, dRg, G2, lane);
-        relu_mask<2>(G2, C2);
-        // colour layer 1, 64 x 64: row block w
-        stage_layer<2, 2>(st, G2, C1, w, lane);
-        dw_blocks<4>(st, 16 * w, X_ROW, aWC1, bWC1, lane);
-        bwd_layer<2, 2, 64>(W + L_WC1, 65, G2, G1, lane);
-        relu_mask<2>(G1, C1);
-        // colour layer 0, 64 x 31 (input 31 = zero column): row block w
-        stage_layer<2, 1>(st, G1, Cin, w, lane);
-        dw_blocks<2>(st, 16 * w, X_ROW, aWC0, bWC0, lane);
-        bwd_layer<1, 2, 64>(W + L_WC0, 33, G1, Gc, lane);  // d cin: rows 0..14 = d geo (SH rows dropped)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int f = rho(r, h);
-            dHd[0][r] = f < 15 ? Gc[0][r] : (f == 15 ? dsig : 0.0f);
-        }
-        // heads [geo 15 | sigma 1] x 64: column block w
-        stage_layer<1, 2>(st, dHd, A2, w, lane);
-        dw_blocks<1>(st, 0, X_ROW + 16 * w, aHD, bHD, lane);
-        f32x16 GA2[2], GA1[2], GH[1];
-        bwd_layer<2, 1, 16>(W + L_WH, 65, dHd, GA2, lane);
-        relu_mask<2>(GA2, A2);
-        // sigma trunk 1, 64 x 64: row block w
-        stage_layer<2, 2>(st, GA2, A1, w, lane);
-        dw_blocks<4>(st, 16 * w, X_ROW, aW1, bW1, lane);
-        bwd_layer<2, 2, 64>(W + L_W1, 65, GA2, GA1, lane);
-        relu_mask<2>(GA1, A1);
-        // sigma trunk 0, 64 x 32: row block w
+    for (int n = 0; n < 2; ++n) { a.aWC0[n] = 0.0f; a.aW0[n] = 0.0f; }
+    a.bWC2 = a.bWC1 = a.bWC0 = a.bHD = a.bW1 = a.bW0 = 0.0f;
+}
+
+// one round: wave w re-runs the forward of its tile (samples m = tile * 32 + j), runs the backward chain
+// and adds its share of every layer's [dW | db] over the workgroup's 128 samples; barriers inside
+__device__ __forceinline__ void dw_round(const float* W, float* st, const float* __restrict__ h0,
+                                         const float* __restrict__ sh, const float* __restrict__ out,
+                                         const float* __restrict__ gout, int64_t m, bool ok, int w, int lane,
+                                         float* __restrict__ gh0, DwAcc& a) {
+    const int h = lane >> 5;
+    f32x16 A1[2], A2[2], Hd[1], Cin[1], C1[2], C2[2], Rg[1];
+    {
         f32x16 X0[1];
-        load_tiles<1>(h0, 32, 0, 32, m, ok, h, X0);  // reloaded (L2-hot) rather than kept live
-        stage_layer<2, 1>(st, GA1, X0, w, lane);
-        dw_blocks<2>(st, 16 * w, X_ROW, aW0, bW0, lane);
-        if (gh0) {
-            bwd_layer<1, 2, 64>(W + L_W0, 33, GA1, GH, lane);
-            store_tiles<1>(gh0, 32, 0, 32, m, ok, h, GH);
+        tile_forward(W, h0, sh, m, ok, lane, X0, A1, A2, Hd, Cin, C1, C2, Rg);
+    }
+    f32x16 dRg[1], dHd[1];
+    dRg[0] = 0.0f;
+    float dsig = 0.0f;
+    if (ok) {
+        if (h == 0) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const float y = out[m * 4 + c];
+                dRg[0][c] = (gout[m * 4 + c] * (1.0f - y)) * y;
+            }
+        } else {
+            dsig = gout[m * 4 + 3] * out[m * 4 + 3];
         }
     }
-    // flush: every element of the workgroup's copy has exactly one owner
-    float* dst = partial + (int64_t)blockIdx.x * NDW;
+    // colour head 3 x 64: column block w, rows 0..15 (0..2 live)
+    stage_layer<1, 2>(st, dRg, C2, w, lane);
+    dw_blocks<1>(st, 0, X_ROW + 16 * w, a.aWC2, a.bWC2, lane);
+    f32x16 G2[2], G1[2], Gc[1];
+    bwd_layer<2, 1, 3>(W + L_WC2, 65, dRg, G2, lane);
+    relu_mask<2>(G2, C2);
+    // colour layer 1, 64 x 64: row block w
+    stage_layer<2, 2>(st, G2, C1, w, lane);
+    dw_blocks<4>(st, 16 * w, X_ROW, a.aWC1, a.bWC1, lane);
+    bwd_layer<2, 2, 64>(W + L_WC1, 65, G2, G1, lane);
+    relu_mask<2>(G1, C1);
+    // colour layer 0, 64 x 31 (input 31 = zero column): row block w
+    stage_layer<2, 1>(st, G1, Cin, w, lane);
+    dw_blocks<2>(st, 16 * w, X_ROW, a.aWC0, a.bWC0, lane);
+    bwd_layer<1, 2, 64>(W + L_WC0, 33, G1, Gc, lane);  // d cin: rows 0..14 = d geo (SH rows dropped)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int f = rho(r, h);
+        dHd[0][r] = f < 15 ? Gc[0][r] : (f == 15 ? dsig : 0.0f);
+    }
+    // heads [geo 15 | sigma 1] x 64: column block w
+    stage_layer<1, 2>(st, dHd, A2, w, lane);
+    dw_blocks<1>(st, 0, X_ROW + 16 * w, a.aHD, a.bHD, lane);
+    f32x16 GA2[2], GA1[2], GH[1];
+    bwd_layer<2, 1, 16>(W + L_WH, 65, dHd, GA2, lane);
+    relu_mask<2>(GA2, A2);
+    // sigma trunk 1, 64 x 64: row block w
+    stage_layer<2, 2>(st, GA2, A1, w, lane);
+    dw_blocks<4>(st, 16 * w, X_ROW, a.aW1, a.bW1, lane);
+    bwd_layer<2, 2, 64>(W + L_W1, 65, GA2, GA1, lane);
+    relu_mask<2>(GA1, A1);
+    // sigma trunk 0, 64 x 32: row block w
+    f32x16 X0[1];
+    load_tiles<1>(h0, 32, 0, 32, m, ok, h, X0);  // reloaded (L2-hot) rather than kept live
+    stage_layer<2, 1>(st, GA1, X0, w, lane);
+    dw_blocks<2>(st, 16 * w, X_ROW, a.aW0, a.bW0, lane);
+    if (gh0) {
+        bwd_layer<1, 2, 64>(W + L_W0, 33, GA1, GH, lane);
+        store_tiles<1>(gh0, 32, 0, 32, m, ok, h, GH);
+    }
+}
+
+// one copy of the 13,715 partial sums: every element has exactly one owner (wave, lane, register)
+__device__ __forceinline__ void dw_flush(DwAcc& a, float* __restrict__ dst, int w, int lane0) {
     const int cw = 16 * w;
-    flush_block(aWC2[0], lane0, [&](int o, int c, float v) { if (o < 3) dst[D_WC2 + 64 * o + cw + c] = v; });
-    flush_block(aHD[0], lane0, [&](int o, int c, float v) {
+    flush_block(a.aWC2[0], lane0, [&](int o, int c, float v) { if (o < 3) dst[D_WC2 + 64 * o + cw + c] = v; });
+    flush_block(a.aHD[0], lane0, [&](int o, int c, float v) {
         dst[o < 15 ? D_WG + 64 * o + cw + c : D_WSH + cw + c] = v;
     });
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
-        flush_block(aWC1[n], lane0, [&](int o, int c, float v) { dst[D_WC1 + 64 * (cw + o) + 16 * n + c] = v; });
-        flush_block(aW1[n], lane0, [&](int o, int c, float v) { dst[D_W1 + 64 * (cw + o) + 16 * n + c] = v; });
+        flush_block(a.aWC1[n], lane0, [&](int o, int c, float v) { dst[D_WC1 + 64 * (cw + o) + 16 * n + c] = v; });
+        flush_block(a.aW1[n], lane0, [&](int o, int c, float v) { dst[D_W1 + 64 * (cw + o) + 16 * n + c] = v; });
     }
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
-        flush_block(aWC0[n], lane0, [&](int o, int c, float v) {
+        flush_block(a.aWC0[n], lane0, [&](int o, int c, float v) {
             if (16 * n + c < 31) dst[D_WC0 + 31 * (cw + o) + 16 * n + c] = v;
         });
-        flush_block(aW0[n], lane0, [&](int o, int c, float v) { dst[D_W0 + 32 * (cw + o) + 16 * n + c] = v; });
+        flush_block(a.aW0[n], lane0, [&](int o, int c, float v) { dst[D_W0 + 32 * (cw + o) + 16 * n + c] = v; });
     }
     // bias rows: lane (i, q) holds the sum over samples 32 q .. 32 q + 31 of row i of its row block
     auto red = [](float v) { v += __shfl_xor(v, 16); return v + __shfl_xor(v, 32); };
-    bWC2 = red(bWC2); bHD = red(bHD); bWC1 = red(bWC1); bWC0 = red(bWC0); bW1 = red(bW1); bW0 = red(bW0);
+    const float bWC2 = red(a.bWC2), bHD = red(a.bHD), bWC1 = red(a.bWC1), bWC0 = red(a.bWC0), bW1 = red(a.bW1),
+                bW0 = red(a.bW0);
     if (lane0 < 16) {
         const int i = lane0;
         if (w == 0) {
@@ -550,6 +567,64 @@ __global__ void __launch_bounds__(256) mlp_bwd_dw_kernel(const float* __restrict
         dst[D_B1 + cw + i] = bW1;
         dst[D_B0 + cw + i] = bW0;
     }
+}
+
+__global__ void __launch_bounds__(256) mlp_bwd_dw_kernel(const float* __restrict__ img, const float* __restrict__ h0,
+                                                         const float* __restrict__ sh, const float* __restrict__ out,
+                                                         const float* __restrict__ gout, int64_t M,
+                                                         float* __restrict__ gh0, float* __restrict__ partial) {
+    __shared__ __attribute__((aligned(16))) float Wl[L_FLOATS];
+    __shared__ __attribute__((aligned(16))) float st_base[128 * SW];
+    stage_weights(img, Wl);
+    __syncthreads();
+    const int lane0 = threadIdx.x & 63, j = lane0 & 31, w = threadIdx.x >> 6;
+    const int64_t ntiles = (M + 31) / 32;
+    DwAcc a;
+    dw_zero(a);
+    // rounds are uniform over the workgroup (barriers inside): tiles past the end have zero gradients
+    for (int64_t base = (int64_t)blockIdx.x * 4; base < ntiles; base += (int64_t)gridDim.x * 4) {
+        const int64_t m = (base + w) * 32 + j;
+        dw_round(Wl + opaque_s(0), st_base + opaque_s(0), h0, sh, out, gout, m, m < M, w, opaque_v(lane0), gh0, a);
+    }
+    dw_flush(a, partial + (int64_t)blockIdx.x * NDW, w, lane0);
+}
+
+// Pair-list variant (routed container): workgroup b takes the contiguous rounds [b R / G, (b+1) R / G)
+// (R = seg[K] / 128 from the device); when the expert of the next round differs, the running sums go
+// to copy (b, expert) and restart, and the new expert's image is staged.  mlp_dw_reduce_pairs_kernel
+// adds, per expert, the copies of the workgroups whose range met that expert's rounds (in b order:
+// deterministic, no atomics).  Padding slots carry zero output gradients.
+__global__ void __launch_bounds__(256) mlp_bwd_dw_pairs_kernel(const float* __restrict__ imgs,
+                                                               const float* __restrict__ h0,
+                                                               const float* __restrict__ sh,
+                                                               const float* __restrict__ out,
+                                                               const float* __restrict__ gout,
+                                                               const int64_t* __restrict__ seg, int K,
+                                                               float* __restrict__ gh0, float* __restrict__ partial) {
+    __shared__ __attribute__((aligned(16))) float Wl[L_FLOATS];
+    __shared__ __attribute__((aligned(16))) float st_base[128 * SW];
+    const int lane0 = threadIdx.x & 63, j = lane0 & 31, w = threadIdx.x >> 6;
+    const int64_t R = seg[K] / 128, G = gridDim.x;
+    const int64_t r0 = (int64_t)blockIdx.x * R / G, r1 = ((int64_t)blockIdx.x + 1) * R / G;
+    DwAcc a;
+    dw_zero(a);
+    int cur = -1;
+    for (int64_t rd = r0; rd < r1; ++rd) {
+        const int k = seg_expert(seg, K, rd * 128);
+        if (k != cur) {
+            if (cur >= 0) {
+                dw_flush(a, partial + ((int64_t)blockIdx.x * K + cur) * NDW, w, lane0);
+                dw_zero(a);
+            }
+            __syncthreads();
+            stage_weights(imgs + (int64_t)k * L_FLOATS, Wl);
+            __syncthreads();
+            cur = k;
+        }
+        const int64_t m = (rd * 4 + w) * 32 + j;
+        dw_round(Wl + opaque_s(0), st_base + opaque_s(0), h0, sh, out, gout, m, true, w, opaque_v(lane0), gh0, a);
+    }
+    if (cur >= 0) dw_flush(a, partial + ((int64_t)blockIdx.x * K + cur) * NDW, w, lane0);
 }
 
 // dw[e] = sum over the nblk partial copies: a block sums 32 consecutive elements, its 8 thread rows
@@ -569,6 +644,67 @@ __global__ void __launch_bounds__(256) mlp_dw_reduce_kernel(const float* __restr
 #pragma unroll
         for (int k = 1; k < 8; ++k) t += red[k][c];
         dw[e] = t;
+    }
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// Routed pair lists (routed.hip): slots grouped by expert, every expert's segment padded to a multiple
+// of 128 (one round = 4 tiles = 128 slots of ONE expert); the slot count seg[K] lives on the device, so
+// grids are fixed and the kernels stride to it (HIP-graph replayable).  A workgroup stages the weight
+// image of the expert of its current round and restages when the expert changes.
+
+__global__ void __launch_bounds__(256) mlp_fwd_pairs_kernel(const float* __restrict__ imgs, const float* __restrict__ h0,
+                                                            const float* __restrict__ sh,
+                                                            const int64_t* __restrict__ seg, int K,
+                                                            float* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) float Wl[L_FLOATS];
+    const int lane = threadIdx.x & 63, h = lane >> 5, j = lane & 31, w = threadIdx.x >> 6;
+    const int64_t rounds = seg[K] / 128;
+    int cur = -1;
+    for (int64_t rd = blockIdx.x; rd < rounds; rd += gridDim.x) {
+        const int k = seg_expert(seg, K, rd * 128);
+        if (k != cur) {
+            __syncthreads();
+            stage_weights(imgs + (int64_t)k * L_FLOATS, Wl);
+            __syncthreads();
+            cur = k;
+        }
+        const int64_t m = (rd * 4 + w) * 32 + j;
+        f32x16 X0[1], A1[2], A2[2], Hd[1], Cin[1], C1[2], C2[2], Rg[1];
+        tile_forward(Wl, h0, sh, m, true, lane, X0, A1, A2, Hd, Cin, C1, C2, Rg);
+        if (h == 0) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) out[m * 4 + c] = acn::sigmoidf_(Rg[0][c]);
+        } else {
+            out[m * 4 + 3] = acn::trunc_exp(Hd[0][7]);
+        }
+    }
+}
+
+// dw[k][e] = sum over the workgroups b whose round range [b R / G, (b+1) R / G) met expert k's rounds of
+// copy (b, k); zero for an expert without pairs.  grid (NDW / 32, K)
+__global__ void __launch_bounds__(256) mlp_dw_reduce_pairs_kernel(const float* __restrict__ partial,
+                                                                  const int64_t* __restrict__ seg, int K, int G,
+                                                                  float* __restrict__ dw) {
+    __shared__ float red[8][32];
+    const int c = threadIdx.x & 31, row = threadIdx.x >> 5;
+    const int k = blockIdx.y;
+    const int e = blockIdx.x * 32 + c;
+    const int64_t R = seg[K] / 128, k0 = seg[k] / 128, k1 = seg[k + 1] / 128;
+    float s = 0.0f;
+    if (e < NDW && k1 > k0)
+        for (int b = row; b < G; b += 8) {
+            const int64_t lo = (int64_t)b * R / G, hi = ((int64_t)b + 1) * R / G;
+            if (lo < hi && lo < k1 && hi > k0) s += partial[((int64_t)b * K + k) * NDW + e];
+        }
+    red[row][c] = s;
+    __syncthreads();
+    if (row == 0 && e < NDW) {
+        float t = red[0][c];
+#pragma unroll
+        for (int q = 1; q < 8; ++q) t += red[q][c];
+        dw[(int64_t)k * NDW + e] = t;
     }
 }
 
@@ -633,4 +769,48 @@ extern "C" int acn_mlp_train_bwd_dw(const float* h0, const float* sh, const floa
     hipLaunchKernelGGL(mlp_dw_reduce_kernel, dim3((NDW + 31) / 32), dim3(256), 0, s, (const float*)partial, nblk,
                        dw);
     return acn_check_launch("acn_mlp_train_bwd_dw");
+}
+
+// ---------------------------------------------------------------------------------------------
+// routed pair lists
+constexpr int PAIR_DW_BLOCKS = 256;
+
+extern "C" size_t acn_mlp_pairs_workspace_bytes(int K) {
+    return ((size_t)K * L_FLOATS + (size_t)PAIR_DW_BLOCKS * K * NDW) * sizeof(float);
+}
+
+extern "C" int acn_mlp_pack_pairs(const acn_mlp* const* w, int K, void* workspace, void* stream) {
+    ACN_REQUIRE(w && workspace && K >= 1 && K <= acn::kMaxK, "acn_mlp_pack_pairs: bad arguments");
+    MlpPtrsK pk{};
+    for (int k = 0; k < K; ++k) {
+        ACN_REQUIRE(w[k], "acn_mlp_pack_pairs: NULL expert %d", k);
+        pk.e[k] = ptrs(w[k]);
+    }
+    hipLaunchKernelGGL(mlp_pack_multi_kernel, dim3((L_FLOATS + 255) / 256, K), dim3(256), 0, (hipStream_t)stream, pk,
+                       (float*)workspace);
+    return acn_check_launch("acn_mlp_pack_pairs");
+}
+
+extern "C" int acn_mlp_train_fwd_pairs(const float* h0, const float* sh, const int64_t* seg, int K,
+                                       const void* workspace, float* out, void* stream) {
+    ACN_REQUIRE(h0 && sh && seg && workspace && out && K >= 1 && K <= acn::kMaxK,
+                "acn_mlp_train_fwd_pairs: bad arguments");
+    hipLaunchKernelGGL(mlp_fwd_pairs_kernel, dim3(512), dim3(256), 0, (hipStream_t)stream, (const float*)workspace, h0,
+                       sh, seg, K, out);
+    return acn_check_launch("acn_mlp_train_fwd_pairs");
+}
+
+extern "C" int acn_mlp_train_bwd_dw_pairs(const float* h0, const float* sh, const float* out, const float* gout,
+                                          const int64_t* seg, int K, void* workspace, float* dw, float* gh0,
+                                          void* stream) {
+    ACN_REQUIRE(h0 && sh && out && gout && seg && workspace && dw && K >= 1 && K <= acn::kMaxK,
+                "acn_mlp_train_bwd_dw_pairs: bad arguments");
+    const float* imgs = (const float*)workspace;
+    float* partial = (float*)workspace + (size_t)K * L_FLOATS;
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(mlp_bwd_dw_pairs_kernel, dim3(PAIR_DW_BLOCKS), dim3(256), 0, s, imgs, h0, sh, out, gout, seg, K,
+                       gh0, partial);
+    hipLaunchKernelGGL(mlp_dw_reduce_pairs_kernel, dim3((NDW + 31) / 32, K), dim3(256), 0, s, (const float*)partial,
+                       seg, K, PAIR_DW_BLOCKS, dw);
+    return acn_check_launch("acn_mlp_train_bwd_dw_pairs");
 }

@@ -202,6 +202,141 @@ __global__ void __launch_bounds__(kThreads) adam_table_kernel(const acn_param_de
     adam_chunk(p, g, m, v, n, scale, k);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Slotted variant (routed container, graph-replayable): tensor t belongs to activity slot
+// flags[t] & 0xffff; slot s < K (an expert) is active in this step iff its routed pair count
+// seg[K + 1 + s] > 0 (routed.hip), slots >= K (shared parameters) always.  Like torch, an inactive
+// expert (grad None in the reference) is skipped entirely: no moment decay, no step increment.  Each
+// slot keeps its own device step counter; the constants come from a table of steps 1..table_steps.
+// flags bit 16: zero the gradient after reading it (the table gradients are scatter-added into
+// persistent buffers, so the next step finds them cleared without a separate memset pass).
+constexpr int kSlotZero = 1 << 16;
+
+__device__ __forceinline__ bool slot_active(const int64_t* __restrict__ seg, int K, int slot) {
+    return slot >= K || seg == nullptr || seg[K + 1 + slot] > 0;
+}
+
+__global__ void bump_slots_kernel(int32_t* __restrict__ step_dev, const int64_t* __restrict__ seg, int K, int nslots) {
+    const int s = threadIdx.x;
+    if (s < nslots && slot_active(seg, K, s)) step_dev[s] += 1;
+}
+
+__global__ void __launch_bounds__(kThreads) sumsq_slots_kernel(const acn_param_desc* __restrict__ descs,
+                                                               const int32_t* __restrict__ chunk_tensor,
+                                                               const int32_t* __restrict__ flags,
+                                                               const int64_t* __restrict__ seg, int K,
+                                                               double* __restrict__ partials) {
+    const int t = chunk_tensor[blockIdx.x];
+    const acn_param_desc d = descs[t];
+    double acc = 0.0;
+    if (d.grad != nullptr && slot_active(seg, K, flags[t] & 0xffff)) {
+        const int64_t base = (int64_t)(blockIdx.x - d.first_chunk) * ACN_OPTIM_CHUNK;
+        const int64_t n = d.numel - base < ACN_OPTIM_CHUNK ? d.numel - base : ACN_OPTIM_CHUNK;
+        const float* g = d.grad + base;
+        if ((reinterpret_cast<uintptr_t>(g) & 15) == 0) {
+            const int64_t n4 = n >> 2;
+            const f4* g4 = reinterpret_cast<const f4*>(g);
+            int64_t i = threadIdx.x;
+            for (; i + (kUnroll - 1) * kThreads < n4; i += kUnroll * kThreads) {
+                f4 v[kUnroll];
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u) v[u] = g4[i + u * kThreads];
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u)
+                    acc += (double)v[u][0] * v[u][0] + (double)v[u][1] * v[u][1] + (double)v[u][2] * v[u][2] +
+                           (double)v[u][3] * v[u][3];
+            }
+            for (; i < n4; i += kThreads) {
+                const f4 v = g4[i];
+                acc += (double)v[0] * v[0] + (double)v[1] * v[1] + (double)v[2] * v[2] + (double)v[3] * v[3];
+            }
+            for (int64_t i2 = (n4 << 2) + threadIdx.x; i2 < n; i2 += kThreads) acc += (double)g[i2] * g[i2];
+        } else {
+            for (int64_t i = threadIdx.x; i < n; i += kThreads) acc += (double)g[i] * g[i];
+        }
+    }
+    const double tot = block_sum(acc);
+    if (threadIdx.x == 0) partials[blockIdx.x] = tot;
+}
+
+// adam_chunk + clearing the gradient vectors that were non-zero
+__device__ __forceinline__ void adam_chunk_zero(float* p, float* g, float* m, float* v, int64_t n, float scale,
+                                                const GroupK& k) {
+    const uintptr_t align = reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) |
+                            reinterpret_cast<uintptr_t>(m) | reinterpret_cast<uintptr_t>(v);
+    int64_t done = 0;
+    if ((align & 15) == 0) {
+        const int64_t n4 = n >> 2;
+        f4* p4 = reinterpret_cast<f4*>(p);
+        f4* g4 = reinterpret_cast<f4*>(g);
+        f4* m4 = reinterpret_cast<f4*>(m);
+        f4* v4 = reinterpret_cast<f4*>(v);
+        const f4 zero = 0.0f;
+        int64_t i = threadIdx.x;
+        for (; i + (kUnroll - 1) * kThreads < n4; i += kUnroll * kThreads) {
+            f4 pp[kUnroll], gg[kUnroll], mm[kUnroll], vv[kUnroll];
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                pp[u] = p4[i + u * kThreads];
+                gg[u] = g4[i + u * kThreads];
+                mm[u] = m4[i + u * kThreads];
+                vv[u] = v4[i + u * kThreads];
+            }
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const bool nz = gg[u][0] != 0.0f || gg[u][1] != 0.0f || gg[u][2] != 0.0f || gg[u][3] != 0.0f;
+                adam_vec(pp[u], gg[u], mm[u], vv[u], scale, k);
+                p4[i + u * kThreads] = pp[u];
+                m4[i + u * kThreads] = mm[u];
+                v4[i + u * kThreads] = vv[u];
+                if (nz) g4[i + u * kThreads] = zero;
+            }
+        }
+        for (; i < n4; i += kThreads) {
+            f4 pp = p4[i], mm = m4[i], vv = v4[i];
+            const f4 gg = g4[i];
+            const bool nz = gg[0] != 0.0f || gg[1] != 0.0f || gg[2] != 0.0f || gg[3] != 0.0f;
+            adam_vec(pp, gg, mm, vv, scale, k);
+            p4[i] = pp;
+            m4[i] = mm;
+            v4[i] = vv;
+            if (nz) g4[i] = zero;
+        }
+        done = n4 << 2;
+    }
+    for (int64_t i = done + threadIdx.x; i < n; i += kThreads) {
+        float a = p[i], b = m[i], e = v[i];
+        adam_elem(a, g[i], b, e, scale, k);
+        p[i] = a; m[i] = b; v[i] = e;
+        g[i] = 0.0f;
+    }
+}
+
+__global__ void __launch_bounds__(kThreads) adam_slots_kernel(const acn_param_desc* __restrict__ descs,
+                                                              const int32_t* __restrict__ chunk_tensor,
+                                                              const int32_t* __restrict__ flags,
+                                                              const GroupK* __restrict__ table, int ngroups,
+                                                              int table_steps, const int32_t* __restrict__ step_dev,
+                                                              const int64_t* __restrict__ seg, int K,
+                                                              const float* __restrict__ grad_scale) {
+    const int t = chunk_tensor[blockIdx.x];
+    const acn_param_desc d = descs[t];
+    const int f = flags[t], slot = f & 0xffff;
+    if (d.grad == nullptr || !slot_active(seg, K, slot)) return;
+    const int row = step_dev[slot] - 1;
+    if (row < 0 || row >= table_steps) return;  // outside the uploaded table: the host refills first
+    const GroupK k = table[(int64_t)row * ngroups + d.group];
+    const float scale = grad_scale ? grad_scale[1] : 1.0f;
+    const int64_t base = (int64_t)(blockIdx.x - d.first_chunk) * ACN_OPTIM_CHUNK;
+    const int64_t n = d.numel - base < ACN_OPTIM_CHUNK ? d.numel - base : ACN_OPTIM_CHUNK;
+    float* p = d.param + base;
+    float* g = const_cast<float*>(d.grad) + base;
+    float* m = d.exp_avg + base;
+    float* v = d.exp_avg_sq + base;
+    if (f & kSlotZero) adam_chunk_zero(p, g, m, v, n, scale, k);
+    else adam_chunk(p, g, m, v, n, scale, k);
+}
+
 // python-float (double) scalars of _single_tensor_adam for one group at one step, cast to fp32 where
 // they meet tensors
 void group_consts(const acn_adam_group& g, GroupK& k) {
@@ -324,4 +459,31 @@ extern "C" int acn_adam_step(const acn_param_desc* descs, const int32_t* chunk_t
     hipLaunchKernelGGL(adam_kernel, dim3((unsigned)nchunks), dim3(kThreads), 0, (hipStream_t)stream, descs,
                        chunk_tensor, ga, grad_scale);
     return acn_check_launch("acn_adam_step");
+}
+
+extern "C" int acn_grad_sumsq_slots(const acn_param_desc* descs, const int32_t* chunk_tensor, int64_t nchunks,
+                                    const int32_t* flags, const int64_t* seg, int K, double* partials, double* total,
+                                    void* stream) {
+    ACN_REQUIRE(nchunks >= 1 && nchunks <= 0x7fffffff && descs && chunk_tensor && flags && partials && total,
+                "acn_grad_sumsq_slots: bad arguments");
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(sumsq_slots_kernel, dim3((unsigned)nchunks), dim3(kThreads), 0, s, descs, chunk_tensor, flags, seg,
+                       K, partials);
+    hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(kThreads), 0, s, partials, nchunks, total);
+    return acn_check_launch("acn_grad_sumsq_slots");
+}
+
+extern "C" int acn_adam_step_slots(const acn_param_desc* descs, const int32_t* chunk_tensor, int64_t nchunks,
+                                   const int32_t* flags, const void* table, int ngroups, int table_steps,
+                                   int32_t* step_dev, int nslots, const int64_t* seg, int K, const float* grad_scale,
+                                   void* stream) {
+    ACN_REQUIRE(nchunks >= 1 && nchunks <= 0x7fffffff && descs && chunk_tensor && flags && table && step_dev,
+                "acn_adam_step_slots: bad arguments");
+    ACN_REQUIRE(ngroups >= 1 && ngroups <= ACN_OPTIM_MAX_GROUPS && table_steps >= 1 && nslots >= 1 && nslots <= 1024,
+                "acn_adam_step_slots: bad ngroups / table_steps / nslots");
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(bump_slots_kernel, dim3(1), dim3(1024), 0, s, step_dev, seg, K, nslots);
+    hipLaunchKernelGGL(adam_slots_kernel, dim3((unsigned)nchunks), dim3(kThreads), 0, s, descs, chunk_tensor, flags,
+                       reinterpret_cast<const GroupK*>(table), ngroups, table_steps, step_dev, seg, K, grad_scale);
+    return acn_check_launch("acn_adam_step_slots");
 }

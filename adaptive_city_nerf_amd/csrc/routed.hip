@@ -73,9 +73,10 @@ __global__ void __launch_bounds__(kBlk) routed_count_kernel(const float* __restr
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
     for (int k = 0; k < kMaxK; ++k) {
-        if (k >= cfg.K) break;
-        const uint64_t b = __ballot(w[k] > 0.0f);
-        if (lane == 0) wcnt[wave][k] = __popcll(b);
+        if (k < cfg.K) {  // wave-uniform
+            const uint64_t b = __ballot(w[k] > 0.0f);
+            if (lane == 0) wcnt[wave][k] = __popcll(b);
+        }
     }
     __syncthreads();
     if (threadIdx.x < cfg.K) {
@@ -88,7 +89,7 @@ __global__ void __launch_bounds__(kBlk) routed_count_kernel(const float* __restr
 
 // one workgroup: per expert, exclusive scan of the block counts (in place) and the segment starts
 __global__ void __launch_bounds__(1024) routed_scan_kernel(int32_t* __restrict__ blk_cnt, int64_t nblk, int K,
-                                                           int64_t* __restrict__ starts) {
+                                                           int align, int64_t* __restrict__ starts) {
     __shared__ int64_t part[1024];
     __shared__ int64_t base;
     const int tid = threadIdx.x;
@@ -115,11 +116,29 @@ __global__ void __launch_bounds__(1024) routed_scan_kernel(int32_t* __restrict__
         __syncthreads();
         if (tid == 0) {
             starts[k] = base;
-            base += part[1023];
+            starts[K + 1 + k] = part[1023];                      // real pair count of expert k
+            base += (part[1023] + align - 1) / align * align;    // segment padded to a multiple of align
         }
         __syncthreads();
     }
     if (tid == 0) starts[K] = base;
+}
+
+// padding slots of every segment: pidx -1 (no sample), x01 0.5, sh 0, pk = k
+__global__ void __launch_bounds__(256) routed_pad_kernel(const int64_t* __restrict__ seg, int K, int align,
+                                                         int32_t* __restrict__ pidx, float* __restrict__ pw,
+                                                         float* __restrict__ x01, float* __restrict__ sh,
+                                                         int32_t* __restrict__ pk) {
+    const int k = blockIdx.x;
+    const int64_t p0 = seg[k] + seg[K + 1 + k], p1 = seg[k + 1];
+    for (int64_t p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
+        pidx[p] = -1;
+        pw[p] = 0.0f;
+        x01[3 * p] = x01[3 * p + 1] = x01[3 * p + 2] = 0.5f;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) sh[16 * p + q] = 0.0f;
+        if (pk) pk[p] = k;
+    }
 }
 
 struct BoxCfg {
@@ -134,7 +153,7 @@ __global__ void __launch_bounds__(kBlk) routed_scatter_kernel(const float* __res
                                                               const int64_t* __restrict__ starts, BoxCfg box,
                                                               int32_t* __restrict__ pidx, float* __restrict__ pw,
                                                               float* __restrict__ x01, float* __restrict__ sh_out,
-                                                              int32_t* __restrict__ pmap) {
+                                                              int32_t* __restrict__ pmap, int32_t* __restrict__ pk) {
     __shared__ int wcnt[kBlk / 64][kMaxK];
     const int64_t M = N * (int64_t)S;
     const int64_t m = (int64_t)blockIdx.x * kBlk + threadIdx.x;
@@ -169,6 +188,7 @@ __global__ void __launch_bounds__(kBlk) routed_scatter_kernel(const float* __res
         for (int q = 0; q < wave; ++q) pos += wcnt[q][k];
         pmap[m * K + k] = (int32_t)pos;
         pidx[pos] = (int32_t)m;
+        if (pk) pk[pos] = k;
         pw[pos] = wk;
         x01[pos * 3 + 0] = clamp_nan((px - box.amin[k][0]) / box.ext[k][0], box.lo, box.hi);
         x01[pos * 3 + 1] = clamp_nan((py - box.amin[k][1]) / box.ext[k][1], box.lo, box.hi);
@@ -200,10 +220,15 @@ __global__ void __launch_bounds__(256) blend_fwd_kernel(const float4* __restrict
 
 __global__ void __launch_bounds__(256) blend_bwd_kernel(const float4* __restrict__ g, const int32_t* __restrict__ pidx,
                                                         const float* __restrict__ pw, int64_t P,
-                                                        float4* __restrict__ gy) {
+                                                        const int64_t* __restrict__ live, float4* __restrict__ gy) {
     const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (p >= P) return;
-    const float4 v = g[pidx[p]];
+    if (p >= P || (live && p >= live[0])) return;  // slots past the live count hold no pair
+    const int32_t m = pidx[p];
+    if (m < 0) {  // padding slot
+        gy[p] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        return;
+    }
+    const float4 v = g[m];
     const float w = pw[p];
     gy[p] = make_float4(v.x * w, v.y * w, v.z * w, v.w * w);
 }
@@ -218,9 +243,9 @@ extern "C" size_t acn_routed_workspace_bytes(int64_t M, int K) {
 }
 
 extern "C" int acn_routed_count(const float* rays, int64_t N, int S, const float* jitter, const acn_routing* routing,
-                                float* t_vals, int64_t* starts, void* workspace, size_t workspace_bytes,
+                                int align, float* t_vals, int64_t* starts, void* workspace, size_t workspace_bytes,
                                 void* stream) {
-    ACN_REQUIRE(N >= 0 && S >= 1 && routing && starts, "acn_routed_count: bad arguments");
+    ACN_REQUIRE(N >= 0 && S >= 1 && routing && starts && align >= 1, "acn_routed_count: bad arguments");
     const int K = routing->K;
     ACN_REQUIRE(K >= 1 && K <= kMaxK, "acn_routed_count: K = %d outside [1, %d]", K, kMaxK);
     const int64_t M = N * (int64_t)S;
@@ -228,7 +253,7 @@ extern "C" int acn_routed_count(const float* rays, int64_t N, int S, const float
                 "acn_routed_count: workspace too small");
     hipStream_t s = (hipStream_t)stream;
     if (M == 0) {
-        const hipError_t e = hipMemsetAsync(starts, 0, (size_t)(K + 1) * sizeof(int64_t), s);
+        const hipError_t e = hipMemsetAsync(starts, 0, (size_t)(2 * K + 1) * sizeof(int64_t), s);
         return e == hipSuccess ? ACN_OK : acn_set_error((int)e, "acn_routed_count: memset failed");
     }
     ACN_REQUIRE(rays && t_vals, "acn_routed_count: NULL pointer");
@@ -244,14 +269,14 @@ extern "C" int acn_routed_count(const float* rays, int64_t N, int S, const float
     const int64_t nblk = (M + kBlk - 1) / kBlk;
     hipLaunchKernelGGL(routed_count_kernel, dim3(blocks_for(M, kBlk)), dim3(kBlk), 0, s, rays, N, S, jitter, cfg, t_vals,
                        W, blk);
-    hipLaunchKernelGGL(routed_scan_kernel, dim3(1), dim3(1024), 0, s, blk, nblk, K, starts);
+    hipLaunchKernelGGL(routed_scan_kernel, dim3(1), dim3(1024), 0, s, blk, nblk, K, align, starts);
     return acn_check_launch("acn_routed_count");
 }
 
 extern "C" int acn_routed_scatter(const float* rays, int64_t N, int S, int K, const float* t_vals,
                                   const int64_t* starts, const float* aabb_min, const float* aabb_extent, float lo,
-                                  float hi, const void* workspace, int32_t* pidx, float* pw, float* x01, float* sh,
-                                  int32_t* pmap, void* stream) {
+                                  float hi, int align, const void* workspace, int32_t* pidx, float* pw, float* x01,
+                                  float* sh, int32_t* pmap, int32_t* pk, void* stream) {
     ACN_REQUIRE(N >= 0 && S >= 1 && K >= 1 && K <= kMaxK && aabb_min && aabb_extent,
                 "acn_routed_scatter: bad arguments");
     const int64_t M = N * (int64_t)S;
@@ -269,7 +294,10 @@ extern "C" int acn_routed_scatter(const float* rays, int64_t N, int S, int K, co
     const float* W = (const float*)workspace;
     const int32_t* blk = (const int32_t*)(W + M * K);
     hipLaunchKernelGGL(routed_scatter_kernel, dim3(blocks_for(M, kBlk)), dim3(kBlk), 0, (hipStream_t)stream, rays, N,
-                       S, K, t_vals, W, blk, starts, box, pidx, pw, x01, sh, pmap);
+                       S, K, t_vals, W, blk, starts, box, pidx, pw, x01, sh, pmap, pk);
+    if (align > 1)
+        hipLaunchKernelGGL(routed_pad_kernel, dim3(K), dim3(256), 0, (hipStream_t)stream, starts, K, align, pidx, pw, x01,
+                           sh, pk);
     return acn_check_launch("acn_routed_scatter");
 }
 
@@ -283,12 +311,12 @@ extern "C" int acn_routed_blend_fwd(const float* y, const float* pw, const int32
     return acn_check_launch("acn_routed_blend_fwd");
 }
 
-extern "C" int acn_routed_blend_bwd(const float* g, const int32_t* pidx, const float* pw, int64_t P, float* gy,
-                                    void* stream) {
+extern "C" int acn_routed_blend_bwd(const float* g, const int32_t* pidx, const float* pw, int64_t P,
+                                    const int64_t* live, float* gy, void* stream) {
     ACN_REQUIRE(P >= 0, "acn_routed_blend_bwd: bad arguments");
     if (P == 0) return ACN_OK;
     ACN_REQUIRE(g && pidx && pw && gy, "acn_routed_blend_bwd: NULL pointer");
     hipLaunchKernelGGL(blend_bwd_kernel, dim3(blocks_for(P, 256)), dim3(256), 0, (hipStream_t)stream,
-                       (const float4*)g, pidx, pw, P, (float4*)gy);
+                       (const float4*)g, pidx, pw, P, live, (float4*)gy);
     return acn_check_launch("acn_routed_blend_bwd");
 }

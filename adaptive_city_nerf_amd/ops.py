@@ -511,11 +511,11 @@ def routed_pairs(rays: torch.Tensor, S: int, jitter: Optional[torch.Tensor], rou
     L = _lib.lib()
     ws = torch.empty(int(L.acn_routed_workspace_bytes(M, K)), dtype=torch.uint8, device=dev)
     t = torch.empty(N, int(S), device=dev, dtype=torch.float32)
-    starts = torch.empty(K + 1, device=dev, dtype=torch.int64)
+    starts = torch.empty(2 * K + 1, device=dev, dtype=torch.int64)
     jit = None if jitter is None else _f32(jitter.to(dev))
-    check(L.acn_routed_count(ptr(r), N, int(S), ptr(jit), C.byref(routing), ptr(t), ptr(starts), ptr(ws),
+    check(L.acn_routed_count(ptr(r), N, int(S), ptr(jit), C.byref(routing), 1, ptr(t), ptr(starts), ptr(ws),
                              ws.numel(), stream_of(r)), "acn_routed_count")
-    st = [int(v) for v in starts.cpu().tolist()]
+    st = [int(v) for v in starts[: K + 1].cpu().tolist()]
     P = st[K]
     pidx = torch.empty(P, device=dev, dtype=torch.int32)
     pw = torch.empty(P, device=dev, dtype=torch.float32)
@@ -528,8 +528,8 @@ def routed_pairs(rays: torch.Tensor, S: int, jitter: Optional[torch.Tensor], rou
     lo = np.float32(eps)
     hi = np.float32(1.0) - lo
     check(L.acn_routed_scatter(ptr(r), N, int(S), K, ptr(t), ptr(starts), C.cast(mins, C.c_void_p),
-                               C.cast(exts, C.c_void_p), C.c_float(lo), C.c_float(hi), ptr(ws), ptr(pidx), ptr(pw),
-                               ptr(x01), ptr(sh), ptr(pmap), stream_of(r)), "acn_routed_scatter")
+                               C.cast(exts, C.c_void_p), C.c_float(lo), C.c_float(hi), 1, ptr(ws), ptr(pidx),
+                               ptr(pw), ptr(x01), ptr(sh), ptr(pmap), None, stream_of(r)), "acn_routed_scatter")
     return t, st, pidx, pw, x01, sh, pmap
 
 
@@ -542,9 +542,12 @@ def routed_blend_fwd(y: torch.Tensor, pw: torch.Tensor, pmap: torch.Tensor) -> t
     return out
 
 
-def routed_blend_bwd(g: torch.Tensor, pidx: torch.Tensor, pw: torch.Tensor) -> torch.Tensor:
+def routed_blend_bwd(g: torch.Tensor, pidx: torch.Tensor, pw: torch.Tensor,
+                     live: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dY per pair slot; ``live``: a device int64 holding the live slot count (capacity-sized buffers),
+    slots past it are left unwritten."""
     P = pidx.shape[0]
     gy = torch.empty(P, 4, device=pidx.device, dtype=torch.float32)
-    check(_lib.lib().acn_routed_blend_bwd(ptr(_f32(g)), ptr(pidx), ptr(pw), P, ptr(gy), stream_of(pidx)),
+    check(_lib.lib().acn_routed_blend_bwd(ptr(_f32(g)), ptr(pidx), ptr(pw), P, ptr(live), ptr(gy), stream_of(pidx)),
           "acn_routed_blend_bwd")
     return gy

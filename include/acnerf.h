@@ -260,6 +260,20 @@ int acn_adam_step_table(const acn_param_desc* descs, const int32_t* chunk_tensor
                         int ngroups, int32_t* step_dev, int first_step, int table_steps, const float* grad_scale,
                         void* stream);
 
+/* Slotted form for the routed container (graph-replayable, no host synchronisation): tensor t belongs
+ * to activity slot flags[t] & 0xffff.  Slot s < K (expert s) is active in a step iff its routed pair
+ * count seg[K+1+s] > 0 (acn_routed_count), slots >= K always; an inactive slot is skipped like a
+ * torch parameter whose grad is None (no moment decay, no step increment).  step_dev[nslots]: per-slot
+ * step counters, advanced on the device for the active slots before the update; table: the per-group
+ * constants of steps 1..table_steps (acn_adam_table_fill with first_step 1).  flags bit 16: clear the
+ * gradient after reading it.  The norm skips inactive slots likewise.                             */
+int acn_grad_sumsq_slots(const acn_param_desc* descs, const int32_t* chunk_tensor, int64_t nchunks,
+                         const int32_t* flags, const int64_t* seg, int K, double* partials, double* total,
+                         void* stream);
+int acn_adam_step_slots(const acn_param_desc* descs, const int32_t* chunk_tensor, int64_t nchunks,
+                        const int32_t* flags, const void* table, int ngroups, int table_steps, int32_t* step_dev,
+                        int nslots, const int64_t* seg, int K, const float* grad_scale, void* stream);
+
 /* ---------------------------------------------------------------------------------------- */
 /* Occupancy-grid renderer.  The reference delegates this to nerfacc 0.5.3
  * (third-party, not vendored): OccGridEstimator.sampling -> traverse_grids, render_weight_from_density,
@@ -434,25 +448,55 @@ int acn_voronoi_route(const float* rays, int64_t N, int ray_samples, const float
  * MetaContainer.forward under autograd (models/inr/meta_container.py:97-134 _routing, :300-343
  * nonzero -> index_select -> expert -> index_add_) and the sample front end of
  * render_rays_stratified (nerfs/ray_rendering.py:262-320) for M = N*S samples:
- *   acn_routed_count   -> t_vals (N,S) (jitter (N,S) uniforms or NULL), and starts[K+1] (int64,
- *                         device): expert k's (sample, expert) pairs occupy [starts[k], starts[k+1]).
- *                         workspace: acn_routed_workspace_bytes(M, K) device bytes (kept for scatter).
+ *   acn_routed_count   -> t_vals (N,S) (jitter (N,S) uniforms or NULL), and seg[2K+1] (int64, device):
+ *                         expert k's (sample, expert) pairs occupy [seg[k], seg[k] + seg[K+1+k]) and its
+ *                         segment [seg[k], seg[k+1]) is padded to a multiple of `align` (seg[K] = total
+ *                         slots).  workspace: acn_routed_workspace_bytes(M, K) device bytes (kept for
+ *                         the scatter).
  *   acn_routed_scatter -> per pair: pidx (sample index), pw (routing weight), x01 (3, expert k's unit
  *                         box clamped to [lo, hi], _world_to_unit meta_ngp.py:155-158), sh (16, SH-4 of
- *                         the ray direction, meta_ngp.py:165-168); pmap (M,K) pair index or -1.
+ *                         the ray direction, meta_ngp.py:165-168); pmap (M,K) pair index or -1; pk
+ *                         (optional) the expert of every slot.  Padding slots: pidx -1, pw 0, x01 0.5,
+ *                         sh 0.  Buffers must hold seg[K] slots (M*K + K*align always suffices).
  *                         aabb_min / aabb_extent: HOST (K,3) floats.  Pairs of expert k are in sample
  *                         order (= index_select(nonzero(w[:, k] > 0))).
  *   acn_routed_blend_fwd -> out (M,4) = sum_k y[p_k] * w[p_k] in expert order from zero (index_add_)
- *   acn_routed_blend_bwd -> gy (P,4) = g[pidx] * pw  (backward of the weighted index_add_)          */
+ *   acn_routed_blend_bwd -> gy (P,4) = g[pidx] * pw  (backward of the weighted index_add_; 0 on padding);
+ *                         live (device, nullable): slots at or past *live (e.g. seg + K) are not touched */
 size_t acn_routed_workspace_bytes(int64_t M, int K);
-int acn_routed_count(const float* rays, int64_t N, int S, const float* jitter, const acn_routing* routing,
-                     float* t_vals, int64_t* starts, void* workspace, size_t workspace_bytes, void* stream);
-int acn_routed_scatter(const float* rays, int64_t N, int S, int K, const float* t_vals, const int64_t* starts,
-                       const float* aabb_min, const float* aabb_extent, float lo, float hi, const void* workspace,
-                       int32_t* pidx, float* pw, float* x01, float* sh, int32_t* pmap, void* stream);
+int acn_routed_count(const float* rays, int64_t N, int S, const float* jitter, const acn_routing* routing, int align,
+                     float* t_vals, int64_t* seg, void* workspace, size_t workspace_bytes, void* stream);
+int acn_routed_scatter(const float* rays, int64_t N, int S, int K, const float* t_vals, const int64_t* seg,
+                       const float* aabb_min, const float* aabb_extent, float lo, float hi, int align,
+                       const void* workspace, int32_t* pidx, float* pw, float* x01, float* sh, int32_t* pmap,
+                       int32_t* pk, void* stream);
 int acn_routed_blend_fwd(const float* y, const float* pw, const int32_t* pmap, int64_t M, int K, float* out,
                          void* stream);
-int acn_routed_blend_bwd(const float* g, const int32_t* pidx, const float* pw, int64_t P, float* gy, void* stream);
+int acn_routed_blend_bwd(const float* g, const int32_t* pidx, const float* pw, int64_t P, const int64_t* live,
+                         float* gy, void* stream);
+
+/* Per-expert kernels over routed pair slots (segments padded to multiples of 128, slot count seg[K] on the
+ * device; fixed grids that stride to it, so a whole step is capturable in a hipGraph):
+ *   acn_hashgrid_fwd_pairs : h0 (slots, L*2) of every slot through its expert's table (tables: HOST array
+ *                            of K device pointers); all experts share res[L], log2T, F = 2.
+ *   acn_hashgrid_bwd_pairs : scatter-add of dL/dh0 into every expert's table gradient (grad_tables: HOST
+ *                            array of K device pointers; float atomics); padding slots (pidx < 0) skipped.
+ *   acn_mlp_pack_pairs     : the K experts' MLP images into workspace (acn_mlp_pairs_workspace_bytes(K)).
+ *   acn_mlp_train_fwd_pairs / acn_mlp_train_bwd_dw_pairs : the fused expert MLP forward / backward (as
+ *                            acn_mlp_train_fwd / _bwd_dw) per slot with its expert's weights; dw (K, 13715)
+ *                            per-expert [dW | db] (zeros for an expert without pairs; summed in a fixed
+ *                            order: deterministic), gh0 (slots, 32).                                   */
+int acn_hashgrid_fwd_pairs(const float* x01, const int32_t* pk, const int64_t* seg, int K, const float* const* tables,
+                           const int32_t* res, int L, int log2T, int interp, float* out, void* stream);
+int acn_hashgrid_bwd_pairs(const float* x01, const int32_t* pk, const int32_t* pidx, const int64_t* seg, int K,
+                           const float* grad_out, float* const* grad_tables, const int32_t* res, int L, int log2T,
+                           int interp, void* stream);
+size_t acn_mlp_pairs_workspace_bytes(int K);
+int acn_mlp_pack_pairs(const acn_mlp* const* w, int K, void* workspace, void* stream);
+int acn_mlp_train_fwd_pairs(const float* h0, const float* sh, const int64_t* seg, int K, const void* workspace,
+                            float* out, void* stream);
+int acn_mlp_train_bwd_dw_pairs(const float* h0, const float* sh, const float* out, const float* gout,
+                               const int64_t* seg, int K, void* workspace, float* dw, float* gh0, void* stream);
 
 #ifdef __cplusplus
 }
