@@ -259,7 +259,8 @@ __global__ void __launch_bounds__(kThreads) sumsq_slots_kernel(const acn_param_d
     if (threadIdx.x == 0) partials[blockIdx.x] = tot;
 }
 
-// adam_chunk + clearing the gradient vectors that were non-zero
+// adam_chunk + clearing the gradient vectors that were non-zero (most table rows get no gradient; A/B
+// measured against rewriting every vector: 1.47-1.52 vs 1.52-1.56 ms over 268M parameters)
 __device__ __forceinline__ void adam_chunk_zero(float* p, float* g, float* m, float* v, int64_t n, float scale,
                                                 const GroupK& k) {
     const uintptr_t align = reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) |
