@@ -146,6 +146,9 @@ struct BoxCfg {
     float lo, hi;
 };
 
+// XD = 0: x01 (3, expert k's unit box) + sh (16) per pair; XD = 1: xd (6) = [world point, ray direction] per
+// pair (the record the expert-parallel layouts send to the expert's owner)
+template <int XD>
 __global__ void __launch_bounds__(kBlk) routed_scatter_kernel(const float* __restrict__ rays, int64_t N, int S,
                                                               int K, const float* __restrict__ t_vals,
                                                               const float* __restrict__ W,
@@ -167,7 +170,11 @@ __global__ void __launch_bounds__(kBlk) routed_scatter_kernel(const float* __res
         px = rp[0] + rp[3] * t;
         py = rp[1] + rp[4] * t;
         pz = rp[2] + rp[5] * t;
-        dir_sh(rp[3], rp[4], rp[5], sh);
+        if (XD) {
+            sh[0] = rp[3]; sh[1] = rp[4]; sh[2] = rp[5];
+        } else {
+            dir_sh(rp[3], rp[4], rp[5], sh);
+        }
     }
     const uint64_t below = (1ull << lane) - 1ull;
     for (int k = 0; k < K; ++k) {
@@ -190,6 +197,12 @@ __global__ void __launch_bounds__(kBlk) routed_scatter_kernel(const float* __res
         pidx[pos] = (int32_t)m;
         if (pk) pk[pos] = k;
         pw[pos] = wk;
+        if (XD) {
+            float* o = x01 + pos * 6;
+            o[0] = px; o[1] = py; o[2] = pz;
+            o[3] = sh[0]; o[4] = sh[1]; o[5] = sh[2];
+            continue;
+        }
         x01[pos * 3 + 0] = clamp_nan((px - box.amin[k][0]) / box.ext[k][0], box.lo, box.hi);
         x01[pos * 3 + 1] = clamp_nan((py - box.amin[k][1]) / box.ext[k][1], box.lo, box.hi);
         x01[pos * 3 + 2] = clamp_nan((pz - box.amin[k][2]) / box.ext[k][2], box.lo, box.hi);
@@ -231,6 +244,24 @@ __global__ void __launch_bounds__(256) blend_bwd_kernel(const float4* __restrict
     const float4 v = g[m];
     const float w = pw[p];
     gy[p] = make_float4(v.x * w, v.y * w, v.z * w, v.w * w);
+}
+
+// owner side of the expert-parallel layouts: world point + direction records of ONE expert -> x01 in its
+// unit box and SH-4 of the direction (the same ops as routed_scatter_kernel<0>)
+__global__ void __launch_bounds__(256) xd_unit_sh_kernel(const float* __restrict__ xd, int64_t P, float3 amin, float3 ext,
+                                                         float lo, float hi, float* __restrict__ x01,
+                                                         float* __restrict__ sh_out) {
+    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= P) return;
+    const float* r = xd + p * 6;
+    x01[p * 3 + 0] = clamp_nan((r[0] - amin.x) / ext.x, lo, hi);
+    x01[p * 3 + 1] = clamp_nan((r[1] - amin.y) / ext.y, lo, hi);
+    x01[p * 3 + 2] = clamp_nan((r[2] - amin.z) / ext.z, lo, hi);
+    float sh[16];
+    dir_sh(r[3], r[4], r[5], sh);
+    float4* o4 = reinterpret_cast<float4*>(sh_out + p * 16);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o4[q] = make_float4(sh[4 * q], sh[4 * q + 1], sh[4 * q + 2], sh[4 * q + 3]);
 }
 
 unsigned blocks_for(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
@@ -293,8 +324,8 @@ extern "C" int acn_routed_scatter(const float* rays, int64_t N, int S, int K, co
     box.hi = hi;
     const float* W = (const float*)workspace;
     const int32_t* blk = (const int32_t*)(W + M * K);
-    hipLaunchKernelGGL(routed_scatter_kernel, dim3(blocks_for(M, kBlk)), dim3(kBlk), 0, (hipStream_t)stream, rays, N,
-                       S, K, t_vals, W, blk, starts, box, pidx, pw, x01, sh, pmap, pk);
+    hipLaunchKernelGGL(routed_scatter_kernel<0>, dim3(blocks_for(M, kBlk)), dim3(kBlk), 0, (hipStream_t)stream, rays,
+                       N, S, K, t_vals, W, blk, starts, box, pidx, pw, x01, sh, pmap, pk);
     if (align > 1)
         hipLaunchKernelGGL(routed_pad_kernel, dim3(K), dim3(256), 0, (hipStream_t)stream, starts, K, align, pidx, pw, x01,
                            sh, pk);
@@ -319,4 +350,30 @@ extern "C" int acn_routed_blend_bwd(const float* g, const int32_t* pidx, const f
     hipLaunchKernelGGL(blend_bwd_kernel, dim3(blocks_for(P, 256)), dim3(256), 0, (hipStream_t)stream,
                        (const float4*)g, pidx, pw, P, live, (float4*)gy);
     return acn_check_launch("acn_routed_blend_bwd");
+}
+
+extern "C" int acn_routed_scatter_xd(const float* rays, int64_t N, int S, int K, const float* t_vals, const int64_t* seg,
+                                     const void* workspace, int32_t* pidx, float* pw, float* xd, int32_t* pmap,
+                                     int32_t* pk, void* stream) {
+    ACN_REQUIRE(N >= 0 && S >= 1 && K >= 1 && K <= kMaxK, "acn_routed_scatter_xd: bad arguments");
+    const int64_t M = N * (int64_t)S;
+    if (M == 0) return ACN_OK;
+    ACN_REQUIRE(rays && t_vals && seg && workspace && pidx && pw && xd && pmap, "acn_routed_scatter_xd: NULL pointer");
+    BoxCfg box{};
+    const float* W = (const float*)workspace;
+    const int32_t* blk = (const int32_t*)(W + M * K);
+    hipLaunchKernelGGL(routed_scatter_kernel<1>, dim3(blocks_for(M, kBlk)), dim3(kBlk), 0, (hipStream_t)stream, rays,
+                       N, S, K, t_vals, W, blk, seg, box, pidx, pw, xd, (float*)nullptr, pmap, pk);
+    return acn_check_launch("acn_routed_scatter_xd");
+}
+
+extern "C" int acn_xd_unit_sh(const float* xd, int64_t P, const float* aabb_min, const float* aabb_extent, float lo,
+                              float hi, float* x01, float* sh, void* stream) {
+    ACN_REQUIRE(P >= 0 && aabb_min && aabb_extent, "acn_xd_unit_sh: bad arguments");
+    if (P == 0) return ACN_OK;
+    ACN_REQUIRE(xd && x01 && sh, "acn_xd_unit_sh: NULL pointer");
+    hipLaunchKernelGGL(xd_unit_sh_kernel, dim3(blocks_for(P, 256)), dim3(256), 0, (hipStream_t)stream, xd, P,
+                       make_float3(aabb_min[0], aabb_min[1], aabb_min[2]),
+                       make_float3(aabb_extent[0], aabb_extent[1], aabb_extent[2]), lo, hi, x01, sh);
+    return acn_check_launch("acn_xd_unit_sh");
 }

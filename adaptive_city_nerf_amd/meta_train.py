@@ -20,9 +20,11 @@ Differences from the reference, all where the reference cannot run as written (D
   (meta_train_step.py:168), so Reptile raises TypeError there; and ``reptile_meta_update`` compares
   the expert-relative fast names with the container's meta-parameter names, so it never updates.
   Here train_step collects the adapted fast weights and prefixes them with ``submodules.{cid}.``.
-* Expert parallelism (``group``): rank r processes the regions cid with cid % world == r; the
-  region/query counts, the shared background-head gradients and the clip norm are all-reduced, so
-  the update equals the single-process one (SURVEY §8(e) "Offline meta-training").
+* Expert parallelism (``group``): rank r processes the regions whose expert it owns
+  (expert_parallel.expert_owner: contiguous blocks of experts per rank, the same placement as the
+  expert-parallel render / adaptation); the region/query counts, the shared background-head
+  gradients and the clip norm are all-reduced, so the update equals the single-process one
+  (SURVEY §8(e) "Offline meta-training").
 """
 from __future__ import annotations
 
@@ -34,6 +36,7 @@ from typing import Dict, List, Mapping, Optional
 import torch
 import torch.distributed as dist
 
+from .expert_parallel import expert_owner, global_clip_grad_norm_
 from .optim import FusedAdam
 from .ray_rendering import second_order
 from .train import compute_mse_loss
@@ -107,11 +110,17 @@ def task_adapt(P, model, support, inner_lr, iterations, active_module=None):
 
 
 # ============================================================================ outer update
-def clip_all_grads(optimizer, grad_clip=1.0):
+def clip_all_grads(optimizer, grad_clip=1.0, group=None, shared=None):
+    """clip_grad_norm_ over every gradient-carrying parameter (meta_core.py:185-194); with an
+    expert-parallel ``group`` the norm is global (own experts all-reduced, ``shared`` counted once)."""
     if grad_clip is None:
         return
-    params = [p for group in optimizer.param_groups for p in group["params"] if p.grad is not None]
-    if params:
+    params = [p for g in optimizer.param_groups for p in g["params"] if p.grad is not None]
+    if not params:
+        return
+    if group is not None and dist.is_initialized() and dist.get_world_size(group) > 1:
+        global_clip_grad_norm_(params, shared or [], grad_clip, group)
+    else:
         torch.nn.utils.clip_grad_norm_(params, grad_clip)
 
 
@@ -126,7 +135,7 @@ def maml_meta_update(optimizer, loss_out, scaler=None, grad_clip=1.0, group=None
         scaler.scale(loss_out).backward()
         scaler.unscale_(optimizer)
         _allreduce_shared_grads(shared, group)
-        clip_all_grads(optimizer, grad_clip)
+        clip_all_grads(optimizer, grad_clip, group, shared)
         scaler.step(optimizer)
         scaler.update()
         return
@@ -137,7 +146,7 @@ def maml_meta_update(optimizer, loss_out, scaler=None, grad_clip=1.0, group=None
             optimizer.shared_params = {id(p) for p in shared}
         optimizer.step(max_norm=grad_clip, sumsq_group=group)
     else:
-        clip_all_grads(optimizer, grad_clip)
+        clip_all_grads(optimizer, grad_clip, group, shared)
         optimizer.step()
 
 
@@ -207,12 +216,13 @@ def _allreduce_shared_grads(shared, group):
 @torch.no_grad()
 def broadcast_experts(model, group=None):
     """Expert parallelism: copy every expert's parameters and buffers from its owner rank
-    (cid % world) to all ranks (e.g. before evaluation or a checkpoint)."""
+    (expert_owner) to all ranks (e.g. before evaluation or a checkpoint)."""
     if not dist.is_initialized() or dist.get_world_size(group) <= 1:
         return
     world = dist.get_world_size(group)
+    owner = expert_owner(len(model.submodules), world)
     for cid, expert in enumerate(model.submodules):
-        src = dist.get_global_rank(group, cid % world) if group is not None else cid % world
+        src = dist.get_global_rank(group, owner[cid]) if group is not None else owner[cid]
         for t in list(expert.parameters()) + list(expert.buffers()):
             dist.broadcast(t.data, src=src, group=group)
 
@@ -237,7 +247,8 @@ def train_step(P, step, model, optimizer, task_data, metric_logger=None, logger=
     world, rank = 1, 0
     if group is not None and dist.is_initialized():
         world, rank = dist.get_world_size(group), dist.get_rank(group)
-    mine = [cid for cid in cids if cid % world == rank]
+    owner = expert_owner(len(model.submodules), world) if hasattr(model, "submodules") else [0] * (max(cids) + 1)
+    mine = [cid for cid in cids if owner[cid] == rank]
     region_inner_sum = {cid: torch.tensor(0.0, device=device) for cid in cids}
     region_inner_count = {cid: 0 for cid in cids}
     region_query_sum = {cid: torch.tensor(0.0, device=device) for cid in cids}

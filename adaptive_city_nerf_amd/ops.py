@@ -178,6 +178,11 @@ class PackCache:
         return self.ws
 
 
+# Optional timing hook (bench.py): when set to a list, render_stratified / field_fwd append a pair of
+# recorded HIP events bracketing exactly the fused kernel on the launch stream.
+EVENT_HOOK = None
+
+
 def field_fwd(x: torch.Tensor, experts: Sequence[ExpertSpec], routing: acn_routing,
               active_module: Optional[int] = None, packed: Optional[torch.Tensor] = None) -> torch.Tensor:
     require_hip(x, "MetaContainer.forward")
@@ -189,15 +194,20 @@ def field_fwd(x: torch.Tensor, experts: Sequence[ExpertSpec], routing: acn_routi
         return out
     ws = packed if packed is not None else pack_experts(experts, routing, active_module)
     arr = _experts_array(experts)
+    hook = EVENT_HOOK
+    if hook is not None:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record()
     check(_lib.lib().acn_field_fwd(ptr(xx), M, xx.shape[1], arr, C.byref(routing),
                                    -1 if active_module is None else int(active_module), ptr(ws),
                                    ws.numel() * 4, ptr(out), stream_of(xx)), "acn_field_fwd")
+    if hook is not None:
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        hook.append((e0, e1))
     return out
 
 
-# Optional timing hook (bench.py): when set to a list, render_stratified appends a pair of
-# recorded HIP events bracketing exactly the fused render kernel on the launch stream.
-EVENT_HOOK = None
 
 # Default of render_stratified(reorder=None): direction-sorted visiting order for small batches
 # (acn_render_stratified_fwd_ordered; outputs are identical either way, only the speed changes).
@@ -551,3 +561,49 @@ def routed_blend_bwd(g: torch.Tensor, pidx: torch.Tensor, pw: torch.Tensor,
     check(_lib.lib().acn_routed_blend_bwd(ptr(_f32(g)), ptr(pidx), ptr(pw), P, ptr(live), ptr(gy), stream_of(pidx)),
           "acn_routed_blend_bwd")
     return gy
+
+
+def routed_pairs_xd(rays: torch.Tensor, S: int, jitter: Optional[torch.Tensor], routing: acn_routing):
+    """t_vals (N,S) and the routed pairs as expert-parallel records: (t_vals, counts (K host ints), pidx, pw,
+    xd (P,6) world point + direction, pmap (M,K), pk (P,)); pairs grouped by expert, in sample order."""
+    require_hip(rays, "expert-parallel render")
+    r = _f32(rays)
+    N = r.shape[0]
+    M = N * int(S)
+    K = int(routing.K)
+    dev = r.device
+    L = _lib.lib()
+    ws = torch.empty(int(L.acn_routed_workspace_bytes(M, K)), dtype=torch.uint8, device=dev)
+    t = torch.empty(N, int(S), device=dev, dtype=torch.float32)
+    seg = torch.empty(2 * K + 1, device=dev, dtype=torch.int64)
+    jit = None if jitter is None else _f32(jitter.to(dev))
+    check(L.acn_routed_count(ptr(r), N, int(S), ptr(jit), C.byref(routing), 1, ptr(t), ptr(seg), ptr(ws),
+                             ws.numel(), stream_of(r)), "acn_routed_count")
+    sh = [int(v) for v in seg.cpu().tolist()]
+    counts = sh[K + 1:]
+    P = sh[K]
+    pidx = torch.empty(P, device=dev, dtype=torch.int32)
+    pw = torch.empty(P, device=dev, dtype=torch.float32)
+    xd = torch.empty(P, 6, device=dev, dtype=torch.float32)
+    pk = torch.empty(P, device=dev, dtype=torch.int32)
+    pmap = torch.empty(M, K, device=dev, dtype=torch.int32)
+    check(L.acn_routed_scatter_xd(ptr(r), N, int(S), K, ptr(t), ptr(seg), ptr(ws), ptr(pidx), ptr(pw), ptr(xd),
+                                  ptr(pmap), ptr(pk), stream_of(r)), "acn_routed_scatter_xd")
+    return t, counts, pidx, pw, xd, pmap, pk
+
+
+def xd_unit_sh(xd: torch.Tensor, aabb_min, aabb_extent, eps: float):
+    """Owner side: (P,6) records -> x01 (P,3) in the expert's unit box and SH-4 (P,16) of the direction."""
+    require_hip(xd, "expert-parallel expert")
+    x = _f32(xd)
+    P = x.shape[0]
+    x01 = torch.empty(P, 3, device=x.device, dtype=torch.float32)
+    sh = torch.empty(P, 16, device=x.device, dtype=torch.float32)
+    mn = (C.c_float * 3)(*aabb_min)
+    ex = (C.c_float * 3)(*aabb_extent)
+    import numpy as np
+    lo = np.float32(eps)
+    hi = np.float32(1.0) - lo
+    check(_lib.lib().acn_xd_unit_sh(ptr(x), P, C.cast(mn, C.c_void_p), C.cast(ex, C.c_void_p), C.c_float(lo),
+                                    C.c_float(hi), ptr(x01), ptr(sh), stream_of(x)), "acn_xd_unit_sh")
+    return x01, sh

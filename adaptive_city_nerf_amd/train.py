@@ -7,9 +7,13 @@ backward is a HIP scatter-add kernel) -> ``clip_grad_norm_`` + Adam as one fused
 step (optim.FusedAdam).  The reference wraps the forward in fp16 autocast with a GradScaler; this
 build computes in fp32 (SURVEY §8(b) "Autocast / dtype"), so the scaler is the identity.
 
-Expert-parallel use: with ``active_module=k`` the step touches only expert k
-(the reference adapts ``model.submodules[active_module]``, whose render has no background head),
-so rank k can adapt expert k with no collective at all.
+Expert-parallel use: ``adapt_step(..., group=)`` on the routed container
+(active_module None, the online stage's call, runtime_adapt.py:88-90) distributes the experts over the
+ranks of ``group`` (expert_parallel.py: all-to-all of per-sample records, complete per-expert
+gradients on the owners, all-reduced background head, global clip norm): the update equals the
+single-process one.  ``active_module=k`` adapts one expert with the container's background head; the
+reference's own runtime_adapt cannot run that configuration (it renders ``base.submodules`` of the
+expert itself), so it stays a single-process placement variant and refuses a group.
 """
 from __future__ import annotations
 
@@ -37,29 +41,25 @@ def adapt_step(P, base, rays, rgbs, optimizer, active_module=None, grad_clip: Op
                group=None, shared: Optional[list] = None, **render_kwargs) -> torch.Tensor:
     """One optimizer update of runtime_adapt (runtime_adapt.py:288-313).  Returns the loss (device).
 
-    Expert parallel (``group``): rank k renders through ``active_module=k``; the gradients of the
-    ``shared`` parameters (the background head every rank renders with) are averaged over the
-    group (one small RCCL all-reduce) and the clip norm is the global one (an all-reduce of one
-    double), so the shared replicas stay bit-identical and every expert sees the clip coefficient a
-    single process adapting all of them would apply."""
+    ``group`` (expert parallel): ``rays`` / ``rgbs`` are this rank's shard of the global batch, the
+    container's experts are distributed over the group (expert_parallel.adapt_step_expert_parallel);
+    ``shared`` are the replicated parameters (default: the background head)."""
+    if group is not None and torch.distributed.is_initialized() and torch.distributed.get_world_size(group) > 1:
+        from .expert_parallel import HipBackend, adapt_step_expert_parallel
+        if active_module is not None:
+            raise ValueError("adapt_step: expert-parallel groups adapt the routed container (active_module=None)")
+        n = torch.tensor([rays.shape[0]], dtype=torch.int64, device=rays.device)
+        torch.distributed.all_reduce(n, group=group)
+        shared = list(base.bg_mlp.parameters()) if shared is None else shared
+        return adapt_step_expert_parallel(P, HipBackend(base), rays, rgbs, optimizer, len(base.submodules), int(n),
+                                          shared, grad_clip=grad_clip, group=group,
+                                          u=render_kwargs.get("jitter_u"))
     optimizer.zero_grad()
     loss = compute_mse_loss(P, model=base, data={"rays": rays, "rgbs": rgbs}, params=None,
                             active_module=active_module, reduction="mean", **render_kwargs)
     loss.backward()
-    if group is not None and torch.distributed.is_initialized() and torch.distributed.get_world_size(group) > 1:
-        grads = [p.grad for p in (shared or []) if p.grad is not None]
-        if grads:
-            flat = torch.cat([g.reshape(-1) for g in grads])
-            torch.distributed.all_reduce(flat, group=group)
-            flat.div_(torch.distributed.get_world_size(group))
-            off = 0
-            for g in grads:
-                g.copy_(flat[off: off + g.numel()].view_as(g))
-                off += g.numel()
     if isinstance(optimizer, FusedAdam):
-        if shared:
-            optimizer.shared_params = {id(p) for p in shared}
-        optimizer.step(max_norm=grad_clip, sumsq_group=group)  # clip_grad_norm_ folded into the fused step
+        optimizer.step(max_norm=grad_clip)  # clip_grad_norm_ folded into the fused step
     else:
         if grad_clip is not None:
             torch.nn.utils.clip_grad_norm_(base.parameters(), grad_clip)

@@ -20,10 +20,13 @@ Other BASELINE configs (``--workload``):
   c4  4x2 grid -> 8 experts (synthetic layout, synthetic.grid_layout), one 800x800 frame x 256
       samples: rays generated on device, sharded by expert, rendered, all-gathered, PSNR
       all-reduced (parallel.render_image_sharded) -- strong scaling.
-  c5  online adaptation (runtime_adapt.py:288-313): 8-expert container, rank r adapts expert r
-      (active_module) on batches of 1000 rays x 96 samples: training render -> MSE -> backward ->
-      clip_grad_norm_ + Adam (one fused HIP step); shared background-head gradients and the clip
-      norm all-reduced over RCCL (weak).  metric value = trained ray-samples/s (fwd+bwd+update).
+  c5  online adaptation (runtime_adapt.py:286-309): the routed 8-expert container (no active_module)
+      on batches of 1000 rays x 96 samples from a 249-camera stream: training render -> MSE ->
+      backward -> clip_grad_norm_ + Adam over every expert hit.  1 GPU: routed_train.RoutedAdaptStep
+      replayed as one HIP graph; N GPUs: experts distributed (expert_parallel.py, all-to-all of
+      per-sample records), each rank streaming its own batches (weak).  metric value = trained
+      ray-samples/s (fwd+bwd+update); also the val PSNR before / after the adaptation.
+  c5a placement variant: rank r adapts expert r alone (active_module), no collective.
 
 Also reported: roofline of the fused render kernel (HIP events bracketing exactly that launch on
 its stream), and on rank 0 at N=1 a CPU baseline: the C oracle (oracle/, a fixture-pinned port of
@@ -341,6 +344,9 @@ def main():
     ap.add_argument("--rays", type=int, default=4096, help="rays per GPU (c2, c3)")
     ap.add_argument("--samples", type=int, default=256)
     ap.add_argument("--frame", type=int, default=800, help="frame side (c4)")
+    ap.add_argument("--layout", choices=["replicated", "expert"], default="replicated",
+                    help="c4: experts replicated + rays sharded by owning expert (all-gather of rendered rays), or "
+                         "one expert per GPU (all-to-all of per-sample records, expert_parallel.py)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-rays", type=int, default=4096, help="rays in the CPU-baseline / PSNR sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -455,7 +461,8 @@ def main():
         model.train()
         opt = aoptim.build_optimizer(P, model)
         pg = dist.group.WORLD if world > 1 else None
-        my_regions = [c for c in range(4) if c % world == rank]
+        from adaptive_city_nerf_amd.expert_parallel import expert_owner
+        my_regions = [c for c in range(4) if expert_owner(4, world)[c] == rank]
         samples_per_step = sum(len(task_data[c]) * (P.inner_iter * nsup + nqry) for c in range(4)) * S
         it = [0]
 
@@ -559,16 +566,19 @@ def main():
         graphed = None
         expert = None
         routed = None
-        if not a.no_graph:  # the whole routed step (no host sync) replayed as one HIP graph
+        pg = dist.group.WORLD if world > 1 else None
+        if world == 1 and not a.no_graph:  # the whole routed step (no host sync) replayed as one HIP graph
             from adaptive_city_nerf_amd.routed_train import RoutedAdaptStep
             routed = RoutedAdaptStep(P, model, bsz, opt, grad_clip=1.0, graph=True, warmup=2)
 
         def step():
+            # N > 1: the experts distributed over the ranks (expert_parallel.py), every rank streaming
+            # its own 1000-ray batches of the global batch
             i = it[0] % nb
             it[0] += 1
             if routed is not None:
                 return routed(pool[i], gtp[i])
-            return adapt_step(P, model, pool[i], gtp[i], opt, grad_clip=1.0)
+            return adapt_step(P, model, pool[i], gtp[i], opt, grad_clip=1.0, group=pg)
         sample_rays = pool[0]
         aoptim.EVENT_HOOK = []
     elif a.workload == "c5a":
@@ -590,7 +600,7 @@ def main():
         it = [0]
 
         graphed = None
-        if world == 1 and not a.no_graph:  # the launch-bound step replayed as one HIP graph
+        if not a.no_graph:  # the launch-bound step replayed as one HIP graph (no collective in this variant)
             from adaptive_city_nerf_amd.train import GraphedAdaptStep
             graphed = GraphedAdaptStep(P, model, pool[0], gtp[0], opt, active_module=expert, grad_clip=1.0,
                                        warmup=2)
@@ -600,8 +610,7 @@ def main():
             it[0] += 1
             if graphed is not None:
                 return graphed(pool[i], gtp[i])
-            return adapt_step(P, model, pool[i], gtp[i], opt, active_module=expert, grad_clip=1.0, group=pg,
-                              shared=shared)
+            return adapt_step(P, model, pool[i], gtp[i], opt, active_module=expert, grad_clip=1.0)
         sample_rays = pool[0]
         aoptim.EVENT_HOOK = []
     else:
@@ -611,6 +620,11 @@ def main():
 
         def step():
             with torch.no_grad():
+                if a.layout == "expert":
+                    from adaptive_city_nerf_amd.expert_parallel import render_image_expert_parallel
+                    return render_image_expert_parallel(model, H=H, W=W, fx=intr[0], fy=intr[1], cx=intr[2],
+                                                        cy=intr[3], c2w=c2w, scene_box=gbox, ray_samples=S,
+                                                        gt_srgb=gt, group=dist.group.WORLD if world > 1 else None)
                 return parallel.render_image_sharded(model, H=H, W=W, fx=intr[0], fy=intr[1], cx=intr[2], cy=intr[3],
                                                      c2w=c2w, scene_box=gbox, ray_samples=S, gt_srgb=gt)
         frays, fvalid = ops.get_rays_image(H, W, *intr, c2w, gbox.aabb, device, near_far_override=(None, None))
@@ -713,7 +727,9 @@ def main():
              "c2": "ray_order_kernel + render_kernel<1,1,0> (one acn_render_stratified_fwd_ordered call: direction "
                    "grouping of the batch, then the fused stratified render, 1 expert; events bracket both)",
              "c3": "render_kernel<1,0,1> (fused stratified render, soft routing over 4 experts)",
-             "c4": "render_kernel<1,0,1> (fused stratified render, soft routing over 8 experts)",
+             "c4": ("field_kernel (fused MFMA field of the owned expert over the received per-sample records)"
+                    if a.layout == "expert" else
+                    "render_slots_kernel (fused stratified render, soft routing over 8 experts, two staged per round)"),
              "occ": "occ_render_kernel<1,1,0> (fused occupancy render over packed marched samples, 1 expert)",
              "meta": "adam_kernel (fused clip + Adam of the outer meta-update over the region experts + shared head)",
              "data": "route_kernel (TaskDataset region clip + DDA max-overlap micro-cell routing + keep tolerance)",
@@ -779,15 +795,19 @@ def main():
                                   "per GPU sharded by owning expert, RCCL all-gather of rendered rays",
                       "rays_per_gpu": a.rays, "experts": 4},
                "c4": {"workload": f"C4: 4x2 grid -> 8 experts (synthetic layout), {a.frame}x{a.frame} frame x "
-                                  f"{S} samples, expert-sharded, RCCL all-gather + PSNR all-reduce",
+                                  f"{S} samples, " + ("experts distributed one per GPU: all-to-all of per-sample "
+                                                      "records + RCCL all-gather + PSNR all-reduce"
+                                                      if a.layout == "expert" else
+                                                      "experts replicated, rays sharded by owning expert, RCCL "
+                                                      "all-gather + PSNR all-reduce"), "layout": a.layout,
                       "frame": [a.frame, a.frame], "experts": 8},
                "c5": {"workload": f"C5: online adaptation (runtime_adapt), the routed 8-expert container (soft routing, "
                                   f"no active_module) on 1000-ray x {S}-sample batches from a 249-camera stream: "
                                   f"train render + MSE + backward + fused clip/Adam over every expert hit",
                       "rays_per_step_per_gpu": 1000, "experts": 8},
-               "c5a": {"workload": f"C5a (placement variant): 8-expert container, rank r adapts expert r on 1000-ray x "
-                                  f"{S}-sample batches (train render + MSE + backward + fused clip/Adam), shared "
-                                  f"background grads + clip norm all-reduced; 1 GPU: the step replayed as one HIP graph"
+               "c5a": {"workload": f"C5a (placement variant, not a reference configuration): rank r adapts expert r "
+                                  f"alone (active_module) on its own 1000-ray x {S}-sample batches, no collective "
+                                  f"(train render + MSE + backward + fused clip/Adam); the step replayed as one HIP graph"
                                   f"{' (disabled)' if a.no_graph else ''}", "rays_per_step_per_gpu": 1000,
                       "experts": 8},
                "occ": {"workload": f"occupancy renderer (render_expert_occ): {a.rays} rays per GPU marched through a "

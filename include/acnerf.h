@@ -475,6 +475,18 @@ int acn_routed_blend_fwd(const float* y, const float* pw, const int32_t* pmap, i
 int acn_routed_blend_bwd(const float* g, const int32_t* pidx, const float* pw, int64_t P, const int64_t* live,
                          float* gy, void* stream);
 
+/* Expert-parallel records (parallel.py, SURVEY §8(e) "one expert per GPU"):
+ *   acn_routed_scatter_xd -> the pairs of acn_routed_count (align 1) as xd (P,6) = [world point o + d t,
+ *                            ray direction], with pidx / pw / pmap / pk as acn_routed_scatter: the 24-B
+ *                            record sent to the GPU owning the pair's expert.
+ *   acn_xd_unit_sh        -> owner side: x01 (P,3) in the expert's unit box (HOST aabb_min / extent,
+ *                            clamped to [lo, hi]) and SH-4 (P,16) of the direction, as acn_routed_scatter. */
+int acn_routed_scatter_xd(const float* rays, int64_t N, int S, int K, const float* t_vals, const int64_t* seg,
+                          const void* workspace, int32_t* pidx, float* pw, float* xd, int32_t* pmap, int32_t* pk,
+                          void* stream);
+int acn_xd_unit_sh(const float* xd, int64_t P, const float* aabb_min, const float* aabb_extent, float lo, float hi,
+                   float* x01, float* sh, void* stream);
+
 /* Per-expert kernels over routed pair slots (segments padded to multiples of 128, slot count seg[K] on the
  * device; fixed grids that stride to it, so a whole step is capturable in a hipGraph):
  *   acn_hashgrid_fwd_pairs : h0 (slots, L*2) of every slot through its expert's table (tables: HOST array

@@ -1,0 +1,224 @@
+"""One expert per GPU (adaptive_city_nerf_amd/expert_parallel.py): the all-to-all of
+per-sample records to the experts' owners and back, for rendering and for the runtime_adapt update of
+the routed 8-expert container (BASELINE C5).
+
+CPU: world size 2 over gloo; every rank holds a contiguous shard of the reference fixture's rays and
+owns 4 of the 8 experts.  The compute is the CPU restatement (oracle/train_ref.py, pinned to the
+reference's own train_k8 fixture) behind the backend interface, so what is checked here is the data
+movement: the distributed render equals the single-process render and the distributed update equals
+the reference's update (loss, clip norm, owned experts' gradients and parameters, the all-reduced
+background head).  GPU: the HIP backend at world size 1 (the same code path, exchanges as copies)
+against the fused render and the fixture.
+"""
+import os
+import socket
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import goldens as G
+from adaptive_city_nerf_amd.expert_parallel import (PairSet, adapt_step_expert_parallel, expert_owner,
+                                                    render_rays_expert_parallel)
+from oracle import oracle as O
+from oracle import train_ref as TR
+
+S = 96
+LRS = {"encoding": 0.01, "sigma": 0.002, "color": 0.002, "background": 0.001}
+P = SimpleNamespace(ray_samples=S, color_space="linear")
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def ref_container(d):
+    sc = G.scene()["masks"][G.MASK["k8"]]
+    K = len(sc["centroids"])
+    state = {k[2:]: torch.from_numpy(v.copy()) for k, v in d.items() if k.startswith("w:")}
+    for k in range(K):
+        state[f"submodules.{k}.xyz_encoder.hash_table"] = torch.from_numpy(
+            G.table(int(d["table_seeds"][k]), float(d["table_scale"])).copy())
+    exts = [d[f"w:submodules.{k}.aabb_extent"] for k in range(K)]
+    return TR.RefContainer(state, K, O.level_resolutions(16, 16, 4096), 20, sc["centroids"], float(d["bm"]), sc["mins"],
+                           exts)
+
+
+class RefBackend:
+    """The backend interface on the CPU restatement (torch CPU autograd)."""
+
+    def __init__(self, m):
+        self.m = m
+
+    def pairs(self, rays, S, u):
+        o, dd = rays[:, :3], rays[:, 3:6]
+        near, far = rays[:, 6], rays[:, 7]
+        t_lin = torch.linspace(0.0, 1.0, S).unsqueeze(0)
+        t = near.unsqueeze(1) * (1.0 - t_lin) + far.unsqueeze(1) * t_lin
+        mids = 0.5 * (t[:, :-1] + t[:, 1:])
+        t = torch.cat([t[:, :1], mids], 1) + (torch.cat([mids, t[:, -1:]], 1) - torch.cat([t[:, :1], mids], 1)) * u
+        pts = (o.unsqueeze(1) + dd.unsqueeze(1) * t.unsqueeze(-1)).reshape(-1, 3)
+        dirs = dd.unsqueeze(1).expand(-1, S, -1).reshape(-1, 3)
+        x = torch.cat([pts, dirs], 1)
+        with torch.no_grad():
+            dist_ = torch.cdist(x[:, 1:3], self.m.cent[:, 1:3]).clamp_min(1e-6)
+            invd = (1.0 / dist_) * (dist_ <= self.m.bm * dist_.min(1, keepdim=True).values)
+            w = invd / invd.sum(1, keepdim=True).clamp_min(1e-6)
+        K = self.m.K
+        pmap = torch.full((x.shape[0], K), -1, dtype=torch.int64)
+        pidx, pw, pk, counts, off = [], [], [], [], 0
+        for k in range(K):
+            sel = (w[:, k] > 0).nonzero(as_tuple=False).squeeze(1)
+            pidx.append(sel); pw.append(w[sel, k]); pk.append(torch.full_like(sel, k)); counts.append(sel.numel())
+            pmap[sel, k] = torch.arange(off, off + sel.numel())
+            off += sel.numel()
+        pidx = torch.cat(pidx)
+        return PairSet(t, counts, pidx, torch.cat(pw), x[pidx], pmap, torch.cat(pk))
+
+    def expert(self, k, xd):
+        return self.m.expert(k, xd)
+
+    def blend(self, y, ps):
+        out = y.new_zeros(ps.pmap.shape[0], 4)
+        off = 0
+        for c in ps.counts:
+            sl = slice(off, off + c)
+            if c:
+                out = out.index_add(0, ps.pidx[sl], y[sl] * ps.pw[sl].unsqueeze(1))
+            off += c
+        return out
+
+    def composite(self, rs, t, rays):
+        rgb = rs[..., :3].clamp(0.0, 1.0)
+        sigma = rs[..., 3].clamp_min(0.0)
+        dists = (t[:, 1:] - t[:, :-1]).clamp_min(1e-4)
+        dists = torch.cat([dists, dists[:, -1:]], 1)
+        alpha = (1.0 - torch.exp(-sigma * dists)).clamp(0.0, 1.0 - 1e-7)
+        T = torch.cumprod(torch.cat([torch.ones_like(alpha[:, :1]), 1.0 - alpha + 1e-10], 1), 1)[:, :-1]
+        w = alpha * T
+        acc = w.sum(1)
+        bg = self.m.background(rays[:, 3:6])
+        return (w.unsqueeze(-1) * rgb).sum(1) + (1.0 - acc.unsqueeze(-1)) * bg, (w * t).sum(1), w, acc
+
+
+def test_owner_blocks():
+    assert expert_owner(8, 8) == list(range(8))
+    assert expert_owner(8, 2) == [0, 0, 0, 0, 1, 1, 1, 1]
+    assert expert_owner(8, 1) == [0] * 8
+    assert expert_owner(4, 3) == [0, 0, 1, 2]
+    for K, W in ((8, 3), (5, 4), (16, 8)):
+        o = expert_owner(K, W)
+        assert o == sorted(o) and set(o) <= set(range(W))
+
+
+def _shard(n, world, rank):
+    lo, hi = n * rank // world, n * (rank + 1) // world
+    return slice(lo, hi)
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.set_num_threads(2)
+        d = G.load("train_k8")
+        m = ref_container(d)
+        be = RefBackend(m)
+        rays = torch.from_numpy(d["train0:rays"])
+        rgbs = torch.from_numpy(d["train0:rgbs"])
+        u = torch.from_numpy(d["train0:u"])
+        sl = _shard(rays.shape[0], world, rank)
+        with torch.no_grad():
+            rgb, depth, w, acc = render_rays_expert_parallel(be, rays[sl], S, m.K, u=u[sl])
+        opt = torch.optim.Adam(m.param_groups(LRS), lr=1e-4)
+        shared = [m.p[f"bg_mlp.{i}.{n}"] for i in (0, 2) for n in ("weight", "bias")]
+        loss = adapt_step_expert_parallel(P, be, rays[sl], rgbs[sl], opt, m.K, rays.shape[0], shared, grad_clip=1.0,
+                                          u=u[sl])
+        owner = expert_owner(m.K, world)
+        res = {"rgb": rgb.numpy(), "loss": float(loss), "norm": opt.last_norm[0],
+               "params": {n: p.detach().numpy().copy() for n, p in m.p.items()
+                          if n.startswith("bg_mlp") or (n.startswith("submodules.") and not n.endswith("hash_table")
+                                                        and owner[int(n.split(".")[1])] == rank)},
+               "grads": {n: p.grad.numpy().copy() for n, p in m.p.items()
+                         if p.grad is not None and not n.endswith("hash_table")},
+               "table_rows": {k: m.p[f"submodules.{k}.xyz_encoder.hash_table"].detach()[
+                   torch.from_numpy(d["train:rows"][k])].numpy() for k in range(m.K) if owner[k] == rank}}
+        out[rank] = res
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_expert_parallel_world2_matches_reference_step():
+    d = G.load("train_k8")
+    world = 2
+    with mp.Manager() as man:
+        out = man.dict()
+        mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+        res = dict(out)
+    # render: the shards concatenated equal the single-process restatement of the same rays
+    m = ref_container(d)
+    with torch.no_grad():
+        ref_rgb = TR.render_train(m, torch.from_numpy(d["train0:rays"]), S, torch.from_numpy(d["train0:u"]))
+    np.testing.assert_allclose(np.concatenate([res[r]["rgb"] for r in range(world)]), ref_rgb.numpy(), rtol=0, atol=1e-6)
+    # the update: the reference's own step (train_k8.npz step 0)
+    for r in range(world):
+        assert abs(res[r]["loss"] - float(d["train0:loss"])) <= 1e-6 * float(d["train0:loss"])
+        assert abs(res[r]["norm"] - float(d["train0:total_norm"])) <= 1e-5 * float(d["train0:total_norm"])
+    owner = expert_owner(8, world)
+    for k in range(8):
+        r = owner[k]
+        for name, v in res[r]["grads"].items():
+            if name.startswith(f"submodules.{k}."):
+                ref = d["train0:grad:" + name]
+                np.testing.assert_allclose(v, ref, rtol=0, atol=1e-5 * (np.abs(ref).max() + 1e-12))
+        if f"train0:grad_rows:{k}" in d:
+            np.testing.assert_allclose(res[r]["table_rows"][k], d[f"train0:table_rows:{k}"], rtol=0, atol=1e-7)
+        for name, v in res[r]["params"].items():
+            if name.startswith(f"submodules.{k}.") and ("train0:param:" + name) in d:
+                np.testing.assert_allclose(v, d["train0:param:" + name], rtol=0, atol=5e-7)
+    for r in range(world):   # the replicated background head: identical update on both ranks
+        for name, v in res[r]["params"].items():
+            if name.startswith("bg_mlp") and ("train0:param:" + name) in d:
+                np.testing.assert_allclose(v, d["train0:param:" + name], rtol=0, atol=5e-7)
+                np.testing.assert_array_equal(v, res[0]["params"][name])
+
+
+# ------------------------------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["render", "render_hi"])
+def test_hip_backend_render_equals_fused(variant):
+    """World size 1: the expert-parallel render (pairs as records, per-expert fused field, blend, HIP
+    compositing) equals the reference fixture and the fused single-launch render."""
+    from adaptive_city_nerf_amd import render_rays
+    from adaptive_city_nerf_amd.expert_parallel import HipBackend
+    from test_k8 import _model
+    d = G.load("render_k8")
+    m, _ = _model(d, "hiw:" if variant == "render_hi" else "w:")
+    rays = torch.from_numpy(d["render:rays"]).cuda()
+    with torch.no_grad():
+        rgb, depth, w, acc = render_rays_expert_parallel(HipBackend(m), rays, 64, len(m.submodules))
+        frgb, fdepth, fw, facc = render_rays(m, rays, ray_samples=64)
+    assert np.abs(rgb.cpu().numpy() - d[f"{variant}:rgb"]).max() <= 1e-4
+    assert np.abs(w.cpu().numpy() - d[f"{variant}:weights"]).max() <= 1e-5
+    torch.testing.assert_close(rgb, frgb, rtol=0, atol=2e-6)
+    torch.testing.assert_close(acc, facc, rtol=0, atol=2e-6)
+
+
+@pytest.mark.gpu
+def test_hip_backend_adapt_step_matches_reference_fixture():
+    """World size 1: adapt_step_expert_parallel on the HIP backend replays the reference's K=8
+    runtime_adapt steps (same checks as the single-process step)."""
+    from test_train import check_adapt_fixture
+    from adaptive_city_nerf_amd.expert_parallel import HipBackend
+
+    def fn(Pk, m, rays, rgbs, opt, u):
+        shared = list(m.bg_mlp.parameters())
+        return adapt_step_expert_parallel(Pk, HipBackend(m), rays, rgbs, opt, len(m.submodules), rays.shape[0],
+                                          shared, grad_clip=1.0, u=u)
+    check_adapt_fixture("k8", fn)
