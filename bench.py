@@ -297,10 +297,11 @@ def cpu_baseline_meta(model, sc, task_data, S, min_seconds):
                       f"{S} samples; oracle/meta_ref.py PyTorch CPU restatement, {threads} threads), {dt:.1f} s"}
 
 
-def load_traffic(name: str = "render"):
-    """Committed per-launch HBM bytes of a workload's dominant kernel (profiles/pmc_<name>_r01.json,
-    from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes: tools/pmc_kernel.sh + pmc_fold.py)."""
-    p = REPO / "profiles" / f"pmc_{name}_r01.json"
+def load_traffic(name: str = "render", rnd: str = "r01"):
+    """Committed per-launch HBM bytes of a workload's dominant kernel (profiles/pmc_<name>_<round>.json,
+    from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes: tools/pmc_kernel.sh + pmc_fold.py,
+    tools/pmc_c5.sh)."""
+    p = REPO / "profiles" / f"pmc_{name}_{rnd}.json"
     if p.exists():
         try:
             return json.loads(p.read_text())
@@ -567,9 +568,9 @@ def main():
         expert = None
         routed = None
         pg = dist.group.WORLD if world > 1 else None
-        if world == 1 and not a.no_graph:  # the whole routed step (no host sync) replayed as one HIP graph
+        if world == 1:  # the whole routed step (no host sync), replayed as one HIP graph (eager with --no-graph)
             from adaptive_city_nerf_amd.routed_train import RoutedAdaptStep
-            routed = RoutedAdaptStep(P, model, bsz, opt, grad_clip=1.0, graph=True, warmup=2)
+            routed = RoutedAdaptStep(P, model, bsz, opt, grad_clip=1.0, graph=not a.no_graph, warmup=2)
 
         def step():
             # N > 1: the experts distributed over the ranks (expert_parallel.py), every rank streaming
@@ -657,6 +658,7 @@ def main():
     if a.workload == "c5" and routed is not None:
         # graph replays run no Python: the Adam launch is timed by eager steps of the same object
         from adaptive_city_nerf_amd import routed_train as RT
+        graph_was = routed.graph
         routed.graph = None
         RT.EVENT_HOOK = aoptim.EVENT_HOOK = []
         for _ in range(3):
@@ -750,6 +752,19 @@ def main():
                     "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kname,
                     "kernel_ms": round(kernel_ms, 4), "params_per_launch": int(nparam),
                     "bytes_per_param": 28, "bytes_algorithmic_per_launch": int(adam_bytes)}
+        if a.workload == "c5":
+            pmc = load_traffic("c5", "r02") or {}
+            ad = pmc.get("adam_slots_kernel", {})
+            if ad.get("params") == int(nparam):   # counters of this exact workload (all 8 experts hit)
+                roofline["traffic"] = ad["hbm_bytes_per_launch"]
+            hb = pmc.get("hashgrid_bwd_pairs", {})
+            roofline["secondary"] = {
+                "kernel": "hashgrid_bwd_pairs (table-gradient scatter-add, float atomics)",
+                "bound": "memory-side atomic request rate (~20 G requests/s chip-wide for scattered 64-B "
+                         "segments: MI355X_MICROARCH.md 'Global float atomics', 64 rows per wave-instruction "
+                         "at 0.08 TB/s)",
+                "atomic_requests_per_launch": hb.get("atomic_requests_per_launch"),
+                "source": "profiles/pmc_c5_r02.json (TCC_EA0_ATOMIC_sum)"}
     if a.workload == "clusters":
         roofline = {"bound": "mfma", "achieved": round(cl_achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": round(cl_achieved / FP32_MFMA_PEAK_TFLOPS, 4),
