@@ -140,6 +140,8 @@ SIGNATURES = {
                            C.c_int),
     "acn_routed_blend_fwd": ([vp, vp, vp, i64, i32, vp, vp], C.c_int),
     "acn_routed_blend_bwd": ([vp, vp, vp, i64, vp, vp, vp], C.c_int),
+    "acn_hashgrid_bwd_det_workspace_bytes": ([i64, i32, i32, i32], C.c_size_t),
+    "acn_hashgrid_bwd_det": ([vp, i64, vp, vp, i32, i32, i32, i32, vp, vp, sz, vp], C.c_int),
     "acn_routed_scatter_xd": ([vp, i64, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp], C.c_int),
     "acn_xd_unit_sh": ([vp, i64, vp, vp, f32, f32, vp, vp, vp], C.c_int),
     "acn_hashgrid_fwd_pairs": ([vp, vp, vp, i32, vp, vp, i32, i32, i32, vp, vp], C.c_int),

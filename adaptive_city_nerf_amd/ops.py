@@ -57,12 +57,24 @@ def hashgrid_fwd(x01: torch.Tensor, table: torch.Tensor, resolutions: Sequence[i
 
 
 def hashgrid_bwd(x01: torch.Tensor, grad_out: torch.Tensor, resolutions: Sequence[int], log2T: int, F: int,
-                 interp: int) -> torch.Tensor:
+                 interp: int, deterministic: Optional[bool] = None) -> torch.Tensor:
+    """Table gradient (scatter-add).  ``deterministic`` (default: torch.are_deterministic_algorithms_enabled())
+    selects the sort-based backward (acn_hashgrid_bwd_det: bitwise reproducible, every row summed in point
+    order) over the float-atomic one."""
     L = len(resolutions)
     x = _f32(x01).view(-1, 3)
     g = _f32(grad_out).view(-1, L * F)
     gt = torch.zeros(L << log2T, F, device=x.device, dtype=torch.float32)
     res = (C.c_int32 * L)(*[int(r) for r in resolutions])
+    if deterministic is None:
+        deterministic = torch.are_deterministic_algorithms_enabled()
+    if deterministic and F == 2:
+        L_ = _lib.lib()
+        ws = torch.empty(max(int(L_.acn_hashgrid_bwd_det_workspace_bytes(x.shape[0], L, log2T, interp)), 1),
+                         dtype=torch.uint8, device=x.device)
+        check(L_.acn_hashgrid_bwd_det(ptr(x), x.shape[0], ptr(g), res, L, log2T, F, interp, ptr(gt), ptr(ws), ws.numel(),
+                                      stream_of(x)), "acn_hashgrid_bwd_det")
+        return gt
     check(_lib.lib().acn_hashgrid_bwd(ptr(x), x.shape[0], ptr(g), res, L, log2T, F, interp, ptr(gt),
                                       stream_of(x)), "acn_hashgrid_bwd")
     return gt

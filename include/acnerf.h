@@ -475,6 +475,15 @@ int acn_routed_blend_fwd(const float* y, const float* pw, const int32_t* pmap, i
 int acn_routed_blend_bwd(const float* g, const int32_t* pidx, const float* pw, int64_t P, const int64_t* live,
                          float* gy, void* stream);
 
+/* Deterministic HashGridEncoder backward: records (row, corner gradient) in (point, level,
+ * corner) order, a stable radix sort by row, one sequential fp32 sum per row -- every row is the sum of
+ * its contributions in point order, as a serial CPU scatter-add (encodings.py:318-329); bitwise
+ * reproducible.  F = 2.  grad_table is accumulated into (zero it first).  workspace:
+ * acn_hashgrid_bwd_det_workspace_bytes(M, L, log2T, interp) device bytes.                          */
+size_t acn_hashgrid_bwd_det_workspace_bytes(int64_t M, int L, int log2T, int interp);
+int acn_hashgrid_bwd_det(const float* x01, int64_t M, const float* grad_out, const int32_t* res, int L, int log2T,
+                         int F, int interp, float* grad_table, void* workspace, size_t workspace_bytes, void* stream);
+
 /* Expert-parallel records (parallel.py, SURVEY §8(e) "one expert per GPU"):
  *   acn_routed_scatter_xd -> the pairs of acn_routed_count (align 1) as xd (P,6) = [world point o + d t,
  *                            ray direction], with pidx / pw / pmap / pk as acn_routed_scatter: the 24-B
