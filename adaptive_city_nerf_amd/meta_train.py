@@ -28,6 +28,9 @@ Differences from the reference, all where the reference cannot run as written (D
 """
 from __future__ import annotations
 
+import contextlib
+import io
+import math
 import random
 import time
 from collections import OrderedDict
@@ -340,3 +343,128 @@ def train_step(P, step, model, optimizer, task_data, metric_logger=None, logger=
         logger.log("[TRAIN] [Step %d] [LossIn %.6f] [LossOut %.6f] [PSNRIn %.2f] [PSNROut %.2f] [InnerLR %.6f]"
                    % (step, out["loss_in"], out["loss_out"], out["psnr_in"], out["psnr_out"], float(P.inner_lr)))
     return out
+
+
+# ============================================================================ graph-replayed meta step
+class GraphedMetaStep:
+    """train_step for FOMAML with every region's task processing replayed as a HIP graph.
+
+    The outer loss of meta_train_step.py:157-159 is ``R * sum_t n_q,t loss_q,t / total_q`` over the
+    step's tasks, so its gradient is the sum of per-task gradients weighted by ``R n_q,t / total_q``:
+    each task's inner loop (task_adapt, meta_core.py:14-67), query loss and backward (into the
+    parameters' persistent .grad buffers) is one captured graph per region (the expert and the task
+    shapes are fixed per region), replayed for every task of the region in the reference's shuffled
+    region order (random.Random(seed + step)); the training jitter is drawn inside the graphs
+    (graph-safe philox) in the same call order.  The outer clip + Adam (FusedAdam's device step table)
+    is one more graph.  Per step the host copies each task into its region's static buffers and reads
+    the loss once (the reference's non-finite-loss skip, meta_core.py:124-126).  The gradient equals the
+    eager step's up to fp32 summation order (per-task accumulation instead of one backward of the sum).
+    Shapes are fixed at construction: every task of a region must have that region's support / query
+    sizes (TaskDataset's S_target / Q_target).  Second-order MAML stays on the eager train_step: the
+    create_graph backward does an operation HIP stream capture does not permit on this stack."""
+
+    def __init__(self, P, model, optimizer, task_data, warmup: int = 1, max_steps: int = 1 << 16):
+        algo = str(getattr(P, "algo", "")).lower()
+        if algo != "fomaml":
+            raise ValueError("GraphedMetaStep: FOMAML only (MAML's second-order backward is not capturable; "
+                             "Reptile has no gradient step) -- use train_step")
+        if not isinstance(optimizer, FusedAdam):
+            raise TypeError("GraphedMetaStep needs FusedAdam (its device step table makes the update replayable)")
+        self.P, self.model, self.opt = P, model, optimizer
+        self.device = next(model.parameters()).device
+        self.cids = sorted(task_data.keys())
+        self.shapes = {}
+        for cid in self.cids:
+            t0 = task_data[cid][0]
+            sup, qry = (t0.support, t0.query) if hasattr(t0, "support") else (t0["support"], t0["query"])
+            self.shapes[cid] = (int(sup["rays"].shape[0]), int(qry["rays"].shape[0]))
+        for _ in range(max(1, int(warmup))):   # real updates: they also create every Adam state
+            with _quiet():
+                train_step(P, 0, model, optimizer, task_data)
+        torch.cuda.synchronize(self.device)
+        dev = self.device
+        self.static = {}
+        for cid in self.cids:
+            ns, nq = self.shapes[cid]
+            self.static[cid] = {"support": {"rays": torch.zeros(ns, 8, device=dev), "rgbs": torch.zeros(ns, 3, device=dev)},
+                                "query": {"rays": torch.zeros(nq, 8, device=dev), "rgbs": torch.zeros(nq, 3, device=dev)},
+                                "wq": torch.zeros((), device=dev)}
+            self._load(cid, task_data[cid][0])
+        self.inner_acc = torch.zeros((), device=dev)
+        self.q_acc = torch.zeros((), device=dev)
+        self.params = [p for g in optimizer.param_groups for p in g["params"] if optimizer.state.get(p)]
+        for p in self.params:   # persistent gradients: the captured backwards accumulate into them
+            p.grad = torch.zeros_like(p)
+        self.grads = [p.grad for p in self.params]
+        optimizer.graph_begin(max_steps)
+        pool = torch.cuda.graph_pool_handle()
+        self.graphs = {}
+        for cid in self.cids:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
+                self._task(cid)
+            self.graphs[cid] = g
+        self.outer = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.outer, pool=pool):
+            optimizer.step(max_norm=getattr(P, "grad_clip", 1.0))
+        optimizer.graph_end_capture()
+        self.replays = 0
+        torch._foreach_zero_(self.grads)
+
+    def _load(self, cid, task) -> None:
+        sup, qry = (task.support, task.query) if hasattr(task, "support") else (task["support"], task["query"])
+        st = self.static[cid]
+        for part, src in (("support", sup), ("query", qry)):
+            if src["rays"].shape[0] != st[part]["rays"].shape[0]:
+                raise ValueError(f"GraphedMetaStep: region {cid} was captured for {st[part]['rays'].shape[0]} "
+                                 f"{part} rays, got {src['rays'].shape[0]}")
+            st[part]["rays"].copy_(src["rays"], non_blocking=True)
+            st[part]["rgbs"].copy_(src["rgbs"], non_blocking=True)
+
+    def _task(self, cid) -> None:
+        P, st = self.P, self.static[cid]
+        ns, nq = self.shapes[cid]
+        fast, inner = task_adapt(P, self.model, st["support"], P.inner_lr, P.inner_iter, active_module=cid)
+        loss_q = compute_loss(P, self.model, st["query"], params=fast, active_module=cid)
+        (loss_q * st["wq"]).backward()
+        if inner:
+            self.inner_acc.add_(inner[-1].detach() * ns)
+        self.q_acc.add_(loss_q.detach() * nq)
+
+    def __call__(self, step: int, task_data) -> Optional[Dict[str, float]]:
+        t0 = time.perf_counter()
+        torch._foreach_zero_(self.grads)
+        self.inner_acc.zero_()
+        self.q_acc.zero_()
+        cids = list(task_data.keys())
+        random.Random(getattr(self.P, "seed", 0) + step).shuffle(cids)
+        total_sup = sum(self.shapes[c][0] * len(task_data[c]) for c in cids)
+        total_q = sum(self.shapes[c][1] * len(task_data[c]) for c in cids)
+        if total_q == 0:
+            return None
+        for cid in cids:
+            self.static[cid]["wq"].fill_(len(cids) * self.shapes[cid][1] / total_q)
+            for task in task_data[cid]:
+                self._load(cid, task)
+                self.graphs[cid].replay()
+        loss_out = float(self.q_acc) / total_q          # the one host read of the step
+        if not math.isfinite(len(cids) * loss_out):
+            print(f"[WARN] Skipping meta-update: non-finite loss_out={len(cids) * loss_out}")
+        else:
+            self.outer.replay()
+            self.replays += 1
+            from .optim import bump_versions
+            bump_versions(self.opt._graph["params"])
+        loss_in = float(self.inner_acc) / max(total_sup, 1)
+        return {"loss_in": loss_in, "loss_out": loss_out, "psnr_in": -10.0 * math.log10(loss_in + 1e-24),
+                "psnr_out": -10.0 * math.log10(loss_out + 1e-24), "tasks": sum(len(v) for v in task_data.values()),
+                "rays_in": total_sup, "rays_out": total_q, "time_total_step": time.perf_counter() - t0}
+
+    def sync_state(self) -> None:
+        self.opt.graph_sync_steps(self.replays)
+
+
+@contextlib.contextmanager
+def _quiet():
+    with contextlib.redirect_stdout(io.StringIO()):
+        yield

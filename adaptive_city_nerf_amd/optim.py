@@ -165,6 +165,9 @@ class FusedAdam(torch.optim.Optimizer):
         device = next(p for g in self.param_groups for p in g["params"]).device
         self._graph = {"table": host.to(device), "step_dev": torch.tensor([cur], dtype=torch.int32, device=device),
                        "first": cur + 1, "steps": int(max_steps), "params": []}
+        rows, _ = self._rows(bump=False)   # the descriptors, built now with plain copies (no 64-tensor
+        if rows:                           # kernel-argument limit inside the capture)
+            self._plan = _Plan(rows, device)
 
     def graph_end_capture(self) -> None:
         """After the capture: undo the host-side step increments the capture pass made."""
@@ -178,8 +181,9 @@ class FusedAdam(torch.optim.Optimizer):
         if replays >= gs["steps"]:
             raise AcnError("FusedAdam: graph replays exceeded the precomputed Adam table; capture again")
 
-    def _rows(self):
-        """(p, grad, exp_avg, exp_avg_sq, kind) rows; kind indexes distinct (group, step) pairs."""
+    def _rows(self, bump: bool = True):
+        """(p, grad, exp_avg, exp_avg_sq, kind) rows; kind indexes distinct (group, step) pairs.  bump:
+        advance state['step'] first (torch increments it before the update)."""
         rows, kinds = [], []
         for gi, group in enumerate(self.param_groups):
             for p in group["params"]:
@@ -193,7 +197,8 @@ class FusedAdam(torch.optim.Optimizer):
                     st["step"] = torch.tensor(0.0, dtype=torch.float32)
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                st["step"] += 1
+                if bump:
+                    st["step"] += 1
                 key = (gi, int(st["step"].item()))
                 if key not in kinds:
                     kinds.append(key)

@@ -466,9 +466,14 @@ def main():
         my_regions = [c for c in range(4) if expert_owner(4, world)[c] == rank]
         samples_per_step = sum(len(task_data[c]) * (P.inner_iter * nsup + nqry) for c in range(4)) * S
         it = [0]
+        graphed_meta = None
+        if world == 1 and not a.no_graph:   # per-region task graphs + the outer clip/Adam graph
+            graphed_meta = MT.GraphedMetaStep(P, model, opt, task_data, warmup=1)
 
         def step():
             it[0] += 1
+            if graphed_meta is not None:
+                return graphed_meta(it[0], task_data)
             import contextlib, io
             with contextlib.redirect_stdout(io.StringIO()):  # meta_update's per-region debug prints
                 return MT.train_step(P, it[0], model, opt, task_data, group=pg)
@@ -665,6 +670,17 @@ def main():
             step()
         torch.cuda.synchronize()
         RT.EVENT_HOOK = None
+    if a.workload == "meta" and graphed_meta is not None:
+        # graph replays run no Python: the outer Adam launch is timed by eager steps afterwards
+        import contextlib, io
+        graphed_meta.sync_state()
+        opt._graph = None
+        aoptim.EVENT_HOOK = []
+        with contextlib.redirect_stdout(io.StringIO()):
+            for _ in range(3):
+                it[0] += 1
+                MT.train_step(P, it[0], model, opt, task_data)
+        torch.cuda.synchronize()
     if a.workload == "c5":
         psnr_after = val_psnr()
     if a.workload in ("c5", "c5a", "meta"):
@@ -833,7 +849,9 @@ def main():
                        "marched_samples_per_gpu": occ_samples if a.workload == "occ" else None},
                "meta": {"workload": "offline meta-training step (meta_train_step.train_step, configs/train.json): 4 "
                                     "regions x 3 tasks, 4000 support + 2000 query rays x 96 samples, 8 inner FOMAML "
-                                    "steps, outer clip + Adam; metric = trained ray-samples (fwd+bwd) per second",
+                                    "steps, outer clip + Adam; metric = trained ray-samples (fwd+bwd) per second; 1 "
+                                    "GPU: per-region task graphs + outer graph (meta_train.GraphedMetaStep)"
+                                    + (" (disabled)" if a.no_graph else ""),
                         "experts": 4, "regions": 4, "tasks_per_region": 3,
                         "inner_iter": a.inner_iter if a.workload == "meta" else None},
                "clusters": {"workload": "cluster creation (create_clusters.py, example dataset g22 configuration): "

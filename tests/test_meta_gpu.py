@@ -107,3 +107,44 @@ def test_train_step_matches_reference(algo):
                                            err_msg=name)
         # Adam's first step moves a parameter by ~lr * sign(g): a few near-zero gradients may flip
         assert _close_frac(got, ref, 1e-3 * lr, 1e-6) >= 0.998, name
+
+
+@pytest.mark.parametrize("algo", ["fomaml"])
+def test_graphed_meta_step_matches_eager(algo):
+    """GraphedMetaStep (per-region task graphs + outer clip/Adam graph, jitter drawn inside the graphs)
+    against eager train_step from the same RNG state: the same updates to fp32 summation order."""
+    from adaptive_city_nerf_amd import meta_train as MT
+    from adaptive_city_nerf_amd.optim import build_optimizer
+    d = G.load(f"meta_{algo}")
+    P = _P(algo)
+    ma, tasks = _model_and_tasks(d)
+    mb, _ = _model_and_tasks(d)
+    oa, ob = build_optimizer(P, ma), build_optimizer(P, mb)
+    torch.manual_seed(7)
+    with contextlib.redirect_stdout(None):
+        for step in range(3):
+            ra = MT.train_step(P, step, ma, oa, tasks)
+    torch.manual_seed(7)
+    g = MT.GraphedMetaStep(P, mb, ob, tasks, warmup=1)
+    for step in (1, 2):
+        rb = g(step, tasks)
+    torch.cuda.synchronize()
+    g.sync_state()
+    assert rb["loss_out"] == pytest.approx(ra["loss_out"], rel=1e-4)
+    for (na, pa), (nb, pb) in zip(ma.named_parameters(), mb.named_parameters()):
+        lr = LRS[_group(na)]
+        assert _close_frac(pb.detach().cpu().numpy(), pa.detach().cpu().numpy(), 1e-3 * lr, 1e-5) >= 0.99, na
+    for pa, pb in zip(ma.parameters(), mb.parameters()):
+        sa, sb = oa.state.get(pa, {}), ob.state.get(pb, {})
+        assert ("step" in sa) == ("step" in sb)
+        if "step" in sa:
+            assert float(sa["step"]) == float(sb["step"]) == 3.0
+
+
+def test_graphed_meta_step_refuses_second_order():
+    from adaptive_city_nerf_amd import meta_train as MT
+    from adaptive_city_nerf_amd.optim import build_optimizer
+    d = G.load("meta_maml")
+    m, tasks = _model_and_tasks(d)
+    with pytest.raises(ValueError):
+        MT.GraphedMetaStep(_P("maml"), m, build_optimizer(_P("maml"), m), tasks)
