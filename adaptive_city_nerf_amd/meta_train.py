@@ -41,7 +41,7 @@ import torch.distributed as dist
 
 from .expert_parallel import expert_owner, global_clip_grad_norm_
 from .optim import FusedAdam
-from .ray_rendering import second_order
+from .ray_rendering import encoding_frozen, second_order
 from .train import compute_mse_loss
 
 
@@ -93,7 +93,7 @@ def task_adapt(P, model, support, inner_lr, iterations, active_module=None):
     fast = extract_module_params(base, copy=(algo == "reptile"))
     inner_losses = []
     for _ in range(int(iterations)):
-        with second_order(not first_order):
+        with second_order(not first_order), encoding_frozen(first_order):
             loss = compute_loss(P, model, support, params=fast, active_module=active_module, grad_buffer={},
                                 update_fisher=True)
         grads = torch.autograd.grad(loss, tuple(fast.values()), create_graph=not first_order, allow_unused=True)

@@ -52,6 +52,20 @@ def _second_order() -> bool:
     return getattr(_GRAPH_MODE, "second_order", False)
 
 
+@contextmanager
+def encoding_frozen(enabled: bool = True):
+    """Within this context, differentiable single-expert renders evaluate the hash grid without autograd:
+    for first-order inner loops (FOMAML / Reptile task_adapt, meta_core.py:14-67), which differentiate
+    w.r.t. the fast MLP weights only, the encoding's backward branch (dL/dh0, the table scatter) is dead
+    work.  The values are unchanged.  Thread-local."""
+    prev = getattr(_GRAPH_MODE, "frozen_encoding", False)
+    _GRAPH_MODE.frozen_encoding = bool(enabled)
+    try:
+        yield
+    finally:
+        _GRAPH_MODE.frozen_encoding = prev
+
+
 # ============================== BG helpers ===============================
 def _get_bg_rgb(model, dirs: Tensor, params, rgb_sigma_or_map, N: int, bg_color_default: str) -> Optional[Tensor]:
     """Background RGB: the model's background head if it has one, else a default colour (:23-45)."""
@@ -310,7 +324,11 @@ def render_rays_stratified(model, rays: Tensor, ray_samples: int, params=None, a
         mn, ext = sub._host_box()
         t_vals, x01, sh = ops.sample_stratified(rays, ray_samples, u if model.training else None, mn, ext,
                                                 ENC_EPS)
-        h0 = sub.xyz_encoder(x01)
+        if getattr(_GRAPH_MODE, "frozen_encoding", False):
+            with torch.no_grad():
+                h0 = sub.xyz_encoder(x01)
+        else:
+            h0 = sub.xyz_encoder(x01)
         ws = [t.contiguous() for t in sub._mlp_tensors(params).values()]
         rgb_sigma = _FusedMLPFn.apply(h0.contiguous(), sh, *ws).view(N, ray_samples, 4)
         bg_rgb = _get_bg_rgb(model, rays[:, 3:6], params, rgb_sigma, N=N, bg_color_default=bg_color_default)

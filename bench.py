@@ -155,10 +155,26 @@ def cpu_baseline(model, sc, rays, S, gpu_rgb, min_seconds):
     dt = time.perf_counter() - t0
     mse = float(np.mean((gpu_rgb.astype(np.float64) - orgb.astype(np.float64)) ** 2))
     psnr = float("inf") if mse == 0 else -10.0 * np.log10(mse)
+    # one thread (SURVEY §8(d) "also report one-thread"): a bounded prefix of the same batch
+    n1 = min(r.shape[0], 256)
+    O.set_threads(1)
+    try:
+        reps1, t1 = 0, time.perf_counter()
+        while True:
+            O.render_stratified(r[:n1], S, experts, np.array(sc["centroids"], np.float32), bm=model.boundary_margin,
+                                bg_mlp=bg, want_weights=False)
+            reps1 += 1
+            if time.perf_counter() - t1 >= min(5.0, min_seconds):
+                break
+        dt1 = time.perf_counter() - t1
+    finally:
+        O.set_threads(cores)
+    single = {"value": n1 * S * reps1 / dt1, "unit": "ray-samples/s", "cores": 1,
+              "sample": f"{reps1} x ({n1} rays x {S} samples), C oracle single thread, {dt1:.1f} s"}
     return {"value": r.shape[0] * S * reps / dt, "unit": "ray-samples/s", "cores": cores, "kind": "port",
             "sample": f"{reps} x ({r.shape[0]} rays x {S} samples) of the benchmark batch, C oracle "
-                      f"(oracle/acn_oracle.c, OpenMP {cores} threads), {dt:.1f} s"}, psnr, float(np.sqrt(mse)), \
-        float(np.max(np.abs(gpu_rgb - orgb)))
+                      f"(oracle/acn_oracle.c, OpenMP {cores} threads), {dt:.1f} s",
+            "single_thread": single}, psnr, float(np.sqrt(mse)), float(np.max(np.abs(gpu_rgb - orgb)))
 
 
 def cpu_baseline_train(model, sc, rays, rgbs, S, expert, min_seconds):
@@ -349,6 +365,9 @@ def main():
                     help="c4: experts replicated + rays sharded by owning expert (all-gather of rendered rays), or "
                          "one expert per GPU (all-to-all of per-sample records, expert_parallel.py)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--tau", type=float, default=0.0,
+                    help="c2: early ray termination threshold on transmittance (wavefront scan; 0 = off, the "
+                         "reference's behaviour); the line then reports the RGB error against tau = 0")
     ap.add_argument("--cpu-rays", type=int, default=4096, help="rays in the CPU-baseline / PSNR sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--inner-iter", type=int, default=8, help="meta: inner steps (configs/train.json)")
@@ -403,7 +422,7 @@ def main():
 
         def step():
             with torch.no_grad():
-                return render_rays(model, rays, ray_samples=S, bg_color_default="white")
+                return render_rays(model, rays, ray_samples=S, bg_color_default="white", early_stop_tau=a.tau)
         sample_rays = rays
     elif a.workload == "occ":
         from adaptive_city_nerf_amd import occ_ops
@@ -821,7 +840,8 @@ def main():
 
     if rank == 0:
         cfg = {"c2": {"workload": "C2: single Instant-NGP expert, 4096 rays x 256 samples per GPU, eval, fused "
-                                  "render_rays", "rays_per_gpu": a.rays, "experts": 1},
+                                  "render_rays" + (f", early ray termination tau={a.tau}" if a.tau > 0 else ""),
+                      "rays_per_gpu": a.rays, "experts": 1},
                "c3": {"workload": "C3: 2x2 Voronoi grid -> 4 experts (soft routing bm 1.05), 4096 rays x 256 samples "
                                   "per GPU sharded by owning expert, RCCL all-gather of rendered rays",
                       "rays_per_gpu": a.rays, "experts": 4},
@@ -878,6 +898,13 @@ def main():
             "psnr_vs_cpu_path_db": None if psnr is None else round(psnr, 2),
             "rgb_max_abs_err_vs_cpu_path": maxerr,
         }
+        if a.workload == "c2" and a.tau > 0:
+            with torch.no_grad():
+                ref0 = render_rays(model, rays, ray_samples=S, bg_color_default="white")[0]
+            line["early_termination"] = {
+                "tau": a.tau, "max_abs_rgb_err_vs_tau0": float((out[0] - ref0).abs().max()),
+                "bound": "2 * tau (the composite drops at most the remaining transmittance)",
+                "note": "wavefront-level prefix product over each 32-sample tile; a ray stops at T < tau"}
         if a.workload == "c5":
             line["val_psnr_db"] = {"before": round(psnr_before, 3), "after": round(psnr_after, 3),
                                    "steps_adapted": int(a.warmup + a.steps + (5 if routed is not None else 0)), "val_rays": int(val_rays.shape[0]),
