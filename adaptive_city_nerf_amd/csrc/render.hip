@@ -982,9 +982,9 @@ __global__ void __launch_bounds__(1024, 4) render_kernel(FieldCfg cfg, BgArgs bg
 // the same one or two experts, so staging is rare).  A sample whose expert is not resident is
 // evaluated from the packed image in global memory (L2), without the SH fold.
 __device__ __forceinline__ uint32_t ray_expert_mask(const FieldCfg& cfg, int route, const RenderParams& p, int64_t ray,
-                                                    float step, int lane) {
+                                                    int64_t lim, float step, int lane) {
     uint32_t m = 0u;
-    if (ray < p.N) {
+    if (ray < lim) {
         const float* rp = p.rays + ray * 8;
         const float ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
         const float near = rp[6], far = rp[7];
@@ -1006,6 +1006,9 @@ __device__ __forceinline__ uint32_t ray_expert_mask(const FieldCfg& cfg, int rou
     return m;
 }
 
+#ifndef ACN_SLOTS_BAND
+#define ACN_SLOTS_BAND 0
+#endif
 #ifndef ACN_SLOTS_THREADS
 #define ACN_SLOTS_THREADS 512  // 2 waves/SIMD, 256 VGPRs: the 1024-thread build spills and was measured wrong
 #endif
@@ -1024,9 +1027,19 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
     if (threadIdx.x < 2) slot_k[threadIdx.x] = -1;
     __syncthreads();
     const int64_t waves_per_wg = blockDim.x >> 6;
-    for (int64_t base = (int64_t)blockIdx.x * waves_per_wg; base < p.N; base += (int64_t)gridDim.x * waves_per_wg) {
+    // XCD bands (as render_kernel): with the grid a multiple of 8, XCD x walks the x-th contiguous
+    // eighth of the rays, so a frame's neighbouring rays share one L2 (ACN_SLOTS_BAND=0: interleaved)
+    int64_t first = (int64_t)blockIdx.x * waves_per_wg, lim = p.N, gstride = (int64_t)gridDim.x * waves_per_wg;
+    if (ACN_SLOTS_BAND && (gridDim.x & 7) == 0) {
+        const int64_t chunk = (((p.N + 7) >> 3) + waves_per_wg - 1) / waves_per_wg * waves_per_wg;
+        const int64_t lo = min(p.N, (int64_t)(blockIdx.x & 7) * chunk);
+        lim = min(p.N, lo + chunk);
+        first = lo + (int64_t)(blockIdx.x >> 3) * waves_per_wg;
+        gstride = (int64_t)(gridDim.x >> 3) * waves_per_wg;
+    }
+    for (int64_t base = first; base < lim; base += gstride) {
         const int64_t ray = base + wave;
-        const uint32_t m = ray_expert_mask(cfg, ROUTE, p, ray, step, lane);
+        const uint32_t m = ray_expert_mask(cfg, ROUTE, p, ray, lim, step, lane);
         if (lane == 0)
             for (int k = 0; k < cfg.K; ++k)
                 if ((m >> k) & 1u) atomicAdd(&cnt[k], 1);
@@ -1062,7 +1075,7 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
 #else
         const int k0 = __builtin_amdgcn_readfirstlane(slot_k[0]), k1 = __builtin_amdgcn_readfirstlane(slot_k[1]);
 #endif
-        if (ray < p.N) {
+        if (ray < lim) {
             render_ray(p, bg, ray, lane, step,
                        [&](float px, float py, float pz, const float (&shv)[8], uint32_t& folded, float& yr, float& yg,
                            float& yb, float& ys) {

@@ -44,6 +44,8 @@ from .optim import FusedAdam, bump_versions
 # Optional timing hook (bench.py): when set to a list, an eager step appends recorded HIP events
 # bracketing the Adam launch (adam_step_slots) on the current stream.
 EVENT_HOOK = None
+# Same for the table-gradient scatter (hashgrid_bwd_pairs), the step's second-largest kernel.
+BWD_HOOK = None
 
 ALIGN = 128                # pair segment alignment = one MLP round (4 tiles x 32 slots)
 ZERO_GRAD_FLAG = 1 << 16   # adam_step_slots: clear the gradient after reading it
@@ -240,9 +242,17 @@ class RoutedAdaptStep:
         gout = ops.routed_blend_bwd(grads[0].reshape(M, 4).contiguous(), self.pidx, self.pw, live=self.seg[K:K + 1])
         check(L.acn_mlp_train_bwd_dw_pairs(ptr(self.h0), ptr(self.sh), ptr(self.out), ptr(gout), ptr(self.seg), K,
                                            ptr(self.mws), ptr(self.dw), ptr(self.gh0), s), "acn_mlp_train_bwd_dw_pairs")
+        bhook = BWD_HOOK if self.graph is None else None
+        if bhook is not None:
+            b0 = torch.cuda.Event(enable_timing=True)
+            b0.record()
         check(L.acn_hashgrid_bwd_pairs(ptr(self.x01), ptr(self.pk), ptr(self.pidx), ptr(self.seg), K, ptr(self.gh0),
                                        self._gtables, self._res, len(enc._res_host), enc.log2_hashmap_size,
                                        enc._interp_code, s), "acn_hashgrid_bwd_pairs")
+        if bhook is not None:
+            b1 = torch.cuda.Event(enable_timing=True)
+            b1.record()
+            bhook.append((b0, b1))
         scale = None
         if self.grad_clip is not None:
             check(L.acn_grad_sumsq_slots(ptr(self.descs), ptr(self.chunk_tensor), self.nchunks, ptr(self.flags),

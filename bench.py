@@ -54,6 +54,8 @@ FLOP_PER_SAMPLE = 26880          # MLP MACs x 2: 32*64+64*64+64+
 BYTES_PER_SAMPLE = 1024.2        # algorithmic hash-table reads + amortised ray I/O
 FP32_MFMA_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 matrix = vector peak (spec)
 HBM_PEAK_GBS = 8000.0
+IC_GATHER_GBS = 8600.0         # Infinity-Cache random-row gather rate (MI355X_MICROARCH.md 'Indexed rows')
+ATOMIC_REQ_PEAK = 1.3e12 / 64   # memory-side float-atomic requests/s (MI355X_MICROARCH.md 'Global float atomics')
 
 
 def build_model(device, n_experts=1, seed=0, table_seed=100, table_scale=0.5, fill=None, occ_conf=None):
@@ -311,6 +313,29 @@ def cpu_baseline_meta(model, sc, task_data, S, min_seconds):
     return {"value": n / dt, "unit": "ray-samples/s", "cores": threads, "kind": "port",
             "sample": f"{reps} meta steps of 1 region x 1 task ({ns} support x {iters} inner + {nq} query rays, "
                       f"{S} samples; oracle/meta_ref.py PyTorch CPU restatement, {threads} threads), {dt:.1f} s"}
+
+
+def hash_bwd_segments(routed) -> int:
+    """Distinct 64-B segments (8 rows of 8 B) of the gradient tables one routed step's table scatter
+    touches: the floor on memory-side atomic requests of any scatter-add of these contributions
+    (MI355X_MICROARCH.md 'Global float atomics': one request per 64-B segment an atomic
+    wave-instruction covers).  Same hash and corner set as hashgrid_bwd_pairs (encoders.hip)."""
+    K = routed.K
+    live = int(routed.seg[K])
+    keep = routed.pidx[:live] >= 0
+    x = routed.x01[:live][keep]
+    pk = routed.pk[:live][keep].long()
+    enc = routed.model.submodules[0].xyz_encoder
+    log2T, mask = enc.log2_hashmap_size, (1 << enc.log2_hashmap_size) - 1
+    P1, P2, U32 = 2654435761, 805459861, 0xFFFFFFFF
+    keys = []
+    for l, r in enumerate(enc._res_host):
+        s = torch.floor(x * float(r)).long()
+        for c in range(8):
+            bx, by, bz = c >> 2, (c >> 1) & 1, c & 1
+            h = (((s[:, 0] + bx) & U32) ^ (((s[:, 1] + by) * P1) & U32) ^ (((s[:, 2] + bz) * P2) & U32)) & mask
+            keys.append((((pk * len(enc._res_host) + l) << log2T) | h) >> 3)
+    return int(torch.unique(torch.cat(keys)).numel())
 
 
 def load_traffic(name: str = "render", rnd: str = "r01"):
@@ -685,10 +710,13 @@ def main():
         graph_was = routed.graph
         routed.graph = None
         RT.EVENT_HOOK = aoptim.EVENT_HOOK = []
+        RT.BWD_HOOK = []
         for _ in range(3):
             step()
         torch.cuda.synchronize()
-        RT.EVENT_HOOK = None
+        hash_bwd_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in RT.BWD_HOOK]))
+        hash_segments = hash_bwd_segments(routed)
+        RT.EVENT_HOOK = RT.BWD_HOOK = None
     if a.workload == "meta" and graphed_meta is not None:
         # graph replays run no Python: the outer Adam launch is timed by eager steps afterwards
         import contextlib, io
@@ -757,7 +785,7 @@ def main():
     # samples one launch of the dominant kernel processes on this rank
     launch_samples = samples_per_step // world // max(kernel_launches, 1)
     achieved = FLOP_PER_SAMPLE * launch_samples / (kernel_ms * 1e-3) / 1e12
-    tr = load_traffic() if a.workload == "c2" else None
+    tr = load_traffic("render", "r02") if a.workload == "c2" else None
     kname = {"c5": "adam_slots_kernel (Adam over every expert with routed samples + background head, clip coefficient "
                    "folded in, table gradients cleared in the same pass)",
              "c5a": "adam_kernel (fused clip + Adam over the adapted expert + background head)",
@@ -773,15 +801,37 @@ def main():
              "clusters": "voronoi_kernel<4,2> (create_clusters Voronoi routing, 256 samples x 4 centroids per ray, "
                          "AABB streaming)"
              }[a.workload]
-    roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+    # The fused render is bound by gathering hash-table lines from beyond the XCD L2 (Infinity Cache,
+    # the tables are cache-resident): PMC shows TD busy and stalled on the texture cache while the MFMA
+    # pipe is mostly idle (profiles/pmc_render_r02.json).  `achieved` is the ALGORITHMIC table bytes
+    # (1024 B/sample) against HBM peak; the measured line traffic against the
+    # Infinity-Cache row-gather rate and the fp32-MFMA fraction ride along.
+    hash_gbs = BYTES_PER_SAMPLE * launch_samples / (kernel_ms * 1e-3) / 1e9
+    roofline = {"bound": "hbm", "achieved": round(hash_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(hash_gbs / HBM_PEAK_GBS, 4),
                 "traffic": (tr or {}).get("hbm_bytes_per_launch"),
                 "kernel": kname, "kernel_ms": round(kernel_ms, 4), "samples_per_launch": int(launch_samples),
-                "flop_per_sample": FLOP_PER_SAMPLE,
-                "hash_bytes_algorithmic_per_launch": int(BYTES_PER_SAMPLE * launch_samples),
-                "hash_gbs_algorithmic": round(BYTES_PER_SAMPLE * launch_samples / (kernel_ms * 1e-3) / 1e9, 1),
-                "mlp_arith": "fp32-accurate 3-term fp16 split (hi*hi + hi*lo + lo*hi) on v_mfma_f32_32x32x16_f16, "
-                             "fp32 accumulate (DESIGN.md 4)"}
+                "bytes_per_sample": BYTES_PER_SAMPLE,
+                "bytes_algorithmic_per_launch": int(BYTES_PER_SAMPLE * launch_samples),
+                "secondary": {"bound": "mfma", "unit": "TFLOP/s", "achieved": round(achieved, 2),
+                              "peak": FP32_MFMA_PEAK_TFLOPS, "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+                              "flop_per_sample": FLOP_PER_SAMPLE,
+                              "mlp_arith": "fp32-accurate 3-term fp16 split (hi*hi + hi*lo + lo*hi) on "
+                                           "v_mfma_f32_32x32x16_f16, fp32 accumulate (DESIGN.md 4)"}}
+    if tr:
+        d = tr.get("derived", {})
+        miss_bytes = d.get("l2_miss_bytes_per_launch_at_128B")
+        lg = {"what": "hash-table lines served from beyond the XCD L2 (TCC_MISS x 128-B line) per launch, "
+                      "against the Infinity-Cache random-row gather rate (MI355X_MICROARCH.md 'Indexed rows': "
+                      "38 MB table, uniformly random rows, 8.6 TB/s chip-wide)",
+              "l2_misses_per_sample": round(d.get("l2_misses_per_sample", 0.0), 2),
+              "l2_hit_rate": round(d.get("l2_hit_rate", 0.0), 3),
+              "line_bytes_per_launch": int(miss_bytes) if miss_bytes else None,
+              "ceiling_gbs": IC_GATHER_GBS, "source": f"profiles/pmc_render_r02.json ({tr.get('round')})"}
+        if miss_bytes and tr.get("rocprof_avg_ns"):
+            lg["achieved_gbs"] = round(miss_bytes / tr["rocprof_avg_ns"], 1)
+            lg["frac"] = round(lg["achieved_gbs"] / IC_GATHER_GBS, 4)
+        roofline["line_gather"] = lg
     if a.workload in ("c5", "c5a", "meta"):
         roofline = {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kname,
@@ -795,11 +845,21 @@ def main():
             hb = pmc.get("hashgrid_bwd_pairs", {})
             roofline["secondary"] = {
                 "kernel": "hashgrid_bwd_pairs (table-gradient scatter-add, float atomics)",
-                "bound": "memory-side atomic request rate (~20 G requests/s chip-wide for scattered 64-B "
-                         "segments: MI355X_MICROARCH.md 'Global float atomics', 64 rows per wave-instruction "
-                         "at 0.08 TB/s)",
+                "bound": "memory-side atomic request rate: 1.3 TB/s of added bytes = 4 x 64-B requests per 256-B "
+                         "wave-instruction = ~20.3 G requests/s chip-wide (MI355X_MICROARCH.md 'Global float "
+                         "atomics'; 64 rows per instruction at 0.08 TB/s is the same request rate)",
+                "peak_requests_per_s": ATOMIC_REQ_PEAK,
                 "atomic_requests_per_launch": hb.get("atomic_requests_per_launch"),
-                "source": "profiles/pmc_c5_r02.json (TCC_EA0_ATOMIC_sum)"}
+                "requests_source": "profiles/pmc_c5_r02.json (TCC_EA0_ATOMIC_sum, same workload)"}
+            if routed is not None:
+                sec = roofline["secondary"]
+                sec["kernel_ms"] = round(hash_bwd_ms, 4)
+                sec["distinct_segments_per_launch"] = hash_segments
+                sec["floor_ms_at_peak"] = round(hash_segments / ATOMIC_REQ_PEAK * 1e3, 4)
+                sec["frac_vs_segment_floor"] = round(hash_segments / ATOMIC_REQ_PEAK * 1e3 / hash_bwd_ms, 4)
+                if sec["atomic_requests_per_launch"]:
+                    sec["requests_over_distinct_segments"] = round(sec["atomic_requests_per_launch"] / hash_segments, 3)
+                    sec["achieved_requests_per_s"] = round(sec["atomic_requests_per_launch"] / (hash_bwd_ms * 1e-3), 1)
     if a.workload == "clusters":
         roofline = {"bound": "mfma", "achieved": round(cl_achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": round(cl_achieved / FP32_MFMA_PEAK_TFLOPS, 4),
@@ -900,9 +960,10 @@ def main():
         }
         if a.workload == "c2" and a.tau > 0:
             with torch.no_grad():
-                ref0 = render_rays(model, rays, ray_samples=S, bg_color_default="white")[0]
+                ref0, _, _, acc0 = render_rays(model, rays, ray_samples=S, bg_color_default="white")
             line["early_termination"] = {
                 "tau": a.tau, "max_abs_rgb_err_vs_tau0": float((out[0] - ref0).abs().max()),
+                "rays_reaching_tau_frac": float(((1.0 - acc0) < a.tau).float().mean()),
                 "bound": "2 * tau (the composite drops at most the remaining transmittance)",
                 "note": "wavefront-level prefix product over each 32-sample tile; a ray stops at T < tau"}
         if a.workload == "c5":
