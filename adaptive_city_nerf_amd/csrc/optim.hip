@@ -15,9 +15,27 @@
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kUnroll = 4;  // 16-B vectors in flight per lane and array: 2 blocks per CU need them to cover HBM latency
+#ifndef ACN_ADAM_UNROLL
+#define ACN_ADAM_UNROLL 4
+#endif
+#ifndef ACN_ADAM_NT
+#define ACN_ADAM_NT 2  // 1: non-temporal stores in the Adam passes, 2: non-temporal loads and stores
+#endif
+constexpr int kUnroll = ACN_ADAM_UNROLL;  // 16-B vectors in flight per lane and array: 2 blocks per CU need them to cover HBM latency
 
 typedef float f4 __attribute__((ext_vector_type(4)));
+
+// The slotted norm and Adam passes touch every byte once (p, g, m, v of 268M parameters >> the 256 MiB
+// Infinity Cache): non-temporal loads and stores, A/B on the C5 step (tools/ab_c5.sh): Adam 1.69 ->
+// 1.42 ms, plain / stores-only NT / 2 or 8 vectors in flight all slower.
+__device__ __forceinline__ f4 ldv(const f4* a) {
+    if (ACN_ADAM_NT >= 2) return __builtin_nontemporal_load(a);
+    return *a;
+}
+__device__ __forceinline__ void stv(f4* a, const f4& v) {
+    if (ACN_ADAM_NT >= 1) __builtin_nontemporal_store(v, a);
+    else *a = v;
+}
 
 __device__ __forceinline__ double block_sum(double v) {
     __shared__ double red[kThreads / 64];
@@ -49,14 +67,14 @@ __global__ void __launch_bounds__(kThreads) sumsq_kernel(const acn_param_desc* _
             for (; i + (kUnroll - 1) * kThreads < n4; i += kUnroll * kThreads) {  // kUnroll loads in flight
                 f4 v[kUnroll];
 #pragma unroll
-                for (int u = 0; u < kUnroll; ++u) v[u] = g4[i + u * kThreads];
+                for (int u = 0; u < kUnroll; ++u) v[u] = ldv(&g4[i + u * kThreads]);
 #pragma unroll
                 for (int u = 0; u < kUnroll; ++u)
                     acc += (double)v[u][0] * v[u][0] + (double)v[u][1] * v[u][1] + (double)v[u][2] * v[u][2] +
                            (double)v[u][3] * v[u][3];
             }
             for (; i < n4; i += kThreads) {
-                const f4 v = g4[i];
+                const f4 v = ldv(&g4[i]);
                 acc += (double)v[0] * v[0] + (double)v[1] * v[1] + (double)v[2] * v[2] + (double)v[3] * v[3];
             }
             for (int64_t i = (n4 << 2) + threadIdx.x; i < n; i += kThreads) acc += (double)g[i] * g[i];
@@ -132,26 +150,26 @@ __device__ __forceinline__ void adam_chunk(float* p, const float* g, float* m, f
             f4 pp[kUnroll], gg[kUnroll], mm[kUnroll], vv[kUnroll];
 #pragma unroll
             for (int u = 0; u < kUnroll; ++u) {
-                pp[u] = p4[i + u * kThreads];
-                gg[u] = g4[i + u * kThreads];
-                mm[u] = m4[i + u * kThreads];
-                vv[u] = v4[i + u * kThreads];
+                pp[u] = ldv(&p4[i + u * kThreads]);
+                gg[u] = ldv(&g4[i + u * kThreads]);
+                mm[u] = ldv(&m4[i + u * kThreads]);
+                vv[u] = ldv(&v4[i + u * kThreads]);
             }
 #pragma unroll
             for (int u = 0; u < kUnroll; ++u) {
                 adam_vec(pp[u], gg[u], mm[u], vv[u], scale, k);
-                p4[i + u * kThreads] = pp[u];
-                m4[i + u * kThreads] = mm[u];
-                v4[i + u * kThreads] = vv[u];
+                stv(&p4[i + u * kThreads], pp[u]);
+                stv(&m4[i + u * kThreads], mm[u]);
+                stv(&v4[i + u * kThreads], vv[u]);
             }
         }
         for (; i < n4; i += kThreads) {
-            f4 pp = p4[i], mm = m4[i], vv = v4[i];
-            const f4 gg = g4[i];
+            f4 pp = ldv(&p4[i]), mm = ldv(&m4[i]), vv = ldv(&v4[i]);
+            const f4 gg = ldv(&g4[i]);
             adam_vec(pp, gg, mm, vv, scale, k);
-            p4[i] = pp;
-            m4[i] = mm;
-            v4[i] = vv;
+            stv(&p4[i], pp);
+            stv(&m4[i], mm);
+            stv(&v4[i], vv);
         }
         done = n4 << 2;
     }
@@ -240,14 +258,14 @@ __global__ void __launch_bounds__(kThreads) sumsq_slots_kernel(const acn_param_d
             for (; i + (kUnroll - 1) * kThreads < n4; i += kUnroll * kThreads) {
                 f4 v[kUnroll];
 #pragma unroll
-                for (int u = 0; u < kUnroll; ++u) v[u] = g4[i + u * kThreads];
+                for (int u = 0; u < kUnroll; ++u) v[u] = ldv(&g4[i + u * kThreads]);
 #pragma unroll
                 for (int u = 0; u < kUnroll; ++u)
                     acc += (double)v[u][0] * v[u][0] + (double)v[u][1] * v[u][1] + (double)v[u][2] * v[u][2] +
                            (double)v[u][3] * v[u][3];
             }
             for (; i < n4; i += kThreads) {
-                const f4 v = g4[i];
+                const f4 v = ldv(&g4[i]);
                 acc += (double)v[0] * v[0] + (double)v[1] * v[1] + (double)v[2] * v[2] + (double)v[3] * v[3];
             }
             for (int64_t i2 = (n4 << 2) + threadIdx.x; i2 < n; i2 += kThreads) acc += (double)g[i2] * g[i2];
@@ -278,30 +296,30 @@ __device__ __forceinline__ void adam_chunk_zero(float* p, float* g, float* m, fl
             f4 pp[kUnroll], gg[kUnroll], mm[kUnroll], vv[kUnroll];
 #pragma unroll
             for (int u = 0; u < kUnroll; ++u) {
-                pp[u] = p4[i + u * kThreads];
-                gg[u] = g4[i + u * kThreads];
-                mm[u] = m4[i + u * kThreads];
-                vv[u] = v4[i + u * kThreads];
+                pp[u] = ldv(&p4[i + u * kThreads]);
+                gg[u] = ldv(&g4[i + u * kThreads]);
+                mm[u] = ldv(&m4[i + u * kThreads]);
+                vv[u] = ldv(&v4[i + u * kThreads]);
             }
 #pragma unroll
             for (int u = 0; u < kUnroll; ++u) {
                 const bool nz = gg[u][0] != 0.0f || gg[u][1] != 0.0f || gg[u][2] != 0.0f || gg[u][3] != 0.0f;
                 adam_vec(pp[u], gg[u], mm[u], vv[u], scale, k);
-                p4[i + u * kThreads] = pp[u];
-                m4[i + u * kThreads] = mm[u];
-                v4[i + u * kThreads] = vv[u];
-                if (nz) g4[i + u * kThreads] = zero;
+                stv(&p4[i + u * kThreads], pp[u]);
+                stv(&m4[i + u * kThreads], mm[u]);
+                stv(&v4[i + u * kThreads], vv[u]);
+                if (nz) stv(&g4[i + u * kThreads], zero);
             }
         }
         for (; i < n4; i += kThreads) {
-            f4 pp = p4[i], mm = m4[i], vv = v4[i];
-            const f4 gg = g4[i];
+            f4 pp = ldv(&p4[i]), mm = ldv(&m4[i]), vv = ldv(&v4[i]);
+            const f4 gg = ldv(&g4[i]);
             const bool nz = gg[0] != 0.0f || gg[1] != 0.0f || gg[2] != 0.0f || gg[3] != 0.0f;
             adam_vec(pp, gg, mm, vv, scale, k);
-            p4[i] = pp;
-            m4[i] = mm;
-            v4[i] = vv;
-            if (nz) g4[i] = zero;
+            stv(&p4[i], pp);
+            stv(&m4[i], mm);
+            stv(&v4[i], vv);
+            if (nz) stv(&g4[i], zero);
         }
         done = n4 << 2;
     }
