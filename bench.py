@@ -390,6 +390,9 @@ def main():
                     help="c4: experts replicated + rays sharded by owning expert (all-gather of rendered rays), or "
                          "one expert per GPU (all-to-all of per-sample records, expert_parallel.py)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--opaque", type=float, default=0.0,
+                    help="c2: add this to every expert's sigma_head bias (density x e^B): a synthetic opaque "
+                         "scene on which early ray termination has rays to stop")
     ap.add_argument("--tau", type=float, default=0.0,
                     help="c2: early ray termination threshold on transmittance (wavefront scan; 0 = off, the "
                          "reference's behaviour); the line then reports the RGB error against tau = 0")
@@ -442,6 +445,10 @@ def main():
                                          occ_conf=occ_conf)
 
     if a.workload == "c2":
+        if a.opaque:
+            with torch.no_grad():
+                for sub in model.submodules:
+                    sub.sigma_head.bias.add_(a.opaque)
         rays = make_rays(scene, gbox, device, a.rays, 1234 + rank)
         samples_per_step = world * a.rays * S
 
@@ -689,9 +696,14 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    mark = os.environ.get("ACN_TRACE_MARK") == "1"   # tools/trace_busy.py: bracket the timed steps in a kernel trace
+    if mark:
+        torch.cuda._sleep(1000)
     t0 = time.perf_counter()
     for _ in range(a.steps):
         out = step()
+    if mark:
+        torch.cuda._sleep(1000)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -900,7 +912,8 @@ def main():
 
     if rank == 0:
         cfg = {"c2": {"workload": "C2: single Instant-NGP expert, 4096 rays x 256 samples per GPU, eval, fused "
-                                  "render_rays" + (f", early ray termination tau={a.tau}" if a.tau > 0 else ""),
+                                  "render_rays" + (f", early ray termination tau={a.tau}" if a.tau > 0 else "")
+                                  + (f", opaque variant (sigma_head bias +{a.opaque})" if a.opaque else ""),
                       "rays_per_gpu": a.rays, "experts": 1},
                "c3": {"workload": "C3: 2x2 Voronoi grid -> 4 experts (soft routing bm 1.05), 4096 rays x 256 samples "
                                   "per GPU sharded by owning expert, RCCL all-gather of rendered rays",
