@@ -34,12 +34,20 @@ constexpr int O_H0 = 0, O_A1 = 33, O_A2 = 98, O_CIN = 163, O_C1 = 195, O_C2 = 26
 constexpr int DS = 275;                 // gradient row: [da1 64][da2 64][dhead 16][dc1 64][dc2 64][drgb 3]
 constexpr int G_A1 = 0, G_A2 = 64, G_HD = 128, G_C1 = 144, G_C2 = 208, G_RGB = 272;
 
-// LDS weight image: row-major, stride = cols + 1 (odd): W0 64x32, W1 64x64, Whead 32x64 (geo rows 0..14,
-// sigma row 15, rows 16..31 zero), Wc0 64x31 (col 31 = 0), Wc1 64x64, Wc2 32x64 (rows 3..31 zero), then
-// the biases (zero-padded to 32 rows likewise).  Padding every layer to whole 32-row tiles lets the
-// kernels read operands unconditionally (no exec-masked LDS loads).
-constexpr int L_W0 = 0, L_W1 = L_W0 + 64 * 33, L_WH = L_W1 + 64 * 65, L_WC0 = L_WH + 32 * 65, L_WC1 = L_WC0 + 64 * 33,
-              L_WC2 = L_WC1 + 64 * 65, L_B0 = L_WC2 + 32 * 65, L_B1 = L_B0 + 64, L_BH = L_B1 + 64, L_BC0 = L_BH + 32,
+#ifndef ACN_TRAIN_F16X3
+#define ACN_TRAIN_F16X3 1  // layer products as the fp32-accurate 3-term fp16 split (0: exact fp32 MFMA)
+#endif
+
+// LDS weight image: row-major, W0 64x32, W1 64x64, Whead 32x64 (geo rows 0..14, sigma row 15, rows
+// 16..31 zero), Wc0 64x31 (col 31 = 0), Wc1 64x64, Wc2 32x64 (rows 3..31 zero), then the biases
+// (zero-padded to 32 rows likewise).  Padding every layer to whole 32-row tiles lets the kernels read
+// operands unconditionally (no exec-masked LDS loads).  fp32 build: one float per weight, odd strides
+// cols + 1 (conflict-free row and column access).  fp16x3 build: each layer region holds a plane of
+// hi = f16(w) then a plane of lo = f16(w - hi), row-major f16 with strides cols + 4 halves (a lane's 4
+// consecutive k-elements are one 8-B read; rows 2 banks apart); biases stay fp32.
+constexpr int S32 = ACN_TRAIN_F16X3 ? 36 : 33, S64 = ACN_TRAIN_F16X3 ? 68 : 65;
+constexpr int L_W0 = 0, L_W1 = L_W0 + 64 * S32, L_WH = L_W1 + 64 * S64, L_WC0 = L_WH + 32 * S64, L_WC1 = L_WC0 + 64 * S32,
+              L_WC2 = L_WC1 + 64 * S64, L_B0 = L_WC2 + 32 * S64, L_B1 = L_B0 + 64, L_BH = L_B1 + 64, L_BC0 = L_BH + 32,
               L_BC1 = L_BC0 + 64, L_BC2 = L_BC1 + 64, L_FLOATS = L_BC2 + 32;
 static_assert(L_FLOATS % 4 == 0, "16-B staging");
 
@@ -68,27 +76,53 @@ __device__ __forceinline__ int64_t fm_index(int64_t m, int nfeat, int f) {
 
 // the padded LDS image, built once per call (one element per thread), then copied by every block of
 // the MLP kernels with 16-B loads
+// weight (row, col) of layer region `layer` (0 W0, 1 W1, 2 head, 3 Wc0, 4 Wc1, 5 Wc2), zero in the padding
+__device__ __forceinline__ float layer_w(const MlpPtrs& p, int layer, int r, int c) {
+    switch (layer) {
+        case 0: return c < 32 ? p.w0[r * 32 + c] : 0.0f;
+        case 1: return c < 64 ? p.w1[r * 64 + c] : 0.0f;
+        case 2: return c < 64 && r < 16 ? (r < 15 ? p.wg[r * 64 + c] : p.wsh[c]) : 0.0f;
+        case 3: return c < 31 ? p.wc0[r * 31 + c] : 0.0f;
+        case 4: return c < 64 ? p.wc1[r * 64 + c] : 0.0f;
+        default: return c < 64 && r < 3 ? p.wc2[r * 64 + c] : 0.0f;
+    }
+}
+
 __device__ __forceinline__ float pack_elem(const MlpPtrs& p, int e) {
-    float v = 0.0f;
-    if (e < L_W1) { const int r = e / 33, c = e % 33; v = c < 32 ? p.w0[r * 32 + c] : 0.0f; }
-    else if (e < L_WH) { const int q = e - L_W1, r = q / 65, c = q % 65; v = c < 64 ? p.w1[r * 64 + c] : 0.0f; }
-    else if (e < L_WC0) {
-        const int q = e - L_WH, r = q / 65, c = q % 65;
-        v = c < 64 && r < 16 ? (r < 15 ? p.wg[r * 64 + c] : p.wsh[c]) : 0.0f;
+    if (e < L_B0) {
+        int layer, base, rows, ld;
+        if (e < L_W1) { layer = 0; base = L_W0; rows = 64; ld = S32; }
+        else if (e < L_WH) { layer = 1; base = L_W1; rows = 64; ld = S64; }
+        else if (e < L_WC0) { layer = 2; base = L_WH; rows = 32; ld = S64; }
+        else if (e < L_WC1) { layer = 3; base = L_WC0; rows = 64; ld = S32; }
+        else if (e < L_WC2) { layer = 4; base = L_WC1; rows = 64; ld = S64; }
+        else { layer = 5; base = L_WC2; rows = 32; ld = S64; }
+        const int q = e - base;
+#if ACN_TRAIN_F16X3
+        // region = hi plane then lo plane, each rows x ld f16 row-major; this dword = halves (2c, 2c + 1)
+        const int plane_dw = rows * ld / 2, part = q / plane_dw, hq = 2 * (q % plane_dw);
+        const int r = hq / ld, c = hq % ld;
+        uint32_t bits = 0;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const float w = layer_w(p, layer, r, c + u);
+            const _Float16 hi = (_Float16)w;
+            const _Float16 v = part ? (_Float16)(w - (float)hi) : hi;
+            bits |= (uint32_t)__builtin_bit_cast(uint16_t, v) << (16 * u);
+        }
+        return __uint_as_float(bits);
+#else
+        (void)rows;
+        return layer_w(p, layer, q / ld, q % ld);
+#endif
     }
-    else if (e < L_WC1) { const int q = e - L_WC0, r = q / 33, c = q % 33; v = c < 31 ? p.wc0[r * 31 + c] : 0.0f; }
-    else if (e < L_WC2) { const int q = e - L_WC1, r = q / 65, c = q % 65; v = c < 64 ? p.wc1[r * 64 + c] : 0.0f; }
-    else if (e < L_B0) {
-        const int q = e - L_WC2, r = q / 65, c = q % 65;
-        v = c < 64 && r < 3 ? p.wc2[r * 64 + c] : 0.0f;
-    }
-    else if (e < L_B1) v = p.b0[e - L_B0];
-    else if (e < L_BH) v = p.b1[e - L_B1];
-    else if (e < L_BC0) { const int q = e - L_BH; v = q < 15 ? p.bg[q] : (q == 15 ? p.bsh[0] : 0.0f); }
-    else if (e < L_BC1) v = p.bc0[e - L_BC0];
-    else if (e < L_BC2) v = p.bc1[e - L_BC1];
-    else { const int q = e - L_BC2; v = q < 3 ? p.bc2[q] : 0.0f; }
-    return v;
+    if (e < L_B1) return p.b0[e - L_B0];
+    if (e < L_BH) return p.b1[e - L_B1];
+    if (e < L_BC0) { const int q = e - L_BH; return q < 15 ? p.bg[q] : (q == 15 ? p.bsh[0] : 0.0f); }
+    if (e < L_BC1) return p.bc0[e - L_BC0];
+    if (e < L_BC2) return p.bc1[e - L_BC1];
+    const int q = e - L_BC2;
+    return q < 3 ? p.bc2[q] : 0.0f;
 }
 
 __global__ void __launch_bounds__(256) mlp_pack_kernel(MlpPtrs p, float* __restrict__ img) {
@@ -111,9 +145,158 @@ __device__ __forceinline__ void stage_weights(const float* __restrict__ img, flo
     for (int e = threadIdx.x; e < L_FLOATS / 4; e += blockDim.x) dst[e] = src[e];
 }
 
+#if ACN_TRAIN_F16X3
+// ---- fp16x3 layers: every product as hi*hi + hi*lo + lo*hi of hi = f16(x), lo = f16(x - hi) on
+// v_mfma_f32_32x32x16_f16 with fp32 accumulation (dropping lo*lo: ~2^-22 relative, like the fused render,
+// DESIGN.md 4).  fp16's range is handled per layer and wave: the layer input (activations, or the
+// output gradients in the backward, which sit far below fp16's normal range) is multiplied by a
+// wave-uniform power of two that brings its max |x| into [2^13, 2^14) and the accumulator is multiplied
+// back -- both exact.  B operand = the input in the accumulator layout of the previous layer: k-element
+// e of lane half h at k-step s is register 8 (s & 1) + e of tile s >> 1, i.e. input row xrow(s, h, e).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x16 mfma_h(const f16x8& a, const f16x8& b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ int xrow(int s, int h, int e) { return 32 * (s >> 1) + 16 * (s & 1) + 8 * (e >> 2) + 4 * h + (e & 3); }
+
+// wave-uniform exponent k with max |x| * 2^k in [2^13, 2^14) (0 for an all-zero / non-finite tile set)
+template <int KT>
+__device__ __forceinline__ int tile_scale_exp(const f32x16 (&X)[KT]) {
+    // max of |x| as the integer order of the magnitude bits (NaN sorts above inf: the tile then gets k = 0)
+    uint32_t m = 0u;
+#pragma unroll
+    for (int t = 0; t < KT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const uint32_t b = __float_as_uint(X[t][r]) & 0x7fffffffu;
+            m = b > m ? b : m;
+        }
+    // within each row of 16 lanes on DPP (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror),
+    // then the four rows through scalar readlanes: no LDS round trip
+    auto dmax = [](uint32_t v, uint32_t w) { return v > w ? v : w; };
+    m = dmax(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0xB1, 0xF, 0xF, false));
+    m = dmax(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x4E, 0xF, 0xF, false));
+    m = dmax(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x141, 0xF, 0xF, false));
+    m = dmax(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x140, 0xF, 0xF, false));
+    uint32_t w = dmax(dmax((uint32_t)__builtin_amdgcn_readlane((int)m, 0), (uint32_t)__builtin_amdgcn_readlane((int)m, 16)),
+                      dmax((uint32_t)__builtin_amdgcn_readlane((int)m, 32), (uint32_t)__builtin_amdgcn_readlane((int)m, 48)));
+    if (w == 0u || w >= 0x7f800000u) return 0;      // all zero, or inf / NaN present
+    // max = f * 2^e, f in [0.5, 1): the biased exponent field gives e (subnormals: treat as 2^-126)
+    const int be = (int)(w >> 23);
+    const int e = (be == 0 ? -126 : be - 127) + 1;
+    int k = 14 - e;
+    return k > 100 ? 100 : (k < -100 ? -100 : k);
+}
+
+// x - f32(half `HI` of the packed pair h), exact, in one v_fma_mix_f32 (the f16 operand converted in the
+// instruction: no separate v_cvt_f32_f16)
+template <int HI>
+__device__ __forceinline__ float sub_f16_part(float x, uint32_t h) {
+    float d;
+    if (HI) asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "=v"(d) : "v"(x), "v"(h));
+    else asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel:[0,0,0] op_sel_hi:[0,0,1]" : "=v"(d) : "v"(x), "v"(h));
+    return d;
+}
+
+template <int KT>
+__device__ __forceinline__ void split_tiles(const f32x16 (&X)[KT], int k, f16x8 (&bh)[2 * KT], f16x8 (&bl)[2 * KT]) {
+    // hi = f16(x) rounded toward zero, lo = f16(x - hi) (the difference is exact): per pair of elements
+    // one packed scale (v_pk_mul_f32), two packed conversions (v_cvt_pkrtz_f16_f32) and two mixed fmas;
+    // hi + lo keeps ~21 bits of x
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    const float sc = ldexpf(1.0f, k);
+    const f32x2 sc2 = {sc, sc};
+#pragma unroll
+    for (int s = 0; s < 2 * KT; ++s) {
+        u32x4 hp, lp;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const f32x2 x = (f32x2){X[s >> 1][8 * (s & 1) + 2 * q], X[s >> 1][8 * (s & 1) + 2 * q + 1]} * sc2;
+            const uint32_t h = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(x[0], x[1]));
+            hp[q] = h;
+            lp[q] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(sub_f16_part<0>(x[0], h),
+                                                                            sub_f16_part<1>(x[1], h)));
+        }
+        bh[s] = __builtin_bit_cast(f16x8, hp);
+        bl[s] = __builtin_bit_cast(f16x8, lp);
+    }
+}
+
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f16x8 cat44(const f16x4& a, const f16x4& b) {
+    return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// Y[to] (rows 32to..) = b + W . X  (W: hi / lo planes of 32*NT padded rows, ld = stride in halves,
+// ROWS = rows of the region; X: KT input tiles)
+template <int NT, int KT, int ROWS>
+__device__ __forceinline__ void fwd_layer(const float* W, int ld, const float* b, const f32x16 (&X)[KT],
+                                          f32x16 (&Y)[NT], int lane) {
+    const int i = lane & 31, h = lane >> 5;
+    const int k = tile_scale_exp<KT>(X);
+    const float usc = ldexpf(1.0f, -k);
+    f16x8 bh[2 * KT], bl[2 * KT];
+    split_tiles<KT>(X, k, bh, bl);
+    const _Float16* Wh = reinterpret_cast<const _Float16*>(W);
+    const _Float16* Wlo = Wh + ROWS * ld;
+#pragma unroll
+    for (int to = 0; to < NT; ++to) {
+        const int ro = (32 * to + i) * ld;
+        f32x16 acc = 0.0f;
+#pragma unroll
+        for (int s = 0; s < 2 * KT; ++s) {
+            const int c0 = ro + 32 * (s >> 1) + 16 * (s & 1) + 4 * h;
+            const f16x8 ahi = cat44(*reinterpret_cast<const f16x4*>(Wh + c0), *reinterpret_cast<const f16x4*>(Wh + c0 + 8));
+            const f16x8 alo = cat44(*reinterpret_cast<const f16x4*>(Wlo + c0), *reinterpret_cast<const f16x4*>(Wlo + c0 + 8));
+            acc = mfma_h(alo, bh[s], acc);
+            acc = mfma_h(ahi, bl[s], acc);
+            acc = mfma_h(ahi, bh[s], acc);
+        }
+        // acc * 2^-k + b in one rounding (the scaling itself is exact)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) Y[to][r] = __builtin_fmaf(acc[r], usc, b[32 * to + rho(r, h)]);
+    }
+}
+
+// dX[ti] (input features 32ti..) = W^T . dY  (W rows = output features; k-steps whose 16 rows are all
+// >= NROW are skipped at compile time, padding rows inside a k-step are zero in the image)
+template <int NT, int KT, int NROW, int ROWS>
+__device__ __forceinline__ void bwd_layer(const float* W, int ld, const f32x16 (&dY)[KT], f32x16 (&dX)[NT],
+                                          int lane) {
+    const int i = lane & 31, h = lane >> 5;
+    const int k = tile_scale_exp<KT>(dY);
+    const float usc = ldexpf(1.0f, -k);
+    f16x8 bh[2 * KT], bl[2 * KT];
+    split_tiles<KT>(dY, k, bh, bl);
+    const _Float16* Wh = reinterpret_cast<const _Float16*>(W);
+    const _Float16* Wlo = Wh + ROWS * ld;
+#pragma unroll
+    for (int ti = 0; ti < NT; ++ti) {
+        f32x16 acc = 0.0f;
+#pragma unroll
+        for (int s = 0; s < 2 * KT; ++s) {
+            if (32 * (s >> 1) + 16 * (s & 1) >= NROW) continue;
+            f16x8 ahi, alo;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const int o = xrow(s, h, e) * ld + 32 * ti + i;
+                ahi[e] = Wh[o];
+                alo[e] = Wlo[o];
+            }
+            acc = mfma_h(alo, bh[s], acc);
+            acc = mfma_h(ahi, bl[s], acc);
+            acc = mfma_h(ahi, bh[s], acc);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dX[ti][r] = acc[r] * usc;
+    }
+}
+#else
 // Y[to] (rows 32to..) = b + W . X  (W: 32*NT padded rows, ld = stride; X: KT input tiles).  The A operands
 // of an output tile are read into registers before its MFMA chain.
-template <int NT, int KT>
+template <int NT, int KT, int ROWS>
 __device__ __forceinline__ void fwd_layer(const float* W, int ld, const float* b, const f32x16 (&X)[KT],
                                           f32x16 (&Y)[NT], int lane) {
     const int i = lane & 31, h = lane >> 5;
@@ -136,7 +319,7 @@ __device__ __forceinline__ void fwd_layer(const float* W, int ld, const float* b
 
 // dX[ti] (input features 32ti..) = W^T . dY  (W rows = output features; k-steps whose rows are all
 // >= NROW are skipped at compile time, the other lane half reads zero padding rows)
-template <int NT, int KT, int NROW>
+template <int NT, int KT, int NROW, int ROWS>
 __device__ __forceinline__ void bwd_layer(const float* W, int ld, const f32x16 (&dY)[KT], f32x16 (&dX)[NT],
                                           int lane) {
     const int i = lane & 31, h = lane >> 5;
@@ -156,6 +339,8 @@ __device__ __forceinline__ void bwd_layer(const float* W, int ld, const f32x16 (
                 if (32 * t + rho(r, 0) < NROW) dX[ti] = mfma32(a[t][r], dY[t][r], dX[ti]);
     }
 }
+
+#endif
 
 template <int NT>
 __device__ __forceinline__ void relu(f32x16 (&Y)[NT]) {
@@ -223,21 +408,21 @@ __device__ __forceinline__ void tile_forward(const float* Wl, const float* h0, c
                                              f32x16 (&Rg)[1]) {
     const int h = lane >> 5;
     load_tiles<1>(h0, 32, 0, 32, m, ok, h, X0);
-    fwd_layer<2, 1>(Wl + L_W0, 33, Wl + L_B0, X0, A1, lane);
+    fwd_layer<2, 1, 64>(Wl + L_W0, S32, Wl + L_B0, X0, A1, lane);
     relu<2>(A1);
-    fwd_layer<2, 2>(Wl + L_W1, 65, Wl + L_B1, A1, A2, lane);
+    fwd_layer<2, 2, 64>(Wl + L_W1, S64, Wl + L_B1, A1, A2, lane);
     relu<2>(A2);
-    fwd_layer<1, 2>(Wl + L_WH, 65, Wl + L_BH, A2, Hd, lane);
+    fwd_layer<1, 2, 32>(Wl + L_WH, S64, Wl + L_BH, A2, Hd, lane);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int f = rho(r, h);
         Cin[0][r] = f < 15 ? Hd[0][r] : ((ok && f < 31) ? sh[m * 16 + (f - 15)] : 0.0f);
     }
-    fwd_layer<2, 1>(Wl + L_WC0, 33, Wl + L_BC0, Cin, C1, lane);
+    fwd_layer<2, 1, 64>(Wl + L_WC0, S32, Wl + L_BC0, Cin, C1, lane);
     relu<2>(C1);
-    fwd_layer<2, 2>(Wl + L_WC1, 65, Wl + L_BC1, C1, C2, lane);
+    fwd_layer<2, 2, 64>(Wl + L_WC1, S64, Wl + L_BC1, C1, C2, lane);
     relu<2>(C2);
-    fwd_layer<1, 2>(Wl + L_WC2, 65, Wl + L_BC2, C2, Rg, lane);
+    fwd_layer<1, 2, 32>(Wl + L_WC2, S64, Wl + L_BC2, C2, Rg, lane);
 }
 
 __global__ void __launch_bounds__(256) mlp_fwd_kernel(const float* __restrict__ img, const float* __restrict__ h0,
@@ -319,21 +504,21 @@ __global__ void __launch_bounds__(256) mlp_bwd_kernel(const float* __restrict__ 
         }
         store_fm<1>(gsave, DS, G_RGB, 3, m, ok, h, dRg);
         f32x16 G2[2], G1[2], Gc[1], mask[2];
-        bwd_layer<2, 1, 3>(Wl + L_WC2, 65, dRg, G2, lane);
+        bwd_layer<2, 1, 3, 32>(Wl + L_WC2, S64, dRg, G2, lane);
         load_fm<2>(save, SS, O_C2, 64, m, ok, h, mask);
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
             for (int r = 0; r < 16; ++r) G2[t][r] = mask[t][r] > 0.0f ? G2[t][r] : 0.0f;
         store_fm<2>(gsave, DS, G_C2, 64, m, ok, h, G2);
-        bwd_layer<2, 2, 64>(Wl + L_WC1, 65, G2, G1, lane);
+        bwd_layer<2, 2, 64, 64>(Wl + L_WC1, S64, G2, G1, lane);
         load_fm<2>(save, SS, O_C1, 64, m, ok, h, mask);
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
             for (int r = 0; r < 16; ++r) G1[t][r] = mask[t][r] > 0.0f ? G1[t][r] : 0.0f;
         store_fm<2>(gsave, DS, G_C1, 64, m, ok, h, G1);
-        bwd_layer<1, 2, 64>(Wl + L_WC0, 33, G1, Gc, lane);  // d cin: rows 0..14 = d geo (SH rows dropped)
+        bwd_layer<1, 2, 64, 64>(Wl + L_WC0, S32, G1, Gc, lane);  // d cin: rows 0..14 = d geo (SH rows dropped)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int f = rho(r, h);
@@ -341,21 +526,21 @@ __global__ void __launch_bounds__(256) mlp_bwd_kernel(const float* __restrict__ 
         }
         store_fm<1>(gsave, DS, G_HD, 16, m, ok, h, dHd);
         f32x16 GA2[2], GA1[2], GH[1];
-        bwd_layer<2, 1, 16>(Wl + L_WH, 65, dHd, GA2, lane);
+        bwd_layer<2, 1, 16, 32>(Wl + L_WH, S64, dHd, GA2, lane);
         load_fm<2>(save, SS, O_A2, 64, m, ok, h, mask);
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
             for (int r = 0; r < 16; ++r) GA2[t][r] = mask[t][r] > 0.0f ? GA2[t][r] : 0.0f;
         store_fm<2>(gsave, DS, G_A2, 64, m, ok, h, GA2);
-        bwd_layer<2, 2, 64>(Wl + L_W1, 65, GA2, GA1, lane);
+        bwd_layer<2, 2, 64, 64>(Wl + L_W1, S64, GA2, GA1, lane);
         load_fm<2>(save, SS, O_A1, 64, m, ok, h, mask);
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
             for (int r = 0; r < 16; ++r) GA1[t][r] = mask[t][r] > 0.0f ? GA1[t][r] : 0.0f;
         store_fm<2>(gsave, DS, G_A1, 64, m, ok, h, GA1);
-        bwd_layer<1, 2, 64>(Wl + L_W0, 33, GA1, GH, lane);
+        bwd_layer<1, 2, 64, 64>(Wl + L_W0, S32, GA1, GH, lane);
         if (gh0) store_tiles<1>(gh0, 32, 0, 32, m, ok, h, GH);
     }
 }
@@ -400,6 +585,9 @@ __device__ __forceinline__ void stage_put(float* st, int row0, const f32x16 (&T)
 template <int NCB>
 __device__ __forceinline__ void dw_blocks(const float* st, int arow, int xrow, f32x4 (&acc)[NCB], float& bsum,
                                           int lane) {
+#if ACN_DIAG_NODW  // diagnostic build only: no weight-gradient contraction
+    return;
+#endif
     const int i = lane & 15, q = lane >> 4;
     const float* pa = st + (arow + i) * SW + 32 * q;
     const float* pb = st + (xrow + i) * SW + 32 * q;
@@ -495,17 +683,17 @@ __device__ __forceinline__ void dw_round(const float* W, float* st, const float*
     stage_layer<1, 2>(st, dRg, C2, w, lane);
     dw_blocks<1>(st, 0, X_ROW + 16 * w, a.aWC2, a.bWC2, lane);
     f32x16 G2[2], G1[2], Gc[1];
-    bwd_layer<2, 1, 3>(W + L_WC2, 65, dRg, G2, lane);
+    bwd_layer<2, 1, 3, 32>(W + L_WC2, S64, dRg, G2, lane);
     relu_mask<2>(G2, C2);
     // colour layer 1, 64 x 64: row block w
     stage_layer<2, 2>(st, G2, C1, w, lane);
     dw_blocks<4>(st, 16 * w, X_ROW, a.aWC1, a.bWC1, lane);
-    bwd_layer<2, 2, 64>(W + L_WC1, 65, G2, G1, lane);
+    bwd_layer<2, 2, 64, 64>(W + L_WC1, S64, G2, G1, lane);
     relu_mask<2>(G1, C1);
     // colour layer 0, 64 x 31 (input 31 = zero column): row block w
     stage_layer<2, 1>(st, G1, Cin, w, lane);
     dw_blocks<2>(st, 16 * w, X_ROW, a.aWC0, a.bWC0, lane);
-    bwd_layer<1, 2, 64>(W + L_WC0, 33, G1, Gc, lane);  // d cin: rows 0..14 = d geo (SH rows dropped)
+    bwd_layer<1, 2, 64, 64>(W + L_WC0, S32, G1, Gc, lane);  // d cin: rows 0..14 = d geo (SH rows dropped)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int f = rho(r, h);
@@ -515,12 +703,12 @@ __device__ __forceinline__ void dw_round(const float* W, float* st, const float*
     stage_layer<1, 2>(st, dHd, A2, w, lane);
     dw_blocks<1>(st, 0, X_ROW + 16 * w, a.aHD, a.bHD, lane);
     f32x16 GA2[2], GA1[2], GH[1];
-    bwd_layer<2, 1, 16>(W + L_WH, 65, dHd, GA2, lane);
+    bwd_layer<2, 1, 16, 32>(W + L_WH, S64, dHd, GA2, lane);
     relu_mask<2>(GA2, A2);
     // sigma trunk 1, 64 x 64: row block w
     stage_layer<2, 2>(st, GA2, A1, w, lane);
     dw_blocks<4>(st, 16 * w, X_ROW, a.aW1, a.bW1, lane);
-    bwd_layer<2, 2, 64>(W + L_W1, 65, GA2, GA1, lane);
+    bwd_layer<2, 2, 64, 64>(W + L_W1, S64, GA2, GA1, lane);
     relu_mask<2>(GA1, A1);
     // sigma trunk 0, 64 x 32: row block w
     f32x16 X0[1];
@@ -528,7 +716,7 @@ __device__ __forceinline__ void dw_round(const float* W, float* st, const float*
     stage_layer<2, 1>(st, GA1, X0, w, lane);
     dw_blocks<2>(st, 16 * w, X_ROW, a.aW0, a.bW0, lane);
     if (gh0) {
-        bwd_layer<1, 2, 64>(W + L_W0, 33, GA1, GH, lane);
+        bwd_layer<1, 2, 64, 64>(W + L_W0, S32, GA1, GH, lane);
         store_tiles<1>(gh0, 32, 0, 32, m, ok, h, GH);
     }
 }

@@ -5,7 +5,7 @@ Compiles csrc/render.hip to gfx950 assembly and counts the instructions of the l
 import collections, re, subprocess, sys
 pat = sys.argv[1] if len(sys.argv) > 1 else "render_kernelILi1ELi1ELi0E"
 extra = sys.argv[2:]
-src = "adaptive_city_nerf_amd/csrc/render.hip"
+src = __import__("os").environ.get("ASM_SRC", "adaptive_city_nerf_amd/csrc/render.hip")
 subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
                 "-mcode-object-version=5", "--offload-device-only", "-S", src, "-o", "/tmp/acn_render.s", *extra],
                check=True, stderr=subprocess.DEVNULL)
