@@ -32,6 +32,16 @@ def main():
     win = hi - lo
     print(f"window {win / steps / 1e6:.3f} ms/step, kernels {busy / steps / 1e6:.3f} ms/step, "
           f"wall/kernel {win / max(busy, 1):.4f}, launches in window {len(ivs)}")
+    top = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+    if top:
+        agg = {}
+        for a, b, n in rows:
+            if b > lo and a < hi and "sleep" not in n.lower() and "spin" not in n.lower():
+                t = agg.setdefault(n[:100], [0, 0])
+                t[0] += b - a
+                t[1] += 1
+        for n, (d, c) in sorted(agg.items(), key=lambda x: -x[1][0])[:top]:
+            print(f"{d / steps / 1e6:9.3f} ms/step {c / steps:8.1f}/step {d / c / 1e3:9.1f} us  {n}")
 
 
 if __name__ == "__main__":
