@@ -171,11 +171,11 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_f2(const float* __restrict__
 template <int INTERP, int PPL>
 __global__ void __launch_bounds__(256) hashgrid_bwd_rle(const float* __restrict__ x01, int64_t M,
                                                         const float* __restrict__ gout, Res32 res, int L,
-                                                        int log2T, float* __restrict__ gtable) {
+                                                        int log2T, float* __restrict__ gtable, int l0) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int l = (int)(wave % L);
-    const int64_t chunk = wave / L;
+    const int l = l0 + (int)(wave % (L - l0));  // levels l0..L-1 (the coarser ones: hashgrid_bwd_merge)
+    const int64_t chunk = wave / (L - l0);
     const int64_t m0 = (chunk * 4 + (lane >> 4)) * PPL;
     if (m0 >= M) return;
     const int f = lane & 1, bx = (lane >> 1) & 1, by = (lane >> 3) & 1, bz = (lane >> 2) & 1;
@@ -252,16 +252,16 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_pairs(const float* __restric
                                                           const int32_t* __restrict__ pidx,
                                                           const int64_t* __restrict__ seg, int K,
                                                           const float* __restrict__ gout, GradTables gt, Res32 res,
-                                                          int L, int log2T) {
+                                                          int L, int log2T, int l0) {
     const int lane = threadIdx.x & 63;
     const int64_t M = seg[K];
-    const int64_t nwaves = ((M + 4 * PPL - 1) / (4 * PPL)) * L;
+    const int64_t nwaves = ((M + 4 * PPL - 1) / (4 * PPL)) * (L - l0);
     const int f = lane & 1, bx = (lane >> 1) & 1, by = (lane >> 3) & 1, bz = (lane >> 2) & 1;
     const uint32_t mask = (uint32_t)((1ull << log2T) - 1ull);
     for (int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; wave < nwaves;
          wave += ((int64_t)gridDim.x * blockDim.x) >> 6) {
-        const int l = (int)(wave % L);
-        const int64_t chunk = wave / L;
+        const int l = l0 + (int)(wave % (L - l0));
+        const int64_t chunk = wave / (L - l0);
         const int64_t m0 = (chunk * 4 + (lane >> 4)) * PPL;
         const float r = (float)res.v[l];
         const int64_t base = ((int64_t)l << log2T) * 2 + f;
@@ -295,6 +295,133 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_pairs(const float* __restric
         }
         if (cur) unsafeAtomicAdd(cur, acc);
     }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Coarse levels of the table-gradient scatter, merged per workgroup.  At the coarse
+// levels many samples -- of one ray and of neighbouring rays -- add into the same rows, but a lane's run
+// merge only sees one corner of one sample stream.  Here a workgroup takes a chunk of C_l consecutive
+// slots at one level, accumulates every (slot, corner) contribution into an LDS hash table keyed by
+// (table, 64-B segment) with LDS float atomics, then flushes each touched segment as 16 consecutive
+// floats (4 segments per wave-instruction = the full-rate shape of MI355X_MICROARCH.md 'Global float
+// atomics').  Memory-side requests fall from one per (run, corner pair) to one per distinct segment of
+// the chunk.  A full table (more distinct segments than kMergeNE) falls back to direct atomics for the
+// overflowing contributions.  Sums stay fp32; their order is as unordered as the atomics they replace.
+constexpr int kMergeLogNE = 10, kMergeNE = 1 << kMergeLogNE;
+constexpr uint32_t kMergeEmpty = 0xffffffffu;
+struct MergeCfg {
+    int LM;                   // levels 0 .. LM-1 are merged here
+    int clog2[ACN_MAX_LEVELS];  // chunk of 2^clog2[l] slots per workgroup item at level l
+};
+
+template <int INTERP>
+__global__ void __launch_bounds__(256) hashgrid_bwd_merge(const float* __restrict__ x01, const int32_t* __restrict__ pk,
+                                                          const int32_t* __restrict__ pidx,
+                                                          const int64_t* __restrict__ seg, int K, int64_t Mhost,
+                                                          const float* __restrict__ gout, GradTables gt, Res32 res,
+                                                          int L, int log2T, MergeCfg cfg) {
+    __shared__ uint32_t keys[kMergeNE];
+    __shared__ __attribute__((aligned(16))) float vals[kMergeNE * 16];
+    const int64_t M = seg ? seg[K] : Mhost;
+    int64_t items = 0;
+    for (int l = 0; l < cfg.LM; ++l) items += (M + (1ll << cfg.clog2[l]) - 1) >> cfg.clog2[l];
+    const uint32_t mask = (uint32_t)((1ull << log2T) - 1ull);
+    for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
+        int l = 0;
+        int64_t rem = it;
+        for (; l < cfg.LM - 1; ++l) {
+            const int64_t n = (M + (1ll << cfg.clog2[l]) - 1) >> cfg.clog2[l];
+            if (rem < n) break;
+            rem -= n;
+        }
+        const int64_t m0 = rem << cfg.clog2[l], m1 = min(M, m0 + (1ll << cfg.clog2[l]));
+        for (int i = threadIdx.x; i < kMergeNE; i += blockDim.x) keys[i] = kMergeEmpty;
+        for (int i = threadIdx.x; i < kMergeNE * 4; i += blockDim.x)
+            reinterpret_cast<float4*>(vals)[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        __syncthreads();
+        const float r = (float)res.v[l];
+        // lanes as in hashgrid_bwd_rle: (stream q, corner, feature f); a lane run-merges 16 consecutive
+        // slots of its stream and adds each finished run into the LDS table (LDS atomics on runs, not on
+        // every contribution: coarse cells repeat along a ray)
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+        const int f = lane & 1, bx = (lane >> 1) & 1, by = (lane >> 3) & 1, bz = (lane >> 2) & 1;
+        auto add_run = [&](uint32_t kx, uint32_t row, float v) {
+            const uint32_t key = (kx << 24) | (row >> 3);
+            uint32_t h = (key * 2654435761u) >> (32 - kMergeLogNE);
+            for (int probe = 0; probe < 32; ++probe) {
+                uint32_t cur = keys[h];
+                if (cur == kMergeEmpty) cur = atomicCAS(&keys[h], kMergeEmpty, key);
+                if (cur == kMergeEmpty || cur == key) {
+                    atomicAdd(&vals[h * 16 + (row & 7) * 2 + f], v);
+                    return;
+                }
+                h = (h + 1) & (kMergeNE - 1);
+            }
+            unsafeAtomicAdd(gt.t[kx] + (((int64_t)l << log2T) + row) * 2 + f, v);  // table crowded
+        };
+        for (int64_t sb = m0 + (int64_t)w * 64; sb < m1; sb += (int64_t)nw * 64) {
+            const int64_t mb = sb + (lane >> 4) * 16;
+            uint32_t cur_row = 0xffffffffu, cur_k = 0;
+            float acc = 0.0f;
+            for (int i = 0; i < 16; ++i) {
+                const int64_t m = mb + i;
+                if (m >= m1) break;
+                if (pidx && pidx[m] < 0) continue;
+                const uint32_t kx = pk ? (uint32_t)pk[m] : 0u;
+                const float sx = x01[3 * m] * r, sy = x01[3 * m + 1] * r, sz = x01[3 * m + 2] * r;
+                const float fx = floorf(sx), fy = floorf(sy), fz = floorf(sz);
+                float wx = sx - fx, wy = sy - fy, wz = sz - fz;
+                if (INTERP == 2) {
+                    wx = (wx * wx) * (3.0f - 2.0f * wx);
+                    wy = (wy * wy) * (3.0f - 2.0f * wy);
+                    wz = (wz * wz) * (3.0f - 2.0f * wz);
+                }
+                const uint32_t xi = (uint32_t)(int)fx + (uint32_t)bx;
+                const uint32_t yi = (uint32_t)(int)fy * acn::kP1 + (by ? acn::kP1 : 0u);
+                const uint32_t zi = (uint32_t)(int)fz * acn::kP2 + (bz ? acn::kP2 : 0u);
+                const uint32_t row = (xi ^ yi ^ zi) & mask;
+                const float gv = ((gout[(m * L + l) * 2 + f] * (bz ? wz : 1.0f - wz)) * (by ? wy : 1.0f - wy)) *
+                                 (bx ? wx : 1.0f - wx);
+                if (row == cur_row && kx == cur_k) {
+                    acc += gv;
+                } else {
+                    if (cur_row != 0xffffffffu) add_run(cur_k, cur_row, acc);
+                    cur_row = row;
+                    cur_k = kx;
+                    acc = gv;
+                }
+            }
+            if (cur_row != 0xffffffffu) add_run(cur_k, cur_row, acc);
+        }
+        __syncthreads();
+        // flush: 16 consecutive lanes per segment
+        for (int i = threadIdx.x; i < kMergeNE * 16; i += blockDim.x) {
+            const uint32_t key = keys[i >> 4];
+            const float v = vals[i];
+            if (key != kMergeEmpty && v != 0.0f)
+                unsafeAtomicAdd(gt.t[key >> 24] + ((int64_t)l << log2T) * 2 + (int64_t)(key & 0xffffffu) * 16 + (i & 15), v);
+        }
+        __syncthreads();
+    }
+}
+
+#ifndef ACN_HASH_BWD_MERGE
+// coarse levels merged per workgroup (0: every level on the run-merge kernel).  Off: measured slower on
+// the C5 step (hash backward 0.36 -> 0.76 / 0.79 / 0.89 ms merging 3 / 6 / 8 levels, tools/ab_c5.sh,
+// DESIGN.md 4g) -- a coarse chunk is one workgroup's serial work (few items in flight), and the runs of
+// neighbouring lanes collide on the same LDS entries
+#define ACN_HASH_BWD_MERGE 0
+#endif
+
+MergeCfg merge_cfg(int L, int log2T) {
+    MergeCfg c{};
+    c.LM = ACN_HASH_BWD_MERGE < L ? ACN_HASH_BWD_MERGE : L;
+    if (log2T > 27) c.LM = 0;  // the LDS key holds a 24-bit segment index
+    // chunks sized so a chunk's distinct segments stay well under kMergeNE at the reference grid
+    // (tools/hash_bwd_analysis.py on the C5 batch: level 0 ~13k segments per 104k slots ... level 5 ~230k)
+    const int lg[8] = {12, 11, 10, 9, 8, 8, 7, 7};
+    for (int l = 0; l < ACN_MAX_LEVELS; ++l) c.clog2[l] = l < 8 ? lg[l] : 7;
+    return c;
 }
 
 template <int DEGREE>
@@ -353,10 +480,22 @@ extern "C" int acn_hashgrid_bwd(const float* x01, int64_t M, const float* grad_o
     hipStream_t s = (hipStream_t)stream;
     if (F == 2 && interp != 0 && ACN_HASH_BWD_PPL > 0) {
         constexpr int PPL = ACN_HASH_BWD_PPL > 0 ? ACN_HASH_BWD_PPL : 1;
-        const int64_t waves = ((M + 4 * PPL - 1) / (4 * PPL)) * L;
-        const dim3 grid((unsigned)((waves + 3) / 4)), block(256);
-        if (interp == 1) hipLaunchKernelGGL((hashgrid_bwd_rle<1, PPL>), grid, block, 0, s, x01, M, grad_out, r, L, log2T, grad_table);
-        else hipLaunchKernelGGL((hashgrid_bwd_rle<2, PPL>), grid, block, 0, s, x01, M, grad_out, r, L, log2T, grad_table);
+        const MergeCfg mc = merge_cfg(L, log2T);
+        if (mc.LM > 0) {
+            GradTables t{};
+            t.t[0] = grad_table;
+            int64_t items = 0;
+            for (int l = 0; l < mc.LM; ++l) items += (M + (1ll << mc.clog2[l]) - 1) >> mc.clog2[l];
+            const dim3 mgrid((unsigned)(items < 1024 ? items : 1024)), block(256);
+            if (interp == 1) hipLaunchKernelGGL(hashgrid_bwd_merge<1>, mgrid, block, 0, s, x01, nullptr, nullptr, nullptr, 1, M, grad_out, t, r, L, log2T, mc);
+            else hipLaunchKernelGGL(hashgrid_bwd_merge<2>, mgrid, block, 0, s, x01, nullptr, nullptr, nullptr, 1, M, grad_out, t, r, L, log2T, mc);
+        }
+        if (mc.LM < L) {
+            const int64_t waves = ((M + 4 * PPL - 1) / (4 * PPL)) * (L - mc.LM);
+            const dim3 grid((unsigned)((waves + 3) / 4)), block(256);
+            if (interp == 1) hipLaunchKernelGGL((hashgrid_bwd_rle<1, PPL>), grid, block, 0, s, x01, M, grad_out, r, L, log2T, grad_table, mc.LM);
+            else hipLaunchKernelGGL((hashgrid_bwd_rle<2, PPL>), grid, block, 0, s, x01, M, grad_out, r, L, log2T, grad_table, mc.LM);
+        }
         return acn_check_launch("acn_hashgrid_bwd");
     }
     if (F == 2 && interp != 0) {
@@ -423,7 +562,14 @@ extern "C" int acn_hashgrid_bwd_pairs(const float* x01, const int32_t* pk, const
     for (int k = 0; k < K; ++k) t.t[k] = grad_tables[k];
     const dim3 grid(2048), block(256);
     hipStream_t s = (hipStream_t)stream;
-    if (interp == 1) hipLaunchKernelGGL((hashgrid_bwd_pairs<1, 16>), grid, block, 0, s, x01, pk, pidx, seg, K, grad_out, t, r, L, log2T);
-    else hipLaunchKernelGGL((hashgrid_bwd_pairs<2, 16>), grid, block, 0, s, x01, pk, pidx, seg, K, grad_out, t, r, L, log2T);
+    const MergeCfg mc = merge_cfg(L, log2T);
+    if (mc.LM > 0) {  // fixed grid (graph-replayable): items are counted from the device slot count
+        if (interp == 1) hipLaunchKernelGGL(hashgrid_bwd_merge<1>, dim3(512), block, 0, s, x01, pk, pidx, seg, K, (int64_t)0, grad_out, t, r, L, log2T, mc);
+        else hipLaunchKernelGGL(hashgrid_bwd_merge<2>, dim3(512), block, 0, s, x01, pk, pidx, seg, K, (int64_t)0, grad_out, t, r, L, log2T, mc);
+    }
+    if (mc.LM < L) {
+        if (interp == 1) hipLaunchKernelGGL((hashgrid_bwd_pairs<1, 16>), grid, block, 0, s, x01, pk, pidx, seg, K, grad_out, t, r, L, log2T, mc.LM);
+        else hipLaunchKernelGGL((hashgrid_bwd_pairs<2, 16>), grid, block, 0, s, x01, pk, pidx, seg, K, grad_out, t, r, L, log2T, mc.LM);
+    }
     return acn_check_launch("acn_hashgrid_bwd_pairs");
 }
