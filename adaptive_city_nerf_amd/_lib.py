@@ -100,6 +100,8 @@ SIGNATURES = {
     "acn_background_fwd": ([vp, i64, vp, vp, vp], C.c_int),
     "acn_volume_render_bwd": ([vp, vp, vp, i64, i32, f32, vp, vp, vp, vp, vp, vp, vp], C.c_int),
     "acn_grad_sumsq": ([vp, vp, i64, vp, vp, vp], C.c_int),
+    "acn_mse_linear_fwd": ([vp, vp, i64, vp, vp], C.c_int),
+    "acn_mse_linear_bwd": ([vp, vp, i64, vp, vp, vp], C.c_int),
     "acn_clip_coef": ([vp, f32, vp, vp], C.c_int),
     "acn_adam_step": ([vp, vp, i64, vp, i32, vp, vp], C.c_int),
     "acn_optim_plan_device": ([vp, i32, vp, vp, i64, vp], C.c_int),

@@ -87,7 +87,7 @@ int bits_for(uint64_t n) {
 
 size_t sort_temp_bytes(int64_t R, int end_bit) {
     size_t bytes = 0;
-    rocprim::radix_sort_pairs((void*)nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+    (void)rocprim::radix_sort_pairs((void*)nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                               (const float2*)nullptr, (float2*)nullptr, (size_t)R, 0u, (unsigned)end_bit);
     return bytes;
 }

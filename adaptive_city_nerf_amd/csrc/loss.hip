@@ -1,0 +1,72 @@
+// loss.hip -- the training loss of the adaptation / meta-training steps on gfx950:
+//   nerfs/losses.py:10-32 compute_mse_loss = F.mse_loss(*color_space_transformer(pred, gt, "linear"))
+//   nerfs/color_space.py:13-19, 22-66 (gt.clamp(0,1) -> srgb_to_linear -> clamp(0,1); pred.clamp(0,1))
+// The reference evaluates this as ~11 elementwise / reduction launches forward and ~5 backward per
+// render; in a meta-training step (108 renders) those 5-us launches cost more than the MLP forward.
+// Here: one single-workgroup launch forward (the batch is thousands of rays; per-thread double partial
+// sums, one fixed reduction order: deterministic) and one elementwise launch backward.
+// Float semantics follow the torch ops: scalars as float (12.92f, 0.055f, 1.055f, 0.04045f), powf with
+// the float exponent, clamps that pass NaN through, and mse_loss_backward's double `2 / numel` factor.
+#include "acn_internal.h"
+
+namespace {
+
+constexpr int kThreads = 1024;
+
+__device__ __forceinline__ float clamp01(float x) { return x < 0.0f ? 0.0f : (x > 1.0f ? 1.0f : x); }
+
+__device__ __forceinline__ float srgb_to_linear(float x) {
+    return x <= 0.04045f ? x / 12.92f : powf((x + 0.055f) / 1.055f, 2.4f);
+}
+
+// gt (sRGB in [0,1] after the clamp) -> linear, clamped again
+__device__ __forceinline__ float gt_linear(float g) { return clamp01(srgb_to_linear(clamp01(g))); }
+
+__global__ void __launch_bounds__(kThreads) mse_linear_fwd_kernel(const float* __restrict__ pred,
+                                                                  const float* __restrict__ gt, int64_t n,
+                                                                  float* __restrict__ loss) {
+    __shared__ double red[kThreads / 64];
+    double acc = 0.0;
+    for (int64_t e = threadIdx.x; e < n; e += kThreads) {
+        const float d = clamp01(pred[e]) - gt_linear(gt[e]);
+        acc += (double)(d * d);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int i = 0; i < kThreads / 64; ++i) t += red[i];
+        loss[0] = (float)(t / (double)n);
+    }
+}
+
+// d loss / d pred: mse_loss_backward (2 / numel * (input - target) * grad_output, in double) through the
+// clamp's backward (gradient where 0 <= pred <= 1)
+__global__ void __launch_bounds__(256) mse_linear_bwd_kernel(const float* __restrict__ pred, const float* __restrict__ gt,
+                                                             int64_t n, const float* __restrict__ g_loss,
+                                                             float* __restrict__ g_pred) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    const float p = pred[e];
+    const float d = clamp01(p) - gt_linear(gt[e]);
+    const float g = (float)((2.0 / (double)n) * (double)d * (double)g_loss[0]);
+    g_pred[e] = (p >= 0.0f && p <= 1.0f) ? g : 0.0f;
+}
+
+}  // namespace
+
+extern "C" int acn_mse_linear_fwd(const float* pred, const float* gt, int64_t n, float* loss, void* stream) {
+    ACN_REQUIRE(n >= 1 && pred && gt && loss, "acn_mse_linear_fwd: bad arguments");
+    hipLaunchKernelGGL(mse_linear_fwd_kernel, dim3(1), dim3(kThreads), 0, (hipStream_t)stream, pred, gt, n, loss);
+    return acn_check_launch("acn_mse_linear_fwd");
+}
+
+extern "C" int acn_mse_linear_bwd(const float* pred, const float* gt, int64_t n, const float* g_loss, float* g_pred,
+                                  void* stream) {
+    ACN_REQUIRE(n >= 1 && pred && gt && g_loss && g_pred, "acn_mse_linear_bwd: bad arguments");
+    hipLaunchKernelGGL(mse_linear_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       pred, gt, n, g_loss, g_pred);
+    return acn_check_launch("acn_mse_linear_bwd");
+}

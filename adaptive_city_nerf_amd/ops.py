@@ -301,6 +301,25 @@ def volume_render_bwd(rgb_sigma: torch.Tensor, t_vals: torch.Tensor, bg_rgb: Opt
     return g_rs, g_bg
 
 
+def mse_linear_fwd(pred: torch.Tensor, gt: torch.Tensor) -> torch.Tensor:
+    """compute_mse_loss's loss in color_space 'linear' (acn_mse_linear_fwd): a 0-d device tensor."""
+    p, g = _f32(pred).reshape(-1), _f32(gt).reshape(-1)
+    if p.numel() != g.numel() or p.numel() == 0:
+        raise ValueError(f"mse_linear: pred / gt sizes {p.numel()} / {g.numel()}")
+    out = torch.empty((), device=p.device, dtype=torch.float32)
+    check(_lib.lib().acn_mse_linear_fwd(ptr(p), ptr(g), p.numel(), ptr(out), stream_of(p)), "acn_mse_linear_fwd")
+    return out
+
+
+def mse_linear_bwd(pred: torch.Tensor, gt: torch.Tensor, g_loss: torch.Tensor) -> torch.Tensor:
+    p, g = _f32(pred).reshape(-1), _f32(gt).reshape(-1)
+    gl = _f32(g_loss.reshape(1))
+    out = torch.empty_like(p)
+    check(_lib.lib().acn_mse_linear_bwd(ptr(p), ptr(g), p.numel(), ptr(gl), ptr(out), stream_of(p)),
+          "acn_mse_linear_bwd")
+    return out.view(pred.shape)
+
+
 def get_rays_image(H: int, W: int, fx: float, fy: float, cx: float, cy: float, c2w: torch.Tensor,
                    aabb: Optional[torch.Tensor], device, center_pixels: bool = True, near: Optional[float] = None,
                    far: Optional[float] = None, near_far_override=None, apply_clamp: bool = True):

@@ -57,7 +57,8 @@ def encoding_frozen(enabled: bool = True):
     """Within this context, differentiable single-expert renders evaluate the hash grid without autograd:
     for first-order inner loops (FOMAML / Reptile task_adapt, meta_core.py:14-67), which differentiate
     w.r.t. the fast MLP weights only, the encoding's backward branch (dL/dh0, the table scatter) is dead
-    work.  The values are unchanged.  Thread-local."""
+    work (the values are unchanged).  The shared background head, not a fast weight either, then runs as
+    its fused HIP launch (values within fp32 rounding of the torch chain).  Thread-local."""
     prev = getattr(_GRAPH_MODE, "frozen_encoding", False)
     _GRAPH_MODE.frozen_encoding = bool(enabled)
     try:
@@ -331,7 +332,11 @@ def render_rays_stratified(model, rays: Tensor, ray_samples: int, params=None, a
             h0 = sub.xyz_encoder(x01)
         ws = [t.contiguous() for t in sub._mlp_tensors(params).values()]
         rgb_sigma = _FusedMLPFn.apply(h0.contiguous(), sh, *ws).view(N, ray_samples, 4)
-        bg_rgb = _get_bg_rgb(model, rays[:, 3:6], params, rgb_sigma, N=N, bg_color_default=bg_color_default)
+        if getattr(_GRAPH_MODE, "frozen_encoding", False):
+            with torch.no_grad():  # nor is the shared background head a fast weight: one fused HIP launch
+                bg_rgb = _get_bg_rgb(model, rays[:, 3:6], params, rgb_sigma, N=N, bg_color_default=bg_color_default)
+        else:
+            bg_rgb = _get_bg_rgb(model, rays[:, 3:6], params, rgb_sigma, N=N, bg_color_default=bg_color_default)
         return volume_render(rgb_sigma, t_vals, bg_rgb=bg_rgb, raw_rgb=False, raw_sigma=False,
                              sigma_scale=sigma_scale)
     if _routed_train_ok(model, rays, active_module):

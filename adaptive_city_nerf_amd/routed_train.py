@@ -34,12 +34,11 @@ from typing import Optional
 
 import numpy as np
 import torch
-import torch.nn.functional as F
 
 from . import _lib, ops
 from ._lib import ACN_OPTIM_CHUNK, AcnError, acn_adam_group, acn_mlp, check, ptr
-from .color_space import color_space_transformer
 from .optim import FusedAdam, bump_versions
+from .train import mse_color_loss
 
 # Optional timing hook (bench.py): when set to a list, an eager step appends recorded HIP events
 # bracketing the Adam launch (adam_step_slots) on the current stream.
@@ -233,8 +232,7 @@ class RoutedAdaptStep:
         with torch.enable_grad():
             bg = self.model.background_color(self.rays[:, 3:6])
             rgb = volume_render(rs, self.t, bg_rgb=bg)[0]
-            pred, gt = color_space_transformer(rgb, self.rgbs, color_space=self.P.color_space)
-            loss = F.mse_loss(pred, gt, reduction="mean")
+            loss = mse_color_loss(rgb, self.rgbs, self.P.color_space)
             grads = torch.autograd.grad(loss, [rs] + self.bg_params)
         self.loss.copy_(loss.detach())
         for g, buf in zip(grads[1:], self.gbg):

@@ -22,9 +22,36 @@ from typing import Dict, Iterable, Optional
 import torch
 import torch.nn.functional as F
 
+from . import ops
 from .color_space import color_space_transformer
 from .optim import FusedAdam
 from .ray_rendering import render_rays
+
+
+class _MSELinearFn(torch.autograd.Function):
+    """F.mse_loss(*color_space_transformer(pred, gt, 'linear')) as two HIP launches (loss.hip) instead of
+    ~16 elementwise / reduction kernels; same float semantics (clamps pass NaN, powf, float scalars)."""
+
+    @staticmethod
+    def forward(ctx, pred, gt):
+        ctx.save_for_backward(pred, gt)
+        return ops.mse_linear_fwd(pred, gt)
+
+    @staticmethod
+    def backward(ctx, g):
+        pred, gt = ctx.saved_tensors
+        return ops.mse_linear_bwd(pred, gt, g.detach()), None
+
+
+def mse_color_loss(pred_rgb, gt_rgb, color_space: str, reduction: str = "mean"):
+    """F.mse_loss(*color_space_transformer(pred, gt, color_space)) (losses.py:10-32)."""
+    from .ray_rendering import _second_order
+    if (str(color_space).lower() == "linear" and reduction == "mean" and pred_rgb.is_cuda
+            and pred_rgb.dtype == torch.float32 and pred_rgb.numel() > 0 and pred_rgb.shape == gt_rgb.shape
+            and not _second_order()):
+        return _MSELinearFn.apply(pred_rgb, gt_rgb.to(pred_rgb.device, torch.float32))
+    pred_rgb, gt_rgb = color_space_transformer(pred_rgb, gt_rgb, color_space=color_space)
+    return F.mse_loss(pred_rgb, gt_rgb, reduction=reduction)
 
 
 def compute_mse_loss(P, model, data, params=None, active_module=None, reduction: str = "mean", **render_kwargs):
@@ -33,8 +60,7 @@ def compute_mse_loss(P, model, data, params=None, active_module=None, reduction:
     rays = data["rays"]
     pred_rgb, *_ = render_rays(model, rays, ray_samples=P.ray_samples, params=params, active_module=active_module,
                                chunk=P.chunk_points, **render_kwargs)
-    pred_rgb, gt_rgb = color_space_transformer(pred_rgb, gt_rgb, color_space=P.color_space)
-    return F.mse_loss(pred_rgb, gt_rgb, reduction=reduction)
+    return mse_color_loss(pred_rgb, gt_rgb, P.color_space, reduction)
 
 
 def adapt_step(P, base, rays, rgbs, optimizer, active_module=None, grad_clip: Optional[float] = 1.0,

@@ -519,6 +519,15 @@ int acn_mlp_train_fwd_pairs(const float* h0, const float* sh, const int64_t* seg
 int acn_mlp_train_bwd_dw_pairs(const float* h0, const float* sh, const float* out, const float* gout,
                                const int64_t* seg, int K, void* workspace, float* dw, float* gh0, void* stream);
 
+/* ---- training loss (round 2): nerfs/losses.py:10-32 compute_mse_loss with color_space="linear"
+ * (nerfs/color_space.py:13-19, 22-66): loss = mean((clamp(pred,0,1) - clamp(srgb_to_linear(clamp(gt,0,1)),0,1))^2)
+ * over n = 3 * rays floats.  fwd: one workgroup, double partials, deterministic; writes loss[0].
+ * bwd: g_pred = 2/n * (clamp(pred) - gt_lin) * g_loss[0] where 0 <= pred <= 1, else 0 (mse_loss_backward
+ * through clamp's backward).  g_loss is a DEVICE scalar (graph-replayable). */
+int acn_mse_linear_fwd(const float* pred, const float* gt, int64_t n, float* loss, void* stream);
+int acn_mse_linear_bwd(const float* pred, const float* gt, int64_t n, const float* g_loss, float* g_pred,
+                       void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,10 +1,8 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py tests/test_train.py tests/test_hash_det.py -m gpu -q --timeout 240 --timeout-method thread -k "hash or adapt or routed or det" > gpurun_out/pt_merge.log 2>&1
+timeout -k 10 900 python -u -m pytest tests/test_loss_gpu.py tests/test_train.py tests/test_meta_gpu.py tests/test_graph_gpu.py tests/test_expert_parallel.py tests/test_mlp_train_gpu.py -m gpu -q --timeout 240 --timeout-method thread > gpurun_out/pt_loss.log 2>&1
 echo pytest rc=$?
-for v in base nomerge m3 m8; do
-  lib=adaptive_city_nerf_amd/libacnerf.so; [ $v = base ] || lib=build_variants/libacnerf_$v.so
-  ACNERF_LIB=$lib timeout -k 10 120 python -u tools/hash_det_time.py > gpurun_out/hdt_$v.txt 2>&1 || exit 1
-done
-bash tools/ab_c5.sh gpurun_out/ab_merge.txt base nomerge m3 m8 base
+timeout -k 10 300 python -u bench.py --workload meta --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/meta_loss.json 2> gpurun_out/meta_loss.err &&
+timeout -k 10 300 python -u bench.py --workload c5 --steps 30 --warmup 5 --no-cpu-baseline > gpurun_out/c5_loss.json 2> gpurun_out/c5_loss.err
+echo rc=$?
