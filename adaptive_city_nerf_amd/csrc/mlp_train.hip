@@ -190,37 +190,29 @@ __device__ __forceinline__ int tile_scale_exp(const f32x16 (&X)[KT]) {
     return k > 100 ? 100 : (k < -100 ? -100 : k);
 }
 
-// x - f32(half `HI` of the packed pair h), exact, in one v_fma_mix_f32 (the f16 operand converted in the
-// instruction: no separate v_cvt_f32_f16)
-template <int HI>
-__device__ __forceinline__ float sub_f16_part(float x, uint32_t h) {
-    float d;
-    if (HI) asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "=v"(d) : "v"(x), "v"(h));
-    else asm("v_fma_mix_f32 %0, %1, 1.0, -%2 op_sel:[0,0,0] op_sel_hi:[0,0,1]" : "=v"(d) : "v"(x), "v"(h));
-    return d;
-}
-
 template <int KT>
 __device__ __forceinline__ void split_tiles(const f32x16 (&X)[KT], int k, f16x8 (&bh)[2 * KT], f16x8 (&bl)[2 * KT]) {
-    // hi = f16(x) rounded toward zero, lo = f16(x - hi) (the difference is exact): per pair of elements
-    // one packed scale (v_pk_mul_f32), two packed conversions (v_cvt_pkrtz_f16_f32) and two mixed fmas;
-    // hi + lo keeps ~21 bits of x
+    // hi = f16(x), lo = f16(x - hi) (the difference is exact), both rounded to nearest even; per pair of
+    // elements the compiler emits one packed scale (v_pk_mul_f32), two packed conversions
+    // (v_cvt_pk_f16_f32), two f16 -> f32 conversions and one packed subtraction -- no inline assembly, so
+    // the compiler's hazard tracking sees every instruction.  hi + lo keeps ~22 bits of x (a truncating
+    // hi, v_cvt_pkrtz, doubles lo and quadruples the dropped lo*lo term).
     typedef float f32x2 __attribute__((ext_vector_type(2)));
+    typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
     const float sc = ldexpf(1.0f, k);
     const f32x2 sc2 = {sc, sc};
 #pragma unroll
     for (int s = 0; s < 2 * KT; ++s) {
-        u32x4 hp, lp;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const f32x2 x = (f32x2){X[s >> 1][8 * (s & 1) + 2 * q], X[s >> 1][8 * (s & 1) + 2 * q + 1]} * sc2;
-            const uint32_t h = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(x[0], x[1]));
-            hp[q] = h;
-            lp[q] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(sub_f16_part<0>(x[0], h),
-                                                                            sub_f16_part<1>(x[1], h)));
+            const f16x2 h = __builtin_convertvector(x, f16x2);
+            const f16x2 l = __builtin_convertvector(x - __builtin_convertvector(h, f32x2), f16x2);
+            bh[s][2 * q] = h[0];
+            bh[s][2 * q + 1] = h[1];
+            bl[s][2 * q] = l[0];
+            bl[s][2 * q + 1] = l[1];
         }
-        bh[s] = __builtin_bit_cast(f16x8, hp);
-        bl[s] = __builtin_bit_cast(f16x8, lp);
     }
 }
 

@@ -51,8 +51,15 @@ def test_graphed_adapt_step_matches_eager(active_module):
     g.sync_state()
     assert abs(float(la) - float(lb)) <= 1e-5 * abs(float(la)) + 1e-8
     for (na, pa), (nb, pb) in zip(ma.named_parameters(), mb.named_parameters()):
-        np.testing.assert_allclose(pb.detach().cpu().numpy(), pa.detach().cpu().numpy(), rtol=1e-5, atol=1e-7,
-                                   err_msg=na)
+        a, b = pa.detach().cpu().numpy(), pb.detach().cpu().numpy()
+        if na.endswith("hash_table"):
+            # the table gradient is a float-atomic scatter-add: rows whose 7-step gradient sits at the
+            # summation-order noise level get Adam steps (~lr / sqrt(v)-normalised) that depend on that
+            # noise, in two eager runs as much as here; a few per million rows, bounded by 1e-4
+            bad = np.abs(a - b) > 1e-5 * np.abs(a) + 1e-7
+            assert bad.mean() <= 1e-5 and np.abs(a - b).max() <= 1e-4, (na, int(bad.sum()), np.abs(a - b).max())
+        else:
+            np.testing.assert_allclose(b, a, rtol=1e-5, atol=1e-7, err_msg=na)
     for pa, pb in zip(ma.parameters(), mb.parameters()):
         sa, sb = oa.state.get(pa, {}), ob.state.get(pb, {})
         assert ("step" in sa) == ("step" in sb)

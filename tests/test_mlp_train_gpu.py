@@ -114,3 +114,42 @@ def test_split_path_still_matches_composed():
         test_fused_mlp_matches_composed(1000)
     finally:
         _FusedMLPFn.DW_FUSED = old
+
+
+@pytest.mark.parametrize("wscale,gscale,tscale", [(1.0, 1e-10, 1.0), (1.0, 1e6, 1.0), (12.0, 1.0, 1.0),
+                                                  (1.0, 1e-8, 0.005)])
+def test_fused_mlp_extreme_ranges(wscale, gscale, tscale):
+    """The fp16x3 layers' per-layer power-of-two scaling (mlp_train.hip): output gradients of 1e-10 or 1e6,
+    activations pushed past fp16's 65504 by large weights, and hash features at the reference's default
+    table scale (|h0| ~ 1e-3): outputs and gradients still match the composed fp32 chain."""
+    from adaptive_city_nerf_amd.ray_rendering import second_order
+    sub = _expert()
+    with torch.no_grad():
+        for n_, p in sub.named_parameters():
+            if n_.endswith("hash_table"):
+                p.mul_(tscale)
+            elif "weight" in n_:
+                p.mul_(wscale)
+    n = 2048
+    xd = _inputs(sub, n, 11)
+    gw = gscale * torch.randn(n, 4, device="cuda", generator=torch.Generator(device="cuda").manual_seed(5))
+    params = list(sub.parameters())
+    out_f = sub(xd)
+    gf = torch.autograd.grad((out_f * gw).sum(), params, allow_unused=True)
+    with second_order():
+        out_c = sub(xd)
+        gc = torch.autograd.grad((out_c * gw).sum(), params, allow_unused=True)
+    # large weights make every layer's sum cancel: the split keeps ~2^-22 per product against fp32's
+    # 2^-24 per fma, so the ill-conditioned case gets a correspondingly wider bound
+    tol = 2e-5 if wscale == 1.0 else 2e-4
+    a, b = out_f.detach().double().cpu().numpy(), out_c.detach().double().cpu().numpy()
+    scale_o = np.maximum(np.abs(b).max(axis=0), 1e-30)
+    assert np.isfinite(a).all()
+    assert (np.abs(a - b) / scale_o).max() <= tol
+    for (name, _), x, y in zip(sub.named_parameters(), gf, gc):
+        if y is None:
+            continue
+        x, y = x.detach().double().cpu().numpy(), y.detach().double().cpu().numpy()
+        scale = max(np.abs(y).max(), 1e-300)
+        assert np.isfinite(x).all(), name
+        assert np.abs(x - y).max() <= 2.5 * tol * scale, (name, np.abs(x - y).max(), scale)

@@ -162,8 +162,9 @@ def check_adapt_fixture(tag, step_fn, make_opt=None):
                 ref = d[gkey]
                 scale = float(np.abs(ref).max()) + 1e-12
                 # from the second step on, the parameters carry the Adam sensitivity described below, so
-                # the gradients are evaluated at slightly different points
-                gtol = 1e-4 if step == 0 else 1e-3
+                # the gradients are evaluated at slightly different points; the spread scales with the
+                # MLP's per-product rounding (fp16x3 split ~2^-22 vs fp32's 2^-24, mlp_train.hip)
+                gtol = 1e-4 if step == 0 else 3e-3
                 np.testing.assert_allclose(p.grad.detach().cpu().numpy(), ref, rtol=0, atol=gtol * scale)
             else:
                 assert p.grad is None or float(p.grad.abs().max()) == 0.0, name
