@@ -1419,14 +1419,21 @@ __device__ __forceinline__ uint32_t spread6(uint32_t v) {
     return v;
 }
 // workgroup-wide reductions (1024 threads = 16 waves) of 3 sums / 4 maxima; every thread gets the result
+// DPP within each 16-lane row (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror), then the
+// four row results through scalar readlanes: no LDS round trips (a ds_bpermute shuffle ladder costs six
+// dependent LDS latencies per value)
 template <int OP>
 __device__ __forceinline__ float wave_reduce(float v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const float o = __shfl_xor(v, off);
-        v = OP == 0 ? v + o : fmaxf(v, o);
-    }
-    return v;
+    auto op = [](float a, float b) { return OP == 0 ? a + b : fmaxf(a, b); };
+    v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false)));
+    v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false)));
+    v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false)));
+    v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false)));
+    const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+    const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+    const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+    const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+    return op(op(r0, r1), op(r2, r3));
 }
 template <int OP>
 __device__ __forceinline__ void block_reduce3(float& a, float& b, float& c, float* red) {
@@ -1526,12 +1533,15 @@ __global__ void __launch_bounds__(1024) ray_order_kernel(const float* __restrict
 #pragma unroll
     for (int c = 0; c < CPT; ++c) h[c] = hist[tid * CPT + c], run += h[c];
     const int lane = tid & 63;
+    // inclusive wave scan on DPP: row_shr 1/2/4/8 inside each 16-lane row, then row_bcast:15 / :31 carry
+    // the row totals upward (gfx9-family DPP)
     int incl = run;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int o = __shfl_up(incl, off);
-        if (lane >= off) incl += o;
-    }
+    incl += __builtin_amdgcn_update_dpp(0, incl, 0x111, 0xF, 0xF, true);
+    incl += __builtin_amdgcn_update_dpp(0, incl, 0x112, 0xF, 0xF, true);
+    incl += __builtin_amdgcn_update_dpp(0, incl, 0x114, 0xF, 0xF, true);
+    incl += __builtin_amdgcn_update_dpp(0, incl, 0x118, 0xF, 0xF, true);
+    incl += __builtin_amdgcn_update_dpp(0, incl, 0x142, 0xA, 0xF, false);
+    incl += __builtin_amdgcn_update_dpp(0, incl, 0x143, 0xC, 0xF, false);
     if (lane == 63) wsum[tid >> 6] = incl;
     __syncthreads();
     int base = incl - run;
