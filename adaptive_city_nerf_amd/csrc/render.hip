@@ -735,6 +735,25 @@ struct RayAcc {
     float r, g, b, d, a;
 };
 
+#ifndef ACN_COMPOSITE_DPP
+#define ACN_COMPOSITE_DPP 1
+#endif
+// a double moved by one DPP control (both 32-bit halves); lanes without a source (or outside ROWMASK)
+// get the multiplicative identity 1.0
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, ROWMASK, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0x3ff00000, (int)(uint32_t)(b >> 32), CTRL, ROWMASK, 0xF, false);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ double lane_f64(double v, int l) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
 __device__ __forceinline__ double wave32_sum(double v) {
 #pragma unroll
     for (int off = 16; off >= 1; off >>= 1) v += __shfl_xor(v, off, 32);
@@ -750,6 +769,18 @@ __device__ __forceinline__ void composite_tile(RayAcc& acc, bool valid, float cr
     float x = (1.0f - alpha) + 1e-10f;
     if (!valid) { x = 1.0f; alpha = 0.0f; }
     double incl = (double)x;
+#if ACN_COMPOSITE_DPP
+    // inclusive product over the 32 samples of each lane half on DPP (no LDS): row_shr 1/2/4/8 inside
+    // each 16-lane row, then row_bcast:15 carries row 0's (row 2's) product into row 1 (row 3); lanes
+    // without a source keep the identity 1.0.  Both halves hold the same samples, so lane 31 = lane 63.
+    incl *= dpp_f64<0x111, 0xF>(incl);
+    incl *= dpp_f64<0x112, 0xF>(incl);
+    incl *= dpp_f64<0x114, 0xF>(incl);
+    incl *= dpp_f64<0x118, 0xF>(incl);
+    incl *= dpp_f64<0x142, 0xA>(incl);
+    double excl = dpp_f64<0x138, 0xF>(incl);  // wave_shr:1
+    if (j == 0) excl = 1.0;
+#else
 #pragma unroll
     for (int off = 1; off < 32; off <<= 1) {
         const double y = __shfl_up(incl, off, 32);
@@ -757,6 +788,7 @@ __device__ __forceinline__ void composite_tile(RayAcc& acc, bool valid, float cr
     }
     double excl = __shfl_up(incl, 1, 32);
     if (j == 0) excl = 1.0;
+#endif
     const float Ts = (float)(acc.T * excl);
     const float w = alpha * Ts;
     if (wout) *wout = w;
@@ -767,7 +799,11 @@ __device__ __forceinline__ void composite_tile(RayAcc& acc, bool valid, float cr
         acc.d += w * t;
         acc.a += w;
     }
+#if ACN_COMPOSITE_DPP
+    acc.T = acc.T * lane_f64(incl, 31);
+#else
     acc.T = acc.T * __shfl(incl, 31, 32);
+#endif
 }
 
 __device__ __forceinline__ void finish_ray(const RayAcc& acc, float& r, float& g, float& b, float& d, float& a) {

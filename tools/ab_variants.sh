@@ -6,7 +6,8 @@ OUT=$1; shift
 mkdir -p gpurun_out
 : > $OUT
 for v in "$@"; do
-  ACNERF_LIB=build_variants/libacnerf_$v.so timeout -k 10 120 python bench.py --steps 50 --warmup 5 --cpu-seconds 0.3 \
+  lib=adaptive_city_nerf_amd/libacnerf.so; [ "$v" = base ] || lib=build_variants/libacnerf_$v.so
+  ACNERF_LIB=$lib timeout -k 10 120 python bench.py --steps 50 --warmup 5 --cpu-seconds 0.3 \
       > gpurun_out/ab_$v.json 2> gpurun_out/ab_$v.err || { echo "variant $v failed"; exit 1; }
   python - "$v" >> $OUT <<'PY'
 import json, sys
