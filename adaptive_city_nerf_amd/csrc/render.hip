@@ -754,10 +754,27 @@ __device__ __forceinline__ double lane_f64(double v, int l) {
     return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 
+// sum over the 32 lanes of half 0 (both halves hold the same per-sample partials): DPP inside each
+// 16-lane row, then rows 0 and 1 through readlanes (a wave-uniform result)
+template <int CTRL>
+__device__ __forceinline__ double dpp_add_f64(double v) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, 0xF, 0xF, false);
+    return v + __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
 __device__ __forceinline__ double wave32_sum(double v) {
+#if ACN_COMPOSITE_DPP
+    v = dpp_add_f64<0xB1>(v);   // quad_perm [1,0,3,2]
+    v = dpp_add_f64<0x4E>(v);   // quad_perm [2,3,0,1]
+    v = dpp_add_f64<0x141>(v);  // row_half_mirror
+    v = dpp_add_f64<0x140>(v);  // row_mirror
+    return lane_f64(v, 0) + lane_f64(v, 16);
+#else
 #pragma unroll
     for (int off = 16; off >= 1; off >>= 1) v += __shfl_xor(v, off, 32);
     return v;
+#endif
 }
 
 __device__ __forceinline__ void composite_tile(RayAcc& acc, bool valid, float cr, float cg, float cb, float sig,
@@ -837,8 +854,19 @@ __device__ __forceinline__ void background(const BgArgs& bg, float dx, float dy,
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         float v = lane < bg.hidden ? hv * bg.w2[c * bg.hidden + lane] : 0.0f;
+#if ACN_COMPOSITE_DPP
+        v = v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+        v = v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
+        v = v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
+        v = v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));
+        v = (__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)) +
+             __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16))) +
+            (__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)) +
+             __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48)));
+#else
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+#endif
         out[c] = sigmoidf_(v + bg.b2[c]);
     }
 }
@@ -1037,9 +1065,10 @@ __device__ __forceinline__ uint32_t ray_expert_mask(const FieldCfg& cfg, int rou
             }
         }
     }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) m |= __shfl_xor(m, off);
-    return m;
+    uint32_t any = 0u;  // OR over the wave: one ballot per expert (scalar), no LDS round trips
+    for (int k = 0; k < cfg.K; ++k)
+        if (__ballot((m >> k) & 1u) != 0ull) any |= 1u << k;
+    return any;
 }
 
 #ifndef ACN_SLOTS_BAND
