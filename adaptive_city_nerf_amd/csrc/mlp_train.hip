@@ -560,6 +560,169 @@ __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+template <int NT>
+__device__ __forceinline__ void relu_mask(f32x16 (&G)[NT], const f32x16 (&Y)[NT]) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) G[t][r] = Y[t][r] > 0.0f ? G[t][r] : 0.0f;
+}
+
+#ifndef ACN_DW_F16X3
+// weight-gradient contraction on the fp16x3 split as well.  Off: measured slower (fused backward 352 ->
+// 383 us at M = 384k, meta step 79.1 -> 82.8 ms): with one wave per SIMD the dW phase is bound by the
+// staging (split + two f16 planes written per element) and LDS traffic, not by the fp32 MFMAs it saves
+#define ACN_DW_F16X3 0
+#endif
+
+struct StageScale {
+    int kY, kX;  // power-of-two exponents the staged dY / X carry (0: unscaled fp32 stage)
+};
+
+#if ACN_DW_F16X3
+// ---- fp16x3 weight gradients.  The stage holds f16 planes (hi, then lo) of [144 rows][SH halves]:
+// rows 0..63 dY, 64..127 X, row 128 ones (rows 129..143 zero) -- the bias sums come out of the MFMA as
+// the contraction with the ones row.  dY and X are scaled by workgroup-uniform powers of two (the
+// contraction mixes the four waves' samples): each wave publishes its max |dY| and max |X| before the
+// stage barrier and all waves take the maximum of the four.  Per round and block the 128-sample
+// contraction is 8 k-steps of v_mfma_f32_16x16x16_f16 x 3 products into a temporary, added to the
+// persistent fp32 accumulator times 2^-(kY + kX).
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+constexpr int SH = 136;                   // stage row stride (halves): 128 samples + 8, 16-B aligned rows
+constexpr int ST_ROWS = 144, ST_ONES = 128;
+constexpr int ST_FLOATS = 2 * ST_ROWS * SH / 2;  // two f16 planes
+__device__ __forceinline__ f32x4 mfma16h(const f16x4& a, const f16x4& b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0);
+}
+typedef f32x4 BiasAcc;
+
+__device__ __forceinline__ void stage_init(float* st) {  // the ones row (both planes zero elsewhere there)
+    _Float16* hp = reinterpret_cast<_Float16*>(st);
+    _Float16* lp = hp + ST_ROWS * SH;
+    for (int e = threadIdx.x; e < (ST_ROWS - ST_ONES) * SH; e += blockDim.x) {
+        hp[ST_ONES * SH + e] = (_Float16)(e < SH ? 1.0f : 0.0f);
+        lp[ST_ONES * SH + e] = (_Float16)0.0f;
+    }
+}
+
+// max |x| bits of this wave's tiles (wave-uniform; DPP + readlanes)
+template <int NT>
+__device__ __forceinline__ uint32_t wave_absmax_bits(const f32x16 (&T)[NT]) {
+    uint32_t m = 0u;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const uint32_t b = __float_as_uint(T[t][r]) & 0x7fffffffu;
+            m = b > m ? b : m;
+        }
+    auto dmax = [](uint32_t v, uint32_t w) { return v > w ? v : w; };
+    m = dmax(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0xB1, 0xF, 0xF, false));
+    m = dmax(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x4E, 0xF, 0xF, false));
+    m = dmax(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x141, 0xF, 0xF, false));
+    m = dmax(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x140, 0xF, 0xF, false));
+    return dmax(dmax((uint32_t)__builtin_amdgcn_readlane((int)m, 0), (uint32_t)__builtin_amdgcn_readlane((int)m, 16)),
+                dmax((uint32_t)__builtin_amdgcn_readlane((int)m, 32), (uint32_t)__builtin_amdgcn_readlane((int)m, 48)));
+}
+__device__ __forceinline__ int exp_for_bits(uint32_t w) {  // as tile_scale_exp
+    if (w == 0u || w >= 0x7f800000u) return 0;
+    const int be = (int)(w >> 23);
+    const int k = 14 - ((be == 0 ? -126 : be - 127) + 1);
+    return k > 100 ? 100 : (k < -100 ? -100 : k);
+}
+
+template <int NT>
+__device__ __forceinline__ void stage_put(float* st, int row0, const f32x16 (&T)[NT], int k, int w, int lane) {
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+    _Float16* hp = reinterpret_cast<_Float16*>(st);
+    _Float16* lp = hp + ST_ROWS * SH;
+    const int j = lane & 31, h = lane >> 5;
+    const float sc = ldexpf(1.0f, k);
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+            const f32x2 x = (f32x2){T[t][r], T[t][r + 1]} * (f32x2){sc, sc};
+            const f16x2 hi = __builtin_convertvector(x, f16x2);
+            const f16x2 lo = __builtin_convertvector(x - __builtin_convertvector(hi, f32x2), f16x2);
+            const int o0 = (row0 + 32 * t + rho(r, h)) * SH + 32 * w + j, o1 = (row0 + 32 * t + rho(r + 1, h)) * SH + 32 * w + j;
+            hp[o0] = hi[0];
+            hp[o1] = hi[1];
+            lp[o0] = lo[0];
+            lp[o1] = lo[1];
+        }
+}
+
+// acc[n] += dY[16 rows from arow] . X[16 features from xrow + 16 n]^T over the 128 staged samples,
+// bacc (column 0) += the dY rows' sums; lane (i = l & 15, q = l >> 4) supplies k-elements = samples
+// 32 q + 4 t + 0..3 of k-step t
+template <int NCB>
+__device__ __forceinline__ void dw_blocks(const float* st, int arow, int xrow, f32x4 (&acc)[NCB], BiasAcc& bacc,
+                                          StageScale sc, int lane) {
+#if ACN_DIAG_NODW  // diagnostic build only: no weight-gradient contraction
+    return;
+#endif
+    const _Float16* hp = reinterpret_cast<const _Float16*>(st);
+    const _Float16* lp = hp + ST_ROWS * SH;
+    const int i = lane & 15, q = lane >> 4;
+    const int oa = (arow + i) * SH + 32 * q, ob = (xrow + i) * SH + 32 * q, oo = (ST_ONES + i) * SH + 32 * q;
+    f32x4 tmp[NCB], tb = 0.0f;
+#pragma unroll
+    for (int n = 0; n < NCB; ++n) tmp[n] = 0.0f;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+        const f16x4 ah = *reinterpret_cast<const f16x4*>(hp + oa + 4 * t);
+        const f16x4 al = *reinterpret_cast<const f16x4*>(lp + oa + 4 * t);
+        const f16x4 on = *reinterpret_cast<const f16x4*>(hp + oo + 4 * t);
+        tb = mfma16h(al, on, tb);
+        tb = mfma16h(ah, on, tb);
+#pragma unroll
+        for (int n = 0; n < NCB; ++n) {
+            const f16x4 bh = *reinterpret_cast<const f16x4*>(hp + ob + 16 * n * SH + 4 * t);
+            const f16x4 bl = *reinterpret_cast<const f16x4*>(lp + ob + 16 * n * SH + 4 * t);
+            tmp[n] = mfma16h(al, bh, tmp[n]);
+            tmp[n] = mfma16h(ah, bl, tmp[n]);
+            tmp[n] = mfma16h(ah, bh, tmp[n]);
+        }
+    }
+    const float ua = ldexpf(1.0f, -sc.kY), uab = ldexpf(1.0f, -(sc.kY + sc.kX));
+#pragma unroll
+    for (int n = 0; n < NCB; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[n][r] = __builtin_fmaf(tmp[n][r], uab, acc[n][r]);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bacc[r] = __builtin_fmaf(tb[r], ua, bacc[r]);
+}
+
+// one layer's stage round: publish this wave's maxima, barrier (previous readers done, maxima visible),
+// put dY / X scaled by the workgroup maxima, barrier
+template <int NO, int NI>
+__device__ __forceinline__ StageScale stage_layer(float* st, const f32x16 (&dY)[NO], const f32x16 (&X)[NI], int w,
+                                                  int lane) {
+    __shared__ uint32_t smax[8];
+    const uint32_t my = wave_absmax_bits<NO>(dY), mx = wave_absmax_bits<NI>(X);
+    if (lane == 0) {
+        smax[w] = my;
+        smax[4 + w] = mx;
+    }
+    __syncthreads();
+    uint32_t ay = 0u, ax = 0u;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        ay = smax[v] > ay ? smax[v] : ay;
+        ax = smax[4 + v] > ax ? smax[4 + v] : ax;
+    }
+    const StageScale sc{exp_for_bits(ay), exp_for_bits(ax)};
+    stage_put<NO>(st, 0, dY, sc.kY, w, lane);
+    stage_put<NI>(st, X_ROW, X, sc.kX, w, lane);
+    __syncthreads();
+    return sc;
+}
+#else
+constexpr int ST_FLOATS = 128 * SW;
+typedef float BiasAcc;
+__device__ __forceinline__ void stage_init(float*) {}
 // rows of accumulator-layout tiles -> stage[row0 + feature][32 * w + sample] (all 32 * NT rows; rows past a
 // layer's width hold zeros in the tiles)
 template <int NT>
@@ -576,7 +739,7 @@ __device__ __forceinline__ void stage_put(float* st, int row0, const f32x16 (&T)
 // lane's share of the bias row sum (the A operand is dY itself).
 template <int NCB>
 __device__ __forceinline__ void dw_blocks(const float* st, int arow, int xrow, f32x4 (&acc)[NCB], float& bsum,
-                                          int lane) {
+                                          StageScale, int lane) {
 #if ACN_DIAG_NODW  // diagnostic build only: no weight-gradient contraction
     return;
 #endif
@@ -598,23 +761,17 @@ __device__ __forceinline__ void dw_blocks(const float* st, int arow, int xrow, f
     }
 }
 
-template <int NT>
-__device__ __forceinline__ void relu_mask(f32x16 (&G)[NT], const f32x16 (&Y)[NT]) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) G[t][r] = Y[t][r] > 0.0f ? G[t][r] : 0.0f;
-}
-
 // one layer's stage round: barrier (previous readers done), put dY / X, barrier
 template <int NO, int NI>
-__device__ __forceinline__ void stage_layer(float* st, const f32x16 (&dY)[NO], const f32x16 (&X)[NI], int w,
-                                            int lane) {
+__device__ __forceinline__ StageScale stage_layer(float* st, const f32x16 (&dY)[NO], const f32x16 (&X)[NI], int w,
+                                                  int lane) {
     __syncthreads();
     stage_put<NO>(st, 0, dY, w, lane);
     stage_put<NI>(st, X_ROW, X, w, lane);
     __syncthreads();
+    return StageScale{0, 0};
 }
+#endif
 
 // D (16x16x4 layout: lane l, reg r = row 4 (l >> 4) + r, col l & 15) of one block -> dst rows / cols
 template <typename Put>
@@ -633,7 +790,7 @@ __device__ __forceinline__ int seg_expert(const int64_t* seg, int K, int64_t p) 
 // the 14 weight-gradient blocks of one wave (56 accumulator registers) and its bias partial sums
 struct DwAcc {
     f32x4 aWC2[1], aWC1[4], aWC0[2], aHD[1], aW1[4], aW0[2];
-    float bWC2, bWC1, bWC0, bHD, bW1, bW0;
+    BiasAcc bWC2, bWC1, bWC0, bHD, bW1, bW0;
 };
 
 __device__ __forceinline__ void dw_zero(DwAcc& a) {
@@ -672,19 +829,25 @@ __device__ __forceinline__ void dw_round(const float* W, float* st, const float*
         }
     }
     // colour head 3 x 64: column block w, rows 0..15 (0..2 live)
-    stage_layer<1, 2>(st, dRg, C2, w, lane);
-    dw_blocks<1>(st, 0, X_ROW + 16 * w, a.aWC2, a.bWC2, lane);
+    {
+        const StageScale sc = stage_layer<1, 2>(st, dRg, C2, w, lane);
+        dw_blocks<1>(st, 0, X_ROW + 16 * w, a.aWC2, a.bWC2, sc, lane);
+    }
     f32x16 G2[2], G1[2], Gc[1];
     bwd_layer<2, 1, 3, 32>(W + L_WC2, S64, dRg, G2, lane);
     relu_mask<2>(G2, C2);
     // colour layer 1, 64 x 64: row block w
-    stage_layer<2, 2>(st, G2, C1, w, lane);
-    dw_blocks<4>(st, 16 * w, X_ROW, a.aWC1, a.bWC1, lane);
+    {
+        const StageScale sc = stage_layer<2, 2>(st, G2, C1, w, lane);
+        dw_blocks<4>(st, 16 * w, X_ROW, a.aWC1, a.bWC1, sc, lane);
+    }
     bwd_layer<2, 2, 64, 64>(W + L_WC1, S64, G2, G1, lane);
     relu_mask<2>(G1, C1);
     // colour layer 0, 64 x 31 (input 31 = zero column): row block w
-    stage_layer<2, 1>(st, G1, Cin, w, lane);
-    dw_blocks<2>(st, 16 * w, X_ROW, a.aWC0, a.bWC0, lane);
+    {
+        const StageScale sc = stage_layer<2, 1>(st, G1, Cin, w, lane);
+        dw_blocks<2>(st, 16 * w, X_ROW, a.aWC0, a.bWC0, sc, lane);
+    }
     bwd_layer<1, 2, 64, 64>(W + L_WC0, S32, G1, Gc, lane);  // d cin: rows 0..14 = d geo (SH rows dropped)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -692,21 +855,27 @@ __device__ __forceinline__ void dw_round(const float* W, float* st, const float*
         dHd[0][r] = f < 15 ? Gc[0][r] : (f == 15 ? dsig : 0.0f);
     }
     // heads [geo 15 | sigma 1] x 64: column block w
-    stage_layer<1, 2>(st, dHd, A2, w, lane);
-    dw_blocks<1>(st, 0, X_ROW + 16 * w, a.aHD, a.bHD, lane);
+    {
+        const StageScale sc = stage_layer<1, 2>(st, dHd, A2, w, lane);
+        dw_blocks<1>(st, 0, X_ROW + 16 * w, a.aHD, a.bHD, sc, lane);
+    }
     f32x16 GA2[2], GA1[2], GH[1];
     bwd_layer<2, 1, 16, 32>(W + L_WH, S64, dHd, GA2, lane);
     relu_mask<2>(GA2, A2);
     // sigma trunk 1, 64 x 64: row block w
-    stage_layer<2, 2>(st, GA2, A1, w, lane);
-    dw_blocks<4>(st, 16 * w, X_ROW, a.aW1, a.bW1, lane);
+    {
+        const StageScale sc = stage_layer<2, 2>(st, GA2, A1, w, lane);
+        dw_blocks<4>(st, 16 * w, X_ROW, a.aW1, a.bW1, sc, lane);
+    }
     bwd_layer<2, 2, 64, 64>(W + L_W1, S64, GA2, GA1, lane);
     relu_mask<2>(GA1, A1);
     // sigma trunk 0, 64 x 32: row block w
     f32x16 X0[1];
     load_tiles<1>(h0, 32, 0, 32, m, ok, h, X0);  // reloaded (L2-hot) rather than kept live
-    stage_layer<2, 1>(st, GA1, X0, w, lane);
-    dw_blocks<2>(st, 16 * w, X_ROW, a.aW0, a.bW0, lane);
+    {
+        const StageScale sc = stage_layer<2, 1>(st, GA1, X0, w, lane);
+        dw_blocks<2>(st, 16 * w, X_ROW, a.aW0, a.bW0, sc, lane);
+    }
     if (gh0) {
         bwd_layer<1, 2, 64, 64>(W + L_W0, S32, GA1, GH, lane);
         store_tiles<1>(gh0, 32, 0, 32, m, ok, h, GH);
@@ -732,6 +901,23 @@ __device__ __forceinline__ void dw_flush(DwAcc& a, float* __restrict__ dst, int 
         });
         flush_block(a.aW0[n], lane0, [&](int o, int c, float v) { dst[D_W0 + 32 * (cw + o) + 16 * n + c] = v; });
     }
+#if ACN_DW_F16X3
+    // bias rows = column 0 of the ones-row contraction blocks: lanes 0, 16, 32, 48 hold rows 4 (l >> 4) + r
+    if ((lane0 & 15) == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = 4 * (lane0 >> 4) + r;
+            if (w == 0) {
+                if (i < 3) dst[D_BC2 + i] = a.bWC2[r];
+                dst[i < 15 ? D_BG + i : D_BSH] = a.bHD[r];
+            }
+            dst[D_BC1 + cw + i] = a.bWC1[r];
+            dst[D_BC0 + cw + i] = a.bWC0[r];
+            dst[D_B1 + cw + i] = a.bW1[r];
+            dst[D_B0 + cw + i] = a.bW0[r];
+        }
+    }
+#else
     // bias rows: lane (i, q) holds the sum over samples 32 q .. 32 q + 31 of row i of its row block
     auto red = [](float v) { v += __shfl_xor(v, 16); return v + __shfl_xor(v, 32); };
     const float bWC2 = red(a.bWC2), bHD = red(a.bHD), bWC1 = red(a.bWC1), bWC0 = red(a.bWC0), bW1 = red(a.bW1),
@@ -747,6 +933,7 @@ __device__ __forceinline__ void dw_flush(DwAcc& a, float* __restrict__ dst, int 
         dst[D_B1 + cw + i] = bW1;
         dst[D_B0 + cw + i] = bW0;
     }
+#endif
 }
 
 __global__ void __launch_bounds__(256) mlp_bwd_dw_kernel(const float* __restrict__ img, const float* __restrict__ h0,
@@ -754,8 +941,9 @@ __global__ void __launch_bounds__(256) mlp_bwd_dw_kernel(const float* __restrict
                                                          const float* __restrict__ gout, int64_t M,
                                                          float* __restrict__ gh0, float* __restrict__ partial) {
     __shared__ __attribute__((aligned(16))) float Wl[L_FLOATS];
-    __shared__ __attribute__((aligned(16))) float st_base[128 * SW];
+    __shared__ __attribute__((aligned(16))) float st_base[ST_FLOATS];
     stage_weights(img, Wl);
+    stage_init(st_base);
     __syncthreads();
     const int lane0 = threadIdx.x & 63, j = lane0 & 31, w = threadIdx.x >> 6;
     const int64_t ntiles = (M + 31) / 32;
@@ -782,7 +970,8 @@ __global__ void __launch_bounds__(256) mlp_bwd_dw_pairs_kernel(const float* __re
                                                                const int64_t* __restrict__ seg, int K,
                                                                float* __restrict__ gh0, float* __restrict__ partial) {
     __shared__ __attribute__((aligned(16))) float Wl[L_FLOATS];
-    __shared__ __attribute__((aligned(16))) float st_base[128 * SW];
+    __shared__ __attribute__((aligned(16))) float st_base[ST_FLOATS];
+    stage_init(st_base);  // published by the staging barrier of the first round
     const int lane0 = threadIdx.x & 63, j = lane0 & 31, w = threadIdx.x >> 6;
     const int64_t R = seg[K] / 128, G = gridDim.x;
     const int64_t r0 = (int64_t)blockIdx.x * R / G, r1 = ((int64_t)blockIdx.x + 1) * R / G;
