@@ -1162,8 +1162,12 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
                                    field_tile<INTERP, FOLD>(Wk, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbk, lane, r, g,
                                                             b, sg);
                                } else {
+#if ACN_SLOTS_NOFALLBACK  // diagnostic only: non-resident experts skipped
+                                   r = g = b = sg = 0.0f;
+#else
                                    field_tile<INTERP, false>(p.packed + (size_t)k * PK_FLOATS, cfg.ex[k], cfg.log2T,
                                                              px, py, pz, shv, nullptr, lane, r, g, b, sg);
+#endif
                                }
                                sg = trunc_exp(sg);
                                if (need) {

@@ -63,6 +63,48 @@ def expert_sorted_plan(keys: Tensor, world: int) -> ShardPlan:
     return ShardPlan(perm, max(1, math.ceil(N / world)), N, world)
 
 
+def direction_cell(rays: Tensor, bits: int = 6) -> Tensor:
+    """Z-order cell of each ray's direction on a 2^bits x 2^bits grid: the gnomonic coordinates
+    (d.e1 / d.m, d.e2 / d.m) about the batch's mean direction m (an image-plane position for one
+    camera), quantised over their bounding box -- the key ray_order_kernel (render.hip) sorts a
+    single-expert batch by.  As a secondary key after the expert it keeps each expert's rays in
+    image-region order, so a workgroup's neighbours (and, with XCD bands, an XCD's L2) share the
+    mid-level hash cells.  Rays with a zero / non-finite direction get cell 0."""
+    d = rays[:, 3:6].double()
+    ok = torch.isfinite(d).all(1) & (d.abs().sum(1) > 0)
+    dn = torch.where(ok.unsqueeze(1), d / d.norm(dim=1, keepdim=True).clamp_min(1e-300), torch.zeros_like(d))
+    m = dn.sum(0)
+    if float(m.norm()) == 0.0:
+        return torch.zeros(rays.shape[0], dtype=torch.int64, device=rays.device)
+    m = m / m.norm()
+    a = torch.tensor([1.0, 0.0, 0.0], dtype=d.dtype, device=d.device)
+    if abs(float(m[0])) > 0.9:
+        a = torch.tensor([0.0, 1.0, 0.0], dtype=d.dtype, device=d.device)
+    e1 = torch.linalg.cross(m, a)
+    e1 = e1 / e1.norm()
+    e2 = torch.linalg.cross(m, e1)
+    dm = dn @ m
+    front = ok & (dm > 1e-6)
+    u = torch.where(front, (dn @ e1) / dm.clamp_min(1e-6), torch.zeros_like(dm))
+    v = torch.where(front, (dn @ e2) / dm.clamp_min(1e-6), torch.zeros_like(dm))
+    n = 1 << bits
+
+    def q(x):
+        lo, hi = float(x[front].min()) if bool(front.any()) else 0.0, float(x[front].max()) if bool(front.any()) else 1.0
+        return ((x - lo) / max(hi - lo, 1e-12) * n).floor().clamp(0, n - 1).to(torch.int64)
+    qx, qy = q(u), q(v)
+    key = torch.zeros_like(qx)
+    for b in range(bits):
+        key |= ((qx >> b) & 1) << (2 * b) | ((qy >> b) & 1) << (2 * b + 1)
+    return torch.where(front, key, torch.zeros_like(key))
+
+
+def expert_spatial_keys(rays: Tensor, model, bits: int = 6) -> Tensor:
+    """Sort key (owning expert, direction cell): ``expert_sorted_plan`` on it groups the rays by
+    expert and, within an expert, by image region."""
+    return dominant_expert(rays, model).to(torch.int64) * (1 << (2 * bits)) + direction_cell(rays, bits)
+
+
 def dominant_expert(rays: Tensor, model) -> Tensor:
     """Expert owning each ray's midpoint o + d (near + far)/2: argmin centroid distance, the hard
     routing rule of meta_container.py:119-121 (HIP kernel acn_routing_fwd)."""

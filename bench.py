@@ -98,7 +98,7 @@ def frame_camera(scene, H=None, W=None, ds=0.25):
     return H, W, [float(intr[0] * s), float(intr[1] * s), W / 2.0, H / 2.0], torch.tensor(cam["c2w"])
 
 
-def make_rays(scene, gbox, device, n_rays, seed):
+def make_rays(scene, gbox, device, n_rays, seed, pixel_order=False):
     from adaptive_city_nerf_amd import ops
     H, W, intr, c2w = frame_camera(scene)
     psf = scene["pose_scale_factor"]
@@ -107,6 +107,8 @@ def make_rays(scene, gbox, device, n_rays, seed):
     vi = torch.nonzero(valid).squeeze(1).cpu()
     g = torch.Generator().manual_seed(seed)
     sel = vi[torch.randperm(vi.numel(), generator=g)[:n_rays]]
+    if pixel_order:
+        sel = torch.sort(sel).values
     return rays[sel.to(device)].contiguous()
 
 
@@ -403,6 +405,14 @@ def main():
     ap.add_argument("--query-rays", type=int, default=2000, help="meta: query rays per task")
     ap.add_argument("--data-rays", type=int, default=1 << 22, help="data: rays in the region table")
     ap.add_argument("--no-graph", action="store_true", help="c5: eager steps instead of the HIP-graph replay")
+    ap.add_argument("--diag-shared-table", action="store_true",
+                    help="diagnostic (c3/c4): every expert reads expert 0's hash table (one 128 MiB table instead of "
+                         "K: isolates the Infinity-Cache capacity effect; outputs differ from the real render)")
+    ap.add_argument("--diag-pixel-order", action="store_true",
+                    help="diagnostic (c3): the batch in scanline pixel order instead of random order before the "
+                         "expert sort")
+    ap.add_argument("--diag-expert-only-order", action="store_true",
+                    help="diagnostic (c3): sort the batch by owning expert only (no direction-cell secondary key)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check: every rank reports (rank, world) over gloo and exits before any GPU call")
     a = ap.parse_args()
@@ -444,6 +454,10 @@ def main():
     model, gbox, scene, sc = build_model(device, K, fill=[rank % K] if a.workload == "c5a" else None,
                                          occ_conf=occ_conf)
 
+    if a.diag_shared_table:
+        with torch.no_grad():
+            for sub in model.submodules[1:]:
+                sub.xyz_encoder.hash_table.data = model.submodules[0].xyz_encoder.hash_table.data
     if a.workload == "c2":
         if a.opaque:
             with torch.no_grad():
@@ -476,8 +490,10 @@ def main():
         sample_rays = rays
     elif a.workload == "c3":
         # global batch (identical on every rank), sharded by owning expert; gather of rendered rays
-        grays = make_rays(scene, gbox, device, world * a.rays, 1234)
-        plan = parallel.expert_sorted_plan(parallel.dominant_expert(grays, model), world)
+        grays = make_rays(scene, gbox, device, world * a.rays, 1234, pixel_order=a.diag_pixel_order)
+        keys = (parallel.dominant_expert(grays, model) if a.diag_expert_only_order
+                else parallel.expert_spatial_keys(grays, model))
+        plan = parallel.expert_sorted_plan(keys, world)
         samples_per_step = grays.shape[0] * S
 
         def render_fn(r):
@@ -803,7 +819,7 @@ def main():
              "c5a": "adam_kernel (fused clip + Adam over the adapted expert + background head)",
              "c2": "ray_order_kernel + render_kernel<1,1,0> (one acn_render_stratified_fwd_ordered call: direction "
                    "grouping of the batch, then the fused stratified render, 1 expert; events bracket both)",
-             "c3": "render_kernel<1,0,1> (fused stratified render, soft routing over 4 experts)",
+             "c3": "render_slots_kernel (fused stratified render, soft routing over 4 experts, two staged per round)",
              "c4": ("field_kernel (fused MFMA field of the owned expert over the received per-sample records)"
                     if a.layout == "expert" else
                     "render_slots_kernel (fused stratified render, soft routing over 8 experts, two staged per round)"),

@@ -73,6 +73,30 @@ def test_expert_plan_groups_experts_and_balances():
     assert [sorted(set(p)) for p in per_rank] == [[0], [1], [2], [3]]
 
 
+def test_direction_cell_is_image_region_zorder():
+    """direction_cell (the C3 plan's secondary key): a camera's pixel rays map to Z-order cells of
+    their image position -- in range, monotone along image rows and columns of the cell grid, the
+    four quadrants of the frame in the four Z-order quarters; bad directions get cell 0."""
+    from adaptive_city_nerf_amd.parallel import direction_cell
+    H = W = 64
+    rays, _ = O.get_rays(H, W, 50.0, 50.0, W / 2, H / 2, np.eye(4, dtype=np.float32)[:3], near_far_override=(0.0, 1.0))
+    r = torch.from_numpy(rays)
+    key = direction_cell(r, bits=3).view(H, W)
+    assert int(key.min()) == 0 and int(key.max()) == 63
+    quarter = key // 16
+    # the camera looks down -z with +x right: one Z-order quarter per frame quadrant, each a single value
+    for qy in (slice(0, H // 2), slice(H // 2, H)):
+        for qx in (slice(0, W // 2), slice(W // 2, W)):
+            assert quarter[qy, qx].unique().numel() == 1
+    assert quarter.unique().numel() == 4
+    bad = r[:3].clone()
+    bad[0, 3:6] = 0.0
+    bad[1, 3] = float("nan")
+    k2 = direction_cell(torch.cat([bad, r]), bits=3)
+    assert int(k2[0]) == 0 and int(k2[1]) == 0
+    assert int(k2[3:].max()) == 63 and (k2[3:] // 16).unique().numel() == 4
+
+
 def test_single_process_gather_is_identity():
     x = torch.arange(30, dtype=torch.float32).view(10, 3)
     plan = expert_sorted_plan(torch.tensor([2, 1, 0, 2, 1, 0, 2, 1, 0, 0]), 1)
