@@ -1045,9 +1045,17 @@ __global__ void __launch_bounds__(1024, 4) render_kernel(FieldCfg cfg, BgArgs bg
 // with rays sorted by owning expert, parallel.expert_sorted_plan, a workgroup's rays mostly need
 // the same one or two experts, so staging is rare).  A sample whose expert is not resident is
 // evaluated from the packed image in global memory (L2), without the SH fold.
+#ifndef ACN_SLOTS_SINGLE
+#define ACN_SLOTS_SINGLE 1  // single-expert rays (kSingleRay) skip the per-sample routing and blend
+#endif
+// Bit kSingleRay of the returned mask: every sample of the ray is routed to ONE expert with weight
+// exactly 1.0f (soft: (1/d)/den with den = 1/d; hard: always), so the container's blend
+// 0 + y_k * 1.0f is y_k bit for bit and the ray can skip the per-sample routing and blend.
+constexpr uint32_t kSingleRay = 1u << 31;
 __device__ __forceinline__ uint32_t ray_expert_mask(const FieldCfg& cfg, int route, const RenderParams& p, int64_t ray,
                                                     int64_t lim, float step, int lane) {
     uint32_t m = 0u;
+    bool exact = true;
     if (ray < lim) {
         const float* rp = p.rays + ray * 8;
         const float ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
@@ -1058,8 +1066,11 @@ __device__ __forceinline__ uint32_t ray_expert_mask(const FieldCfg& cfg, int rou
             const float px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;
             if (route == 1) {
                 const RouteState st = route_prep<1>(cfg, px, py, pz);
-                for (int k = 0; k < cfg.K; ++k)
-                    if (route_weight(cfg, st, k, px, py, pz) > 0.0f) m |= 1u << k;
+                for (int k = 0; k < cfg.K; ++k) {
+                    const float w = route_weight(cfg, st, k, px, py, pz);
+                    if (w > 0.0f) m |= 1u << k;
+                    exact = exact && (w == 0.0f || w == 1.0f);
+                }
             } else {
                 m |= 1u << route_prep<2>(cfg, px, py, pz).hard;
             }
@@ -1068,6 +1079,7 @@ __device__ __forceinline__ uint32_t ray_expert_mask(const FieldCfg& cfg, int rou
     uint32_t any = 0u;  // OR over the wave: one ballot per expert (scalar), no LDS round trips
     for (int k = 0; k < cfg.K; ++k)
         if (__ballot((m >> k) & 1u) != 0ull) any |= 1u << k;
+    if (ACN_SLOTS_SINGLE && __builtin_popcount(any) == 1 && __ballot(!exact) == 0ull) any |= kSingleRay;
     return any;
 }
 
@@ -1141,9 +1153,31 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
         const int k0 = __builtin_amdgcn_readfirstlane(slot_k[0]), k1 = __builtin_amdgcn_readfirstlane(slot_k[1]);
 #endif
         if (ray < lim) {
+            const bool single = (m & kSingleRay) != 0u;
+            const int k_single = __builtin_ctz(m | kSingleRay);
             render_ray(p, bg, ray, lane, step,
                        [&](float px, float py, float pz, const float (&shv)[8], uint32_t& folded, float& yr, float& yg,
                            float& yb, float& ys) {
+                           if (single) {  // wave-uniform: one expert, weight 1.0f on every sample
+                               const int k = k_single;
+                               const int sl = (k == k0) ? 0 : ((k == k1) ? 1 : -1);
+                               float sg;
+                               if (sl >= 0) {
+                                   const float* Wk = smem + sl * PK_FLOATS;
+                                   float* cbk = FOLD ? cb + sl * 64 : nullptr;
+                                   if (FOLD && !((folded >> sl) & 1u)) {
+                                       fold_sh_bias(Wk, shv, lane, cbk);
+                                       folded |= 1u << sl;
+                                   }
+                                   field_tile<INTERP, FOLD>(Wk, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbk, lane, yr,
+                                                            yg, yb, sg);
+                               } else {
+                                   field_tile<INTERP, false>(p.packed + (size_t)k * PK_FLOATS, cfg.ex[k], cfg.log2T,
+                                                             px, py, pz, shv, nullptr, lane, yr, yg, yb, sg);
+                               }
+                               ys = trunc_exp(sg);
+                               return;
+                           }
                            const RouteState st = route_prep<ROUTE>(cfg, px, py, pz);
                            yr = yg = yb = ys = 0.0f;
                            for (int k = 0; k < cfg.K; ++k) {

@@ -102,6 +102,46 @@ def test_render_rays_k8_vs_reference(variant, tau):
     assert np.abs(w.cpu().numpy() - d[f"{variant}:weights"]).max() <= 1e-5
 
 
+def _single_expert_rays(rays, S, sc, bm):
+    """Per ray: the one expert every sample routes to with weight exactly 1.0f (else -1), from the
+    oracle's routing at the eval t-values (linspace as torch CPU, ray_rendering.py:278-287)."""
+    i = np.arange(S)
+    step = np.float32(1.0) / np.float32(S - 1)
+    u = np.where(i < S // 2, (step * i.astype(np.float32)).astype(np.float32),
+                 (np.float32(1.0) - step * (S - 1 - i).astype(np.float32)).astype(np.float32)).astype(np.float32)
+    near, far = rays[:, 6:7], rays[:, 7:8]
+    t = (near * (np.float32(1) - u) + far * u).astype(np.float32)
+    pts = (rays[:, None, :3] + rays[:, None, 3:6] * t[..., None]).astype(np.float32)
+    W, _ = O.routing(pts.reshape(-1, 3), np.array(sc["centroids"], np.float32), sc["cluster_2d"], bm)
+    W = W.reshape(rays.shape[0], S, -1)
+    one = ((W > 0).sum(-1) == 1) & ((W == 1.0) | (W == 0.0)).all(-1)
+    k = W.argmax(-1)
+    ok = one.all(1) & (k == k[:, :1]).all(1)
+    return np.where(ok, k[:, 0], -1)
+
+
+@pytest.mark.gpu
+def test_single_expert_rays_bit_identical_to_active_module():
+    """render_slots_kernel's single-expert fast path (every sample of the ray routed to one expert
+    with weight exactly 1.0: the blend 0 + y_k * 1.0f is y_k) renders those rays bit for bit like the
+    active_module render of that expert (render_kernel, same field tile and compositing code)."""
+    from adaptive_city_nerf_amd import render_rays
+    d = G.load("render_k8")
+    m, _ = _model(d)
+    sc = G.scene()["masks"][MASK]
+    rays = d["render:rays"]
+    ks = _single_expert_rays(rays, 64, sc, float(d["bm"]))
+    vals, cnt = np.unique(ks[ks >= 0], return_counts=True)
+    assert cnt.sum() >= rays.shape[0] // 2, "fixture rays should be mostly single-expert"
+    k = int(vals[np.argmax(cnt)])
+    sel = torch.from_numpy(rays[ks == k]).cuda()
+    with torch.no_grad():
+        a = render_rays(m, sel, ray_samples=64, bg_color_default="white")
+        b = render_rays(m, sel, ray_samples=64, bg_color_default="white", active_module=k)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("which", ["field", "field_default"])
 def test_container_forward_k8_vs_reference(which):
