@@ -382,7 +382,9 @@ def maybe_launch(argv, n_gpus: int) -> Optional[int]:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default 200 for the sub-millisecond c2 / c3 steps, whose fixed start-up "
+                         "latency would otherwise weigh on a 20-step window; 20 for the others)")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "c5a", "occ", "meta", "data", "clusters"], default="c2")
     ap.add_argument("--rays", type=int, default=4096, help="rays per GPU (c2, c3)")
@@ -416,6 +418,8 @@ def main():
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check: every rank reports (rank, world) over gloo and exits before any GPU call")
     a = ap.parse_args()
+    if a.steps is None:
+        a.steps = 200 if a.workload in ("c2", "c3") else 20
     rc = maybe_launch(sys.argv[1:], a.gpus)
     if rc is not None:
         sys.exit(rc)
@@ -706,7 +710,10 @@ def main():
     for _ in range(a.warmup):
         out = step()
     torch.cuda.synchronize()
-    ops.EVENT_HOOK = []
+    # c2: one acn call per step, timed by two HIP events bracketing the K timed calls on the launch stream
+    # (a per-call event pair costs ~8 us of queue time per step, 2.5% of a C2 step: tools/event_overhead.py)
+    bracket = a.workload == "c2"
+    ops.EVENT_HOOK = None if bracket else []
     if a.workload == "occ":
         occ_ops.EVENT_HOOK = ops.EVENT_HOOK
     if world > 1:
@@ -716,8 +723,13 @@ def main():
     if mark:
         torch.cuda._sleep(1000)
     t0 = time.perf_counter()
+    if bracket:
+        eb = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        eb[0].record()
     for _ in range(a.steps):
         out = step()
+    if bracket:
+        eb[1].record()
     if mark:
         torch.cuda._sleep(1000)
     torch.cuda.synchronize()
@@ -762,9 +774,13 @@ def main():
         from adaptive_city_nerf_amd import optim as aoptim
         hook = aoptim.EVENT_HOOK[-a.steps:]
         aoptim.EVENT_HOOK = None
+    elif bracket:
+        hook = [(eb[0], eb[1])] * a.steps     # one launch per step; average = bracketed time / K
     else:
         hook = ops.EVENT_HOOK
     kernel_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in hook]))
+    if bracket:
+        kernel_ms /= a.steps
     if a.workload == "data":
         # route_kernel (~0.1 ms) is shorter than the host gap between a per-call event and its launch
         # (the step syncs for the bin counts, so the queue is empty): time it back to back instead
@@ -818,7 +834,8 @@ def main():
                    "folded in, table gradients cleared in the same pass)",
              "c5a": "adam_kernel (fused clip + Adam over the adapted expert + background head)",
              "c2": "ray_order_kernel + render_kernel<1,1,0> (one acn_render_stratified_fwd_ordered call: direction "
-                   "grouping of the batch, then the fused stratified render, 1 expert; events bracket both)",
+                   "grouping of the batch, then the fused stratified render, 1 expert; kernel_ms = two HIP events "
+                   "bracketing the K timed calls on the launch stream / K)",
              "c3": "render_slots_kernel (fused stratified render, soft routing over 4 experts, two staged per round)",
              "c4": ("field_kernel (fused MFMA field of the owned expert over the received per-sample records)"
                     if a.layout == "expert" else

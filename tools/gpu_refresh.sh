@@ -14,4 +14,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout
 && timeout -k 10 300 python -u bench.py --workload c4 --samples 96 > gpurun_out/bench_c4s96_$TAG.json 2> gpurun_out/bench_c4s96_$TAG.err \
 && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c3_$TAG -o run -- python3 bench.py --workload c3 --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/prof_c3_$TAG.log 2>&1 && keep_stats gpurun_out/prof_c3_$TAG \
 && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c4_$TAG -o run -- python3 bench.py --workload c4 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/prof_c4_$TAG.log 2>&1 && keep_stats gpurun_out/prof_c4_$TAG
-echo "gpu_refresh exit=$?"
+rc=$?
+[ $rc = 0 ] && ACN_TRACE_MARK=1 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace_c2_$TAG -o run -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline > gpurun_out/trace_c2_$TAG.log 2>&1 \
+  && python tools/trace_busy.py gpurun_out/trace_c2_$TAG 50 > gpurun_out/trace_c2_$TAG.txt; rc=$?
+echo "gpu_refresh exit=$rc"
