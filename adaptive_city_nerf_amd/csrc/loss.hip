@@ -27,6 +27,8 @@ __global__ void __launch_bounds__(kThreads) mse_linear_fwd_kernel(const float* _
                                                                   float* __restrict__ loss) {
     __shared__ double red[kThreads / 64];
     double acc = 0.0;
+    // unrolled: the loads of 8 strides are issued together (same accumulation order per thread)
+#pragma unroll 8
     for (int64_t e = threadIdx.x; e < n; e += kThreads) {
         const float d = clamp01(pred[e]) - gt_linear(gt[e]);
         acc += (double)(d * d);
