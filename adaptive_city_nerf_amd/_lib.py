@@ -148,11 +148,13 @@ SIGNATURES = {
     "acn_xd_unit_sh": ([vp, i64, vp, vp, f32, f32, vp, vp, vp], C.c_int),
     "acn_hashgrid_fwd_pairs": ([vp, vp, vp, i32, vp, vp, i32, i32, i32, vp, vp], C.c_int),
     "acn_hashgrid_bwd_pairs": ([vp, vp, vp, vp, i32, vp, vp, vp, i32, i32, i32, vp], C.c_int),
+    "acn_hashgrid_bwd_pairs_sumsq": ([vp, vp, vp, vp, i32, vp, vp, vp, i32, i32, i32, vp, vp], C.c_int),
     "acn_mlp_pairs_workspace_bytes": ([i32], C.c_size_t),
     "acn_mlp_pack_pairs": ([vp, i32, vp, vp], C.c_int),
     "acn_mlp_train_fwd_pairs": ([vp, vp, vp, i32, vp, vp, vp], C.c_int),
     "acn_mlp_train_bwd_dw_pairs": ([vp, vp, vp, vp, vp, i32, vp, vp, vp, vp], C.c_int),
     "acn_grad_sumsq_slots": ([vp, vp, i64, vp, vp, i32, vp, vp, vp], C.c_int),
+    "acn_grad_sumsq_slots_ex": ([vp, vp, i64, vp, vp, i32, vp, vp, vp, vp], C.c_int),
     "acn_adam_step_slots": ([vp, vp, i64, vp, vp, i32, i32, vp, i32, vp, i32, vp, vp], C.c_int),
     # clusters.hip
     "acn_voronoi_route": ([vp, i64, i32, vp, i32, i32, C.c_double, i32, i32, vp, vp, vp, vp, vp, vp], C.c_int),

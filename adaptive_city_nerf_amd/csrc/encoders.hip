@@ -247,17 +247,32 @@ __global__ void __launch_bounds__(256) hashgrid_fwd_pairs(const float* __restric
 
 // hashgrid_bwd_rle over pair slots: the run key is the target address, so a stretch may cross an
 // expert boundary; padding slots (pidx < 0) add nothing
-template <int INTERP, int PPL>
+// TELE: returning atomics; every run adds new^2 - old^2 (new = old + run sum, the value the atomic
+// leaves) to *sq.  Per row these telescope to (final value)^2 - 0, so *sq gains the squared norm of the
+// table-gradient update without a pass over the 128 MiB gradient buffers (clip_grad_norm_'s sum of
+// squares, runtime_adapt.py:305-307).  Doubles: new^2 and old^2 are exact, so only the differences and
+// their sum round (~1e-16 relative).
+template <int INTERP, int PPL, bool TELE>
 __global__ void __launch_bounds__(256) hashgrid_bwd_pairs(const float* __restrict__ x01, const int32_t* __restrict__ pk,
                                                           const int32_t* __restrict__ pidx,
                                                           const int64_t* __restrict__ seg, int K,
                                                           const float* __restrict__ gout, GradTables gt, Res32 res,
-                                                          int L, int log2T, int l0) {
+                                                          int L, int log2T, int l0, double* __restrict__ sq) {
     const int lane = threadIdx.x & 63;
     const int64_t M = seg[K];
     const int64_t nwaves = ((M + 4 * PPL - 1) / (4 * PPL)) * (L - l0);
     const int f = lane & 1, bx = (lane >> 1) & 1, by = (lane >> 3) & 1, bz = (lane >> 2) & 1;
     const uint32_t mask = (uint32_t)((1ull << log2T) - 1ull);
+    double tsq = 0.0;
+    auto flush = [&](float* a, float v) {
+        if (TELE) {
+            const float o = atomicAdd(a, v);
+            const float nv = o + v;
+            tsq += (double)nv * (double)nv - (double)o * (double)o;
+        } else {
+            unsafeAtomicAdd(a, v);
+        }
+    };
     for (int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; wave < nwaves;
          wave += ((int64_t)gridDim.x * blockDim.x) >> 6) {
         const int l = l0 + (int)(wave % (L - l0));
@@ -288,12 +303,17 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_pairs(const float* __restric
             if (a == cur) {
                 acc += gv;
             } else {
-                if (cur) unsafeAtomicAdd(cur, acc);
+                if (cur) flush(cur, acc);
                 cur = a;
                 acc = gv;
             }
         }
-        if (cur) unsafeAtomicAdd(cur, acc);
+        if (cur) flush(cur, acc);
+    }
+    if (TELE) {  // one double atomic per wave
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) tsq += __shfl_xor(tsq, off);
+        if (lane == 0 && tsq != 0.0) atomicAdd(sq, tsq);
     }
 }
 
@@ -552,6 +572,14 @@ extern "C" int acn_hashgrid_fwd_pairs(const float* x01, const int32_t* pk, const
 extern "C" int acn_hashgrid_bwd_pairs(const float* x01, const int32_t* pk, const int32_t* pidx, const int64_t* seg,
                                       int K, const float* grad_out, float* const* grad_tables, const int32_t* res,
                                       int L, int log2T, int interp, void* stream) {
+    return acn_hashgrid_bwd_pairs_sumsq(x01, pk, pidx, seg, K, grad_out, grad_tables, res, L, log2T, interp, nullptr,
+                                        stream);
+}
+
+extern "C" int acn_hashgrid_bwd_pairs_sumsq(const float* x01, const int32_t* pk, const int32_t* pidx,
+                                            const int64_t* seg, int K, const float* grad_out,
+                                            float* const* grad_tables, const int32_t* res, int L, int log2T,
+                                            int interp, double* table_sumsq, void* stream) {
     ACN_REQUIRE(K >= 1 && K <= acn::kMaxK && grad_tables && res && seg && x01 && pk && pidx && grad_out,
                 "acn_hashgrid_bwd_pairs: bad arguments");
     ACN_REQUIRE(L >= 1 && L <= ACN_MAX_LEVELS && log2T >= 1 && log2T <= 30 && (interp == 1 || interp == 2),
@@ -563,13 +591,17 @@ extern "C" int acn_hashgrid_bwd_pairs(const float* x01, const int32_t* pk, const
     const dim3 grid(2048), block(256);
     hipStream_t s = (hipStream_t)stream;
     const MergeCfg mc = merge_cfg(L, log2T);
+    ACN_REQUIRE(!(table_sumsq && mc.LM > 0), "acn_hashgrid_bwd_pairs_sumsq: not available with the merged coarse "
+                "levels (ACN_HASH_BWD_MERGE)");
     if (mc.LM > 0) {  // fixed grid (graph-replayable): items are counted from the device slot count
         if (interp == 1) hipLaunchKernelGGL(hashgrid_bwd_merge<1>, dim3(512), block, 0, s, x01, pk, pidx, seg, K, (int64_t)0, grad_out, t, r, L, log2T, mc);
         else hipLaunchKernelGGL(hashgrid_bwd_merge<2>, dim3(512), block, 0, s, x01, pk, pidx, seg, K, (int64_t)0, grad_out, t, r, L, log2T, mc);
     }
     if (mc.LM < L) {
-        if (interp == 1) hipLaunchKernelGGL((hashgrid_bwd_pairs<1, 16>), grid, block, 0, s, x01, pk, pidx, seg, K, grad_out, t, r, L, log2T, mc.LM);
-        else hipLaunchKernelGGL((hashgrid_bwd_pairs<2, 16>), grid, block, 0, s, x01, pk, pidx, seg, K, grad_out, t, r, L, log2T, mc.LM);
+#define ACN_BWD_PAIRS(I, T) hipLaunchKernelGGL((hashgrid_bwd_pairs<I, 16, T>), grid, block, 0, s, x01, pk, pidx, seg, K, grad_out, t, r, L, log2T, mc.LM, table_sumsq)
+        if (table_sumsq) { if (interp == 1) ACN_BWD_PAIRS(1, true); else ACN_BWD_PAIRS(2, true); }
+        else { if (interp == 1) ACN_BWD_PAIRS(1, false); else ACN_BWD_PAIRS(2, false); }
+#undef ACN_BWD_PAIRS
     }
     return acn_check_launch("acn_hashgrid_bwd_pairs");
 }

@@ -86,12 +86,21 @@ __global__ void __launch_bounds__(kThreads) sumsq_kernel(const acn_param_desc* _
     if (threadIdx.x == 0) partials[blockIdx.x] = t;
 }
 
+// extra (optional): a sum of squares produced elsewhere (the table-gradient scatter's telescoped sum,
+// acn_hashgrid_bwd_pairs_sumsq), added to the total and reset to 0 for the next step
 __global__ void __launch_bounds__(kThreads) reduce_kernel(const double* __restrict__ partials, int64_t n,
-                                                          double* __restrict__ total) {
+                                                          double* __restrict__ total, double* __restrict__ extra) {
     double acc = 0.0;
     for (int64_t i = threadIdx.x; i < n; i += kThreads) acc += partials[i];
     const double t = block_sum(acc);
-    if (threadIdx.x == 0) total[0] = t;
+    if (threadIdx.x == 0) {
+        if (extra) {
+            total[0] = t + extra[0];
+            extra[0] = 0.0;
+        } else {
+            total[0] = t;
+        }
+    }
 }
 
 // clip_grad_norm_ (torch/nn/utils/clip_grad.py): total_norm, clip_coef = max_norm / (total_norm +
@@ -229,6 +238,7 @@ __global__ void __launch_bounds__(kThreads) adam_table_kernel(const acn_param_de
 // flags bit 16: zero the gradient after reading it (the table gradients are scatter-added into
 // persistent buffers, so the next step finds them cleared without a separate memset pass).
 constexpr int kSlotZero = 1 << 16;
+constexpr int kSlotNormElsewhere = 1 << 17;  // sum of squares supplied by acn_hashgrid_bwd_pairs_sumsq
 
 __device__ __forceinline__ bool slot_active(const int64_t* __restrict__ seg, int K, int slot) {
     return slot >= K || seg == nullptr || seg[K + 1 + slot] > 0;
@@ -247,7 +257,7 @@ __global__ void __launch_bounds__(kThreads) sumsq_slots_kernel(const acn_param_d
     const int t = chunk_tensor[blockIdx.x];
     const acn_param_desc d = descs[t];
     double acc = 0.0;
-    if (d.grad != nullptr && slot_active(seg, K, flags[t] & 0xffff)) {
+    if (d.grad != nullptr && slot_active(seg, K, flags[t] & 0xffff) && !(flags[t] & kSlotNormElsewhere)) {
         const int64_t base = (int64_t)(blockIdx.x - d.first_chunk) * ACN_OPTIM_CHUNK;
         const int64_t n = d.numel - base < ACN_OPTIM_CHUNK ? d.numel - base : ACN_OPTIM_CHUNK;
         const float* g = d.grad + base;
@@ -452,7 +462,7 @@ extern "C" int acn_grad_sumsq(const acn_param_desc* descs, const int32_t* chunk_
     ACN_REQUIRE(descs && chunk_tensor && partials, "acn_grad_sumsq: NULL pointer");
     ACN_REQUIRE(nchunks <= 0x7fffffff, "acn_grad_sumsq: too many chunks");
     hipLaunchKernelGGL(sumsq_kernel, dim3((unsigned)nchunks), dim3(kThreads), 0, s, descs, chunk_tensor, partials);
-    hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(kThreads), 0, s, partials, nchunks, total);
+    hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(kThreads), 0, s, partials, nchunks, total, (double*)nullptr);
     return acn_check_launch("acn_grad_sumsq");
 }
 
@@ -483,12 +493,18 @@ extern "C" int acn_adam_step(const acn_param_desc* descs, const int32_t* chunk_t
 extern "C" int acn_grad_sumsq_slots(const acn_param_desc* descs, const int32_t* chunk_tensor, int64_t nchunks,
                                     const int32_t* flags, const int64_t* seg, int K, double* partials, double* total,
                                     void* stream) {
+    return acn_grad_sumsq_slots_ex(descs, chunk_tensor, nchunks, flags, seg, K, partials, total, nullptr, stream);
+}
+
+extern "C" int acn_grad_sumsq_slots_ex(const acn_param_desc* descs, const int32_t* chunk_tensor, int64_t nchunks,
+                                       const int32_t* flags, const int64_t* seg, int K, double* partials, double* total,
+                                       double* extra, void* stream) {
     ACN_REQUIRE(nchunks >= 1 && nchunks <= 0x7fffffff && descs && chunk_tensor && flags && partials && total,
                 "acn_grad_sumsq_slots: bad arguments");
     hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(sumsq_slots_kernel, dim3((unsigned)nchunks), dim3(kThreads), 0, s, descs, chunk_tensor, flags, seg,
                        K, partials);
-    hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(kThreads), 0, s, partials, nchunks, total);
+    hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(kThreads), 0, s, partials, nchunks, total, extra);
     return acn_check_launch("acn_grad_sumsq_slots");
 }
 

@@ -30,6 +30,7 @@ the FusedAdam state tensors, state['step'] is synchronised from the per-expert d
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Optional
 
 import numpy as np
@@ -48,6 +49,10 @@ BWD_HOOK = None
 
 ALIGN = 128                # pair segment alignment = one MLP round (4 tiles x 32 slots)
 ZERO_GRAD_FLAG = 1 << 16   # adam_step_slots: clear the gradient after reading it
+NORM_ELSEWHERE_FLAG = 1 << 17  # grad_sumsq_slots_ex: this tensor's sum of squares comes from the table scatter
+# The tables' share of the clip norm from the scatter's returning atomics (acn_hashgrid_bwd_pairs_sumsq)
+# instead of a pass over the K x 128 MiB gradient buffers
+TELESCOPED_TABLE_NORM = os.environ.get("ACN_TELE_NORM", "1") != "0"
 
 
 def _stream(device) -> int:
@@ -82,6 +87,7 @@ class RoutedAdaptStep:
         # clear_in_adam=False keeps the gradients readable after the step (tests): the table gradients
         # are then zeroed at the start of the next step instead of by the Adam pass
         self.clear_in_adam = bool(clear_in_adam)
+        self.tele = TELESCOPED_TABLE_NORM and grad_clip is not None
         dev = e0.hash_table.device
         self.device = dev
         K = len(model.submodules)
@@ -157,7 +163,10 @@ class RoutedAdaptStep:
                 s = slot_of[id(p)]
                 slots_seen.setdefault(s, int(st["step"].item()))
                 rows.append((p, p.grad, st["exp_avg"], st["exp_avg_sq"], gi))
-                flags.append(s | (ZERO_GRAD_FLAG if zero_of.get(id(p)) and self.clear_in_adam else 0))
+                fl = s | (ZERO_GRAD_FLAG if zero_of.get(id(p)) and self.clear_in_adam else 0)
+                if zero_of.get(id(p)) and self.tele:
+                    fl |= NORM_ELSEWHERE_FLAG
+                flags.append(fl)
         self.rows = rows
         self.nslots = K + 1
         arr = (_lib.acn_param_desc * len(rows))()
@@ -173,6 +182,7 @@ class RoutedAdaptStep:
         self.flags = torch.tensor(flags, **i32)
         self.partials = torch.empty(first, device=dev, dtype=torch.float64)
         self.total = torch.empty(1, device=dev, dtype=torch.float64)
+        self.table_sumsq = torch.zeros(1, device=dev, dtype=torch.float64)  # reset by grad_sumsq_slots_ex
         self.scale = torch.ones(2, **f32)
         self.step_dev = torch.tensor([slots_seen.get(s, 0) for s in range(self.nslots)], **i32)
         ng = len(optimizer.param_groups)
@@ -244,18 +254,21 @@ class RoutedAdaptStep:
         if bhook is not None:
             b0 = torch.cuda.Event(enable_timing=True)
             b0.record()
-        check(L.acn_hashgrid_bwd_pairs(ptr(self.x01), ptr(self.pk), ptr(self.pidx), ptr(self.seg), K, ptr(self.gh0),
-                                       self._gtables, self._res, len(enc._res_host), enc.log2_hashmap_size,
-                                       enc._interp_code, s), "acn_hashgrid_bwd_pairs")
+        check(L.acn_hashgrid_bwd_pairs_sumsq(ptr(self.x01), ptr(self.pk), ptr(self.pidx), ptr(self.seg), K,
+                                             ptr(self.gh0), self._gtables, self._res, len(enc._res_host),
+                                             enc.log2_hashmap_size, enc._interp_code,
+                                             ptr(self.table_sumsq) if self.tele else None, s),
+              "acn_hashgrid_bwd_pairs_sumsq")
         if bhook is not None:
             b1 = torch.cuda.Event(enable_timing=True)
             b1.record()
             bhook.append((b0, b1))
         scale = None
         if self.grad_clip is not None:
-            check(L.acn_grad_sumsq_slots(ptr(self.descs), ptr(self.chunk_tensor), self.nchunks, ptr(self.flags),
-                                         ptr(self.seg), K, ptr(self.partials), ptr(self.total), s),
-                  "acn_grad_sumsq_slots")
+            check(L.acn_grad_sumsq_slots_ex(ptr(self.descs), ptr(self.chunk_tensor), self.nchunks, ptr(self.flags),
+                                            ptr(self.seg), K, ptr(self.partials), ptr(self.total),
+                                            ptr(self.table_sumsq) if self.tele else None, s),
+                  "acn_grad_sumsq_slots_ex")
             check(L.acn_clip_coef(ptr(self.total), float(self.grad_clip), ptr(self.scale), s), "acn_clip_coef")
             scale = self.scale
         hook = EVENT_HOOK if self.graph is None else None

@@ -270,6 +270,12 @@ int acn_adam_step_table(const acn_param_desc* descs, const int32_t* chunk_tensor
 int acn_grad_sumsq_slots(const acn_param_desc* descs, const int32_t* chunk_tensor, int64_t nchunks,
                          const int32_t* flags, const int64_t* seg, int K, double* partials, double* total,
                          void* stream);
+/* As acn_grad_sumsq_slots, but tensors whose flag has bit 17 set are skipped and *extra (a device double:
+ * the table gradients' sum of squares from acn_hashgrid_bwd_pairs_sumsq) is added to the total, then
+ * reset to 0 (ready for the next step).  extra may be NULL. */
+int acn_grad_sumsq_slots_ex(const acn_param_desc* descs, const int32_t* chunk_tensor, int64_t nchunks,
+                            const int32_t* flags, const int64_t* seg, int K, double* partials, double* total,
+                            double* extra, void* stream);
 int acn_adam_step_slots(const acn_param_desc* descs, const int32_t* chunk_tensor, int64_t nchunks,
                         const int32_t* flags, const void* table, int ngroups, int table_steps, int32_t* step_dev,
                         int nslots, const int64_t* seg, int K, const float* grad_scale, void* stream);
@@ -512,6 +518,14 @@ int acn_hashgrid_fwd_pairs(const float* x01, const int32_t* pk, const int64_t* s
 int acn_hashgrid_bwd_pairs(const float* x01, const int32_t* pk, const int32_t* pidx, const int64_t* seg, int K,
                            const float* grad_out, float* const* grad_tables, const int32_t* res, int L, int log2T,
                            int interp, void* stream);
+/* acn_hashgrid_bwd_pairs that also adds, to the device double *table_sumsq, the change of the squared
+ * norm of the gradient tables (returning atomics: sum of new^2 - old^2, which telescopes per row), i.e.
+ * the tables' share of clip_grad_norm_'s sum of squares (runtime_adapt.py:305-307) when the tables start
+ * the step at zero -- no pass over the K x 128 MiB gradients.  Not combinable with the merged coarse
+ * levels (ACN_HASH_BWD_MERGE builds: returns an error). */
+int acn_hashgrid_bwd_pairs_sumsq(const float* x01, const int32_t* pk, const int32_t* pidx, const int64_t* seg,
+                                 int K, const float* grad_out, float* const* grad_tables, const int32_t* res, int L,
+                                 int log2T, int interp, double* table_sumsq, void* stream);
 size_t acn_mlp_pairs_workspace_bytes(int K);
 int acn_mlp_pack_pairs(const acn_mlp* const* w, int K, void* workspace, void* stream);
 int acn_mlp_train_fwd_pairs(const float* h0, const float* sh, const int64_t* seg, int K, const void* workspace,

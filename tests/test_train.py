@@ -367,3 +367,37 @@ def test_routed_adapt_step_matches_reference_fixture(tag, graph):
     """RoutedAdaptStep (pair kernels, device-side expert activity, slotted Adam; eager and replayed as a
     HIP graph) reproduces the reference's runtime_adapt steps of the routed container."""
     check_adapt_fixture(tag, _routed_step_fn(graph))
+
+
+@pytest.mark.gpu
+def test_routed_step_telescoped_table_norm_equals_full_pass():
+    """The tables' share of the clip norm taken from the scatter's returning atomics (sum of new^2 - old^2,
+    telescoping per row) equals the sum of squares over the finished gradient buffers: same step, same
+    jitter, the two modes' total norms within 1e-6 relative (double sums, different order)."""
+    from adaptive_city_nerf_amd import routed_train as RT
+    from adaptive_city_nerf_amd.optim import build_optimizer
+    from test_module_api import build_model, reference_state_dict
+    d = G.load("train_k8")
+    Pk = SimpleNamespace(**{**vars(P), "ray_samples": 96, "chunk_points": 4_000_000})
+    norms = []
+    for tele in (True, False):
+        m, _ = build_model("k8")
+        m.load_state_dict(reference_state_dict(d, len(m.submodules), "w:"))
+        m = m.cuda().train()
+        opt = build_optimizer(Pk, m)
+        was = RT.TELESCOPED_TABLE_NORM
+        RT.TELESCOPED_TABLE_NORM = tele
+        try:
+            st = RT.RoutedAdaptStep(Pk, m, 1000, opt, grad_clip=1.0, graph=False, jitter="given")
+        finally:
+            RT.TELESCOPED_TABLE_NORM = was
+        assert st.tele == tele
+        rays = torch.from_numpy(d["train0:rays"]).cuda()
+        rgbs = torch.from_numpy(d["train0:rgbs"]).cuda()
+        u = torch.from_numpy(d["train0:u"]).cuda()
+        st(rays, rgbs, jitter_u=u)
+        st(rays, rgbs, jitter_u=u)   # second step: the Adam pass cleared the tables in between
+        torch.cuda.synchronize()
+        norms.append(float(st.last_norm[0]))
+        assert float(st.table_sumsq[0]) == 0.0   # reset for the next step
+    assert abs(norms[0] - norms[1]) <= 1e-6 * norms[1], norms
