@@ -1066,11 +1066,22 @@ __global__ void __launch_bounds__(256) mlp_dw_reduce_pairs_kernel(const float* _
     const int e = blockIdx.x * 32 + c;
     const int64_t R = seg[K] / 128, k0 = seg[k] / 128, k1 = seg[k + 1] / 128;
     float s = 0.0f;
-    if (e < NDW && k1 > k0)
-        for (int b = row; b < G; b += 8) {
+    if (e < NDW && k1 > k0) {
+        // only the workgroups whose round range [b R / G, (b+1) R / G) meets [k0, k1) hold a copy (the
+        // ranges are monotone in b: stop past k1); same summation order as before, the loads issued
+        // unconditionally (every copy slot is allocated) so 8 copies are in flight together -- a
+        // load under the condition made this a chain of memory latencies (40 us per step at K = 8)
+        // first b whose range can meet [k0, k1): (b + 1) R / G > k0 needs b >= k0 G / R - 1
+        const int64_t bf = R > 0 ? (k0 * G) / R - 1 : 0;
+        const int b0 = (int)((bf < 0 ? 0 : bf) & ~(int64_t)7) + row;  // same residue mod 8: same order
+#pragma unroll 8
+        for (int b = b0; b < G; b += 8) {
             const int64_t lo = (int64_t)b * R / G, hi = ((int64_t)b + 1) * R / G;
-            if (lo < hi && lo < k1 && hi > k0) s += partial[((int64_t)b * K + k) * NDW + e];
+            if (lo >= k1) break;
+            const float v = partial[((int64_t)b * K + k) * NDW + e];
+            if (lo < hi && hi > k0) s += v;
         }
+    }
     red[row][c] = s;
     __syncthreads();
     if (row == 0 && e < NDW) {
