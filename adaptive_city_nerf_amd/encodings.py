@@ -8,7 +8,9 @@ absent), reproduced bit-exactly by the HIP kernels (tests/test_gpu_kernels.py). 
 """
 from __future__ import annotations
 
+import contextlib
 import math
+import threading
 from typing import Literal, Optional
 
 import torch
@@ -89,11 +91,30 @@ class SHEncoder(nn.Module):
         return ops.sh_fwd(d, self.levels).to(d.dtype)
 
 
+_ACC = threading.local()
+
+
+@contextlib.contextmanager
+def accumulate_table_grad():
+    """Inside this context a hash-grid backward scatters the table gradient straight into the table's
+    existing ``.grad`` buffer (float atomics onto the accumulated values) and hands autograd None for the
+    table: no 128 MiB zero-fill for a fresh gradient and no 128 MiB AccumulateGrad add per backward.
+    The sum is the same (up to fp32 summation order, which the atomics leave unordered anyway).  Used by
+    the graph-replayed meta step, whose persistent .grad buffers are accumulated over its tasks."""
+    prev = getattr(_ACC, "on", False)
+    _ACC.on = True
+    try:
+        yield
+    finally:
+        _ACC.on = prev
+
+
 class _HashGridFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x01, table, enc):
         ctx.save_for_backward(x01)
         ctx.enc = enc
+        ctx.table = table
         return ops.hashgrid_fwd(x01, table, enc._res_host, enc.log2_hashmap_size, enc.features_per_level,
                                 enc._interp_code)
 
@@ -106,6 +127,12 @@ class _HashGridFn(torch.autograd.Function):
                            "path (the reference pipelines never request them)")
         gt = None
         if ctx.needs_input_grad[1]:
+            tab = ctx.table
+            into = tab.grad if getattr(_ACC, "on", False) and not torch.are_deterministic_algorithms_enabled() else None
+            if into is not None and into.shape == tab.shape and into.dtype == torch.float32 and into.is_contiguous():
+                ops.hashgrid_bwd(x01, g.contiguous(), enc._res_host, enc.log2_hashmap_size, enc.features_per_level,
+                                 enc._interp_code, out=into)
+                return None, None, None
             gt = ops.hashgrid_bwd(x01, g.contiguous(), enc._res_host, enc.log2_hashmap_size, enc.features_per_level,
                                   enc._interp_code)
         return None, gt, None

@@ -40,6 +40,7 @@ import torch
 import torch.distributed as dist
 
 from .expert_parallel import expert_owner, global_clip_grad_norm_
+from .encodings import accumulate_table_grad
 from .optim import FusedAdam
 from .ray_rendering import encoding_frozen, second_order
 from .train import compute_mse_loss
@@ -85,6 +86,21 @@ def snapshot_model_dict(model):
 
 
 # ============================================================================ inner loop
+_ONES = {}
+
+
+def _ones_like_scalar(loss):
+    """A persistent 1.0 of the loss's device / dtype as autograd's output gradient (autograd would fill a
+    fresh one per backward: one more launch per inner step; the value is the same)."""
+    if loss.dim() != 0:
+        return None
+    key = (loss.device, loss.dtype)
+    t = _ONES.get(key)
+    if t is None:
+        t = _ONES[key] = torch.ones((), device=loss.device, dtype=loss.dtype)
+    return t
+
+
 def task_adapt(P, model, support, inner_lr, iterations, active_module=None):
     """Inner-loop adaptation of the fast weights on a support set (meta_core.py:14-67)."""
     algo = str(getattr(P, "algo", "")).lower()
@@ -96,7 +112,8 @@ def task_adapt(P, model, support, inner_lr, iterations, active_module=None):
         with second_order(not first_order), encoding_frozen(first_order):
             loss = compute_loss(P, model, support, params=fast, active_module=active_module, grad_buffer={},
                                 update_fisher=True)
-        grads = torch.autograd.grad(loss, tuple(fast.values()), create_graph=not first_order, allow_unused=True)
+        grads = torch.autograd.grad(loss, tuple(fast.values()), grad_outputs=_ones_like_scalar(loss),
+                                    create_graph=not first_order, allow_unused=True)
         live = [k for k, g in enumerate(grads) if g is not None]
         if first_order and live:
             # the same w - lr * g (mul, then sub: bitwise equal) as two multi-tensor launches instead of
@@ -426,7 +443,16 @@ class GraphedMetaStep:
         ns, nq = self.shapes[cid]
         fast, inner = task_adapt(P, self.model, st["support"], P.inner_lr, P.inner_iter, active_module=cid)
         loss_q = compute_loss(P, self.model, st["query"], params=fast, active_module=cid)
-        (loss_q * st["wq"]).backward()
+        # the task's outer gradient added into the persistent .grad buffers: the table scatter adds into
+        # its buffer directly (encodings.accumulate_table_grad), the other tensors with one multi-tensor
+        # add instead of an AccumulateGrad launch each (same sums as .backward())
+        targets = self.params   # every optimised tensor (those the task does not reach come back None)
+        with accumulate_table_grad():
+            lq = loss_q * st["wq"]
+            gs = torch.autograd.grad(lq, targets, grad_outputs=_ones_like_scalar(lq), allow_unused=True)
+        live = [(p.grad, g) for p, g in zip(targets, gs) if g is not None]
+        if live:
+            torch._foreach_add_([a for a, _ in live], [b for _, b in live])
         if inner:
             self.inner_acc.add_(inner[-1].detach() * ns)
         self.q_acc.add_(loss_q.detach() * nq)

@@ -57,14 +57,21 @@ def hashgrid_fwd(x01: torch.Tensor, table: torch.Tensor, resolutions: Sequence[i
 
 
 def hashgrid_bwd(x01: torch.Tensor, grad_out: torch.Tensor, resolutions: Sequence[int], log2T: int, F: int,
-                 interp: int, deterministic: Optional[bool] = None) -> torch.Tensor:
+                 interp: int, deterministic: Optional[bool] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Table gradient (scatter-add).  ``deterministic`` (default: torch.are_deterministic_algorithms_enabled())
     selects the sort-based backward (acn_hashgrid_bwd_det: bitwise reproducible, every row summed in point
-    order) over the float-atomic one."""
+    order) over the float-atomic one.  ``out``: an existing (L * 2^log2T, F) fp32 buffer the float-atomic
+    scatter adds into (accumulation; not with the deterministic backward)."""
     L = len(resolutions)
     x = _f32(x01).view(-1, 3)
     g = _f32(grad_out).view(-1, L * F)
-    gt = torch.zeros(L << log2T, F, device=x.device, dtype=torch.float32)
+    if out is not None:
+        if deterministic:
+            raise ValueError("hashgrid_bwd: out= accumulates with atomics; not available in deterministic mode")
+        if tuple(out.shape) != (L << log2T, F) or out.dtype != torch.float32 or not out.is_contiguous():
+            raise ValueError("hashgrid_bwd: out must be a contiguous fp32 (L * 2^log2T, F) buffer")
+        deterministic = False
+    gt = out if out is not None else torch.zeros(L << log2T, F, device=x.device, dtype=torch.float32)
     res = (C.c_int32 * L)(*[int(r) for r in resolutions])
     if deterministic is None:
         deterministic = torch.are_deterministic_algorithms_enabled()

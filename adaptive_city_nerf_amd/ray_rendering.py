@@ -137,6 +137,9 @@ class _VolumeRenderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, rgb_sigma, t_vals, bg_rgb, sigma_scale):
         rgb, depth, w, acc = ops.volume_render(rgb_sigma, t_vals, bg_rgb, sigma_scale=sigma_scale)
+        # outputs the loss does not use (depth, weights, acc in training) reach backward as None: the
+        # kernel treats a NULL output gradient as zero, so autograd need not zero-fill them (3 launches)
+        ctx.set_materialize_grads(False)
         ctx.save_for_backward(rgb_sigma, t_vals, bg_rgb)
         ctx.sigma_scale = sigma_scale
         return rgb, depth, w, acc
