@@ -101,6 +101,8 @@ SIGNATURES = {
     "acn_volume_render_bwd": ([vp, vp, vp, i64, i32, f32, vp, vp, vp, vp, vp, vp, vp], C.c_int),
     "acn_grad_sumsq": ([vp, vp, i64, vp, vp, vp], C.c_int),
     "acn_mse_linear_fwd": ([vp, vp, i64, vp, vp], C.c_int),
+    "acn_mse_linear_workspace_bytes": ([], C.c_size_t),
+    "acn_mse_linear_fwd_ws": ([vp, vp, i64, vp, vp, C.c_size_t, vp], C.c_int),
     "acn_mse_linear_bwd": ([vp, vp, i64, vp, vp, vp], C.c_int),
     "acn_clip_coef": ([vp, f32, vp, vp], C.c_int),
     "acn_adam_step": ([vp, vp, i64, vp, i32, vp, vp], C.c_int),

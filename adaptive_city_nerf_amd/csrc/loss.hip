@@ -44,6 +44,47 @@ __global__ void __launch_bounds__(kThreads) mse_linear_fwd_kernel(const float* _
     }
 }
 
+// Multi-workgroup form (acn_mse_linear_fwd_ws): G workgroups of 256 threads, thread i of workgroup b
+// sums elements b*256 + i, + G*256, ... in double; the workgroup sums in a fixed order into partials[b];
+// the last workgroup to finish (ticket counter) adds partials[0..G) in order, writes the loss and resets
+// the counter.  Deterministic (fixed assignment and order for a given n).
+constexpr int kWsThreads = 256;
+constexpr int kWsMaxBlocks = 64;
+__global__ void __launch_bounds__(kWsThreads) mse_linear_fwd_ws_kernel(const float* __restrict__ pred,
+                                                                       const float* __restrict__ gt, int64_t n,
+                                                                       double* __restrict__ partials,
+                                                                       unsigned int* __restrict__ counter,
+                                                                       float* __restrict__ loss) {
+    __shared__ double red[kWsThreads / 64];
+    __shared__ bool last;
+    double acc = 0.0;
+    const int64_t stride = (int64_t)gridDim.x * kWsThreads;
+#pragma unroll 8
+    for (int64_t e = (int64_t)blockIdx.x * kWsThreads + threadIdx.x; e < n; e += stride) {
+        const float d = clamp01(pred[e]) - gt_linear(gt[e]);
+        acc += (double)(d * d);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int i = 0; i < kWsThreads / 64; ++i) t += red[i];
+        partials[blockIdx.x] = t;
+        __threadfence();
+        last = atomicAdd(counter, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last && threadIdx.x == 0) {
+        __threadfence();
+        double t = 0.0;
+        for (unsigned int b = 0; b < gridDim.x; ++b) t += __hip_atomic_load(&partials[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        loss[0] = (float)(t / (double)n);
+        counter[0] = 0u;
+    }
+}
+
 // d loss / d pred: mse_loss_backward (2 / numel * (input - target) * grad_output, in double) through the
 // clamp's backward (gradient where 0 <= pred <= 1)
 __global__ void __launch_bounds__(256) mse_linear_bwd_kernel(const float* __restrict__ pred, const float* __restrict__ gt,
@@ -63,6 +104,21 @@ extern "C" int acn_mse_linear_fwd(const float* pred, const float* gt, int64_t n,
     ACN_REQUIRE(n >= 1 && pred && gt && loss, "acn_mse_linear_fwd: bad arguments");
     hipLaunchKernelGGL(mse_linear_fwd_kernel, dim3(1), dim3(kThreads), 0, (hipStream_t)stream, pred, gt, n, loss);
     return acn_check_launch("acn_mse_linear_fwd");
+}
+
+extern "C" size_t acn_mse_linear_workspace_bytes(void) { return kWsMaxBlocks * sizeof(double) + 16; }
+
+extern "C" int acn_mse_linear_fwd_ws(const float* pred, const float* gt, int64_t n, float* loss, void* workspace,
+                                     size_t workspace_bytes, void* stream) {
+    ACN_REQUIRE(n >= 1 && pred && gt && loss && workspace, "acn_mse_linear_fwd_ws: bad arguments");
+    ACN_REQUIRE(workspace_bytes >= acn_mse_linear_workspace_bytes(), "acn_mse_linear_fwd_ws: workspace too small");
+    int64_t g = (n + kWsThreads * 8 - 1) / (kWsThreads * 8);
+    g = g < 1 ? 1 : (g > kWsMaxBlocks ? kWsMaxBlocks : g);
+    double* partials = (double*)workspace;
+    unsigned int* counter = (unsigned int*)((char*)workspace + kWsMaxBlocks * sizeof(double));
+    hipLaunchKernelGGL(mse_linear_fwd_ws_kernel, dim3((unsigned)g), dim3(kWsThreads), 0, (hipStream_t)stream, pred, gt,
+                       n, partials, counter, loss);
+    return acn_check_launch("acn_mse_linear_fwd_ws");
 }
 
 extern "C" int acn_mse_linear_bwd(const float* pred, const float* gt, int64_t n, const float* g_loss, float* g_pred,

@@ -314,8 +314,24 @@ def mse_linear_fwd(pred: torch.Tensor, gt: torch.Tensor) -> torch.Tensor:
     if p.numel() != g.numel() or p.numel() == 0:
         raise ValueError(f"mse_linear: pred / gt sizes {p.numel()} / {g.numel()}")
     out = torch.empty((), device=p.device, dtype=torch.float32)
-    check(_lib.lib().acn_mse_linear_fwd(ptr(p), ptr(g), p.numel(), ptr(out), stream_of(p)), "acn_mse_linear_fwd")
+    ws = _mse_ws(p.device)
+    check(_lib.lib().acn_mse_linear_fwd_ws(ptr(p), ptr(g), p.numel(), ptr(out), ptr(ws), ws.numel(), stream_of(p)),
+          "acn_mse_linear_fwd_ws")
     return out
+
+
+_MSE_WS = {}
+
+
+def _mse_ws(device) -> torch.Tensor:
+    """Zeroed workspace of acn_mse_linear_fwd_ws per (device, stream): its ticket counter returns to 0
+    after every call, so one buffer serves every later call (and graph replay) on that stream."""
+    key = (device, int(torch.cuda.current_stream(device).cuda_stream))
+    ws = _MSE_WS.get(key)
+    if ws is None:
+        ws = _MSE_WS[key] = torch.zeros(int(_lib.lib().acn_mse_linear_workspace_bytes()), dtype=torch.uint8,
+                                        device=device)
+    return ws
 
 
 def mse_linear_bwd(pred: torch.Tensor, gt: torch.Tensor, g_loss: torch.Tensor) -> torch.Tensor:
