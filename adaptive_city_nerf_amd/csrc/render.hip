@@ -1083,6 +1083,9 @@ __device__ __forceinline__ uint32_t ray_expert_mask(const FieldCfg& cfg, int rou
     return any;
 }
 
+#ifndef ACN_ORDER_DIAG
+#define ACN_ORDER_DIAG 0  // diagnostic builds of ray_order_kernel (1-3: stop after a phase; wrong orders)
+#endif
 #ifndef ACN_SLOTS_BAND
 #define ACN_SLOTS_BAND 0
 #endif
@@ -1586,6 +1589,10 @@ __global__ void __launch_bounds__(1024) ray_order_kernel(const float* __restrict
             }
         }
     }
+#if ACN_ORDER_DIAG == 3  // diagnostic only (tools/order_diag.sh): loads, then the identity order
+    for (int i = tid; i < N; i += 1024) order[i] = i + (int)(sx * 0.0f);
+    return;
+#endif
     block_reduce3<0>(sx, sy, sz, red);
     const float mn = sqrtf(sx * sx + sy * sy + sz * sz);
     float mx = 0.0f, my = 0.0f, mz = 1.0f;
@@ -1613,9 +1620,17 @@ __global__ void __launch_bounds__(1024) ray_order_kernel(const float* __restrict
         float u, v;
         if (coords(i, u, v)) umin = fminf(umin, u), umax = fmaxf(umax, u), vmin = fminf(vmin, v), vmax = fmaxf(vmax, v);
     }
+#if ACN_ORDER_DIAG == 2  // diagnostic only: + mean direction and the coordinate pass, identity order
+    for (int i = tid; i < N; i += 1024) order[i] = i + (int)(umin * 0.0f + umax * 0.0f);
+    return;
+#endif
+#if ACN_ORDER_DIAG == 1  // diagnostic only: fixed range instead of the bounding-box reduction
+    umin = -2.0f, vmin = -2.0f, umax = 2.0f, vmax = 2.0f;
+#else
     umin = -umin, vmin = -vmin;  // one max-reduction for all four
     block_reduce4max(umin, vmin, umax, vmax, red);
     umin = -umin, vmin = -vmin;
+#endif
     const float su = umax > umin ? 63.999f / (umax - umin) : 0.0f;
     const float sv = vmax > vmin ? 63.999f / (vmax - vmin) : 0.0f;
     for (int i = tid; i < N; i += 1024) {

@@ -1,5 +1,6 @@
 #!/bin/bash
-# ray_order_kernel cost: rocprof kernel stats of the C2 bench (base build and any build_variants given)
+# ray_order_kernel cost: rocprof kernel stats of the C2 bench (base build and any build_variants given,
+# e.g. tools/build_variants.sh od1:render.hip:"-DACN_ORDER_DIAG=1" ... ; then tools/order_diag.sh od1 od2 od3)
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
