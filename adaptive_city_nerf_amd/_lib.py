@@ -98,6 +98,8 @@ SIGNATURES = {
     "acn_clamp_rays": ([vp, i64, i32, i32, f32, i32, f32, f32, f32, vp, vp], C.c_int),
     "acn_routing_fwd": ([vp, i64, i64, vp, vp, vp, vp], C.c_int),
     "acn_background_fwd": ([vp, i64, vp, vp, vp], C.c_int),
+    "acn_background_bwd_workspace_bytes": ([], C.c_size_t),
+    "acn_background_bwd": ([vp, i64, vp, vp, vp, vp, vp, vp, vp, C.c_size_t, vp], C.c_int),
     "acn_volume_render_bwd": ([vp, vp, vp, i64, i32, f32, vp, vp, vp, vp, vp, vp, vp], C.c_int),
     "acn_grad_sumsq": ([vp, vp, i64, vp, vp, vp], C.c_int),
     "acn_mse_linear_fwd": ([vp, vp, i64, vp, vp], C.c_int),

@@ -1387,6 +1387,83 @@ __global__ void __launch_bounds__(256) background_kernel(BgArgs bg, const float*
     }
 }
 
+// Background head backward (the autograd of MetaContainer.background_color's bg_mlp, meta_container.py
+// :347-382): per ray the forward is re-run (lane j = hidden unit j), then with do = g (1 - y) y
+// (sigmoid_backward), dW2[c][j] += do_c h_j, db2 += do, dh_j = sum_c W2[c][j] do_c where h_j > 0
+// (threshold_backward), dW1[j][:] += dh_j sh, db1[j] += dh_j.  Every wave of the fixed grid keeps its
+// lane's sums for its rays (grid-stride) and writes them once; bg_bwd_reduce_kernel adds the waves'
+// copies in wave order (deterministic, no atomics).
+constexpr int kBgWaves = 256;   // 64 workgroups x 4 waves
+constexpr int kBgLane = 23;     // per lane: dW1 row (16), db1, dW2 column (3), db2 (3, lane 0)
+__global__ void __launch_bounds__(256) background_bwd_kernel(BgArgs bg, const float* __restrict__ d, int64_t N,
+                                                             const float* __restrict__ g,
+                                                             float* __restrict__ partial) {
+    const int lane = threadIdx.x & 63;
+    const int wave = (int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+    float a[kBgLane];
+#pragma unroll
+    for (int i = 0; i < kBgLane; ++i) a[i] = 0.0f;
+    const int H = bg.hidden;
+    for (int64_t r = wave; r < N; r += kBgWaves) {
+        const float dx = d[3 * r], dy = d[3 * r + 1], dz = d[3 * r + 2];
+        const float n = clamp_min_nan(norm3(dx, dy, dz), 1e-12f);
+        float sh[16];
+        sh_encode<3>(dx / n, dy / n, dz / n, sh);
+        float hv = 0.0f;
+        if (lane < H) {
+            float s = 0.0f;
+            for (int k = 0; k < 16; ++k) s = fmaf(sh[k], bg.w1[lane * 16 + k], s);
+            hv = s + bg.b1[lane];
+            hv = hv < 0.0f ? 0.0f : hv;
+        }
+        float dov[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            float v = lane < H ? hv * bg.w2[c * H + lane] : 0.0f;
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+            const float y = sigmoidf_(v + bg.b2[c]);
+            dov[c] = (g[3 * r + c] * (1.0f - y)) * y;
+        }
+        if (lane < H) {
+            float dh = 0.0f;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                a[17 + c] += dov[c] * hv;
+                dh += bg.w2[c * H + lane] * dov[c];
+            }
+            dh = hv > 0.0f ? dh : 0.0f;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) a[k] += dh * sh[k];
+            a[16] += dh;
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) a[20 + c] += dov[c];
+        }
+    }
+    float* dst = partial + ((int64_t)wave * 64 + lane) * kBgLane;
+#pragma unroll
+    for (int i = 0; i < kBgLane; ++i) dst[i] = a[i];
+}
+
+// gw1 (H,16), gb1 (H), gw2 (3,H), gb2 (3): the sum of the waves' copies, in wave order
+__global__ void __launch_bounds__(256) bg_bwd_reduce_kernel(const float* __restrict__ partial, int H,
+                                                            float* __restrict__ gw1, float* __restrict__ gb1,
+                                                            float* __restrict__ gw2, float* __restrict__ gb2) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;  // (lane, slot)
+    if (e >= 64 * kBgLane) return;
+    const int lane = e / kBgLane, i = e - lane * kBgLane;
+    if (i >= 20 ? lane != 0 : lane >= H) return;
+    float s = 0.0f;
+#pragma unroll 8
+    for (int w = 0; w < kBgWaves; ++w) s += partial[((int64_t)w * 64 + lane) * kBgLane + i];
+    if (i < 16) gw1[lane * 16 + i] = s;
+    else if (i == 16) gb1[lane] = s;
+    else if (i < 20) gw2[(i - 17) * H + lane] = s;
+    else gb2[i - 20] = s;
+}
+
 // ------------------------------------------------------------------------------------------
 int g_num_cus = 0;
 int num_cus() {
@@ -1799,6 +1876,24 @@ extern "C" int acn_routing_fwd(const float* pts, int64_t M, int64_t ld, const ac
     hipLaunchKernelGGL(routing_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, (hipStream_t)stream, cfg, pts, M,
                        ld, weights, hard);
     return acn_check_launch("acn_routing_fwd");
+}
+
+extern "C" size_t acn_background_bwd_workspace_bytes(void) { return (size_t)kBgWaves * 64 * kBgLane * sizeof(float); }
+
+extern "C" int acn_background_bwd(const float* dirs, int64_t N, const acn_background* bg, const float* g_out,
+                                  float* g_w1, float* g_b1, float* g_w2, float* g_b2, void* workspace,
+                                  size_t workspace_bytes, void* stream) {
+    ACN_REQUIRE(N >= 1 && bg && dirs && g_out && g_w1 && g_b1 && g_w2 && g_b2 && workspace,
+                "acn_background_bwd: bad arguments");
+    ACN_REQUIRE(bg->mode == ACN_BG_MLP && bg->w1 && bg->b1 && bg->w2 && bg->b2, "acn_background_bwd: MLP background only");
+    ACN_REQUIRE(bg->hidden >= 1 && bg->hidden <= 64, "bg_hidden must be in [1, 64], got %d", bg->hidden);
+    ACN_REQUIRE(workspace_bytes >= acn_background_bwd_workspace_bytes(), "acn_background_bwd: workspace too small");
+    BgArgs b{bg->mode, bg->hidden, {bg->color[0], bg->color[1], bg->color[2]}, bg->w1, bg->b1, bg->w2, bg->b2};
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(background_bwd_kernel, dim3(kBgWaves / 4), dim3(256), 0, s, b, dirs, N, g_out, (float*)workspace);
+    hipLaunchKernelGGL(bg_bwd_reduce_kernel, dim3((64 * kBgLane + 255) / 256), dim3(256), 0, s, (const float*)workspace,
+                       bg->hidden, g_w1, g_b1, g_w2, g_b2);
+    return acn_check_launch("acn_background_bwd");
 }
 
 extern "C" int acn_background_fwd(const float* dirs, int64_t N, const acn_background* bg, float* out, void* stream) {

@@ -448,6 +448,26 @@ def background_fwd(dirs: torch.Tensor, background) -> torch.Tensor:
     return out
 
 
+def background_bwd(dirs: torch.Tensor, background, g_out: torch.Tensor, grads: Sequence[torch.Tensor]) -> None:
+    """Gradients of the MLP background head's four tensors (written into ``grads`` = [gw1, gb1, gw2, gb2],
+    overwritten) for dL/d(bg rgb) ``g_out`` (N,3) (acn_background_bwd)."""
+    d = _f32(dirs).view(-1, 3)
+    g = _f32(g_out).view(-1, 3)
+    for t in grads:
+        if not (t.is_contiguous() and t.dtype == torch.float32 and t.device == d.device):
+            raise AcnError("background_bwd: gradient buffers must be contiguous fp32 on the rays' device")
+    L = _lib.lib()
+    key = (d.device, int(torch.cuda.current_stream(d.device).cuda_stream))
+    ws = _BG_WS.get(key)
+    if ws is None:
+        ws = _BG_WS[key] = torch.empty(int(L.acn_background_bwd_workspace_bytes()), dtype=torch.uint8, device=d.device)
+    check(L.acn_background_bwd(ptr(d), d.shape[0], C.byref(background), ptr(g), *[ptr(t) for t in grads], ptr(ws),
+                               ws.numel(), stream_of(d)), "acn_background_bwd")
+
+
+_BG_WS = {}
+
+
 # ------------------------------------------------------------------------------------------
 # expert MLP of the training path (mlp_train.hip)
 MLP_SAVE_COLS, MLP_GRAD_COLS = 325, 275

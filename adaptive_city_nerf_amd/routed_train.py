@@ -53,6 +53,9 @@ NORM_ELSEWHERE_FLAG = 1 << 17  # grad_sumsq_slots_ex: this tensor's sum of squar
 # The tables' share of the clip norm from the scatter's returning atomics (acn_hashgrid_bwd_pairs_sumsq)
 # instead of a pass over the K x 128 MiB gradient buffers
 TELESCOPED_TABLE_NORM = os.environ.get("ACN_TELE_NORM", "1") != "0"
+# The background head's forward / backward as two HIP launches (acn_background_fwd / _bwd) instead of the
+# ~15 torch launches of its autograd graph
+FUSED_BACKGROUND = os.environ.get("ACN_FUSED_BG", "1") != "0"
 
 
 def _stream(device) -> int:
@@ -122,6 +125,11 @@ class RoutedAdaptStep:
         self.gtables = [torch.zeros_like(e.hash_table) for e in encs]
         self.bg_params = list(model.bg_mlp.parameters())
         self.gbg = [torch.zeros_like(p) for p in self.bg_params]
+        self.dirs = torch.zeros(N, 3, **f32)
+        try:   # (acn_background, the tensors it points into)
+            self.bg_spec, self._bg_keep = model.background_spec() if FUSED_BACKGROUND else (None, None)
+        except AcnError:
+            self.bg_spec, self._bg_keep = None, None
         slot_of, zero_of = {}, {}
         for k, sub in enumerate(model.submodules):
             sub.xyz_encoder.hash_table.grad = self.gtables[k]
@@ -237,17 +245,29 @@ class RoutedAdaptStep:
         check(L.acn_mlp_train_fwd_pairs(ptr(self.h0), ptr(self.sh), ptr(self.seg), K, ptr(self.mws), ptr(self.out), s),
               "acn_mlp_train_fwd_pairs")
         rs = ops.routed_blend_fwd(self.out, self.pw, self.pmap).view(N, S, 4).requires_grad_(True)
-        # the shared part under torch autograd: background head, compositing, colour transform, MSE
+        # the shared part: compositing, colour transform and MSE under torch autograd (HIP kernels); the
+        # background head as its fused HIP forward and backward (writing the persistent .grad buffers), or
+        # under autograd when the head is not the HIP-supported SH-4 MLP
         from .ray_rendering import volume_render
-        with torch.enable_grad():
-            bg = self.model.background_color(self.rays[:, 3:6])
-            rgb = volume_render(rs, self.t, bg_rgb=bg)[0]
-            loss = mse_color_loss(rgb, self.rgbs, self.P.color_space)
-            grads = torch.autograd.grad(loss, [rs] + self.bg_params)
+        if self.bg_spec is not None:
+            self.dirs.copy_(self.rays[:, 3:6])
+            bg = ops.background_fwd(self.dirs, self.bg_spec).requires_grad_(True)
+            with torch.enable_grad():
+                rgb = volume_render(rs, self.t, bg_rgb=bg)[0]
+                loss = mse_color_loss(rgb, self.rgbs, self.P.color_space)
+                g_rs, g_bg = torch.autograd.grad(loss, [rs, bg])
+            ops.background_bwd(self.dirs, self.bg_spec, g_bg, self.gbg)
+        else:
+            with torch.enable_grad():
+                bg = self.model.background_color(self.rays[:, 3:6])
+                rgb = volume_render(rs, self.t, bg_rgb=bg)[0]
+                loss = mse_color_loss(rgb, self.rgbs, self.P.color_space)
+                grads = torch.autograd.grad(loss, [rs] + self.bg_params)
+            g_rs = grads[0]
+            for g, buf in zip(grads[1:], self.gbg):
+                buf.copy_(g)
         self.loss.copy_(loss.detach())
-        for g, buf in zip(grads[1:], self.gbg):
-            buf.copy_(g)
-        gout = ops.routed_blend_bwd(grads[0].reshape(M, 4).contiguous(), self.pidx, self.pw, live=self.seg[K:K + 1])
+        gout = ops.routed_blend_bwd(g_rs.reshape(M, 4).contiguous(), self.pidx, self.pw, live=self.seg[K:K + 1])
         check(L.acn_mlp_train_bwd_dw_pairs(ptr(self.h0), ptr(self.sh), ptr(self.out), ptr(gout), ptr(self.seg), K,
                                            ptr(self.mws), ptr(self.dw), ptr(self.gh0), s), "acn_mlp_train_bwd_dw_pairs")
         bhook = BWD_HOOK if self.graph is None else None

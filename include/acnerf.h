@@ -205,6 +205,13 @@ int acn_routing_fwd(const float* pts, int64_t M, int64_t ld, const acn_routing* 
 
 /* MetaContainer.background_color (meta_container.py:347-382): dirs (N,3) -> rgb (N,3). */
 int acn_background_fwd(const float* dirs, int64_t N, const acn_background* bg, float* out, void* stream);
+/* Backward of the MLP background head (the autograd of bg_mlp in MetaContainer.background_color,
+ * meta_container.py:347-382) for dL/d(bg rgb) g_out (N,3): writes (overwrites) the gradients of
+ * bg_mlp.0.weight (H,16), .0.bias (H), bg_mlp.2.weight (3,H), .2.bias (3).  Deterministic (per-wave sums
+ * added in wave order); workspace of acn_background_bwd_workspace_bytes(). */
+size_t acn_background_bwd_workspace_bytes(void);
+int acn_background_bwd(const float* dirs, int64_t N, const acn_background* bg, const float* g_out, float* g_w1,
+                       float* g_b1, float* g_w2, float* g_b2, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------- */
 /* Optimizer step of the online adaptation loop (pipelines/online_stage/runtime_adapt.py:305-309):

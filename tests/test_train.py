@@ -401,3 +401,34 @@ def test_routed_step_telescoped_table_norm_equals_full_pass():
         norms.append(float(st.last_norm[0]))
         assert float(st.table_sumsq[0]) == 0.0   # reset for the next step
     assert abs(norms[0] - norms[1]) <= 1e-6 * norms[1], norms
+
+
+@pytest.mark.gpu
+def test_background_head_backward_matches_autograd():
+    """acn_background_bwd (fused re-run forward + backward of the SH-4 background MLP, per-wave sums added
+    in wave order) against torch autograd of MetaContainer.background_color's composed chain, including
+    directions of mixed length, zero hidden units (ReLU mask) and saturated sigmoids."""
+    from adaptive_city_nerf_amd import ops
+    from test_module_api import build_model
+    m, _ = build_model("k4")
+    m = m.cuda()
+    g = torch.Generator().manual_seed(11)
+    with torch.no_grad():
+        m.bg_mlp[0].weight.copy_(torch.randn(m.bg_mlp[0].weight.shape, generator=g))
+        m.bg_mlp[0].bias.copy_(torch.randn(m.bg_mlp[0].bias.shape, generator=g))
+        m.bg_mlp[2].weight.copy_(torch.randn(m.bg_mlp[2].weight.shape, generator=g) * 3)
+    N = 3001
+    d = (torch.randn(N, 3, generator=g) * torch.rand(N, 1, generator=g) * 5).cuda()
+    go = torch.randn(N, 3, generator=g).cuda()
+    params = list(m.bg_mlp.parameters())
+    with torch.enable_grad():
+        ref = torch.autograd.grad((m.background_color(d) * go).sum(), params)
+        spec, _keep = m.background_spec()
+    fwd = ops.background_fwd(d, spec)
+    with torch.no_grad():
+        np.testing.assert_allclose(fwd.cpu().numpy(), m.background_color(d).cpu().numpy(), rtol=0, atol=2e-6)
+    got = [torch.full_like(p, float("nan")) for p in params]
+    ops.background_bwd(d, spec, go, got)
+    for a, b in zip(got, ref):
+        scale = float(b.abs().max())
+        np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=0, atol=1e-5 * scale)
