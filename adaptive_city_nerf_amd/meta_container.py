@@ -30,6 +30,26 @@ def build_expert(nerf_variant: str, **nerf_kwargs) -> nn.Module:
                               "(the reference's MetaNeRF variant is itself broken, SURVEY §2)")
 
 
+class _BackgroundFn(torch.autograd.Function):
+    """The SH-4 background head with the HIP forward (acn_background_fwd) and backward
+    (acn_background_bwd: the 643 parameter gradients in two launches instead of the ~15 of the torch
+    chain's autograd graph).  First-order: the directions get no gradient."""
+
+    @staticmethod
+    def forward(ctx, d, bg, w1, b1, w2, b2):
+        ctx.save_for_backward(d)
+        ctx.bg = bg
+        ctx.shapes = [t.shape for t in (w1, b1, w2, b2)]
+        return ops.background_fwd(d, bg)
+
+    @staticmethod
+    def backward(ctx, g):
+        (d,) = ctx.saved_tensors
+        grads = [torch.empty(sh, device=d.device, dtype=torch.float32) for sh in ctx.shapes]
+        ops.background_bwd(d, ctx.bg, g.contiguous(), grads)
+        return (None, None, *[gr if need else None for gr, need in zip(grads, ctx.needs_input_grad[2:])])
+
+
 class MetaContainer(MetaModule):
     def __init__(self, num_submodules: int, centroids: torch.Tensor, aabb: torch.Tensor,
                  nerf_variant: Literal["instant", "vanilla"] = "instant", boundary_margin: float = 1.0,
@@ -197,6 +217,16 @@ class MetaContainer(MetaModule):
             raise ValueError(f"background_color expects (N,3) or (B,N,3), got {tuple(d.shape)}")
         shape = d.shape
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.bg_mlp.parameters()):
+            from .ray_rendering import _second_order
+            if d.is_cuda and not d.requires_grad and not _second_order():
+                try:
+                    bg, keep = self.background_spec()
+                except ops.AcnError:
+                    bg = None
+                if bg is not None:   # fused HIP forward + backward (acn_background_fwd / _bwd)
+                    m = self.bg_mlp
+                    return _BackgroundFn.apply(d.reshape(-1, 3).float().contiguous(), bg, m[0].weight, m[0].bias,
+                                               m[2].weight, m[2].bias).view(*shape[:-1], 3)
             dn = F.normalize(d.reshape(-1, 3), dim=-1)
             enc = self.bg_dir_enc(dn).to(self.bg_mlp[0].weight.dtype)
             return self.bg_mlp(enc).view(*shape[:-1], 3)
