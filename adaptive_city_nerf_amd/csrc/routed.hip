@@ -90,38 +90,54 @@ __global__ void __launch_bounds__(kBlk) routed_count_kernel(const float* __restr
 // one workgroup: per expert, exclusive scan of the block counts (in place) and the segment starts
 __global__ void __launch_bounds__(1024) routed_scan_kernel(int32_t* __restrict__ blk_cnt, int64_t nblk, int K,
                                                            int align, int64_t* __restrict__ starts) {
-    __shared__ int64_t part[1024];
-    __shared__ int64_t base;
-    const int tid = threadIdx.x;
+    // all K experts' scans at once: per-thread chunk sums, an inclusive wave scan (shuffles, no
+    // barriers), then the 16 wave totals through LDS (one barrier) -- integer sums, so the result equals
+    // the serial prefix sums exactly (a Hillis-Steele pass per expert cost 20 barriers each)
+    __shared__ int64_t wtot[16][kMaxK];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int64_t per = (nblk + 1023) / 1024;
     const int64_t b0 = tid * per, b1 = b0 + per < nblk ? b0 + per : nblk;
-    if (tid == 0) base = 0;
-    for (int k = 0; k < K; ++k) {
-        int64_t s = 0;
-        for (int64_t b = b0; b < b1; ++b) s += blk_cnt[b * K + k];
-        part[tid] = s;
-        __syncthreads();
-        for (int off = 1; off < 1024; off <<= 1) {  // inclusive Hillis-Steele scan
-            const int64_t v = tid >= off ? part[tid - off] : 0;
-            __syncthreads();
-            part[tid] += v;
-            __syncthreads();
+    int64_t sum[kMaxK], incl[kMaxK];
+#pragma unroll
+    for (int k = 0; k < kMaxK; ++k) sum[k] = 0;
+    for (int64_t b = b0; b < b1; ++b)
+#pragma unroll
+        for (int k = 0; k < kMaxK; ++k)
+            if (k < K) sum[k] += blk_cnt[b * K + k];
+#pragma unroll
+    for (int k = 0; k < kMaxK; ++k) {
+        int64_t v = sum[k];
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int64_t u = __shfl_up(v, off);
+            if (lane >= off) v += u;
         }
-        int64_t run = part[tid] - s;  // exclusive prefix of this thread's chunk
+        incl[k] = v;
+        if (lane == 63 && k < K) wtot[w][k] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kMaxK; ++k) {
+        if (k >= K) break;
+        int64_t run = incl[k] - sum[k];
+        for (int i = 0; i < w; ++i) run += wtot[i][k];
         for (int64_t b = b0; b < b1; ++b) {
             const int32_t c = blk_cnt[b * K + k];
             blk_cnt[b * K + k] = (int32_t)run;
             run += c;
         }
-        __syncthreads();
-        if (tid == 0) {
-            starts[k] = base;
-            starts[K + 1 + k] = part[1023];                      // real pair count of expert k
-            base += (part[1023] + align - 1) / align * align;    // segment padded to a multiple of align
-        }
-        __syncthreads();
     }
-    if (tid == 0) starts[K] = base;
+    if (tid == 0) {
+        int64_t base = 0;
+        for (int k = 0; k < K; ++k) {
+            int64_t total = 0;
+            for (int i = 0; i < 16; ++i) total += wtot[i][k];
+            starts[k] = base;
+            starts[K + 1 + k] = total;                        // real pair count of expert k
+            base += (total + align - 1) / align * align;      // segment padded to a multiple of align
+        }
+        starts[K] = base;
+    }
 }
 
 // padding slots of every segment: pidx -1 (no sample), x01 0.5, sh 0, pk = k
