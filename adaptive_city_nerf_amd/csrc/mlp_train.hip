@@ -252,8 +252,23 @@ __device__ __forceinline__ void fwd_layer(const float* W, int ld, const float* b
     }
 }
 
+#ifndef ACN_BWD_TR16
+#define ACN_BWD_TR16 1  // transposed weight reads of the backward layers on ds_read_b64_tr_b16 (0: ds_read_u16)
+#endif
+typedef __fp16 hf16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) hf16x4 lds_hf16x4;
+// ds_read_b64_tr_b16 (gfx950): per 16-lane group, lane 4q + p supplies the address of row q, columns 4p..4p+3
+// of a 4 x 16 block of 16-bit elements; lane i of the group receives column i, row q in element q.  The
+// address must point into LDS, 8-B aligned; EXEC must be all ones (every caller is wave-uniform).
+__device__ __forceinline__ f16x4 ds_read_tr16(const _Float16* p) {
+    return __builtin_bit_cast(f16x4, __builtin_amdgcn_ds_read_tr16_b64_v4f16((lds_hf16x4*)(p)));
+}
+
 // dX[ti] (input features 32ti..) = W^T . dY  (W rows = output features; k-steps whose 16 rows are all
-// >= NROW are skipped at compile time, padding rows inside a k-step are zero in the image)
+// >= NROW are skipped at compile time, padding rows inside a k-step are zero in the image).  The A operand
+// of lane (i, h) at k-step s is column 32 ti + i of W at rows xrow(s, h, 0..7) = base + 4h + 0..3 and
+// base + 8 + 4h + 0..3: two 4-row blocks, each one transposed read per plane (lane (g, q, p) of 16-lane
+// group g addresses row base [+ 8] + 4h + q, columns 32 ti + 16 (g & 1) + 4p).
 template <int NT, int KT, int NROW, int ROWS>
 __device__ __forceinline__ void bwd_layer(const float* W, int ld, const f32x16 (&dY)[KT], f32x16 (&dX)[NT],
                                           int lane) {
@@ -264,6 +279,9 @@ __device__ __forceinline__ void bwd_layer(const float* W, int ld, const f32x16 (
     split_tiles<KT>(dY, k, bh, bl);
     const _Float16* Wh = reinterpret_cast<const _Float16*>(W);
     const _Float16* Wlo = Wh + ROWS * ld;
+#if ACN_BWD_TR16
+    const int trow = 4 * h + ((lane >> 2) & 3), tcol = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+#endif
 #pragma unroll
     for (int ti = 0; ti < NT; ++ti) {
         f32x16 acc = 0.0f;
@@ -271,12 +289,20 @@ __device__ __forceinline__ void bwd_layer(const float* W, int ld, const f32x16 (
         for (int s = 0; s < 2 * KT; ++s) {
             if (32 * (s >> 1) + 16 * (s & 1) >= NROW) continue;
             f16x8 ahi, alo;
+#if ACN_BWD_TR16
+            {
+                const int o = (32 * (s >> 1) + 16 * (s & 1) + trow) * ld + 32 * ti + tcol;
+                ahi = cat44(ds_read_tr16(Wh + o), ds_read_tr16(Wh + o + 8 * ld));
+                alo = cat44(ds_read_tr16(Wlo + o), ds_read_tr16(Wlo + o + 8 * ld));
+            }
+#else
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
                 const int o = xrow(s, h, e) * ld + 32 * ti + i;
                 ahi[e] = Wh[o];
                 alo[e] = Wlo[o];
             }
+#endif
             acc = mfma_h(alo, bh[s], acc);
             acc = mfma_h(ahi, bl[s], acc);
             acc = mfma_h(ahi, bh[s], acc);

@@ -31,6 +31,7 @@ from __future__ import annotations
 import contextlib
 import io
 import math
+import os
 import random
 import time
 from collections import OrderedDict
@@ -248,12 +249,75 @@ def broadcast_experts(model, group=None):
 
 
 # ============================================================================ one meta step
+# train_step's FOMAML steps through the cached GraphedMetaStep (ACN_FAST_META=0: the eager step every time)
+FAST_META_STEP = os.environ.get("ACN_FAST_META", "1") != "0"
+
+
+def _graph_eligible(P, model, optimizer, scheduler, grad_scaler, group) -> bool:
+    if not FAST_META_STEP or str(getattr(P, "algo", "")).lower() != "fomaml" or not isinstance(optimizer, FusedAdam):
+        return False
+    if grad_scaler is not None and getattr(grad_scaler, "is_enabled", lambda: False)():
+        return False
+    if group is not None and dist.is_initialized() and dist.get_world_size(group) > 1:
+        return False
+    return hasattr(model, "submodules") and not getattr(model, "use_occ", False)
+
+
 def train_step(P, step, model, optimizer, task_data, metric_logger=None, logger=None, scheduler=None,
                grad_scaler=None, group=None):
     """One offline meta-training step over tasks grouped by region (meta_train_step.py:18-253).
 
     ``task_data``: {cid: [task, ...]} with task.support / task.query (or dict keys) holding
-    {"rays": (n, 8), "rgbs": (n, 3)}.  Returns a dict of the step's losses and timings."""
+    {"rays": (n, 8), "rgbs": (n, 3)}.  Returns a dict of the step's losses and timings.
+
+    FOMAML on one process with FusedAdam (the reference's configs/train.json setup) goes through a
+    GraphedMetaStep cached on the optimizer: the first call is the eager step, after which the per-region
+    task graphs and the outer update are captured, and later calls replay them (a step whose task shapes
+    the graphs do not cover runs eagerly inside it).  The replayed step skips meta_update's per-region
+    debug prints.  Everything else (MAML, Reptile, expert-parallel groups, a GradScaler) is eager."""
+    out = None
+    g = optimizer.__dict__.get("_acn_meta_graph") if _graph_eligible(P, model, optimizer, scheduler, grad_scaler,
+                                                                      group) else False
+    if g == "pending":   # second eligible call: capture now (the first call's gradients stayed readable)
+        try:
+            g = optimizer._acn_meta_graph = GraphedMetaStep(P, model, optimizer, task_data, warmup=0)
+        except (ValueError, TypeError):
+            g = optimizer._acn_meta_graph = False   # shapes the graphs cannot cover: stay eager
+    if isinstance(g, GraphedMetaStep):
+        out = g(step, task_data)
+        if out is not None and scheduler is not None:
+            scheduler.step()
+    else:
+        out = _train_step_eager(P, step, model, optimizer, task_data, scheduler, grad_scaler, group, logger)
+        if g is None:
+            optimizer._acn_meta_graph = "pending"
+    if out is None:
+        return None
+    for k in ("time_setup", "time_data", "time_inner", "time_outer", "time_misc"):
+        out.setdefault(k, 0.0)
+    if metric_logger is not None:
+        metric_logger.meters["batch_time"].update(out["time_total_step"], n=1)
+        metric_logger.meters["tasks"].update(out["tasks"], n=1)
+        metric_logger.meters["loss_in"].update(out["loss_in"], n=out["rays_in"])
+        metric_logger.meters["psnr_in"].update(out["psnr_in"], n=out["rays_in"])
+        metric_logger.meters["loss_out"].update(out["loss_out"], n=out["rays_out"])
+        metric_logger.meters["psnr_out"].update(out["psnr_out"], n=out["rays_out"])
+        if hasattr(metric_logger, "synchronize_between_processes"):
+            metric_logger.synchronize_between_processes()
+    if logger is not None and step % getattr(P, "print_step", 1) == 0:
+        logger.log_dirname(f"Step {step}")
+        for k in ("loss_in", "loss_out", "psnr_in", "psnr_out"):
+            logger.scalar_summary(f"train/{k}", out[k], step)
+        for k in ("time_setup", "time_data", "time_inner", "time_outer", "time_misc", "time_total_step"):
+            logger.scalar_summary(f"train/{k}", out[k], step)
+        logger.log("[TRAIN] [Step %d] [LossIn %.6f] [LossOut %.6f] [PSNRIn %.2f] [PSNROut %.2f] [InnerLR %.6f]"
+                   % (step, out["loss_in"], out["loss_out"], out["psnr_in"], out["psnr_out"], float(P.inner_lr)))
+    return out
+
+
+def _train_step_eager(P, step, model, optimizer, task_data, scheduler=None, grad_scaler=None, group=None,
+                      logger=None):
+    """The eager body of train_step (meta_train_step.py:18-253) without the metric / logger updates."""
     t_step_start = time.perf_counter()
     model.train()
     device = next(model.parameters()).device
@@ -338,28 +402,10 @@ def train_step(P, step, model, optimizer, task_data, metric_logger=None, logger=
         loss_in, loss_out = s[0].float(), s[1].float()
     t_total = time.perf_counter() - t_step_start
     t_misc = max(0.0, t_total - (time_setup + time_data + time_inner + time_outer))
-    out = {"loss_in": float(loss_in), "loss_out": float(loss_out), "psnr_in": float(psnr(loss_in)),
-           "psnr_out": float(psnr(loss_out)), "tasks": total_tasks, "rays_in": total_sup, "rays_out": total_q,
-           "time_setup": time_setup, "time_data": time_data, "time_inner": time_inner, "time_outer": time_outer,
-           "time_misc": t_misc, "time_total_step": t_total}
-    if metric_logger is not None:
-        metric_logger.meters["batch_time"].update(t_total, n=1)
-        metric_logger.meters["tasks"].update(total_tasks, n=1)
-        metric_logger.meters["loss_in"].update(out["loss_in"], n=total_sup)
-        metric_logger.meters["psnr_in"].update(out["psnr_in"], n=total_sup)
-        metric_logger.meters["loss_out"].update(out["loss_out"], n=total_q)
-        metric_logger.meters["psnr_out"].update(out["psnr_out"], n=total_q)
-        if hasattr(metric_logger, "synchronize_between_processes"):
-            metric_logger.synchronize_between_processes()
-    if logger is not None and step % getattr(P, "print_step", 1) == 0:
-        logger.log_dirname(f"Step {step}")
-        for k in ("loss_in", "loss_out", "psnr_in", "psnr_out"):
-            logger.scalar_summary(f"train/{k}", out[k], step)
-        for k in ("time_setup", "time_data", "time_inner", "time_outer", "time_misc", "time_total_step"):
-            logger.scalar_summary(f"train/{k}", out[k], step)
-        logger.log("[TRAIN] [Step %d] [LossIn %.6f] [LossOut %.6f] [PSNRIn %.2f] [PSNROut %.2f] [InnerLR %.6f]"
-                   % (step, out["loss_in"], out["loss_out"], out["psnr_in"], out["psnr_out"], float(P.inner_lr)))
-    return out
+    return {"loss_in": float(loss_in), "loss_out": float(loss_out), "psnr_in": float(psnr(loss_in)),
+            "psnr_out": float(psnr(loss_out)), "tasks": total_tasks, "rays_in": total_sup, "rays_out": total_q,
+            "time_setup": time_setup, "time_data": time_data, "time_inner": time_inner, "time_outer": time_outer,
+            "time_misc": t_misc, "time_total_step": t_total}
 
 
 # ============================================================================ graph-replayed meta step
@@ -368,17 +414,21 @@ class GraphedMetaStep:
 
     The outer loss of meta_train_step.py:157-159 is ``R * sum_t n_q,t loss_q,t / total_q`` over the
     step's tasks, so its gradient is the sum of per-task gradients weighted by ``R n_q,t / total_q``:
-    each task's inner loop (task_adapt, meta_core.py:14-67), query loss and backward (into the
-    parameters' persistent .grad buffers) is one captured graph per region (the expert and the task
-    shapes are fixed per region), replayed for every task of the region in the reference's shuffled
-    region order (random.Random(seed + step)); the training jitter is drawn inside the graphs
-    (graph-safe philox) in the same call order.  The outer clip + Adam (FusedAdam's device step table)
-    is one more graph.  Per step the host copies each task into its region's static buffers and reads
-    the loss once (the reference's non-finite-loss skip, meta_core.py:124-126).  The gradient equals the
-    eager step's up to fp32 summation order (per-task accumulation instead of one backward of the sum).
-    Shapes are fixed at construction: every task of a region must have that region's support / query
-    sizes (TaskDataset's S_target / Q_target).  Second-order MAML stays on the eager train_step: the
-    create_graph backward does an operation HIP stream capture does not permit on this stack."""
+    each task's inner loop (task_adapt, meta_core.py:14-67), query loss and backward (into persistent
+    gradient buffers) is one captured graph per region (the expert and the task shapes are fixed per
+    region), replayed for every task of the region in the reference's shuffled region order
+    (random.Random(seed + step)); the training jitter is drawn inside the graphs (graph-safe philox) in the
+    same call order.  The outer clip + Adam is one more graph on optim.SlottedAdam: expert k is updated
+    only when region k processed a task this step (a per-step activity vector the host writes), with its
+    own device step counter -- torch.optim.Adam skips a parameter whose .grad is None, and an expert whose
+    region has no tasks gets none (meta_core.py:126-143).  Per step the host copies each task into its
+    region's static buffers and reads the loss once (the reference's non-finite-loss skip,
+    meta_core.py:124-126).  Empty tasks are skipped as the reference skips them; a task whose non-empty
+    shapes differ from the captured ones, or a region that was not captured, sends that step through the
+    eager train_step (state carried over in both directions).  The gradient equals the eager step's up to
+    fp32 summation order (per-task accumulation instead of one backward of the sum).  Second-order MAML
+    stays on the eager train_step: the create_graph backward does an operation HIP stream capture does not
+    permit on this stack."""
 
     def __init__(self, P, model, optimizer, task_data, warmup: int = 1, max_steps: int = 1 << 16):
         algo = str(getattr(P, "algo", "")).lower()
@@ -386,18 +436,24 @@ class GraphedMetaStep:
             raise ValueError("GraphedMetaStep: FOMAML only (MAML's second-order backward is not capturable; "
                              "Reptile has no gradient step) -- use train_step")
         if not isinstance(optimizer, FusedAdam):
-            raise TypeError("GraphedMetaStep needs FusedAdam (its device step table makes the update replayable)")
+            raise TypeError("GraphedMetaStep needs FusedAdam (its slotted device step makes the update replayable)")
+        from .optim import SlottedAdam
         self.P, self.model, self.opt = P, model, optimizer
         self.device = next(model.parameters()).device
-        self.cids = sorted(task_data.keys())
         self.shapes = {}
-        for cid in self.cids:
-            t0 = task_data[cid][0]
-            sup, qry = (t0.support, t0.query) if hasattr(t0, "support") else (t0["support"], t0["query"])
-            self.shapes[cid] = (int(sup["rays"].shape[0]), int(qry["rays"].shape[0]))
-        for _ in range(max(1, int(warmup))):   # real updates: they also create every Adam state
+        for cid, tasks in task_data.items():
+            for t in tasks:
+                ns, nq = _task_shapes(t)
+                if ns == 0 or nq == 0:
+                    continue
+                if self.shapes.setdefault(cid, (ns, nq)) != (ns, nq):
+                    raise ValueError(f"GraphedMetaStep: region {cid} has tasks of different shapes")
+        self.cids = sorted(self.shapes)
+        if not self.cids:
+            raise ValueError("GraphedMetaStep: no non-empty task to capture")
+        for _ in range(max(0, int(warmup))):   # real updates
             with _quiet():
-                train_step(P, 0, model, optimizer, task_data)
+                _train_step_eager(P, 0, model, optimizer, task_data)
         torch.cuda.synchronize(self.device)
         dev = self.device
         self.static = {}
@@ -406,14 +462,26 @@ class GraphedMetaStep:
             self.static[cid] = {"support": {"rays": torch.zeros(ns, 8, device=dev), "rgbs": torch.zeros(ns, 3, device=dev)},
                                 "query": {"rays": torch.zeros(nq, 8, device=dev), "rgbs": torch.zeros(nq, 3, device=dev)},
                                 "wq": torch.zeros((), device=dev)}
-            self._load(cid, task_data[cid][0])
+            self._load(cid, next(t for t in task_data[cid] if _task_shapes(t) == self.shapes[cid]))
         self.inner_acc = torch.zeros((), device=dev)
         self.q_acc = torch.zeros((), device=dev)
-        self.params = [p for g in optimizer.param_groups for p in g["params"] if optimizer.state.get(p)]
+        K = len(model.submodules)
+        slot_of = {}
+        for k, sub in enumerate(model.submodules):
+            for p in sub.parameters():
+                slot_of[id(p)] = k
+        for p in model.parameters():
+            slot_of.setdefault(id(p), K)          # the shared background head
+        self.params = [p for g in optimizer.param_groups for p in g["params"] if id(p) in slot_of]
         for p in self.params:   # persistent gradients: the captured backwards accumulate into them
             p.grad = torch.zeros_like(p)
         self.grads = [p.grad for p in self.params]
-        optimizer.graph_begin(max_steps)
+        self.adam = SlottedAdam(optimizer, slot_of, {id(p): p.grad for p in self.params}, K, K + 1,
+                                max_steps=max_steps)
+        self.K = K
+        # activity of the outer update: seg[K + 1 + k] > 0 <=> region k processed a task (SlottedAdam)
+        self.act = torch.zeros(2 * K + 1, dtype=torch.int64, device=dev)
+        self.act_host = torch.zeros(2 * K + 1, dtype=torch.int64).pin_memory()
         pool = torch.cuda.graph_pool_handle()
         self.graphs = {}
         for cid in self.cids:
@@ -423,9 +491,9 @@ class GraphedMetaStep:
             self.graphs[cid] = g
         self.outer = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.outer, pool=pool):
-            optimizer.step(max_norm=getattr(P, "grad_clip", 1.0))
-        optimizer.graph_end_capture()
+            self.adam.step(self.act, getattr(P, "grad_clip", 1.0))
         self.replays = 0
+        self.eager_steps = 0
         torch._foreach_zero_(self.grads)
 
     def _load(self, cid, task) -> None:
@@ -457,37 +525,83 @@ class GraphedMetaStep:
             self.inner_acc.add_(inner[-1].detach() * ns)
         self.q_acc.add_(loss_q.detach() * nq)
 
+    def _covers(self, task_data) -> bool:
+        for cid, tasks in task_data.items():
+            for t in tasks:
+                sh = _task_shapes(t)
+                if sh[0] == 0 or sh[1] == 0:
+                    continue   # skipped, as the reference skips empty tasks
+                if self.shapes.get(cid) != sh:
+                    return False
+        return True
+
+    def _eager(self, step, task_data):
+        """A step the graphs do not cover: the eager train_step on the same optimizer, state carried over."""
+        live = [c for c, ts in task_data.items() if any(min(_task_shapes(t)) > 0 for t in ts)]
+        self.adam.sync_state(extra_slots=set(live) | {self.K})   # the slots the eager step will update
+        for p in self.params:
+            p.grad = None
+        with _quiet():
+            out = _train_step_eager(self.P, step, self.model, self.opt, task_data)
+        self.adam.load_state()
+        for p, g in zip(self.params, self.grads):
+            p.grad = g
+        torch._foreach_zero_(self.grads)
+        self.eager_steps += 1
+        return out
+
     def __call__(self, step: int, task_data) -> Optional[Dict[str, float]]:
+        if not self._covers(task_data):
+            return self._eager(step, task_data)
         t0 = time.perf_counter()
         torch._foreach_zero_(self.grads)
         self.inner_acc.zero_()
         self.q_acc.zero_()
         cids = list(task_data.keys())
         random.Random(getattr(self.P, "seed", 0) + step).shuffle(cids)
-        total_sup = sum(self.shapes[c][0] * len(task_data[c]) for c in cids)
-        total_q = sum(self.shapes[c][1] * len(task_data[c]) for c in cids)
+        live = {c: [t for t in task_data[c] if min(_task_shapes(t)) > 0] for c in cids}
+        total_sup = sum(self.shapes[c][0] * len(live[c]) for c in cids if live[c])
+        total_q = sum(self.shapes[c][1] * len(live[c]) for c in cids if live[c])
         if total_q == 0:
             return None
+        self.adam.refresh()   # an LR scheduler may have changed the groups since the last step
         for cid in cids:
+            if not live[cid]:
+                continue
             self.static[cid]["wq"].fill_(len(cids) * self.shapes[cid][1] / total_q)
-            for task in task_data[cid]:
+            for task in live[cid]:
                 self._load(cid, task)
                 self.graphs[cid].replay()
         loss_out = float(self.q_acc) / total_q          # the one host read of the step
         if not math.isfinite(len(cids) * loss_out):
             print(f"[WARN] Skipping meta-update: non-finite loss_out={len(cids) * loss_out}")
         else:
+            self.act_host.zero_()
+            for cid in cids:
+                if live[cid]:
+                    self.act_host[self.K + 1 + cid] = 1
+            self.act.copy_(self.act_host, non_blocking=True)
             self.outer.replay()
             self.replays += 1
             from .optim import bump_versions
-            bump_versions(self.opt._graph["params"])
+            bump_versions([r[0] for r in self.adam.rows])
         loss_in = float(self.inner_acc) / max(total_sup, 1)
         return {"loss_in": loss_in, "loss_out": loss_out, "psnr_in": -10.0 * math.log10(loss_in + 1e-24),
                 "psnr_out": -10.0 * math.log10(loss_out + 1e-24), "tasks": sum(len(v) for v in task_data.values()),
                 "rays_in": total_sup, "rays_out": total_q, "time_total_step": time.perf_counter() - t0}
 
+    @property
+    def last_norm(self) -> torch.Tensor:
+        return self.adam.scale
+
     def sync_state(self) -> None:
-        self.opt.graph_sync_steps(self.replays)
+        """Host state['step'] of every parameter from the per-slot device counters (state_dict)."""
+        self.adam.sync_state()
+
+
+def _task_shapes(task):
+    sup, qry = (task.support, task.query) if hasattr(task, "support") else (task["support"], task["query"])
+    return int(sup["rays"].shape[0]), int(qry["rays"].shape[0])
 
 
 @contextlib.contextmanager

@@ -321,11 +321,18 @@ def mse_linear_fwd(pred: torch.Tensor, gt: torch.Tensor) -> torch.Tensor:
 
 
 _MSE_WS = {}
+_MSE_WS_CAPTURED = []   # workspaces baked into captured graphs (kept alive with them)
 
 
 def _mse_ws(device) -> torch.Tensor:
     """Zeroed workspace of acn_mse_linear_fwd_ws per (device, stream): its ticket counter returns to 0
-    after every call, so one buffer serves every later call (and graph replay) on that stream."""
+    after every call, so one buffer serves every later call on that stream.  Under stream capture every
+    captured call gets a workspace of its own: graphs captured on torch's shared capture stream would
+    otherwise share one ticket counter, and two of them replayed concurrently would race on it."""
+    if torch.cuda.is_current_stream_capturing():
+        ws = torch.zeros(int(_lib.lib().acn_mse_linear_workspace_bytes()), dtype=torch.uint8, device=device)
+        _MSE_WS_CAPTURED.append(ws)
+        return ws
     key = (device, int(torch.cuda.current_stream(device).cuda_stream))
     ws = _MSE_WS.get(key)
     if ws is None:
@@ -457,10 +464,15 @@ def background_bwd(dirs: torch.Tensor, background, g_out: torch.Tensor, grads: S
         if not (t.is_contiguous() and t.dtype == torch.float32 and t.device == d.device):
             raise AcnError("background_bwd: gradient buffers must be contiguous fp32 on the rays' device")
     L = _lib.lib()
-    key = (d.device, int(torch.cuda.current_stream(d.device).cuda_stream))
-    ws = _BG_WS.get(key)
-    if ws is None:
-        ws = _BG_WS[key] = torch.empty(int(L.acn_background_bwd_workspace_bytes()), dtype=torch.uint8, device=d.device)
+    if torch.cuda.is_current_stream_capturing():   # one workspace per captured call (see _mse_ws)
+        ws = torch.empty(int(L.acn_background_bwd_workspace_bytes()), dtype=torch.uint8, device=d.device)
+        _MSE_WS_CAPTURED.append(ws)
+    else:
+        key = (d.device, int(torch.cuda.current_stream(d.device).cuda_stream))
+        ws = _BG_WS.get(key)
+        if ws is None:
+            ws = _BG_WS[key] = torch.empty(int(L.acn_background_bwd_workspace_bytes()), dtype=torch.uint8,
+                                           device=d.device)
     check(L.acn_background_bwd(ptr(d), d.shape[0], C.byref(background), ptr(g), *[ptr(t) for t in grads], ptr(ws),
                                ws.numel(), stream_of(d)), "acn_background_bwd")
 
@@ -527,6 +539,20 @@ def mlp_train_bwd(save: torch.Tensor, out: torch.Tensor, gout: torch.Tensor, ws:
 MLP_DW_SHAPES = ((64, 32), (64,), (64, 64), (64,), (1, 64), (1,), (15, 64), (15,), (64, 31), (64,), (64, 64), (64,),
                  (3, 64), (3,))
 MLP_DW_FLOATS = 13715
+# Optional timing hook (bench.py --workload meta): when set to a list, every acn_mlp_train_bwd_dw call appends
+# (start event, end event, M, want_h0) recorded on the current stream around the call (weight pack +
+# mlp_bwd_dw_kernel + mlp_dw_reduce_kernel)
+DW_HOOK = None
+# Algorithmic MACs per sample of the fused MLP backward (SURVEY §8(d) MLP shapes): dW = every weight
+# (32x64 + 64x64 + 64x[15|1] + 31x64 + 64x64 + 64x3 = 13,440); dX = the layer-input gradients the chain
+# needs (64x3 + 64x64 + 64x15 geo columns + 64x16 heads + 64x64 = 10,368, + 32x64 when dL/dh0 is wanted).
+# The in-register forward recompute (13,440 MACs) is extra work of this design, not counted.
+MLP_BWD_MACS_DW, MLP_BWD_MACS_DX, MLP_BWD_MACS_DX0, MLP_FWD_MACS = 13440, 10368, 2048, 13440
+
+
+def mlp_bwd_flops(M: int, want_h0: bool) -> int:
+    """Algorithmic FLOPs (2 per MAC) of one fused MLP backward over M samples: dW + dX, no recompute."""
+    return 2 * M * (MLP_BWD_MACS_DW + MLP_BWD_MACS_DX + (MLP_BWD_MACS_DX0 if want_h0 else 0))
 
 
 def mlp_train_bwd_dw(h0: torch.Tensor, sh: torch.Tensor, out: torch.Tensor, gout: torch.Tensor,
@@ -539,9 +565,17 @@ def mlp_train_bwd_dw(h0: torch.Tensor, sh: torch.Tensor, out: torch.Tensor, gout
     gh = torch.empty(M, 32, device=out.device, dtype=torch.float32) if want_h0 else None
     wsp = torch.empty(int(_lib.lib().acn_mlp_dw_workspace_bytes()), dtype=torch.uint8, device=out.device)
     w = _mlp_struct(ws)
+    hook = DW_HOOK
+    if hook is not None:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record()
     check(_lib.lib().acn_mlp_train_bwd_dw(ptr(h0), ptr(sh), ptr(out), ptr(gout), M, C.byref(w), ptr(dw),
                                           ptr(gh) if want_h0 else None, ptr(wsp), stream_of(out)),
           "acn_mlp_train_bwd_dw")
+    if hook is not None:
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        hook.append((e0, e1, int(M), bool(want_h0)))
     grads, o = [], 0
     for shp in MLP_DW_SHAPES:
         n = 1

@@ -281,6 +281,149 @@ class FusedAdam(torch.optim.Optimizer):
         return loss
 
 
+ZERO_GRAD_FLAG = 1 << 16       # adam_step_slots: clear the gradient after reading it
+NORM_ELSEWHERE_FLAG = 1 << 17  # grad_sumsq_slots_ex: this tensor's sum of squares comes from elsewhere
+
+
+class SlottedAdam:
+    """clip_grad_norm_ + torch.optim.Adam.step() of a FusedAdam's parameters with per-slot activity and
+    step counters on the device, so a captured update replays correctly whichever slots a step reached.
+
+    Every parameter belongs to a slot (``slot_of``: id(p) -> slot; slots 0..K-1 are experts, K.. are
+    shared).  Expert slot k is active in a step iff ``seg[K + 1 + k] > 0`` on the device (the routed pair
+    counts of routed.hip, or an activity vector written by the host); an inactive slot is skipped
+    entirely -- no moment decay, no step increment -- which is what torch.optim.Adam does for a parameter
+    whose .grad is None (runtime_adapt.py:305-309, meta_core.py:126-143).  Each slot has its own device
+    step counter indexing a precomputed table of Adam constants (acn_adam_table_fill).  Gradients are the
+    persistent buffers ``grads`` (id(p) -> tensor); ``flags`` adds ZERO_GRAD_FLAG / NORM_ELSEWHERE_FLAG bits
+    per parameter.  Built outside any capture (plain host-to-device copies: the graph bakes in the
+    addresses)."""
+
+    def __init__(self, optimizer: FusedAdam, slot_of, grads, K: int, nslots: int, flags=None,
+                 max_steps: int = 1 << 16):
+        L = _lib.lib()
+        self.opt, self.K, self.nslots = optimizer, int(K), int(nslots)
+        flags = flags or {}
+        rows, fl, slots_seen = [], [], {}
+        # torch creates a parameter's state at its first update: the moments of a parameter without state
+        # are held here and enter optimizer.state once its slot has stepped (sync_state)
+        self._pending = {}
+        for gi, group in enumerate(optimizer.param_groups):
+            for p in group["params"]:
+                if id(p) not in slot_of:
+                    continue  # parameters the step never differentiates
+                st = optimizer.state.get(p)
+                if not st:
+                    st = self._pending[p] = {"step": torch.tensor(0.0, dtype=torch.float32),
+                                             "exp_avg": torch.zeros_like(p), "exp_avg_sq": torch.zeros_like(p)}
+                s = slot_of[id(p)]
+                slots_seen[s] = max(slots_seen.get(s, 0), int(st["step"].item()))
+                rows.append((p, grads[id(p)], st["exp_avg"], st["exp_avg_sq"], gi))
+                fl.append(s | flags.get(id(p), 0))
+        if not rows:
+            raise AcnError("SlottedAdam: no parameter of the optimizer belongs to a slot")
+        dev = rows[0][0].device
+        self.device = dev
+        self.rows = rows
+        arr = (_lib.acn_param_desc * len(rows))()
+        first = 0
+        for t, (p, g, m, v, gi) in enumerate(rows):
+            arr[t] = _lib.acn_param_desc(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(), gi, first)
+            first += (p.numel() + ACN_OPTIM_CHUNK - 1) // ACN_OPTIM_CHUNK
+        self.nchunks = first
+        self.descs = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(dev)
+        self.chunk_tensor = torch.cat([torch.full(((r[0].numel() + ACN_OPTIM_CHUNK - 1) // ACN_OPTIM_CHUNK,), t,
+                                                  dtype=torch.int32) for t, r in enumerate(rows)]).to(dev)
+        self.flags = torch.tensor(fl, device=dev, dtype=torch.int32)
+        self._flags_host = list(fl)
+        self.partials = torch.empty(first, device=dev, dtype=torch.float64)
+        self.total = torch.empty(1, device=dev, dtype=torch.float64)
+        self.scale = torch.ones(2, device=dev, dtype=torch.float32)
+        self.step_dev = torch.tensor([slots_seen.get(s, 0) for s in range(self.nslots)], device=dev,
+                                     dtype=torch.int32)
+        self.ngroups = len(optimizer.param_groups)
+        self.step0 = int(max(slots_seen.values(), default=0))
+        self.table_steps = self.step0 + int(max_steps)
+        self.table = torch.empty(int(L.acn_adam_table_bytes(self.ngroups, self.table_steps)), dtype=torch.uint8,
+                                 device=dev)
+        self._hparams = None
+        self.refresh()
+
+    def _group_hparams(self):
+        return tuple((float(g["lr"]), tuple(float(b) for b in g["betas"]), float(g["eps"]), float(g["weight_decay"]))
+                     for g in self.opt.param_groups)
+
+    def refresh(self) -> None:
+        """Re-fill the Adam constant table in place when a group's hyper-parameters changed (an LR
+        scheduler); a captured graph keeps reading the same table.  Call outside capture, between steps."""
+        hp = self._group_hparams()
+        if hp == self._hparams:
+            return
+        L = _lib.lib()
+        groups = (acn_adam_group * self.ngroups)()
+        for i, (lr, (b1, b2), eps, wd) in enumerate(hp):
+            groups[i] = acn_adam_group(lr, b1, b2, eps, wd, 1, 0)
+        host = torch.empty(self.table.numel(), dtype=torch.uint8)
+        check(L.acn_adam_table_fill(groups, self.ngroups, 1, self.table_steps, host.data_ptr(), host.numel()),
+              "acn_adam_table_fill")
+        self.table.copy_(host)
+        self._hparams = hp
+
+    def step(self, seg: torch.Tensor, max_norm: Optional[float], table_sumsq: Optional[torch.Tensor] = None,
+             hook=None) -> None:
+        """Clip norm over the active slots' gradients (+ ``table_sumsq``, a device double some kernel
+        accumulated for NORM_ELSEWHERE tensors; reset by the norm pass), clip coefficient, then Adam over
+        the active slots; per-slot step counters advance on the device."""
+        L = _lib.lib()
+        s = _stream(self.device)
+        from ._lib import ptr
+        scale = None
+        if max_norm is not None:
+            check(L.acn_grad_sumsq_slots_ex(ptr(self.descs), ptr(self.chunk_tensor), self.nchunks, ptr(self.flags),
+                                            ptr(seg), self.K, ptr(self.partials), ptr(self.total),
+                                            ptr(table_sumsq), s), "acn_grad_sumsq_slots_ex")
+            check(L.acn_clip_coef(ptr(self.total), float(max_norm), ptr(self.scale), s), "acn_clip_coef")
+            scale = self.scale
+        if hook is not None:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+        check(L.acn_adam_step_slots(ptr(self.descs), ptr(self.chunk_tensor), self.nchunks, ptr(self.flags),
+                                    ptr(self.table), self.ngroups, self.table_steps, ptr(self.step_dev), self.nslots,
+                                    ptr(seg), self.K, ptr(scale), s), "acn_adam_step_slots")
+        if hook is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            hook.append((e0, e1))
+
+    def sync_state(self, extra_slots=()) -> None:
+        """Host state['step'] of every parameter from the per-slot device counters (state_dict, or before
+        an eager FusedAdam step on the same optimizer).  A parameter enters optimizer.state once its slot
+        has stepped, or when its slot is in ``extra_slots`` (about to step eagerly: the eager step then
+        uses these moment tensors)."""
+        steps = self.step_dev.cpu().tolist()
+        if max(steps) > self.table_steps:
+            raise AcnError("SlottedAdam: the Adam constant table is exhausted; build a new step object")
+        for (p, g, m, v, gi), f in zip(self.rows, self._flags_host):
+            slot = f & 0xffff
+            if p in self._pending:
+                if steps[slot] == 0 and slot not in extra_slots:
+                    continue
+                self.opt.state[p] = self._pending.pop(p)
+            self.opt.state[p]["step"].fill_(float(steps[slot]))
+
+    def load_state(self) -> int:
+        """Per-slot device step counters from the optimizer's host state['step'] (after eager FusedAdam
+        steps on the same optimizer); returns the highest step."""
+        steps = [0] * self.nslots
+        for (p, g, m, v, gi), f in zip(self.rows, self._flags_host):
+            st = self._pending.get(p) or self.opt.state[p]
+            steps[f & 0xffff] = max(steps[f & 0xffff], int(st["step"].item()))
+        if max(steps) + 1 > self.table_steps:
+            raise AcnError("SlottedAdam: the Adam constant table is exhausted; build a new step object")
+        self.step_dev.copy_(torch.tensor(steps, dtype=torch.int32))
+        return max(steps)
+
+
 def build_optimizer(P, model, fused: bool = True):
     """get_optimizer (common/utils.py:16-75) with FusedAdam for 'adam' (the online-stage config)."""
     base_lr = getattr(P, "lr", 1e-3)

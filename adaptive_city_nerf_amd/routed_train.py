@@ -37,8 +37,8 @@ import numpy as np
 import torch
 
 from . import _lib, ops
-from ._lib import ACN_OPTIM_CHUNK, AcnError, acn_adam_group, acn_mlp, check, ptr
-from .optim import FusedAdam, bump_versions
+from ._lib import AcnError, acn_mlp, check, ptr
+from .optim import NORM_ELSEWHERE_FLAG, ZERO_GRAD_FLAG, FusedAdam, SlottedAdam, bump_versions
 from .train import mse_color_loss
 
 # Optional timing hook (bench.py): when set to a list, an eager step appends recorded HIP events
@@ -48,14 +48,22 @@ EVENT_HOOK = None
 BWD_HOOK = None
 
 ALIGN = 128                # pair segment alignment = one MLP round (4 tiles x 32 slots)
-ZERO_GRAD_FLAG = 1 << 16   # adam_step_slots: clear the gradient after reading it
-NORM_ELSEWHERE_FLAG = 1 << 17  # grad_sumsq_slots_ex: this tensor's sum of squares comes from the table scatter
 # The tables' share of the clip norm from the scatter's returning atomics (acn_hashgrid_bwd_pairs_sumsq)
 # instead of a pass over the K x 128 MiB gradient buffers
 TELESCOPED_TABLE_NORM = os.environ.get("ACN_TELE_NORM", "1") != "0"
 # The background head's forward / backward as two HIP launches (acn_background_fwd / _bwd) instead of the
 # ~15 torch launches of its autograd graph
 FUSED_BACKGROUND = os.environ.get("ACN_FUSED_BG", "1") != "0"
+
+
+def draw_jitter(n: int, S: int, device) -> torch.Tensor:
+    """The training jitter of one step: stratified_t_vals' rand_like of the (n, S) t grid
+    (nerfs/ray_rendering.py:262-287), graph-safe philox under capture."""
+    return torch.rand(n, S, device=device)
+
+
+# the jitter source of jitter='draw' steps (tests substitute a recorded stream)
+JITTER = draw_jitter
 
 
 def _stream(device) -> int:
@@ -65,9 +73,11 @@ def _stream(device) -> int:
 class RoutedAdaptStep:
     """One runtime_adapt update of a MetaContainer (routed, no active_module) per call.
 
-    ``graph=True`` captures the step once (after ``warmup`` eager steps, which are real updates) and
-    replays it; ``jitter='draw'`` draws the training jitter inside the step like the reference, a
-    caller-supplied (N, S) tensor per call otherwise (``jitter='given'``, for fixture replays)."""
+    ``graph=True``: the first ``warmup`` calls run eagerly -- real updates on the caller's real batches --
+    and the step is then captured once (the capture itself runs nothing) and replayed for every later
+    full batch of ``n_rays`` rays.  A smaller batch (a loader's ragged last batch) runs eagerly through the
+    same buffers.  ``jitter='draw'`` draws the training jitter inside the step like the reference, a
+    caller-supplied (n, S) tensor per call otherwise (``jitter='given'``, for fixture replays)."""
 
     def __init__(self, P, model, n_rays: int, optimizer: FusedAdam, grad_clip: Optional[float] = 1.0,
                  graph: bool = True, warmup: int = 1, max_steps: int = 1 << 16, jitter: str = "draw",
@@ -157,83 +167,49 @@ class RoutedAdaptStep:
         lo = np.float32(1e-6)
         self._lo, self._hi = C.c_float(lo), C.c_float(np.float32(1.0) - lo)
         self.routing = model.routing_spec()
-        # ---- slotted optimizer plan over every parameter of the optimizer's groups
-        rows, flags, slots_seen = [], [], {}
-        for gi, group in enumerate(optimizer.param_groups):
-            for p in group["params"]:
-                if id(p) not in slot_of:
-                    continue  # parameters the routed step never differentiates (none in the reference setup)
-                st = optimizer.state[p]
-                if len(st) == 0:
-                    st["step"] = torch.tensor(0.0, dtype=torch.float32)
-                    st["exp_avg"] = torch.zeros_like(p)
-                    st["exp_avg_sq"] = torch.zeros_like(p)
-                s = slot_of[id(p)]
-                slots_seen.setdefault(s, int(st["step"].item()))
-                rows.append((p, p.grad, st["exp_avg"], st["exp_avg_sq"], gi))
-                fl = s | (ZERO_GRAD_FLAG if zero_of.get(id(p)) and self.clear_in_adam else 0)
-                if zero_of.get(id(p)) and self.tele:
-                    fl |= NORM_ELSEWHERE_FLAG
-                flags.append(fl)
-        self.rows = rows
-        self.nslots = K + 1
-        arr = (_lib.acn_param_desc * len(rows))()
-        first = 0
-        for t, (p, g, m, v, gi) in enumerate(rows):
-            arr[t] = _lib.acn_param_desc(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(), gi, first)
-            first += (p.numel() + ACN_OPTIM_CHUNK - 1) // ACN_OPTIM_CHUNK
-        self.nchunks = first
-        # built outside any capture: plain host-to-device copies (the graph bakes in the device addresses)
-        self.descs = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(dev)
-        self.chunk_tensor = torch.cat([torch.full(((r[0].numel() + ACN_OPTIM_CHUNK - 1) // ACN_OPTIM_CHUNK,), t,
-                                                  dtype=torch.int32) for t, r in enumerate(rows)]).to(dev)
-        self.flags = torch.tensor(flags, **i32)
-        self.partials = torch.empty(first, device=dev, dtype=torch.float64)
-        self.total = torch.empty(1, device=dev, dtype=torch.float64)
+        # ---- slotted clip + Adam over every parameter of the optimizer's groups (optim.SlottedAdam)
+        grads = {id(p): p.grad for p in model.parameters() if id(p) in slot_of}
+        flags = {}
+        for i in zero_of:
+            flags[i] = (ZERO_GRAD_FLAG if self.clear_in_adam else 0) | (NORM_ELSEWHERE_FLAG if self.tele else 0)
+        self.adam = SlottedAdam(optimizer, slot_of, grads, K, K + 1, flags, max_steps=max_steps)
+        self.rows, self.flags, self.step_dev = self.adam.rows, self.adam.flags, self.adam.step_dev
+        self.nslots, self.table_steps, self._step0 = self.adam.nslots, self.adam.table_steps, self.adam.step0
+        self.scale = self.adam.scale
         self.table_sumsq = torch.zeros(1, device=dev, dtype=torch.float64)  # reset by grad_sumsq_slots_ex
-        self.scale = torch.ones(2, **f32)
-        self.step_dev = torch.tensor([slots_seen.get(s, 0) for s in range(self.nslots)], **i32)
-        ng = len(optimizer.param_groups)
-        self._step0 = int(max(slots_seen.values(), default=0))
-        self.table_steps = self._step0 + int(max_steps)
-        groups = (acn_adam_group * ng)()
-        for i, g in enumerate(optimizer.param_groups):
-            b1, b2 = g["betas"]
-            groups[i] = acn_adam_group(float(g["lr"]), float(b1), float(b2), float(g["eps"]), float(g["weight_decay"]),
-                                       1, 0)
-        nbytes = int(L.acn_adam_table_bytes(ng, self.table_steps))
-        host = torch.empty(nbytes, dtype=torch.uint8)
-        check(L.acn_adam_table_fill(groups, ng, 1, self.table_steps, host.data_ptr(), nbytes), "acn_adam_table_fill")
-        self.table = host.to(dev)
-        self.ngroups = ng
-        self.replays = 0
+        self.replays = 0          # graph replays
+        self.steps_done = 0       # every update this object ran (eager and replayed): Adam table rows used
         self.graph = None
-        self._params = [r[0] for r in rows]
-        if graph:
-            side = torch.cuda.Stream(dev)
-            side.wait_stream(torch.cuda.current_stream(dev))
-            with torch.cuda.stream(side):
-                for _ in range(max(1, int(warmup))):
-                    self._step()
-            torch.cuda.current_stream(dev).wait_stream(side)
-            torch.cuda.synchronize(dev)
-            self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph):
-                self._step()
+        self._params = [r[0] for r in self.rows]
+        self._eager_left = max(1, int(warmup)) if graph else 0   # eager real steps before the capture
+
+    def _capture(self) -> None:
+        """Record the full-batch step into one HIP graph (nothing executes; the static buffers keep their
+        contents)."""
+        dev = self.device
+        torch.cuda.synchronize(dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._step(self.N)
+        torch.cuda.synchronize(dev)
+        self.graph = g
 
     # ------------------------------------------------------------------------------------------
-    def _step(self) -> None:
+    def _step(self, n: Optional[int] = None) -> None:
         L = _lib.lib()
-        dev, K, N, S, M = self.device, self.K, self.N, self.S, self.M
+        dev, K, S = self.device, self.K, self.S
+        N = self.N if n is None else int(n)
+        M = N * S
         s = _stream(dev)
         if not self.clear_in_adam:
             for g in self.gtables:
                 g.zero_()
+        u, t = self.u[:N], self.t[:N]
         if self.jitter_mode == "draw":
-            self.u.copy_(torch.rand(N, S, device=dev))  # the reference's rand_like(low) draw
-        check(L.acn_routed_count(ptr(self.rays), N, S, ptr(self.u), C.byref(self.routing), ALIGN, ptr(self.t),
+            u.copy_(JITTER(N, S, dev))  # the reference's rand_like(low) draw
+        check(L.acn_routed_count(ptr(self.rays), N, S, ptr(u), C.byref(self.routing), ALIGN, ptr(t),
                                  ptr(self.seg), ptr(self.rws), self.rws.numel(), s), "acn_routed_count")
-        check(L.acn_routed_scatter(ptr(self.rays), N, S, K, ptr(self.t), ptr(self.seg), C.cast(self._mins, C.c_void_p),
+        check(L.acn_routed_scatter(ptr(self.rays), N, S, K, ptr(t), ptr(self.seg), C.cast(self._mins, C.c_void_p),
                                    C.cast(self._exts, C.c_void_p), self._lo, self._hi, ALIGN, ptr(self.rws),
                                    ptr(self.pidx), ptr(self.pw), ptr(self.x01), ptr(self.sh), ptr(self.pmap),
                                    ptr(self.pk), s), "acn_routed_scatter")
@@ -244,24 +220,25 @@ class RoutedAdaptStep:
         check(L.acn_mlp_pack_pairs(self._mlp_ptrs, K, ptr(self.mws), s), "acn_mlp_pack_pairs")
         check(L.acn_mlp_train_fwd_pairs(ptr(self.h0), ptr(self.sh), ptr(self.seg), K, ptr(self.mws), ptr(self.out), s),
               "acn_mlp_train_fwd_pairs")
-        rs = ops.routed_blend_fwd(self.out, self.pw, self.pmap).view(N, S, 4).requires_grad_(True)
+        rs = ops.routed_blend_fwd(self.out, self.pw, self.pmap[:M]).view(N, S, 4).requires_grad_(True)
+        rays, rgbs, dirs = self.rays[:N], self.rgbs[:N], self.dirs[:N]
         # the shared part: compositing, colour transform and MSE under torch autograd (HIP kernels); the
         # background head as its fused HIP forward and backward (writing the persistent .grad buffers), or
         # under autograd when the head is not the HIP-supported SH-4 MLP
         from .ray_rendering import volume_render
         if self.bg_spec is not None:
-            self.dirs.copy_(self.rays[:, 3:6])
-            bg = ops.background_fwd(self.dirs, self.bg_spec).requires_grad_(True)
+            dirs.copy_(rays[:, 3:6])
+            bg = ops.background_fwd(dirs, self.bg_spec).requires_grad_(True)
             with torch.enable_grad():
-                rgb = volume_render(rs, self.t, bg_rgb=bg)[0]
-                loss = mse_color_loss(rgb, self.rgbs, self.P.color_space)
+                rgb = volume_render(rs, t, bg_rgb=bg)[0]
+                loss = mse_color_loss(rgb, rgbs, self.P.color_space)
                 g_rs, g_bg = torch.autograd.grad(loss, [rs, bg])
-            ops.background_bwd(self.dirs, self.bg_spec, g_bg, self.gbg)
+            ops.background_bwd(dirs, self.bg_spec, g_bg, self.gbg)
         else:
             with torch.enable_grad():
-                bg = self.model.background_color(self.rays[:, 3:6])
-                rgb = volume_render(rs, self.t, bg_rgb=bg)[0]
-                loss = mse_color_loss(rgb, self.rgbs, self.P.color_space)
+                bg = self.model.background_color(rays[:, 3:6])
+                rgb = volume_render(rs, t, bg_rgb=bg)[0]
+                loss = mse_color_loss(rgb, rgbs, self.P.color_space)
                 grads = torch.autograd.grad(loss, [rs] + self.bg_params)
             g_rs = grads[0]
             for g, buf in zip(grads[1:], self.gbg):
@@ -283,42 +260,34 @@ class RoutedAdaptStep:
             b1 = torch.cuda.Event(enable_timing=True)
             b1.record()
             bhook.append((b0, b1))
-        scale = None
-        if self.grad_clip is not None:
-            check(L.acn_grad_sumsq_slots_ex(ptr(self.descs), ptr(self.chunk_tensor), self.nchunks, ptr(self.flags),
-                                            ptr(self.seg), K, ptr(self.partials), ptr(self.total),
-                                            ptr(self.table_sumsq) if self.tele else None, s),
-                  "acn_grad_sumsq_slots_ex")
-            check(L.acn_clip_coef(ptr(self.total), float(self.grad_clip), ptr(self.scale), s), "acn_clip_coef")
-            scale = self.scale
-        hook = EVENT_HOOK if self.graph is None else None
-        if hook is not None:
-            e0 = torch.cuda.Event(enable_timing=True)
-            e0.record()
-        check(L.acn_adam_step_slots(ptr(self.descs), ptr(self.chunk_tensor), self.nchunks, ptr(self.flags),
-                                    ptr(self.table), self.ngroups, self.table_steps, ptr(self.step_dev), self.nslots,
-                                    ptr(self.seg), K, ptr(scale), s), "acn_adam_step_slots")
-        if hook is not None:
-            e1 = torch.cuda.Event(enable_timing=True)
-            e1.record()
-            hook.append((e0, e1))
+        self.adam.step(self.seg, self.grad_clip, self.table_sumsq if self.tele else None,
+                       hook=EVENT_HOOK if self.graph is None else None)
 
     def __call__(self, rays: torch.Tensor, rgbs: torch.Tensor, jitter_u: Optional[torch.Tensor] = None) -> torch.Tensor:
-        if tuple(rays.shape) != (self.N, 8) or tuple(rgbs.shape) != (self.N, 3):
-            raise AcnError(f"RoutedAdaptStep was built for {self.N} rays; got {tuple(rays.shape)}, {tuple(rgbs.shape)}")
-        if self._step0 + self.replays + 1 > self.table_steps:
+        n = int(rays.shape[0])
+        if rays.dim() != 2 or rays.shape[1] != 8 or tuple(rgbs.shape) != (n, 3) or not 0 < n <= self.N:
+            raise AcnError(f"RoutedAdaptStep was built for batches of up to {self.N} rays; got {tuple(rays.shape)}, "
+                           f"{tuple(rgbs.shape)}")
+        # every update, eager or replayed, consumes one row of the Adam constant table (per-slot device
+        # counters never run ahead of the number of updates)
+        if self._step0 + self.steps_done + 1 > self.table_steps:
             raise AcnError("RoutedAdaptStep: the Adam constant table is exhausted; build a new step object")
-        self.rays.copy_(rays, non_blocking=True)
-        self.rgbs.copy_(rgbs, non_blocking=True)
+        self.rays[:n].copy_(rays, non_blocking=True)
+        self.rgbs[:n].copy_(rgbs, non_blocking=True)
         if self.jitter_mode == "given":
-            if jitter_u is None:
-                raise AcnError("RoutedAdaptStep(jitter='given') needs jitter_u per call")
-            self.u.copy_(jitter_u, non_blocking=True)
-        if self.graph is not None:
+            if jitter_u is None or tuple(jitter_u.shape) != (n, self.S):
+                raise AcnError(f"RoutedAdaptStep(jitter='given') needs jitter_u of shape ({n}, {self.S}) per call")
+            self.u[:n].copy_(jitter_u, non_blocking=True)
+        if n == self.N and self.graph is not None:
             self.graph.replay()
+            self.replays += 1
         else:
-            self._step()
-        self.replays += 1
+            self._step(n)
+            if n == self.N and self._eager_left > 0:
+                self._eager_left -= 1
+                if self._eager_left == 0:
+                    self._capture()
+        self.steps_done += 1
         bump_versions(self._params)  # the kernels wrote them: packed render images are stale
         return self.loss
 
@@ -328,9 +297,14 @@ class RoutedAdaptStep:
         return self.scale
 
     def sync_state(self) -> None:
-        """Host state['step'] of every parameter from the per-slot device counters (state_dict)."""
-        steps = self.step_dev.cpu().tolist()
-        if max(steps) >= self.table_steps:
-            raise AcnError("RoutedAdaptStep: the Adam constant table is exhausted; build a new step object")
-        for (p, g, m, v, gi), f in zip(self.rows, self.flags.cpu().tolist()):
-            self.opt.state[p]["step"].fill_(float(steps[f & 0xffff]))
+        """Host state['step'] of every parameter from the per-slot device counters (state_dict, or before
+        an eager FusedAdam step on the same optimizer)."""
+        self.adam.sync_state()
+
+    def load_state(self) -> None:
+        """Per-slot device step counters from the optimizer's host state['step'] (after eager FusedAdam
+        steps taken on the same optimizer outside this object), and the Adam constants from the current
+        group hyper-parameters."""
+        top = self.adam.load_state()
+        self.adam.refresh()
+        self._step0 = top - self.steps_done   # keeps the exhaustion guard exact

@@ -17,6 +17,7 @@ expert itself), so it stays a single-process placement variant and refuses a gro
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, Iterable, Optional
 
 import torch
@@ -155,21 +156,66 @@ class GraphedAdaptStep:
         self.args[2].graph_sync_steps(self.replays)
 
 
+def _routed_step_for(P, model, optimizer, n_rays: int, grad_clip):
+    """The RoutedAdaptStep cached on ``optimizer`` for ``model`` (built on first use, sized for the first
+    batch), or None when the configuration is outside what the routed pair kernels cover (then the eager
+    adapt_step runs).  A batch larger than the cached step's capacity rebuilds it (state carried over
+    through the optimizer's host state)."""
+    from .meta_container import MetaContainer
+    from .routed_train import RoutedAdaptStep
+    from ._lib import AcnError
+    if not (FAST_RUNTIME_ADAPT and isinstance(model, MetaContainer) and isinstance(optimizer, FusedAdam)):
+        return None
+    cache = optimizer.__dict__.setdefault("_acn_routed_steps", {})
+    key = (id(model), grad_clip, int(P.ray_samples), str(P.color_space))
+    st = cache.get(key)
+    if st is not None and n_rays <= st.N:
+        st.load_state()   # eager steps on this optimizer since the last call advanced the host counters
+        return st
+    if st is not None:
+        st.sync_state()
+        del cache[key]
+    try:
+        st = RoutedAdaptStep(P, model, n_rays, optimizer, grad_clip=grad_clip, graph=True, warmup=1)
+    except AcnError:
+        return None
+    cache[key] = st
+    return st
+
+
+# runtime_adapt's full batches through the cached, graph-replayed RoutedAdaptStep (ACN_FAST_ADAPT=0: the
+# eager adapt_step for every batch)
+FAST_RUNTIME_ADAPT = os.environ.get("ACN_FAST_ADAPT", "1") != "0"
+
+
 def runtime_adapt(*, P, model, data_loader: Iterable, optimizer, steps: Optional[int] = None,
                   active_module: Optional[int] = None, grad_clip: Optional[float] = 1.0) -> Dict[str, float]:
     """runtime_adapt.py:213-315: adapt in place; one pass over the loader (steps=None) or exactly
-    ``steps`` updates cycling over it."""
+    ``steps`` updates cycling over it.
+
+    The online stage's configuration -- the routed container (``active_module=None``) with FusedAdam --
+    runs through one RoutedAdaptStep per (model, optimizer): the first full batch is an eager update, the
+    step is then captured and every later batch of that size replays one HIP graph with no host
+    synchronisation; a smaller (ragged last) batch runs the same kernels eagerly.  The loss is read once,
+    at the end (the reference reads it every step).  Other configurations take the eager adapt_step."""
     device = next(model.parameters()).device
     model.train()
     # the reference clips base.parameters(); parameters outside base get no gradient from the loss
     # (zero_grad sets them to None), so FusedAdam's norm over gradient-carrying tensors is the same
     base = model.submodules[active_module] if active_module is not None else model
     last_loss, step_count = None, 0
+    fast = [None, active_module is None]   # [RoutedAdaptStep, still worth trying]
 
     def run(rays, rgbs):
         nonlocal last_loss, step_count
         rays, rgbs = rays.to(device, non_blocking=True), rgbs.to(device, non_blocking=True)
-        last_loss = adapt_step(P, base, rays, rgbs, optimizer, active_module=active_module, grad_clip=grad_clip)
+        if fast[1] and (fast[0] is None or rays.shape[0] > fast[0].N):
+            fast[0] = _routed_step_for(P, base, optimizer, int(rays.shape[0]), grad_clip)
+            fast[1] = fast[0] is not None
+        if fast[0] is not None:
+            last_loss = fast[0](rays, rgbs)
+        else:
+            last_loss = adapt_step(P, base, rays, rgbs, optimizer, active_module=active_module, grad_clip=grad_clip)
         step_count += 1
 
     if steps is None:
@@ -184,4 +230,6 @@ def runtime_adapt(*, P, model, data_loader: Iterable, optimizer, steps: Optional
                 it = iter(data_loader)
                 rays, rgbs = next(it)
             run(rays, rgbs)
+    if fast[0] is not None:
+        fast[0].sync_state()   # host state['step'] current (state_dict, a later eager step)
     return {"loss": 0.0 if last_loss is None else float(last_loss), "steps": step_count}

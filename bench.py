@@ -407,6 +407,9 @@ def main():
     ap.add_argument("--query-rays", type=int, default=2000, help="meta: query rays per task")
     ap.add_argument("--data-rays", type=int, default=1 << 22, help="data: rays in the region table")
     ap.add_argument("--no-graph", action="store_true", help="c5: eager steps instead of the HIP-graph replay")
+    ap.add_argument("--driver", choices=["step", "runtime_adapt"], default="step",
+                    help="c5: time RoutedAdaptStep calls (step), or the drop-in train.runtime_adapt(steps=K) over a "
+                         "loader-like list of device batches (what a reference caller of runtime_adapt gets)")
     ap.add_argument("--diag-shared-table", action="store_true",
                     help="diagnostic (c3/c4): every expert reads expert 0's hash table (one 128 MiB table instead of "
                          "K: isolates the Infinity-Cache capacity effect; outputs differ from the real render)")
@@ -458,6 +461,7 @@ def main():
     model, gbox, scene, sc = build_model(device, K, fill=[rank % K] if a.workload == "c5a" else None,
                                          occ_conf=occ_conf)
 
+    run_k = None   # set when the timed region is one call performing K updates (c5 --driver runtime_adapt)
     if a.diag_shared_table:
         with torch.no_grad():
             for sub in model.submodules[1:]:
@@ -537,16 +541,15 @@ def main():
         my_regions = [c for c in range(4) if expert_owner(4, world)[c] == rank]
         samples_per_step = sum(len(task_data[c]) * (P.inner_iter * nsup + nqry) for c in range(4)) * S
         it = [0]
-        graphed_meta = None
-        if world == 1 and not a.no_graph:   # per-region task graphs + the outer clip/Adam graph
-            graphed_meta = MT.GraphedMetaStep(P, model, opt, task_data, warmup=1)
+        # the drop-in train_step: at one process, FOMAML + FusedAdam, its first call is the eager step and
+        # the later ones replay the per-region task graphs + the outer graph (meta_train.GraphedMetaStep,
+        # cached on the optimizer); --no-graph: ACN_FAST_META off, every step eager
+        MT.FAST_META_STEP = not a.no_graph
 
         def step():
             it[0] += 1
-            if graphed_meta is not None:
-                return graphed_meta(it[0], task_data)
             import contextlib, io
-            with contextlib.redirect_stdout(io.StringIO()):  # meta_update's per-region debug prints
+            with contextlib.redirect_stdout(io.StringIO()):  # meta_update's per-region debug prints (eager)
                 return MT.train_step(P, it[0], model, opt, task_data, group=pg)
         sample_rays = pool[:1]
         aoptim.EVENT_HOOK = []
@@ -644,9 +647,18 @@ def main():
         expert = None
         routed = None
         pg = dist.group.WORLD if world > 1 else None
-        if world == 1:  # the whole routed step (no host sync), replayed as one HIP graph (eager with --no-graph)
+        loader = [(pool[i], gtp[i]) for i in range(nb)]   # a runtime_adapt data loader's batches (device)
+        if world == 1 and a.driver == "step":  # the whole routed step (no host sync), one HIP graph (eager: --no-graph)
             from adaptive_city_nerf_amd.routed_train import RoutedAdaptStep
             routed = RoutedAdaptStep(P, model, bsz, opt, grad_clip=1.0, graph=not a.no_graph, warmup=2)
+        if a.driver == "runtime_adapt":
+            if world > 1:
+                raise SystemExit("bench.py: --driver runtime_adapt is the single-process drop-in (the reference's "
+                                 "runtime_adapt has no process group); use --driver step for N > 1")
+            from adaptive_city_nerf_amd import train as atrain
+
+            def run_k(k):    # ONE drop-in call performing k updates, cycling over the loader
+                return atrain.runtime_adapt(P=P, model=model, data_loader=loader, optimizer=opt, steps=k)
 
         def step():
             # N > 1: the experts distributed over the ranks (expert_parallel.py), every rank streaming
@@ -707,8 +719,11 @@ def main():
         frays, fvalid = ops.get_rays_image(H, W, *intr, c2w, gbox.aabb, device, near_far_override=(None, None))
         sample_rays = frays
 
-    for _ in range(a.warmup):
-        out = step()
+    if run_k is not None:
+        out = run_k(a.warmup)
+    else:
+        for _ in range(a.warmup):
+            out = step()
     torch.cuda.synchronize()
     # c2: one acn call per step, timed by two HIP events bracketing the K timed calls on the launch stream
     # (a per-call event pair costs ~8 us of queue time per step, 2.5% of a C2 step: tools/event_overhead.py)
@@ -726,8 +741,11 @@ def main():
     if bracket:
         eb = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         eb[0].record()
-    for _ in range(a.steps):
-        out = step()
+    if run_k is not None:
+        out = run_k(a.steps)
+    else:
+        for _ in range(a.steps):
+            out = step()
     if bracket:
         eb[1].record()
     if mark:
@@ -744,6 +762,8 @@ def main():
         aoptim.EVENT_HOOK = []
         adapt_step(P, model, pool[0], gtp[0], opt, active_module=expert, grad_clip=1.0)
         torch.cuda.synchronize()
+    if a.workload == "c5" and run_k is not None:   # the step object the drop-in call built and replayed
+        routed = next(iter(opt._acn_routed_steps.values()), None)
     if a.workload == "c5" and routed is not None:
         # graph replays run no Python: the Adam launch is timed by eager steps of the same object
         from adaptive_city_nerf_amd import routed_train as RT
@@ -757,17 +777,26 @@ def main():
         hash_bwd_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in RT.BWD_HOOK]))
         hash_segments = hash_bwd_segments(routed)
         RT.EVENT_HOOK = RT.BWD_HOOK = None
-    if a.workload == "meta" and graphed_meta is not None:
-        # graph replays run no Python: the outer Adam launch is timed by eager steps afterwards
+    if a.workload == "meta":
+        # graph replays run no Python: the fused MLP backward (the step's dominant kernel) and the outer Adam
+        # launch are timed by eager steps afterwards
         import contextlib, io
-        graphed_meta.sync_state()
-        opt._graph = None
+        graphed_meta = opt.__dict__.get("_acn_meta_graph") or None
+        if graphed_meta is not None:
+            graphed_meta.sync_state()
+        MT.FAST_META_STEP = False
         aoptim.EVENT_HOOK = []
+        ops.DW_HOOK = []
         with contextlib.redirect_stdout(io.StringIO()):
             for _ in range(3):
                 it[0] += 1
-                MT.train_step(P, it[0], model, opt, task_data)
+                MT.train_step(P, it[0], model, opt, task_data, group=pg)
         torch.cuda.synchronize()
+        dw_hook, ops.DW_HOOK = ops.DW_HOOK, None
+        dw_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1, _, _ in dw_hook]))
+        dw_flop = float(np.mean([ops.mlp_bwd_flops(m, wh) for _, _, m, wh in dw_hook]))
+        dw_samples = float(np.mean([m for _, _, m, _ in dw_hook]))
+        dw_launches = len(dw_hook) // 3
     if a.workload == "c5":
         psnr_after = val_psnr()
     if a.workload in ("c5", "c5a", "meta"):
@@ -905,6 +934,26 @@ def main():
                 if sec["atomic_requests_per_launch"]:
                     sec["requests_over_distinct_segments"] = round(sec["atomic_requests_per_launch"] / hash_segments, 3)
                     sec["achieved_requests_per_s"] = round(sec["atomic_requests_per_launch"] / (hash_bwd_ms * 1e-3), 1)
+    if a.workload == "meta":
+        # dominant kernel: the fused MLP backward (mlp_bwd_dw_kernel, ~40% of the step); FLOP roofline on the
+        # algorithmic dW + dX MACs x 2 (ops.mlp_bwd_flops) against the fp32 matrix peak (the products are
+        # fp32-accurate: fp16x3 split for dX, fp32 MFMA for dW); the forward recompute is stated beside it
+        dw_tf = dw_flop / (dw_ms * 1e-3) / 1e12
+        adam = roofline
+        roofline = {"bound": "mfma", "achieved": round(dw_tf, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(dw_tf / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                    "kernel": "mlp_bwd_dw_kernel (fused MLP backward: forward recompute in registers, dX chain on the "
+                              "fp16x3 split, dW + db on fp32 MFMA; kernel_ms = HIP events around the "
+                              "acn_mlp_train_bwd_dw call = weight pack + mlp_bwd_dw_kernel + mlp_dw_reduce_kernel)",
+                    "kernel_ms": round(dw_ms, 4), "launches_per_step": dw_launches,
+                    "share_of_step": round(dw_ms * dw_launches / ms_per_step, 4),
+                    "samples_per_launch": int(dw_samples), "flop_per_launch": int(dw_flop),
+                    "flop_per_sample": {"dW": 2 * ops.MLP_BWD_MACS_DW, "dX": 2 * ops.MLP_BWD_MACS_DX,
+                                        "dX_h0_when_wanted": 2 * ops.MLP_BWD_MACS_DX0},
+                    "recompute_flop_per_sample_not_counted": 2 * ops.MLP_FWD_MACS,
+                    "achieved_incl_recompute": round((dw_flop + 2 * ops.MLP_FWD_MACS * dw_samples)
+                                                     / (dw_ms * 1e-3) / 1e12, 2),
+                    "secondary": adam}
     if a.workload == "clusters":
         roofline = {"bound": "mfma", "achieved": round(cl_achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": round(cl_achieved / FP32_MFMA_PEAK_TFLOPS, 4),
@@ -960,8 +1009,10 @@ def main():
                       "frame": [a.frame, a.frame], "experts": 8},
                "c5": {"workload": f"C5: online adaptation (runtime_adapt), the routed 8-expert container (soft routing, "
                                   f"no active_module) on 1000-ray x {S}-sample batches from a 249-camera stream: "
-                                  f"train render + MSE + backward + fused clip/Adam over every expert hit",
-                      "rays_per_step_per_gpu": 1000, "experts": 8},
+                                  f"train render + MSE + backward + fused clip/Adam over every expert hit"
+                                  + ("; timed as ONE drop-in train.runtime_adapt(steps=K) call over a loader-like "
+                                     "list of device batches" if a.driver == "runtime_adapt" else ""),
+                      "rays_per_step_per_gpu": 1000, "experts": 8, "driver": a.driver},
                "c5a": {"workload": f"C5a (placement variant, not a reference configuration): rank r adapts expert r "
                                   f"alone (active_module) on its own 1000-ray x {S}-sample batches, no collective "
                                   f"(train render + MSE + backward + fused clip/Adam); the step replayed as one HIP graph"

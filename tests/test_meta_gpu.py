@@ -109,10 +109,24 @@ def test_train_step_matches_reference(algo):
         assert _close_frac(got, ref, 1e-3 * lr, 1e-6) >= 0.998, name
 
 
+def _compare_meta_runs(ma, oa, mb, ob, ra, rb, steps_expected):
+    assert rb["loss_out"] == pytest.approx(ra["loss_out"], rel=1e-4)
+    for (na, pa), (nb, pb) in zip(ma.named_parameters(), mb.named_parameters()):
+        lr = LRS[_group(na)]
+        assert _close_frac(pb.detach().cpu().numpy(), pa.detach().cpu().numpy(), 1e-3 * lr, 1e-5) >= 0.99, na
+    for (na, pa), pb in zip(ma.named_parameters(), mb.parameters()):
+        sa, sb = oa.state.get(pa, {}), ob.state.get(pb, {})
+        assert ("step" in sa) == ("step" in sb), na
+        if "step" in sa:
+            assert float(sa["step"]) == float(sb["step"]) == float(steps_expected(na)), na
+
+
 @pytest.mark.parametrize("algo", ["fomaml"])
-def test_graphed_meta_step_matches_eager(algo):
-    """GraphedMetaStep (per-region task graphs + outer clip/Adam graph, jitter drawn inside the graphs)
-    against eager train_step from the same RNG state: the same updates to fp32 summation order."""
+@pytest.mark.parametrize("how", ["object", "drop_in"])
+def test_graphed_meta_step_matches_eager(algo, how, monkeypatch):
+    """GraphedMetaStep (per-region task graphs + outer slotted clip/Adam graph, jitter drawn inside the
+    graphs) -- built explicitly, or reached through the drop-in train_step (first call eager, then capture
+    + replay) -- against the eager train_step from the same RNG state: the same updates to fp32 order."""
     from adaptive_city_nerf_amd import meta_train as MT
     from adaptive_city_nerf_amd.optim import build_optimizer
     d = G.load(f"meta_{algo}")
@@ -120,25 +134,62 @@ def test_graphed_meta_step_matches_eager(algo):
     ma, tasks = _model_and_tasks(d)
     mb, _ = _model_and_tasks(d)
     oa, ob = build_optimizer(P, ma), build_optimizer(P, mb)
+    monkeypatch.setattr(MT, "FAST_META_STEP", False)
     torch.manual_seed(7)
     with contextlib.redirect_stdout(None):
         for step in range(3):
             ra = MT.train_step(P, step, ma, oa, tasks)
+    monkeypatch.setattr(MT, "FAST_META_STEP", True)
     torch.manual_seed(7)
-    g = MT.GraphedMetaStep(P, mb, ob, tasks, warmup=1)
-    for step in (1, 2):
-        rb = g(step, tasks)
+    if how == "object":
+        g = MT.GraphedMetaStep(P, mb, ob, tasks, warmup=1)
+        for step in (1, 2):
+            rb = g(step, tasks)
+    else:
+        with contextlib.redirect_stdout(None):
+            for step in range(3):
+                rb = MT.train_step(P, step, mb, ob, tasks)
+        g = ob._acn_meta_graph
+        assert isinstance(g, MT.GraphedMetaStep) and g.replays == 2 and g.eager_steps == 0
     torch.cuda.synchronize()
     g.sync_state()
-    assert rb["loss_out"] == pytest.approx(ra["loss_out"], rel=1e-4)
-    for (na, pa), (nb, pb) in zip(ma.named_parameters(), mb.named_parameters()):
-        lr = LRS[_group(na)]
-        assert _close_frac(pb.detach().cpu().numpy(), pa.detach().cpu().numpy(), 1e-3 * lr, 1e-5) >= 0.99, na
-    for pa, pb in zip(ma.parameters(), mb.parameters()):
-        sa, sb = oa.state.get(pa, {}), ob.state.get(pb, {})
-        assert ("step" in sa) == ("step" in sb)
-        if "step" in sa:
-            assert float(sa["step"]) == float(sb["step"]) == 3.0
+    _compare_meta_runs(ma, oa, mb, ob, ra, rb, lambda n: 3)
+
+
+def test_graphed_meta_step_region_without_tasks(monkeypatch):
+    """a region with no task this step gets no gradient, so torch's Adam skips its expert (no
+    moment decay, no step increment); the graphed step's slotted outer update does the same, and a step
+    whose task shapes the graphs do not cover runs eagerly with the state carried over."""
+    from adaptive_city_nerf_amd import meta_train as MT
+    from adaptive_city_nerf_amd.optim import build_optimizer
+    d = G.load("meta_fomaml")
+    P = _P("fomaml")
+    ma, tasks = _model_and_tasks(d)
+    mb, _ = _model_and_tasks(d)
+    oa, ob = build_optimizer(P, ma), build_optimizer(P, mb)
+    cids = sorted(tasks)
+    drop = cids[-1]
+    partial = {c: (tasks[c] if c != drop else []) for c in cids}
+    def _short(t):   # same region, fewer support rays: not covered by the captured shapes
+        sup, qry = (t.support, t.query) if hasattr(t, "support") else (t["support"], t["query"])
+        n = sup["rays"].shape[0] // 2
+        return {"support": {k: v[:n] for k, v in sup.items()}, "query": qry}
+    odd = {c: [_short(t) for t in tasks[c]] for c in cids}
+    seq = [tasks, partial, tasks, odd, partial, tasks]
+    results = []
+    for fast, m, o in ((False, ma, oa), (True, mb, ob)):
+        monkeypatch.setattr(MT, "FAST_META_STEP", fast)
+        torch.manual_seed(11)
+        with contextlib.redirect_stdout(None):
+            for step, td in enumerate(seq):
+                r = MT.train_step(P, step, m, o, td)
+        results.append(r)
+    g = ob._acn_meta_graph
+    assert isinstance(g, MT.GraphedMetaStep) and g.eager_steps == 1 and g.replays == 4
+    g.sync_state()
+    n_drop = sum(1 for td in seq if td[drop])
+    _compare_meta_runs(ma, oa, mb, ob, results[0], results[1],
+                       lambda n: n_drop if n.startswith(f"submodules.{drop}.") else len(seq))
 
 
 def test_graphed_meta_step_refuses_second_order():

@@ -107,9 +107,10 @@ LRS = {"encoding": 0.01, "sigma": 0.002, "color": 0.002, "background": 0.001}
 FIXTURES = {"k4": ("train_k4", 32, 2), "k8": ("train_k8", 96, 3)}   # tag: (fixture, samples, steps)
 
 
-def check_adapt_fixture(tag, step_fn, make_opt=None):
+def check_adapt_fixture(tag, step_fn, make_opt=None, check_grads=True):
     """Replay the reference's runtime_adapt steps of fixture ``tag`` through ``step_fn(P, model, rays,
-    rgbs, opt, u) -> loss`` and compare loss, clip norm, gradients and parameters after every step."""
+    rgbs, opt, u) -> loss`` and compare loss, clip norm, gradients (``check_grads``: steps that clear
+    the gradients in the Adam pass leave none to compare) and parameters after every step."""
     from test_module_api import build_model, reference_state_dict
     from adaptive_city_nerf_amd.optim import build_optimizer
     name_, S, nsteps = FIXTURES[tag]
@@ -142,7 +143,7 @@ def check_adapt_fixture(tag, step_fn, make_opt=None):
         assert abs(float(loss) - ref_loss) <= 1e-5 * ref_loss, (float(loss), ref_loss)
         assert abs(float(opt.last_norm[0]) - float(d[pre + "total_norm"])) <= 1e-4 * float(d[pre + "total_norm"])
         named = dict(m.named_parameters())
-        for name, p in named.items():
+        for name, p in (named.items() if check_grads else ()):
             gkey = pre + "grad:" + name
             if name.endswith("hash_table"):
                 k = int(name.split(".")[1])
@@ -432,3 +433,99 @@ def test_background_head_backward_matches_autograd():
     for a, b in zip(got, ref):
         scale = float(b.abs().max())
         np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=0, atol=1e-5 * scale)
+
+
+def _runtime_adapt_step_fn():
+    """check_adapt_fixture step through the drop-in train.runtime_adapt itself (steps=1 per call, one-batch
+    loader): the fast path caches a RoutedAdaptStep on the optimizer -- call 1 eager + capture, calls 2..
+    replay the graph; the fixture's jitter reaches the step through routed_train.JITTER, filled by the
+    loader as it yields the batch."""
+    from adaptive_city_nerf_amd import routed_train as RT
+    from adaptive_city_nerf_amd import train as T
+
+    def fn(Pk, m, rays, rgbs, opt, u):
+        st = getattr(opt, "_u_static", None)
+        if st is None:
+            st = opt._u_static = torch.zeros_like(u)
+
+        def loader():
+            st.copy_(u)
+            yield rays, rgbs
+        out = T.runtime_adapt(P=Pk, model=m, data_loader=list(loader()), optimizer=opt, steps=1)
+        step = next(iter(opt._acn_routed_steps.values()))
+        opt.last_norm = step.last_norm
+        return out["loss"]
+    return fn
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tag", ["k4", "k8"])
+def test_runtime_adapt_drop_in_uses_graphed_routed_step(tag, monkeypatch):
+    """train.runtime_adapt (the function INTEGRATION.md swaps in for runtime_adapt.py:213-315) goes through
+    the cached, graph-replayed RoutedAdaptStep and reproduces the reference's runtime_adapt steps: loss,
+    clip norm and parameters after every step."""
+    from adaptive_city_nerf_amd import routed_train as RT
+    holder = {}
+    monkeypatch.setattr(RT, "JITTER", lambda n, S, dev: holder["opt"]._u_static[:n])
+
+    def make_opt(Pk, m):
+        from adaptive_city_nerf_amd.optim import build_optimizer
+        holder["opt"] = build_optimizer(Pk, m)
+        return holder["opt"]
+    m, opt = check_adapt_fixture(tag, _runtime_adapt_step_fn(), make_opt=make_opt, check_grads=False)
+    st = next(iter(opt._acn_routed_steps.values()))
+    nsteps = FIXTURES[tag][2]
+    assert st.graph is not None and st.replays == nsteps - 1 and st.steps_done == nsteps
+    # runtime_adapt leaves the host optimizer state current (state_dict): the shared head stepped every time
+    for p in m.bg_mlp.parameters():
+        assert float(opt.state[p]["step"]) == float(nsteps)
+
+
+@pytest.mark.gpu
+def test_runtime_adapt_ragged_batches_match_eager_steps(monkeypatch):
+    """A loader whose last batch is short (drop_last=False): full batches replay the graph, the short one
+    runs the same kernels eagerly through the step object's buffers; the parameters equal those of the
+    eager adapt_step loop on the same batches and jitter (pair kernels vs the same kernels without the
+    graph: identical launches, so identical up to float-atomic ordering)."""
+    from test_module_api import build_model, reference_state_dict
+    from adaptive_city_nerf_amd import routed_train as RT
+    from adaptive_city_nerf_amd import train as T
+    from adaptive_city_nerf_amd.optim import build_optimizer
+    d = G.load("train_k8")
+    Pk = SimpleNamespace(**{**vars(P), "ray_samples": 96, "chunk_points": 4_000_000})
+    rays = torch.from_numpy(d["train0:rays"]).cuda()
+    rgbs = torch.from_numpy(d["train0:rgbs"]).cuda()
+    g = torch.Generator(device="cuda").manual_seed(3)
+    sizes = [1000, 1000, 1000, 600]
+    batches = []
+    for n in sizes:
+        sel = torch.randperm(1000, device="cuda", generator=g)[:n]
+        batches.append((rays[sel].contiguous(), rgbs[sel].contiguous(), torch.rand(n, 96, device="cuda", generator=g)))
+    results = []
+    for fast in (True, False):
+        m, _ = build_model("k8")
+        m.load_state_dict(reference_state_dict(d, 8, "w:"))
+        m = m.cuda().train()
+        opt = build_optimizer(Pk, m)
+        if fast:
+            ustat = torch.zeros(1000, 96, device="cuda")
+            monkeypatch.setattr(RT, "JITTER", lambda n, S, dev: ustat[:n])
+
+            def loader():
+                for r, c, u in batches:
+                    ustat[:u.shape[0]].copy_(u)
+                    yield r, c
+            out = T.runtime_adapt(P=Pk, model=m, data_loader=loader(), optimizer=opt)
+            st = next(iter(opt._acn_routed_steps.values()))
+            assert st.replays == 2 and st.steps_done == 4 and out["steps"] == 4
+        else:
+            for r, c, u in batches:
+                T.adapt_step(Pk, m, r, c, opt, grad_clip=1.0, jitter_u=u)
+        torch.cuda.synchronize()
+        results.append(({n: p.detach().clone() for n, p in m.named_parameters()},
+                        {n: float(opt.state[p]["step"]) for n, p in m.named_parameters() if p in opt.state}))
+    (pa, sa), (pb, sb) = results
+    assert sa == sb   # the same experts stepped the same number of times
+    for n in pa:
+        lr = 0.01 if n.endswith("hash_table") else 0.001 if n.startswith("bg_mlp") else 0.002
+        assert _close_frac(pa[n].cpu().numpy(), pb[n].cpu().numpy(), 1e-3 * lr, 1e-6) >= 0.95, n
