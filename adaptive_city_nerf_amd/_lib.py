@@ -149,6 +149,12 @@ SIGNATURES = {
     "acn_hashgrid_bwd_det_workspace_bytes": ([i64, i32, i32, i32], C.c_size_t),
     "acn_hashgrid_bwd_det": ([vp, i64, vp, vp, i32, i32, i32, i32, vp, vp, sz, vp], C.c_int),
     "acn_routed_scatter_xd": ([vp, i64, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp], C.c_int),
+    "acn_routed_count_fixed": ([vp, i64, i32, vp, vp, i64, vp, vp, vp, sz, vp], C.c_int),
+    "acn_routed_pad_pairs": ([vp, i32, i64, vp, vp, vp], C.c_int),
+    "acn_ep_workspace_bytes": ([i32, i32], sz),
+    "acn_ep_gather": ([vp, vp, i32, i32, i64, i32, vp, vp, f32, f32, vp, vp, vp, vp, vp, vp, vp, vp], C.c_int),
+    "acn_ep_scatter_back": ([vp, vp, vp, i32, vp, vp], C.c_int),
+    "acn_ep_gather_grad": ([vp, vp, vp, i32, vp, vp], C.c_int),
     "acn_xd_unit_sh": ([vp, i64, vp, vp, f32, f32, vp, vp, vp], C.c_int),
     "acn_hashgrid_fwd_pairs": ([vp, vp, vp, i32, vp, vp, i32, i32, i32, vp, vp], C.c_int),
     "acn_hashgrid_bwd_pairs": ([vp, vp, vp, vp, i32, vp, vp, vp, i32, i32, i32, vp], C.c_int),
@@ -160,9 +166,17 @@ SIGNATURES = {
     "acn_grad_sumsq_slots": ([vp, vp, i64, vp, vp, i32, vp, vp, vp], C.c_int),
     "acn_grad_sumsq_slots_ex": ([vp, vp, i64, vp, vp, i32, vp, vp, vp, vp], C.c_int),
     "acn_adam_step_slots": ([vp, vp, i64, vp, vp, i32, i32, vp, i32, vp, i32, vp, vp], C.c_int),
+    "acn_adam_step_slots_segmap": ([vp, vp, i64, vp, vp, i32, i32, vp, i32, vp, i32, vp, vp, vp], C.c_int),
+    "acn_hashgrid_bwd_pairs_segmap": ([vp, vp, vp, vp, i32, vp, vp, vp, i32, i32, i32, vp, vp, vp], C.c_int),
+    "acn_hashgrid_pairs_mark": ([vp, vp, vp, vp, i32, vp, i32, i32, i32, vp, vp], C.c_int),
     # clusters.hip
     "acn_voronoi_route": ([vp, i64, i32, vp, i32, i32, C.c_double, i32, i32, vp, vp, vp, vp, vp, vp], C.c_int),
 }
+# the exact-fp32 training MLP: the same nine entry points, suffixed _exact (mlp_train.hip built twice)
+MLP_ENTRY_POINTS = ("acn_mlp_workspace_bytes", "acn_mlp_train_fwd", "acn_mlp_train_bwd", "acn_mlp_dw_workspace_bytes",
+                    "acn_mlp_train_bwd_dw", "acn_mlp_pairs_workspace_bytes", "acn_mlp_pack_pairs",
+                    "acn_mlp_train_fwd_pairs", "acn_mlp_train_bwd_dw_pairs")
+SIGNATURES.update({n + "_exact": SIGNATURES[n] for n in MLP_ENTRY_POINTS})
 
 
 def lib():

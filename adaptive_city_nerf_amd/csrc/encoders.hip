@@ -226,6 +226,9 @@ struct Tables {
 struct GradTables {
     float* t[acn::kMaxK];
 };
+struct SegMaps {   // per expert: the "touched this step" byte map of its table's 64-B segments (or null)
+    uint8_t* t[acn::kMaxK];
+};
 
 template <int INTERP>
 __global__ void __launch_bounds__(256) hashgrid_fwd_pairs(const float* __restrict__ x01, const int32_t* __restrict__ pk,
@@ -252,12 +255,13 @@ __global__ void __launch_bounds__(256) hashgrid_fwd_pairs(const float* __restric
 // table-gradient update without a pass over the 128 MiB gradient buffers (clip_grad_norm_'s sum of
 // squares, runtime_adapt.py:305-307).  Doubles: new^2 and old^2 are exact, so only the differences and
 // their sum round (~1e-16 relative).
-template <int INTERP, int PPL, bool TELE>
+template <int INTERP, int PPL, bool TELE, bool MARK_ONLY = false>
 __global__ void __launch_bounds__(256) hashgrid_bwd_pairs(const float* __restrict__ x01, const int32_t* __restrict__ pk,
                                                           const int32_t* __restrict__ pidx,
                                                           const int64_t* __restrict__ seg, int K,
                                                           const float* __restrict__ gout, GradTables gt, Res32 res,
-                                                          int L, int log2T, int l0, double* __restrict__ sq) {
+                                                          int L, int log2T, int l0, double* __restrict__ sq,
+                                                          SegMaps smaps) {
     const int lane = threadIdx.x & 63;
     const int64_t M = seg[K];
     const int64_t nwaves = ((M + 4 * PPL - 1) / (4 * PPL)) * (L - l0);
@@ -265,6 +269,7 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_pairs(const float* __restric
     const uint32_t mask = (uint32_t)((1ull << log2T) - 1ull);
     double tsq = 0.0;
     auto flush = [&](float* a, float v) {
+        if (MARK_ONLY) return;   // acn_hashgrid_pairs_mark: segment maps only
         if (TELE) {
             const float o = atomicAdd(a, v);
             const float nv = o + v;
@@ -281,6 +286,7 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_pairs(const float* __restric
         const float r = (float)res.v[l];
         const int64_t base = ((int64_t)l << log2T) * 2 + f;
         float* cur = nullptr;
+        uint8_t* cseg = nullptr;   // the segment-map byte of cur's 64-B segment (segment maps on)
         float acc = 0.0f;
         for (int i = 0; i < PPL; ++i) {
             const int64_t m = m0 + i;
@@ -297,18 +303,27 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_pairs(const float* __restric
             const uint32_t xi = (uint32_t)(int)fx + (uint32_t)bx;
             const uint32_t yi = (uint32_t)(int)fy * acn::kP1 + (by ? acn::kP1 : 0u);
             const uint32_t zi = (uint32_t)(int)fz * acn::kP2 + (bz ? acn::kP2 : 0u);
-            float* a = gt.t[pk[m]] + base + (int64_t)((xi ^ yi ^ zi) & mask) * 2;
-            const float gv = ((gout[(m * L + l) * 2 + f] * (bz ? wz : 1.0f - wz)) * (by ? wy : 1.0f - wy)) *
-                             (bx ? wx : 1.0f - wx);
+            const int kk = pk[m];
+            const uint32_t row = (xi ^ yi ^ zi) & mask;
+            float* a = gt.t[kk] + base + (int64_t)row * 2;
+            const float gv = MARK_ONLY ? 0.0f : ((gout[(m * L + l) * 2 + f] * (bz ? wz : 1.0f - wz)) *
+                                                 (by ? wy : 1.0f - wy)) * (bx ? wx : 1.0f - wx);
             if (a == cur) {
                 acc += gv;
             } else {
-                if (cur) flush(cur, acc);
+                if (cur) {
+                    flush(cur, acc);
+                    if (cseg && f == 0) *cseg = 1;   // idempotent plain byte store (feature 1 shares the row)
+                }
                 cur = a;
+                cseg = smaps.t[kk] ? smaps.t[kk] + ((((int64_t)l << log2T) + row) >> 3) : nullptr;
                 acc = gv;
             }
         }
-        if (cur) flush(cur, acc);
+        if (cur) {
+            flush(cur, acc);
+            if (cseg && f == 0) *cseg = 1;
+        }
     }
     if (TELE) {  // one double atomic per wave
 #pragma unroll
@@ -580,6 +595,15 @@ extern "C" int acn_hashgrid_bwd_pairs_sumsq(const float* x01, const int32_t* pk,
                                             const int64_t* seg, int K, const float* grad_out,
                                             float* const* grad_tables, const int32_t* res, int L, int log2T,
                                             int interp, double* table_sumsq, void* stream) {
+    return acn_hashgrid_bwd_pairs_segmap(x01, pk, pidx, seg, K, grad_out, grad_tables, res, L, log2T, interp,
+                                         table_sumsq, nullptr, stream);
+}
+
+extern "C" int acn_hashgrid_bwd_pairs_segmap(const float* x01, const int32_t* pk, const int32_t* pidx,
+                                             const int64_t* seg, int K, const float* grad_out,
+                                             float* const* grad_tables, const int32_t* res, int L, int log2T,
+                                             int interp, double* table_sumsq, uint8_t* const* seg_now,
+                                             void* stream) {
     ACN_REQUIRE(K >= 1 && K <= acn::kMaxK && grad_tables && res && seg && x01 && pk && pidx && grad_out,
                 "acn_hashgrid_bwd_pairs: bad arguments");
     ACN_REQUIRE(L >= 1 && L <= ACN_MAX_LEVELS && log2T >= 1 && log2T <= 30 && (interp == 1 || interp == 2),
@@ -588,20 +612,49 @@ extern "C" int acn_hashgrid_bwd_pairs_sumsq(const float* x01, const int32_t* pk,
     for (int i = 0; i < L; ++i) r.v[i] = res[i];
     GradTables t{};
     for (int k = 0; k < K; ++k) t.t[k] = grad_tables[k];
+    SegMaps sm{};
+    if (seg_now)
+        for (int k = 0; k < K; ++k) sm.t[k] = seg_now[k];
     const dim3 grid(2048), block(256);
     hipStream_t s = (hipStream_t)stream;
     const MergeCfg mc = merge_cfg(L, log2T);
     ACN_REQUIRE(!(table_sumsq && mc.LM > 0), "acn_hashgrid_bwd_pairs_sumsq: not available with the merged coarse "
                 "levels (ACN_HASH_BWD_MERGE)");
+    ACN_REQUIRE(!(seg_now && mc.LM > 0), "acn_hashgrid_bwd_pairs_segmap: not available with the merged coarse levels");
     if (mc.LM > 0) {  // fixed grid (graph-replayable): items are counted from the device slot count
         if (interp == 1) hipLaunchKernelGGL(hashgrid_bwd_merge<1>, dim3(512), block, 0, s, x01, pk, pidx, seg, K, (int64_t)0, grad_out, t, r, L, log2T, mc);
         else hipLaunchKernelGGL(hashgrid_bwd_merge<2>, dim3(512), block, 0, s, x01, pk, pidx, seg, K, (int64_t)0, grad_out, t, r, L, log2T, mc);
     }
     if (mc.LM < L) {
-#define ACN_BWD_PAIRS(I, T) hipLaunchKernelGGL((hashgrid_bwd_pairs<I, 16, T>), grid, block, 0, s, x01, pk, pidx, seg, K, grad_out, t, r, L, log2T, mc.LM, table_sumsq)
+#define ACN_BWD_PAIRS(I, T) hipLaunchKernelGGL((hashgrid_bwd_pairs<I, 16, T>), grid, block, 0, s, x01, pk, pidx, seg, K, grad_out, t, r, L, log2T, mc.LM, table_sumsq, sm)
         if (table_sumsq) { if (interp == 1) ACN_BWD_PAIRS(1, true); else ACN_BWD_PAIRS(2, true); }
         else { if (interp == 1) ACN_BWD_PAIRS(1, false); else ACN_BWD_PAIRS(2, false); }
 #undef ACN_BWD_PAIRS
     }
     return acn_check_launch("acn_hashgrid_bwd_pairs");
+}
+
+extern "C" int acn_hashgrid_pairs_mark(const float* x01, const int32_t* pk, const int32_t* pidx, const int64_t* seg,
+                                       int K, const int32_t* res, int L, int log2T, int interp,
+                                       uint8_t* const* seg_now, void* stream) {
+    ACN_REQUIRE(K >= 1 && K <= acn::kMaxK && res && seg && x01 && pk && pidx && seg_now,
+                "acn_hashgrid_pairs_mark: bad arguments");
+    ACN_REQUIRE(L >= 1 && L <= ACN_MAX_LEVELS && log2T >= 1 && log2T <= 30 && (interp == 1 || interp == 2),
+                "acn_hashgrid_pairs_mark: Linear / Smoothstep interpolation only");
+    Res32 r{};
+    for (int i = 0; i < L; ++i) r.v[i] = res[i];
+    GradTables t{};
+    SegMaps sm{};
+    for (int k = 0; k < K; ++k) {
+        sm.t[k] = seg_now[k];
+        t.t[k] = reinterpret_cast<float*>(seg_now[k]);   // address arithmetic only: nothing is written through it
+    }
+    hipStream_t s = (hipStream_t)stream;
+    if (interp == 1)
+        hipLaunchKernelGGL((hashgrid_bwd_pairs<1, 16, false, true>), dim3(2048), dim3(256), 0, s, x01, pk, pidx, seg, K,
+                           (const float*)nullptr, t, r, L, log2T, 0, (double*)nullptr, sm);
+    else
+        hipLaunchKernelGGL((hashgrid_bwd_pairs<2, 16, false, true>), dim3(2048), dim3(256), 0, s, x01, pk, pidx, seg, K,
+                           (const float*)nullptr, t, r, L, log2T, 0, (double*)nullptr, sm);
+    return acn_check_launch("acn_hashgrid_pairs_mark");
 }

@@ -9,9 +9,13 @@
 //      gradient in the forward's chain-rule order ((g * wz') * wy') * wx' -- generated in (m, l, c) order;
 //   2. a stable LSD radix sort of the records by key (rocPRIM), so equal keys keep generation order;
 //   3. one lane per run of equal keys sums it sequentially in fp32 and stores the row.
-// Every row is therefore the fp32 sum of its contributions in (point, corner) order -- the order of a
-// serial CPU loop over the points (the reference's index_put_(accumulate=True) backward,
-// models/encodings.py:318-329, accumulates serially on the CPU).  Bitwise reproducible run to run.
+// Every row is therefore the fp32 sum of its contributions in (point, corner) order, continued from the row's
+// current value: equal, bit for bit, to a serial CPU scatter-add over (point, level, corner)
+// (tests/test_hash_det.py), and bitwise reproducible run to run.  It is NOT the reference's own summation
+// order: there (models/encodings.py:318-381) each of the 8 corners is a separate gather whose backward
+// index_put_(accumulate=True) sums that corner's contributions, and autograd then adds the 8 per-corner
+// table gradients.  The caller bounds the workspace (~24 B x 8 x L per point) by chunking the points
+// (ops.hashgrid_bwd): chunks run in point order, so the rows continue the same serial sums.
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include "acn_device.h"

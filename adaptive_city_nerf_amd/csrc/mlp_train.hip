@@ -21,6 +21,16 @@
 #include "acn_device.h"
 #include "acn_internal.h"
 
+// This file is compiled twice into libacnerf.so: the default build (fp16x3 layer products) exports the
+// acn_mlp_* entry points, a second object built with -DACN_TRAIN_F16X3=0 -DACN_MLP_SUFFIX=_exact exports
+// the exact-fp32 variants as acn_mlp_*_exact (a runtime precision switch: ops.set_train_mlp_precision).
+#ifndef ACN_MLP_SUFFIX
+#define ACN_MLP_SUFFIX
+#endif
+#define ACN_MLP_CAT2(a, b) a##b
+#define ACN_MLP_CAT(a, b) ACN_MLP_CAT2(a, b)
+#define ACN_MLP_API(name) ACN_MLP_CAT(name, ACN_MLP_SUFFIX)
+
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 namespace {
@@ -1130,9 +1140,9 @@ unsigned grid_for(int64_t M) {  // 4 waves per block, grid-stride over 32-sample
 
 }  // namespace
 
-extern "C" size_t acn_mlp_workspace_bytes(void) { return (size_t)L_FLOATS * sizeof(float); }
+extern "C" size_t ACN_MLP_API(acn_mlp_workspace_bytes)(void) { return (size_t)L_FLOATS * sizeof(float); }
 
-extern "C" int acn_mlp_train_fwd(const float* h0, const float* sh, int64_t M, const acn_mlp* w, float* out,
+extern "C" int ACN_MLP_API(acn_mlp_train_fwd)(const float* h0, const float* sh, int64_t M, const acn_mlp* w, float* out,
                                  float* save, void* workspace, void* stream) {
     ACN_REQUIRE(M >= 0 && w && workspace, "acn_mlp_train_fwd: bad arguments");
     if (M == 0) return ACN_OK;
@@ -1144,7 +1154,7 @@ extern "C" int acn_mlp_train_fwd(const float* h0, const float* sh, int64_t M, co
     return acn_check_launch("acn_mlp_train_fwd");
 }
 
-extern "C" int acn_mlp_train_bwd(const float* save, const float* out, const float* gout, int64_t M, const acn_mlp* w,
+extern "C" int ACN_MLP_API(acn_mlp_train_bwd)(const float* save, const float* out, const float* gout, int64_t M, const acn_mlp* w,
                                  float* gsave, float* gh0, void* workspace, void* stream) {
     ACN_REQUIRE(M >= 0 && w && workspace, "acn_mlp_train_bwd: bad arguments");
     if (M == 0) return ACN_OK;
@@ -1156,11 +1166,11 @@ extern "C" int acn_mlp_train_bwd(const float* save, const float* out, const floa
     return acn_check_launch("acn_mlp_train_bwd");
 }
 
-extern "C" size_t acn_mlp_dw_workspace_bytes(void) {
+extern "C" size_t ACN_MLP_API(acn_mlp_dw_workspace_bytes)(void) {
     return ((size_t)L_FLOATS + (size_t)MAX_DW_BLOCKS * NDW) * sizeof(float);
 }
 
-extern "C" int acn_mlp_train_bwd_dw(const float* h0, const float* sh, const float* out, const float* gout, int64_t M,
+extern "C" int ACN_MLP_API(acn_mlp_train_bwd_dw)(const float* h0, const float* sh, const float* out, const float* gout, int64_t M,
                                     const acn_mlp* w, float* dw, float* gh0, void* workspace, void* stream) {
     ACN_REQUIRE(M >= 0 && w && workspace && dw, "acn_mlp_train_bwd_dw: bad arguments");
     hipStream_t s = (hipStream_t)stream;
@@ -1185,11 +1195,11 @@ extern "C" int acn_mlp_train_bwd_dw(const float* h0, const float* sh, const floa
 // routed pair lists
 constexpr int PAIR_DW_BLOCKS = 256;
 
-extern "C" size_t acn_mlp_pairs_workspace_bytes(int K) {
+extern "C" size_t ACN_MLP_API(acn_mlp_pairs_workspace_bytes)(int K) {
     return ((size_t)K * L_FLOATS + (size_t)PAIR_DW_BLOCKS * K * NDW) * sizeof(float);
 }
 
-extern "C" int acn_mlp_pack_pairs(const acn_mlp* const* w, int K, void* workspace, void* stream) {
+extern "C" int ACN_MLP_API(acn_mlp_pack_pairs)(const acn_mlp* const* w, int K, void* workspace, void* stream) {
     ACN_REQUIRE(w && workspace && K >= 1 && K <= acn::kMaxK, "acn_mlp_pack_pairs: bad arguments");
     MlpPtrsK pk{};
     for (int k = 0; k < K; ++k) {
@@ -1201,7 +1211,7 @@ extern "C" int acn_mlp_pack_pairs(const acn_mlp* const* w, int K, void* workspac
     return acn_check_launch("acn_mlp_pack_pairs");
 }
 
-extern "C" int acn_mlp_train_fwd_pairs(const float* h0, const float* sh, const int64_t* seg, int K,
+extern "C" int ACN_MLP_API(acn_mlp_train_fwd_pairs)(const float* h0, const float* sh, const int64_t* seg, int K,
                                        const void* workspace, float* out, void* stream) {
     ACN_REQUIRE(h0 && sh && seg && workspace && out && K >= 1 && K <= acn::kMaxK,
                 "acn_mlp_train_fwd_pairs: bad arguments");
@@ -1210,7 +1220,7 @@ extern "C" int acn_mlp_train_fwd_pairs(const float* h0, const float* sh, const i
     return acn_check_launch("acn_mlp_train_fwd_pairs");
 }
 
-extern "C" int acn_mlp_train_bwd_dw_pairs(const float* h0, const float* sh, const float* out, const float* gout,
+extern "C" int ACN_MLP_API(acn_mlp_train_bwd_dw_pairs)(const float* h0, const float* sh, const float* out, const float* gout,
                                           const int64_t* seg, int K, void* workspace, float* dw, float* gh0,
                                           void* stream) {
     ACN_REQUIRE(h0 && sh && out && gout && seg && workspace && dw && K >= 1 && K <= acn::kMaxK,

@@ -341,13 +341,51 @@ __device__ __forceinline__ void adam_chunk_zero(float* p, float* g, float* m, fl
     }
 }
 
+// Segment-mapped chunk (the sparse hash-table gradients of the routed step): a tensor whose 64-B segments
+// (16 floats = 8 table rows) carry two byte maps -- now[s]: the table scatter added into segment s this
+// step; ever[s]: segment s was updated before.  A segment neither touched now nor ever holds m = v = g = 0,
+// where torch's Adam (weight_decay 0) leaves p, m, v bit-identical (m' = 0, v' = 0, p' = p + (-step * 0) /
+// eps = p): it is skipped, nothing read or written.  A segment not touched now has g = 0 (the gradient
+// buffer is cleared after every use): its update reads p, m, v only.  A vector = 4 floats, so segment
+// s = vector / 4; the 4 vectors of a segment are 4 consecutive lanes of one wave-instruction (the map
+// loads precede the map stores for all of them); the first lane updates the maps.  chunk base is a
+// multiple of ACN_OPTIM_CHUNK floats (segment aligned).
+__device__ __forceinline__ void adam_chunk_seg(float* p, float* g, float* m, float* v, int64_t n, float scale,
+                                               const GroupK& k, uint8_t* __restrict__ now, uint8_t* __restrict__ ever,
+                                               bool clear) {
+    f4* p4 = reinterpret_cast<f4*>(p);
+    f4* g4 = reinterpret_cast<f4*>(g);
+    f4* m4 = reinterpret_cast<f4*>(m);
+    f4* v4 = reinterpret_cast<f4*>(v);
+    const int64_t n4 = n >> 2;   // n is a multiple of 16 (checked by the host)
+    const f4 zero = 0.0f;
+    for (int64_t i = threadIdx.x; i < n4; i += kThreads) {
+        const int64_t sgi = i >> 2;
+        const uint8_t nw = now[sgi], ev = ever[sgi];
+        if (nw | ev) {
+            f4 pp = ldv(&p4[i]), mm = ldv(&m4[i]), vv = ldv(&v4[i]);
+            const f4 gg = nw ? ldv(&g4[i]) : zero;
+            adam_vec(pp, gg, mm, vv, scale, k);
+            stv(&p4[i], pp);
+            stv(&m4[i], mm);
+            stv(&v4[i], vv);
+            if (clear && nw && (gg[0] != 0.0f || gg[1] != 0.0f || gg[2] != 0.0f || gg[3] != 0.0f)) stv(&g4[i], zero);
+        }
+        if ((i & 3) == 0 && nw) {
+            now[sgi] = 0;
+            if (!ev) ever[sgi] = 1;
+        }
+    }
+}
+
 __global__ void __launch_bounds__(kThreads) adam_slots_kernel(const acn_param_desc* __restrict__ descs,
                                                               const int32_t* __restrict__ chunk_tensor,
                                                               const int32_t* __restrict__ flags,
                                                               const GroupK* __restrict__ table, int ngroups,
                                                               int table_steps, const int32_t* __restrict__ step_dev,
                                                               const int64_t* __restrict__ seg, int K,
-                                                              const float* __restrict__ grad_scale) {
+                                                              const float* __restrict__ grad_scale,
+                                                              uint8_t* const* __restrict__ segmaps) {
     const int t = chunk_tensor[blockIdx.x];
     const acn_param_desc d = descs[t];
     const int f = flags[t], slot = f & 0xffff;
@@ -362,8 +400,16 @@ __global__ void __launch_bounds__(kThreads) adam_slots_kernel(const acn_param_de
     float* g = const_cast<float*>(d.grad) + base;
     float* m = d.exp_avg + base;
     float* v = d.exp_avg_sq + base;
-    if (f & kSlotZero) adam_chunk_zero(p, g, m, v, n, scale, k);
-    else adam_chunk(p, g, m, v, n, scale, k);
+    uint8_t* smap = segmaps ? segmaps[2 * t] : nullptr;
+    if (smap) {
+        const int64_t s0 = base >> 4, nseg = (d.numel + 15) >> 4;
+        adam_chunk_seg(p, g, m, v, n, scale, k, smap + s0, segmaps[2 * t + 1] + s0, (f & kSlotZero) != 0);
+        (void)nseg;
+    } else if (f & kSlotZero) {
+        adam_chunk_zero(p, g, m, v, n, scale, k);
+    } else {
+        adam_chunk(p, g, m, v, n, scale, k);
+    }
 }
 
 // python-float (double) scalars of _single_tensor_adam for one group at one step, cast to fp32 where
@@ -519,6 +565,23 @@ extern "C" int acn_adam_step_slots(const acn_param_desc* descs, const int32_t* c
     hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(bump_slots_kernel, dim3(1), dim3(1024), 0, s, step_dev, seg, K, nslots);
     hipLaunchKernelGGL(adam_slots_kernel, dim3((unsigned)nchunks), dim3(kThreads), 0, s, descs, chunk_tensor, flags,
-                       reinterpret_cast<const GroupK*>(table), ngroups, table_steps, step_dev, seg, K, grad_scale);
+                       reinterpret_cast<const GroupK*>(table), ngroups, table_steps, step_dev, seg, K, grad_scale,
+                       (uint8_t* const*)nullptr);
     return acn_check_launch("acn_adam_step_slots");
+}
+
+extern "C" int acn_adam_step_slots_segmap(const acn_param_desc* descs, const int32_t* chunk_tensor, int64_t nchunks,
+                                          const int32_t* flags, const void* table, int ngroups, int table_steps,
+                                          int32_t* step_dev, int nslots, const int64_t* seg, int K,
+                                          const float* grad_scale, uint8_t* const* segmaps, void* stream) {
+    ACN_REQUIRE(nchunks >= 1 && nchunks <= 0x7fffffff && descs && chunk_tensor && flags && table && step_dev && segmaps,
+                "acn_adam_step_slots_segmap: bad arguments");
+    ACN_REQUIRE(ngroups >= 1 && ngroups <= ACN_OPTIM_MAX_GROUPS && table_steps >= 1 && nslots >= 1 && nslots <= 1024,
+                "acn_adam_step_slots_segmap: bad ngroups / table_steps / nslots");
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(bump_slots_kernel, dim3(1), dim3(1024), 0, s, step_dev, seg, K, nslots);
+    hipLaunchKernelGGL(adam_slots_kernel, dim3((unsigned)nchunks), dim3(kThreads), 0, s, descs, chunk_tensor, flags,
+                       reinterpret_cast<const GroupK*>(table), ngroups, table_steps, step_dev, seg, K, grad_scale,
+                       segmaps);
+    return acn_check_launch("acn_adam_step_slots_segmap");
 }

@@ -880,6 +880,8 @@ struct RenderParams {
     float sigma_scale, tau;
     float *rgb, *depth, *weights, *acc;
     const int32_t* order;  // optional visiting order (ray_order_kernel); NULL = rays in the given order
+    const int32_t* norder; // render_slots_kernel: device count of `order` entries (the multi-expert rays of the
+                           // split routed render); NULL = N
 };
 
 #ifndef ACN_SHFOLD
@@ -1045,6 +1047,9 @@ __global__ void __launch_bounds__(1024, 4) render_kernel(FieldCfg cfg, BgArgs bg
 // with rays sorted by owning expert, parallel.expert_sorted_plan, a workgroup's rays mostly need
 // the same one or two experts, so staging is rare).  A sample whose expert is not resident is
 // evaluated from the packed image in global memory (L2), without the SH fold.
+#ifndef ACN_SPLIT_ROUTED
+#define ACN_SPLIT_ROUTED 1  // K > 2: single-expert rays through render_single_kernel, the rest through render_slots_kernel
+#endif
 #ifndef ACN_SLOTS_SINGLE
 #define ACN_SLOTS_SINGLE 1  // single-expert rays (kSingleRay) skip the per-sample routing and blend
 #endif
@@ -1053,10 +1058,10 @@ __global__ void __launch_bounds__(1024, 4) render_kernel(FieldCfg cfg, BgArgs bg
 // 0 + y_k * 1.0f is y_k bit for bit and the ray can skip the per-sample routing and blend.
 constexpr uint32_t kSingleRay = 1u << 31;
 __device__ __forceinline__ uint32_t ray_expert_mask(const FieldCfg& cfg, int route, const RenderParams& p, int64_t ray,
-                                                    int64_t lim, float step, int lane) {
+                                                    bool live, float step, int lane) {
     uint32_t m = 0u;
     bool exact = true;
-    if (ray < lim) {
+    if (live) {
         const float* rp = p.rays + ray * 8;
         const float ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
         const float near = rp[6], far = rp[7];
@@ -1109,8 +1114,9 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
     const int64_t waves_per_wg = blockDim.x >> 6;
     // XCD bands (as render_kernel): with the grid a multiple of 8, XCD x walks the x-th contiguous
     // eighth of the rays, so a frame's neighbouring rays share one L2 (ACN_SLOTS_BAND=0: interleaved)
-    int64_t first = (int64_t)blockIdx.x * waves_per_wg, lim = p.N, gstride = (int64_t)gridDim.x * waves_per_wg;
-    if (ACN_SLOTS_BAND && (gridDim.x & 7) == 0) {
+    int64_t first = (int64_t)blockIdx.x * waves_per_wg, lim = p.norder ? (int64_t)p.norder[0] : p.N,
+            gstride = (int64_t)gridDim.x * waves_per_wg;
+    if (ACN_SLOTS_BAND && (gridDim.x & 7) == 0 && !p.norder) {
         const int64_t chunk = (((p.N + 7) >> 3) + waves_per_wg - 1) / waves_per_wg * waves_per_wg;
         const int64_t lo = min(p.N, (int64_t)(blockIdx.x & 7) * chunk);
         lim = min(p.N, lo + chunk);
@@ -1118,8 +1124,10 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
         gstride = (int64_t)(gridDim.x >> 3) * waves_per_wg;
     }
     for (int64_t base = first; base < lim; base += gstride) {
-        const int64_t ray = base + wave;
-        const uint32_t m = ray_expert_mask(cfg, ROUTE, p, ray, lim, step, lane);
+        const bool live = base + wave < lim;
+        const int64_t ray = !live ? 0 : (p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[base + wave])
+                                                 : base + wave);
+        const uint32_t m = ray_expert_mask(cfg, ROUTE, p, ray, live, step, lane);
         if (lane == 0)
             for (int k = 0; k < cfg.K; ++k)
                 if ((m >> k) & 1u) atomicAdd(&cnt[k], 1);
@@ -1155,7 +1163,7 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
 #else
         const int k0 = __builtin_amdgcn_readfirstlane(slot_k[0]), k1 = __builtin_amdgcn_readfirstlane(slot_k[1]);
 #endif
-        if (ray < lim) {
+        if (live) {
             const bool single = (m & kSingleRay) != 0u;
             const int k_single = __builtin_ctz(m | kSingleRay);
             render_ray(p, bg, ray, lane, step,
@@ -1220,6 +1228,154 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
                            }
                        });
         }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Split routed render (C3 / C4, K > 2).  The single-expert rays (every sample routed to ONE expert with
+// weight exactly 1.0f: kSingleRay) are most of a batch (C3 ~91%, C4 ~60%); they go through
+// render_single_kernel -- 16 waves per CU, <= 128 VGPRs, no per-ray routing or blend, one expert image in
+// LDS per workgroup, restaged only where the expert changes -- and only the multi-expert rays through
+// render_slots_kernel.  Every ray is still rendered by one wave and written at its own index with the
+// same arithmetic as the slots kernel's single path (0 + y_k * 1.0f == y_k), so the outputs are
+// bit-identical to the unsplit render.
+//   ray_class_kernel : one wave per ray, ray_expert_mask -> code[ray] = k (single expert k) or K (multi)
+//   ray_lists_kernel : one workgroup, stable counting sort of the codes: expert k's rays at
+//                      list[hdr[k] .. hdr[k] + n_k), its segment padded to 16 (one ray per wave of a
+//                      workgroup round) with -1; hdr[K] = single entries; the multi rays in input order in
+//                      multi[0 .. hdr[K + 1])
+template <int ROUTE>
+__global__ void __launch_bounds__(256) ray_class_kernel(FieldCfg cfg, RenderParams p, int32_t* __restrict__ code) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const float step = 1.0f / (float)(p.S - 1);
+    for (int64_t ray = wave; ray < p.N; ray += (int64_t)gridDim.x * 4) {
+        const uint32_t m = ray_expert_mask(cfg, ROUTE, p, ray, true, step, lane);
+        if (lane == 0) code[ray] = (m & kSingleRay) ? (int32_t)__builtin_ctz(m & ~kSingleRay) : cfg.K;
+    }
+}
+
+__global__ void __launch_bounds__(1024) ray_lists_kernel(const int32_t* __restrict__ code, int64_t N, int K,
+                                                         int32_t* __restrict__ list, int32_t* __restrict__ multi,
+                                                         int32_t* __restrict__ hdr) {
+    __shared__ int cnt[kMaxK + 1], base[kMaxK + 1], wtot[16][kMaxK + 1];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid <= K) cnt[tid] = 0;
+    __syncthreads();
+    int mine[kMaxK + 1];
+#pragma unroll
+    for (int c = 0; c <= kMaxK; ++c) mine[c] = 0;
+    for (int64_t i = tid; i < N; i += 1024) {
+        const int c = code[i];
+#pragma unroll
+        for (int q = 0; q <= kMaxK; ++q) mine[q] += (q == c) ? 1 : 0;
+    }
+#pragma unroll
+    for (int c = 0; c <= kMaxK; ++c)
+        if (c <= K && mine[c]) atomicAdd(&cnt[c], mine[c]);
+    __syncthreads();
+    if (tid == 0) {
+        int b = 0;
+        for (int k = 0; k < K; ++k) {
+            hdr[k] = b;
+            base[k] = b;
+            b += (cnt[k] + 15) & ~15;
+        }
+        hdr[K] = b;
+        base[K] = 0;   // the multi-expert rays: their own list
+        hdr[K + 1] = cnt[K];
+    }
+    __syncthreads();
+    for (int k = 0; k < K; ++k) {   // padding entries of every single-expert segment
+        const int p0 = base[k] + cnt[k], p1 = base[k] + ((cnt[k] + 15) & ~15);
+        for (int q = p0 + tid; q < p1; q += 1024) list[q] = -1;
+    }
+    const uint64_t below = (1ull << lane) - 1ull;
+    for (int64_t c0 = 0; c0 < N; c0 += 1024) {
+        const int64_t i = c0 + tid;
+        const int c = i < N ? code[i] : -1;
+        int pre = 0, mc = -1;
+        for (int q = 0; q <= K; ++q) {
+            const uint64_t b = __ballot(c == q);
+            if (lane == 0) wtot[w][q] = __popcll(b);
+            if (c == q) {
+                pre = __popcll(b & below);
+                mc = q;
+            }
+        }
+        __syncthreads();
+        if (mc >= 0) {
+            int off = base[mc] + pre;
+            for (int v = 0; v < w; ++v) off += wtot[v][mc];
+            (mc == K ? multi : list)[off] = (int32_t)i;
+        }
+        __syncthreads();
+        if (tid <= K) {
+            int t = 0;
+            for (int v = 0; v < 16; ++v) t += wtot[v][tid];
+            base[tid] += t;
+        }
+        __syncthreads();
+    }
+}
+
+#ifndef ACN_SINGLE_DBG
+#define ACN_SINGLE_DBG 0  // diagnostic builds: 1 no SH fold, 2 a workgroup barrier after every round
+#endif
+template <int INTERP>
+__global__ void __launch_bounds__(1024, 4) render_single_kernel(FieldCfg cfg, BgArgs bg, RenderParams p,
+                                                                const int32_t* __restrict__ list,
+                                                                const int32_t* __restrict__ hdr) {
+    constexpr bool FOLD = ACN_SHFOLD != 0 && ACN_SINGLE_DBG != 1;
+    __shared__ __attribute__((aligned(16))) float smem[PK_FLOATS];
+    __shared__ __attribute__((aligned(16))) float cbuf[FOLD ? 16 * 64 : 4];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float* cb = FOLD ? cbuf + wave * 64 : nullptr;
+    const float step = 1.0f / (float)(p.S - 1);
+    const int K = cfg.K;
+    const int64_t G = (int64_t)hdr[K] >> 4;   // workgroup rounds of 16 rays
+    // contiguous round ranges per workgroup (the expert changes at most a few times per workgroup), in XCD
+    // bands: with the grid a multiple of 8, XCD x (blocks b = x mod 8) takes the x-th eighth of the rounds
+    int64_t g0, g1;
+    if ((gridDim.x & 7) == 0) {
+        const int64_t x = blockIdx.x & 7, slot = blockIdx.x >> 3, nx = gridDim.x >> 3;
+        const int64_t lo = G * x / 8, hi = G * (x + 1) / 8;
+        g0 = lo + (hi - lo) * slot / nx;
+        g1 = lo + (hi - lo) * (slot + 1) / nx;
+    } else {
+        g0 = G * blockIdx.x / gridDim.x;
+        g1 = G * (blockIdx.x + 1) / gridDim.x;
+    }
+    int cur = -1;
+    for (int64_t g = g0; g < g1; ++g) {
+        int k = 0;
+        while (k + 1 < K && hdr[k + 1] <= 16 * g) ++k;
+        k = __builtin_amdgcn_readfirstlane(k);
+        if (k != cur) {   // uniform over the workgroup: every wave walks the same rounds
+            __syncthreads();
+            const f32x4* src = reinterpret_cast<const f32x4*>(p.packed + (size_t)k * PK_FLOATS);
+            f32x4* dst = reinterpret_cast<f32x4*>(smem);
+            for (int i = threadIdx.x; i < PK_FLOATS / 4; i += blockDim.x) dst[i] = src[i];
+            __syncthreads();
+            cur = k;
+        }
+        const int32_t ray = __builtin_amdgcn_readfirstlane(list[16 * g + wave]);
+#if ACN_SINGLE_DBG == 2
+        __syncthreads();
+#endif
+        if (ray < 0) continue;   // padding of expert k's segment
+        render_ray(p, bg, ray, lane, step,
+                   [&](float px, float py, float pz, const float (&shv)[8], uint32_t& folded, float& yr, float& yg,
+                       float& yb, float& ys) {
+                       if (FOLD && !(folded & 1u)) {
+                           fold_sh_bias(smem, shv, lane, cb);
+                           folded |= 1u;
+                       }
+                       float sg;
+                       field_tile<INTERP, FOLD>(smem, cfg.ex[k], cfg.log2T, px, py, pz, shv, cb, lane, yr, yg, yb, sg);
+                       ys = trunc_exp(sg);
+                   });
     }
 }
 
@@ -1749,8 +1905,14 @@ __global__ void __launch_bounds__(1024) ray_order_kernel(const float* __restrict
 
 extern "C" size_t acn_workspace_bytes(int K) { return (size_t)(K < 1 ? 1 : K) * PK_BYTES; }
 
+// scratch of the split routed render: code[N], list[N + 16 kMaxK], multi[N], hdr[kMaxK + 2]
+static size_t split_bytes(int64_t N) { return (size_t)(3 * N + 16 * kMaxK + kMaxK + 2) * sizeof(int32_t); }
+
 extern "C" size_t acn_render_order_bytes(int64_t N) {
-    return N >= 1 && N <= ACN_ORDER_MAX ? (size_t)N * sizeof(int32_t) : 0;
+    if (N < 1) return 0;
+    const size_t ord = N <= ACN_ORDER_MAX ? (size_t)N * sizeof(int32_t) : 0;
+    const size_t spl = ACN_SPLIT_ROUTED ? split_bytes(N) : 0;
+    return ord > spl ? ord : spl;
 }
 
 extern "C" int acn_pack_experts(const acn_expert* experts, const acn_routing* routing, int active_module,
@@ -1820,6 +1982,35 @@ extern "C" int acn_render_stratified_fwd_ordered(const float* rays, int64_t N, i
     if (order_scratch && !slots && N <= ACN_ORDER_MAX && order_bytes >= (size_t)N * sizeof(int32_t)) {
         hipLaunchKernelGGL(ray_order_kernel, dim3(1), dim3(1024), 0, s, rays, (int)N, (int32_t*)order_scratch);
         p.order = (const int32_t*)order_scratch;
+    }
+    if (slots && ACN_SPLIT_ROUTED && order_scratch && order_bytes >= split_bytes(N)) {
+        // split: single-expert rays through render_single_kernel, the rest through render_slots_kernel
+        int32_t* code = (int32_t*)order_scratch;
+        int32_t* list = code + N;
+        int32_t* multi = list + N + 16 * kMaxK;
+        int32_t* hdr = multi + N;
+        const int64_t cwg = (N + 3) / 4;
+        const dim3 cgrid((unsigned)(cwg < 4 * num_cus() ? cwg : 4 * num_cus()));
+        if (cfg.routing == 1) hipLaunchKernelGGL((ray_class_kernel<1>), cgrid, dim3(256), 0, s, cfg, p, code);
+        else hipLaunchKernelGGL((ray_class_kernel<2>), cgrid, dim3(256), 0, s, cfg, p, code);
+        hipLaunchKernelGGL(ray_lists_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)code, N, K, list, multi, hdr);
+        int64_t swgs = (N + 15) / 16;
+        if ((num_cus() & 7) == 0) swgs = (swgs + 7) & ~(int64_t)7;
+        const dim3 sgrid((unsigned)(swgs < num_cus() ? swgs : num_cus()));
+        if (interp == 1) hipLaunchKernelGGL(render_single_kernel<1>, sgrid, block, 0, s, cfg, b, p, list, hdr);
+        else if (interp == 0) hipLaunchKernelGGL(render_single_kernel<0>, sgrid, block, 0, s, cfg, b, p, list, hdr);
+        else hipLaunchKernelGGL(render_single_kernel<2>, sgrid, block, 0, s, cfg, b, p, list, hdr);
+        RenderParams pm = p;
+        pm.order = multi;
+        pm.norder = hdr + K + 1;
+#define ACN_MULTI_LAUNCH(I, R) hipLaunchKernelGGL((render_slots_kernel<I, R>), grid, dim3(ACN_SLOTS_THREADS), 0, s, cfg, b, pm)
+        if (cfg.routing == 1) {
+            if (interp == 1) ACN_MULTI_LAUNCH(1, 1); else if (interp == 0) ACN_MULTI_LAUNCH(0, 1); else ACN_MULTI_LAUNCH(2, 1);
+        } else {
+            if (interp == 1) ACN_MULTI_LAUNCH(1, 2); else if (interp == 0) ACN_MULTI_LAUNCH(0, 2); else ACN_MULTI_LAUNCH(2, 2);
+        }
+#undef ACN_MULTI_LAUNCH
+        return acn_check_launch("acn_render_stratified_fwd");
     }
 #define ACN_RENDER_LAUNCH(I, KL, R)                                                                    \
     do {                                                                                              \

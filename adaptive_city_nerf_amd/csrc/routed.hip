@@ -88,8 +88,10 @@ __global__ void __launch_bounds__(kBlk) routed_count_kernel(const float* __restr
 }
 
 // one workgroup: per expert, exclusive scan of the block counts (in place) and the segment starts
+// cap > 0: fixed layout -- expert k's segment is [k cap, (k + 1) cap) whatever the counts (cap >= M, so no
+// segment can overflow): the expert-parallel send buffer, grouped by owner, with host-known split sizes
 __global__ void __launch_bounds__(1024) routed_scan_kernel(int32_t* __restrict__ blk_cnt, int64_t nblk, int K,
-                                                           int align, int64_t* __restrict__ starts) {
+                                                           int align, int64_t cap, int64_t* __restrict__ starts) {
     // all K experts' scans at once: per-thread chunk sums, an inclusive wave scan (shuffles, no
     // barriers), then the 16 wave totals through LDS (one barrier) -- integer sums, so the result equals
     // the serial prefix sums exactly (a Hillis-Steele pass per expert cost 20 barriers each)
@@ -132,11 +134,11 @@ __global__ void __launch_bounds__(1024) routed_scan_kernel(int32_t* __restrict__
         for (int k = 0; k < K; ++k) {
             int64_t total = 0;
             for (int i = 0; i < 16; ++i) total += wtot[i][k];
-            starts[k] = base;
+            starts[k] = cap > 0 ? k * cap : base;
             starts[K + 1 + k] = total;                        // real pair count of expert k
             base += (total + align - 1) / align * align;      // segment padded to a multiple of align
         }
-        starts[K] = base;
+        starts[K] = cap > 0 ? K * cap : base;
     }
 }
 
@@ -282,6 +284,102 @@ __global__ void __launch_bounds__(256) xd_unit_sh_kernel(const float* __restrict
 
 unsigned blocks_for(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
 
+// ---- expert-parallel exchange (expert_parallel.ExpertParallelAdaptStep).  Sender: pairs in the fixed
+// layout of acn_routed_count_fixed; slots past a segment's live count get pidx -1, pw 0.
+__global__ void __launch_bounds__(256) pad_pairs_kernel(const int64_t* __restrict__ seg, int K, int32_t* __restrict__ pidx,
+                                                        float* __restrict__ pw) {
+    const int k = blockIdx.y;
+    const int64_t p0 = seg[k] + seg[K + 1 + k], p1 = seg[k + 1];
+    for (int64_t p = p0 + (int64_t)blockIdx.x * 256 + threadIdx.x; p < p1; p += (int64_t)gridDim.x * 256) {
+        pidx[p] = -1;
+        pw[p] = 0.0f;
+    }
+}
+
+// Owner: the received layout is [src s][local expert j][cap] records with live counts cnt[s][j]; the compact
+// pair list holds local expert j's records in (s, i) order in a segment padded to `align`.  One thread:
+// off[s][j] = sum_{s' < s} cnt[s'][j], seg[j] (padded starts), seg[E] = slots, seg[E + 1 + j] = live count.
+__global__ void ep_seg_kernel(const int64_t* __restrict__ cnt, int W, int E, int align, int64_t* __restrict__ off,
+                              int64_t* __restrict__ seg) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    int64_t base = 0;
+    for (int j = 0; j < E; ++j) {
+        int64_t run = 0;
+        for (int s = 0; s < W; ++s) {
+            off[(int64_t)s * E + j] = run;
+            run += cnt[(int64_t)s * E + j];
+        }
+        seg[j] = base;
+        seg[E + 1 + j] = run;
+        base += (run + align - 1) / align * align;
+    }
+    seg[E] = base;
+}
+
+// per compact slot p < seg[E]: (s, i) of its record, x01 in the expert's unit box + SH-4 (as
+// routed_scatter_kernel<0>), pk = j, pflag = 0 (pair) / -1 (padding), back = received-layout index or -1
+__global__ void __launch_bounds__(256) ep_gather_kernel(const float* __restrict__ xd, const int64_t* __restrict__ cnt,
+                                                        const int64_t* __restrict__ off, const int64_t* __restrict__ seg,
+                                                        int W, int E, int64_t cap, BoxCfg box, float* __restrict__ x01,
+                                                        float* __restrict__ sh_out, int32_t* __restrict__ pk,
+                                                        int32_t* __restrict__ pflag, int64_t* __restrict__ back) {
+    const int64_t total = seg[E];
+    for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < total; p += (int64_t)gridDim.x * 256) {
+        int j = 0;
+        while (j + 1 < E && seg[j + 1] <= p) ++j;
+        const int64_t q = p - seg[j];
+        pk[p] = j;
+        if (q >= seg[E + 1 + j]) {  // padding of segment j
+            pflag[p] = -1;
+            back[p] = -1;
+            x01[3 * p] = x01[3 * p + 1] = x01[3 * p + 2] = 0.5f;
+            float4* o4 = reinterpret_cast<float4*>(sh_out + p * 16);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) o4[c] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            continue;
+        }
+        int s = 0;
+        while (s + 1 < W && off[(int64_t)(s + 1) * E + j] <= q) ++s;
+        const int64_t i = q - off[(int64_t)s * E + j];
+        const int64_t src = ((int64_t)s * E + j) * cap + i;
+        const float* r = xd + src * 6;
+        pflag[p] = 0;
+        back[p] = src;
+        x01[3 * p + 0] = clamp_nan((r[0] - box.amin[j][0]) / box.ext[j][0], box.lo, box.hi);
+        x01[3 * p + 1] = clamp_nan((r[1] - box.amin[j][1]) / box.ext[j][1], box.lo, box.hi);
+        x01[3 * p + 2] = clamp_nan((r[2] - box.amin[j][2]) / box.ext[j][2], box.lo, box.hi);
+        float sh[16];
+        dir_sh(r[3], r[4], r[5], sh);
+        float4* o4 = reinterpret_cast<float4*>(sh_out + p * 16);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) o4[c] = make_float4(sh[4 * c], sh[4 * c + 1], sh[4 * c + 2], sh[4 * c + 3]);
+    }
+}
+
+// owner: field outputs of the compact slots back to the received layout (-> the senders' pair slots)
+__global__ void __launch_bounds__(256) ep_scatter_back_kernel(const float4* __restrict__ out, const int64_t* __restrict__ back,
+                                                              const int64_t* __restrict__ seg, int E,
+                                                              float4* __restrict__ ret) {
+    const int64_t total = seg[E];
+    for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < total; p += (int64_t)gridDim.x * 256) {
+        const int64_t b = back[p];
+        if (b >= 0) ret[b] = out[p];
+    }
+}
+
+// owner: the senders' dL/d(rgb, sigma) of the received layout -> the compact slots (0 on padding)
+__global__ void __launch_bounds__(256) ep_gather_grad_kernel(const float4* __restrict__ gy, const int64_t* __restrict__ back,
+                                                             const int64_t* __restrict__ seg, int E,
+                                                             float4* __restrict__ gout) {
+    const int64_t total = seg[E];
+    for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < total; p += (int64_t)gridDim.x * 256) {
+        const int64_t b = back[p];
+        gout[p] = b >= 0 ? gy[b] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+}
+
+constexpr unsigned kEpBlocks = 1024;  // fixed grids (graph-replayable): they stride to the device slot count
+
 }  // namespace
 
 extern "C" size_t acn_routed_workspace_bytes(int64_t M, int K) {
@@ -316,8 +414,39 @@ extern "C" int acn_routed_count(const float* rays, int64_t N, int S, const float
     const int64_t nblk = (M + kBlk - 1) / kBlk;
     hipLaunchKernelGGL(routed_count_kernel, dim3(blocks_for(M, kBlk)), dim3(kBlk), 0, s, rays, N, S, jitter, cfg, t_vals,
                        W, blk);
-    hipLaunchKernelGGL(routed_scan_kernel, dim3(1), dim3(1024), 0, s, blk, nblk, K, align, starts);
+    hipLaunchKernelGGL(routed_scan_kernel, dim3(1), dim3(1024), 0, s, blk, nblk, K, align, (int64_t)0, starts);
     return acn_check_launch("acn_routed_count");
+}
+
+extern "C" int acn_routed_count_fixed(const float* rays, int64_t N, int S, const float* jitter,
+                                      const acn_routing* routing, int64_t cap, float* t_vals, int64_t* starts,
+                                      void* workspace, size_t workspace_bytes, void* stream) {
+    ACN_REQUIRE(N >= 0 && S >= 1 && routing && starts, "acn_routed_count_fixed: bad arguments");
+    const int K = routing->K;
+    ACN_REQUIRE(K >= 1 && K <= kMaxK, "acn_routed_count_fixed: K = %d outside [1, %d]", K, kMaxK);
+    const int64_t M = N * (int64_t)S;
+    ACN_REQUIRE(cap >= M && cap >= 1, "acn_routed_count_fixed: capacity %lld below the %lld samples (a segment could "
+                "overflow)", (long long)cap, (long long)M);
+    ACN_REQUIRE(workspace && workspace_bytes >= acn_routed_workspace_bytes(M, K),
+                "acn_routed_count_fixed: workspace too small");
+    hipStream_t s = (hipStream_t)stream;
+    RouteCfg cfg{};
+    cfg.K = K;
+    cfg.cluster_2d = routing->cluster_2d;
+    cfg.bm = routing->boundary_margin;
+    cfg.routing = routing->boundary_margin > 1.0f ? 1 : 2;
+    for (int k = 0; k < K; ++k)
+        for (int a = 0; a < 3; ++a) cfg.cent[k][a] = routing->centroids[k][a];
+    float* W = (float*)workspace;
+    int32_t* blk = (int32_t*)(W + M * K);
+    const int64_t nblk = (M + kBlk - 1) / kBlk;
+    if (M > 0) {
+        ACN_REQUIRE(rays && t_vals, "acn_routed_count_fixed: NULL pointer");
+        hipLaunchKernelGGL(routed_count_kernel, dim3(blocks_for(M, kBlk)), dim3(kBlk), 0, s, rays, N, S, jitter, cfg,
+                           t_vals, W, blk);
+    }
+    hipLaunchKernelGGL(routed_scan_kernel, dim3(1), dim3(1024), 0, s, blk, nblk, K, 1, cap, starts);
+    return acn_check_launch("acn_routed_count_fixed");
 }
 
 extern "C" int acn_routed_scatter(const float* rays, int64_t N, int S, int K, const float* t_vals,
@@ -392,4 +521,54 @@ extern "C" int acn_xd_unit_sh(const float* xd, int64_t P, const float* aabb_min,
                        make_float3(aabb_min[0], aabb_min[1], aabb_min[2]),
                        make_float3(aabb_extent[0], aabb_extent[1], aabb_extent[2]), lo, hi, x01, sh);
     return acn_check_launch("acn_xd_unit_sh");
+}
+
+extern "C" int acn_routed_pad_pairs(const int64_t* seg, int K, int64_t max_pad, int32_t* pidx, float* pw, void* stream) {
+    ACN_REQUIRE(seg && pidx && pw && K >= 1 && K <= kMaxK && max_pad >= 0, "acn_routed_pad_pairs: bad arguments");
+    if (max_pad == 0) return ACN_OK;
+    hipLaunchKernelGGL(pad_pairs_kernel, dim3(blocks_for(max_pad, 256) < 256 ? blocks_for(max_pad, 256) : 256, K),
+                       dim3(256), 0, (hipStream_t)stream, seg, K, pidx, pw);
+    return acn_check_launch("acn_routed_pad_pairs");
+}
+
+extern "C" size_t acn_ep_workspace_bytes(int W, int E) { return (size_t)W * (size_t)E * sizeof(int64_t); }
+
+extern "C" int acn_ep_gather(const float* recv_xd, const int64_t* recv_cnt, int W, int E, int64_t cap, int align,
+                             const float* aabb_min, const float* aabb_extent, float lo, float hi, int64_t* seg,
+                             void* workspace, float* x01, float* sh, int32_t* pk, int32_t* pflag, int64_t* back,
+                             void* stream) {
+    ACN_REQUIRE(W >= 1 && E >= 1 && E <= kMaxK && cap >= 1 && align >= 1 && aabb_min && aabb_extent,
+                "acn_ep_gather: bad arguments");
+    ACN_REQUIRE(recv_xd && recv_cnt && seg && workspace && x01 && sh && pk && pflag && back,
+                "acn_ep_gather: NULL pointer");
+    BoxCfg box{};
+    for (int j = 0; j < E; ++j)
+        for (int a = 0; a < 3; ++a) {
+            box.amin[j][a] = aabb_min[3 * j + a];
+            box.ext[j][a] = aabb_extent[3 * j + a];
+        }
+    box.lo = lo;
+    box.hi = hi;
+    hipStream_t s = (hipStream_t)stream;
+    int64_t* off = (int64_t*)workspace;
+    hipLaunchKernelGGL(ep_seg_kernel, dim3(1), dim3(64), 0, s, recv_cnt, W, E, align, off, seg);
+    hipLaunchKernelGGL(ep_gather_kernel, dim3(kEpBlocks), dim3(256), 0, s, recv_xd, recv_cnt, (const int64_t*)off,
+                       (const int64_t*)seg, W, E, cap, box, x01, sh, pk, pflag, back);
+    return acn_check_launch("acn_ep_gather");
+}
+
+extern "C" int acn_ep_scatter_back(const float* out, const int64_t* back, const int64_t* seg, int E, float* ret,
+                                   void* stream) {
+    ACN_REQUIRE(out && back && seg && ret && E >= 1 && E <= kMaxK, "acn_ep_scatter_back: bad arguments");
+    hipLaunchKernelGGL(ep_scatter_back_kernel, dim3(kEpBlocks), dim3(256), 0, (hipStream_t)stream, (const float4*)out,
+                       back, seg, E, (float4*)ret);
+    return acn_check_launch("acn_ep_scatter_back");
+}
+
+extern "C" int acn_ep_gather_grad(const float* gy, const int64_t* back, const int64_t* seg, int E, float* gout,
+                                  void* stream) {
+    ACN_REQUIRE(gy && back && seg && gout && E >= 1 && E <= kMaxK, "acn_ep_gather_grad: bad arguments");
+    hipLaunchKernelGGL(ep_gather_grad_kernel, dim3(kEpBlocks), dim3(256), 0, (hipStream_t)stream, (const float4*)gy,
+                       back, seg, E, (float4*)gout);
+    return acn_check_launch("acn_ep_gather_grad");
 }

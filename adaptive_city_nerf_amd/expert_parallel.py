@@ -255,3 +255,334 @@ def render_image_expert_parallel(model, *, H: int, W: int, fx: float, fy: float,
         sse, cnt = local_sse(rgb_img.view(-1, 3)[idx], gt_srgb.to(rgb_img.device).view(-1, 3)[idx], metrics_space)
         psnr = psnr_reduce(sse, cnt, rgb_img.device, group)
     return rgb_img, full[:, 3], full[:, 4], psnr
+
+
+# ============================================================================ sync-free expert-parallel step
+class _Comm:
+    """The step's collectives on device buffers of host-known constant sizes (no count exchange on the
+    host): RCCL directly (``nccl`` backend), ``gloo`` through staged host copies (the multi-process tests of
+    this same exchange code on one GPU or on CPU-only hosts), plain copies at world size 1."""
+
+    def __init__(self, group=None):
+        self.world, self.rank = world_rank(group)
+        self.group = group
+        self.staged = self.world > 1 and dist.get_backend(group) == "gloo"
+
+    def all_to_all(self, out: Tensor, inp: Tensor, out_splits: Sequence[int], in_splits: Sequence[int]) -> None:
+        if self.world == 1:
+            out.copy_(inp)
+        elif self.staged:
+            oc = torch.empty(out.shape, dtype=out.dtype)
+            dist.all_to_all_single(oc, inp.cpu(), list(out_splits), list(in_splits), group=self.group)
+            out.copy_(oc)
+        else:
+            dist.all_to_all_single(out, inp, list(out_splits), list(in_splits), group=self.group)
+
+    def all_reduce(self, t: Tensor) -> None:
+        if self.world == 1:
+            return
+        if self.staged:
+            c = t.cpu()
+            dist.all_reduce(c, group=self.group)
+            t.copy_(c)
+        else:
+            dist.all_reduce(t, group=self.group)
+
+
+class ExpertParallelAdaptStep:
+    """runtime_adapt's update of the routed container (runtime_adapt.py:286-309, active_module None) with
+    the experts distributed over the ranks of ``group`` -- expert k on rank expert_owner(K, W)[k] -- and no
+    host synchronisation: every exchange has a constant size, so a step is a fixed sequence of launches and
+    collectives that a HIP graph can hold (at world size 1 the exchanges are copies and ``graph=True``
+    captures the step after ``warmup`` eager real steps; at W > 1 the RCCL collectives run eagerly by default,
+    ``graph=True`` opts in to capturing them as well).
+
+    Per step, on every rank:
+      sender  rays (this rank's shard) -> t, routing, (sample, expert) pairs in the FIXED layout of
+              acn_routed_count_fixed (expert k at [k C, (k+1) C), C = n_rays * S >= any expert's count) as
+              24-B xd records -- grouped by owner, so the pair buffer is the all-to-all send buffer
+      a2a #0  the per-expert live counts (int64) to the owners;  a2a #1 the xd records (constant splits)
+      owner   acn_ep_gather: compact per-expert pair lists (padded to 128) -> hash grid + fused MLP of its
+              experts -> acn_ep_scatter_back into the received layout
+      a2a #2  (rgb, sigma) back to the senders, at their pairs' slots -> blend (expert order) + background +
+              compositing + loss (scaled by n / N_global: the global mean)
+      a2a #3  dL/d(rgb, sigma) back to the owners -> fused MLP backward + table scatter of the owned experts;
+              the background head's gradients all-reduced (sum over the ranks' rays)
+      update  optim.SlottedAdam over the owned experts (an expert no rank routed a sample to is skipped, as
+              torch skips grad None) + the replicated head; clip norm = all-reduced owned part + the head once.
+    ``n_rays_global``: the batch the loss averages over -- W * n (weak: every rank streams its own batches) or
+    the reference's batch split over the ranks (strong: each rank holds n = N / W of one runtime_adapt batch,
+    and the update is exactly that batch's).  Reference: models/inr/meta_container.py:300-337."""
+
+    def __init__(self, P, model, n_rays: int, optimizer: FusedAdam, n_rays_global: Optional[int] = None,
+                 grad_clip: Optional[float] = 1.0, group=None, graph: bool = False, warmup: int = 1,
+                 jitter: str = "draw", clear_in_adam: bool = True, max_steps: int = 1 << 16):
+        import ctypes as C
+        import numpy as np
+        from . import _lib, ops
+        from ._lib import AcnError, acn_mlp
+        from .meta_container import MetaContainer
+        from .optim import NORM_ELSEWHERE_FLAG, ZERO_GRAD_FLAG, FusedAdam, SlottedAdam
+        from .routed_train import ALIGN, FUSED_BACKGROUND, TELESCOPED_TABLE_NORM
+        if not isinstance(model, MetaContainer) or not all(s._fusable for s in model.submodules):
+            raise AcnError("ExpertParallelAdaptStep: a MetaContainer of reference-configuration experts is required")
+        if not isinstance(optimizer, FusedAdam):
+            raise AcnError("ExpertParallelAdaptStep needs FusedAdam")
+        if not model.use_bg_nerf:
+            raise AcnError("ExpertParallelAdaptStep: the background head is part of the reference configuration")
+        encs = [s.xyz_encoder for s in model.submodules]
+        e0 = encs[0]
+        if any(e._res_host != e0._res_host or e.log2_hashmap_size != e0.log2_hashmap_size
+               or e._interp_code != e0._interp_code for e in encs) or e0._interp_code == 0:
+            raise AcnError("ExpertParallelAdaptStep: experts must share one Linear/Smoothstep hash-grid configuration")
+        self.comm = comm = _Comm(group)
+        W, rank = comm.world, comm.rank
+        self.P, self.model, self.opt, self.grad_clip = P, model, optimizer, grad_clip
+        self.mlp_precision = ops.TRAIN_MLP_PRECISION   # training MLP kernels (ops.set_train_mlp_precision)
+        self.jitter_mode = jitter
+        self.clear_in_adam = bool(clear_in_adam)
+        self.tele = TELESCOPED_TABLE_NORM and grad_clip is not None
+        dev = e0.hash_table.device
+        self.device = dev
+        K = len(model.submodules)
+        owner = expert_owner(K, W)
+        own = [k for k in range(K) if owner[k] == rank]
+        if not own:
+            raise AcnError(f"ExpertParallelAdaptStep: rank {rank} owns no expert (K = {K} < W = {W})")
+        E = len(own)
+        eo = [owner.count(o) for o in range(W)]      # experts per owner (contiguous blocks)
+        S, N = int(P.ray_samples), int(n_rays)
+        M = N * S
+        Cc = M                                          # capacity of one (sender, expert) segment
+        self.K, self.E, self.W, self.N, self.S, self.M, self.C = K, E, W, N, S, M, Cc
+        self.own, self.eo = own, eo
+        self.n_global = int(n_rays_global) if n_rays_global is not None else N * W
+        # splits (rows): sender -> owner o: its experts' segments; owner <- every sender: E segments
+        self.split_send = [e * Cc for e in eo]
+        self.split_recv = [E * Cc] * W
+        self.split_cnt_send, self.split_cnt_recv = list(eo), [E] * W
+        f32 = dict(device=dev, dtype=torch.float32)
+        i32 = dict(device=dev, dtype=torch.int32)
+        i64 = dict(device=dev, dtype=torch.int64)
+        L = _lib.lib()
+        # ---- sender buffers
+        self.rays = torch.zeros(N, 8, **f32)
+        self.rgbs = torch.zeros(N, 3, **f32)
+        self.u = torch.zeros(N, S, **f32)
+        self.t = torch.empty(N, S, **f32)
+        self.seg = torch.zeros(2 * K + 1, **i64)
+        self.rws = torch.empty(int(L.acn_routed_workspace_bytes(M, K)), device=dev, dtype=torch.uint8)
+        self.pidx = torch.empty(K * Cc, **i32)
+        self.pw = torch.empty(K * Cc, **f32)
+        self.pk = torch.empty(K * Cc, **i32)
+        self.xd = torch.empty(K * Cc, 6, **f32)
+        self.pmap = torch.empty(M, K, **i32)
+        self.yr = torch.empty(K * Cc, 4, **f32)         # (rgb, sigma) of this rank's pairs, from the owners
+        self.rgbs_dirs = torch.zeros(N, 3, **f32)
+        # ---- owner buffers
+        R = W * E * Cc                                   # received records
+        cap = R + E * ALIGN                              # compact slots (segments padded to ALIGN)
+        self.recv_cnt = torch.zeros(W * E, **i64)
+        self.recv_xd = torch.empty(R, 6, **f32)
+        self.eseg = torch.zeros(2 * E + 1, **i64)
+        self.ews = torch.empty(int(L.acn_ep_workspace_bytes(W, E)), device=dev, dtype=torch.uint8)
+        self.x01 = torch.empty(cap, 3, **f32)
+        self.sh = torch.empty(cap, 16, **f32)
+        self.pkl = torch.empty(cap, **i32)
+        self.pflag = torch.empty(cap, **i32)
+        self.back = torch.empty(cap, **i64)
+        self.h0 = torch.empty(cap, 32, **f32)
+        self.out = torch.empty(cap, 4, **f32)
+        self.gh0 = torch.empty(cap, 32, **f32)
+        self.gout = torch.empty(cap, 4, **f32)
+        self.ret = torch.zeros(R, 4, **f32)
+        self.recv_gy = torch.empty(R, 4, **f32)
+        self.mws = torch.empty(int(ops.mlp_fn("acn_mlp_pairs_workspace_bytes", self.mlp_precision)(E)), device=dev,
+                               dtype=torch.uint8)
+        self.dw = torch.zeros(E, ops.MLP_DW_FLOATS, **f32)
+        self.loss = torch.zeros((), **f32)
+        self.loss_global = torch.zeros(1, **f32)
+        # ---- persistent gradients of the owned experts and the (replicated) background head
+        self.gtables = [torch.zeros_like(encs[k].hash_table) for k in own]
+        self.bg_params = list(model.bg_mlp.parameters())
+        nbg = sum(p.numel() for p in self.bg_params)
+        self.gbg_flat = torch.zeros(nbg, **f32)
+        self.gbg, o = [], 0
+        for p in self.bg_params:
+            self.gbg.append(self.gbg_flat[o:o + p.numel()].view_as(p))
+            o += p.numel()
+        try:
+            self.bg_spec, self._bg_keep = model.background_spec() if FUSED_BACKGROUND else (None, None)
+        except AcnError:
+            self.bg_spec, self._bg_keep = None, None
+        slot_of, zero_of = {}, set()
+        for j, k in enumerate(own):
+            sub = model.submodules[k]
+            sub.xyz_encoder.hash_table.grad = self.gtables[j]
+            slot_of[id(sub.xyz_encoder.hash_table)] = j
+            zero_of.add(id(sub.xyz_encoder.hash_table))
+            views, off = [], 0
+            for shp in ops.MLP_DW_SHAPES:
+                n = int(np.prod(shp))
+                views.append(self.dw[j, off:off + n].view(shp))
+                off += n
+            for (name, t), g in zip(sub._mlp_tensors(None).items(), views):
+                t.grad = g
+                slot_of[id(t)] = j
+        for p, g in zip(self.bg_params, self.gbg):
+            p.grad = g
+            slot_of[id(p)] = E
+        self._mlp_structs = [ops._mlp_struct([t for t in model.submodules[k]._mlp_tensors(None).values()]) for k in own]
+        self._mlp_ptrs = (C.POINTER(acn_mlp) * E)(*[C.pointer(w) for w in self._mlp_structs])
+        self._tables = (C.c_void_p * E)(*[encs[k].hash_table.data_ptr() for k in own])
+        self._gtables = (C.c_void_p * E)(*[g.data_ptr() for g in self.gtables])
+        self._res = (C.c_int32 * len(e0._res_host))(*e0._res_host)
+        boxes = [model.submodules[k]._host_box() for k in own]
+        self._mins = (C.c_float * (3 * E))(*[float(v) for b in boxes for v in b[0]])
+        self._exts = (C.c_float * (3 * E))(*[float(v) for b in boxes for v in b[1]])
+        lo = np.float32(1e-6)
+        self._lo, self._hi = C.c_float(lo), C.c_float(np.float32(1.0) - lo)
+        self.routing = model.routing_spec()
+        grads = {i: None for i in slot_of}
+        for p in model.parameters():
+            if id(p) in slot_of:
+                grads[id(p)] = p.grad
+        flags = {i: (ZERO_GRAD_FLAG if self.clear_in_adam else 0) | (NORM_ELSEWHERE_FLAG if self.tele else 0)
+                 for i in zero_of}
+        self.adam = SlottedAdam(optimizer, slot_of, grads, E, E + 1, flags, max_steps=max_steps, split_norm=W > 1)
+        self.table_sumsq = torch.zeros(1, device=dev, dtype=torch.float64)
+        self._params = [r[0] for r in self.adam.rows]
+        self.replays = 0
+        self.steps_done = 0
+        self.graph = None
+        self._eager_left = max(1, int(warmup)) if graph else 0
+
+    def _step(self, n: int) -> None:
+        import ctypes as C
+        from . import _lib, ops
+        from ._lib import check, ptr
+        from .ray_rendering import volume_render
+        from .routed_train import ALIGN, JITTER
+        from .train import mse_color_loss
+        L = _lib.lib()
+        dev, K, E, S, Cc, comm = self.device, self.K, self.E, self.S, self.C, self.comm
+        s = int(torch.cuda.current_stream(dev).cuda_stream)
+        M = n * S
+        if not self.clear_in_adam:
+            for g in self.gtables:
+                g.zero_()
+        u, t = self.u[:n], self.t[:n]
+        if self.jitter_mode == "draw":
+            u.copy_(JITTER(n, S, dev))   # the reference's rand_like(low) draw
+        # sender: pairs in the fixed owner-grouped layout
+        check(L.acn_routed_count_fixed(ptr(self.rays), n, S, ptr(u), C.byref(self.routing), Cc, ptr(t), ptr(self.seg),
+                                       ptr(self.rws), self.rws.numel(), s), "acn_routed_count_fixed")
+        check(L.acn_routed_scatter_xd(ptr(self.rays), n, S, K, ptr(t), ptr(self.seg), ptr(self.rws), ptr(self.pidx),
+                                      ptr(self.pw), ptr(self.xd), ptr(self.pmap), ptr(self.pk), s),
+              "acn_routed_scatter_xd")
+        check(L.acn_routed_pad_pairs(ptr(self.seg), K, Cc, ptr(self.pidx), ptr(self.pw), s), "acn_routed_pad_pairs")
+        comm.all_to_all(self.recv_cnt, self.seg[K + 1:], self.split_cnt_recv, self.split_cnt_send)
+        comm.all_to_all(self.recv_xd, self.xd, self.split_recv, self.split_send)
+        # owner: compact pair lists of the owned experts, field, results back into the received layout
+        check(L.acn_ep_gather(ptr(self.recv_xd), ptr(self.recv_cnt), self.W, E, Cc, ALIGN,
+                              C.cast(self._mins, C.c_void_p), C.cast(self._exts, C.c_void_p), self._lo, self._hi,
+                              ptr(self.eseg), ptr(self.ews), ptr(self.x01), ptr(self.sh), ptr(self.pkl),
+                              ptr(self.pflag), ptr(self.back), s), "acn_ep_gather")
+        enc = self.model.submodules[self.own[0]].xyz_encoder
+        check(L.acn_hashgrid_fwd_pairs(ptr(self.x01), ptr(self.pkl), ptr(self.eseg), E, self._tables, self._res,
+                                       len(enc._res_host), enc.log2_hashmap_size, enc._interp_code, ptr(self.h0), s),
+              "acn_hashgrid_fwd_pairs")
+        mfn = lambda name: ops.mlp_fn(name, self.mlp_precision)  # noqa: E731
+        check(mfn("acn_mlp_pack_pairs")(self._mlp_ptrs, E, ptr(self.mws), s), "acn_mlp_pack_pairs")
+        check(mfn("acn_mlp_train_fwd_pairs")(ptr(self.h0), ptr(self.sh), ptr(self.eseg), E, ptr(self.mws), ptr(self.out), s),
+              "acn_mlp_train_fwd_pairs")
+        check(L.acn_ep_scatter_back(ptr(self.out), ptr(self.back), ptr(self.eseg), E, ptr(self.ret), s),
+              "acn_ep_scatter_back")
+        comm.all_to_all(self.yr, self.ret, self.split_send, self.split_recv)
+        # sender: blend, background, compositing, loss (the global batch mean), their gradients
+        rs = ops.routed_blend_fwd(self.yr, self.pw, self.pmap[:M]).view(n, S, 4).requires_grad_(True)
+        rays, rgbs, dirs = self.rays[:n], self.rgbs[:n], self.rgbs_dirs[:n]
+        frac = float(n) / float(self.n_global)
+        if self.bg_spec is not None:
+            dirs.copy_(rays[:, 3:6])
+            bg = ops.background_fwd(dirs, self.bg_spec).requires_grad_(True)
+            with torch.enable_grad():
+                rgb = volume_render(rs, t, bg_rgb=bg)[0]
+                loss = mse_color_loss(rgb, rgbs, self.P.color_space) * frac
+                g_rs, g_bg = torch.autograd.grad(loss, [rs, bg])
+            ops.background_bwd(dirs, self.bg_spec, g_bg, self.gbg)
+        else:
+            with torch.enable_grad():
+                bg = self.model.background_color(rays[:, 3:6])
+                rgb = volume_render(rs, t, bg_rgb=bg)[0]
+                loss = mse_color_loss(rgb, rgbs, self.P.color_space) * frac
+                grads = torch.autograd.grad(loss, [rs] + self.bg_params)
+            g_rs = grads[0]
+            for g, buf in zip(grads[1:], self.gbg):
+                buf.copy_(g)
+        self.loss.copy_(loss.detach())
+        comm.all_reduce(self.gbg_flat)
+        gy = ops.routed_blend_bwd(g_rs.reshape(M, 4).contiguous(), self.pidx, self.pw)
+        comm.all_to_all(self.recv_gy, gy, self.split_recv, self.split_send)
+        # owner: backward of the owned experts
+        check(L.acn_ep_gather_grad(ptr(self.recv_gy), ptr(self.back), ptr(self.eseg), E, ptr(self.gout), s),
+              "acn_ep_gather_grad")
+        check(mfn("acn_mlp_train_bwd_dw_pairs")(ptr(self.h0), ptr(self.sh), ptr(self.out), ptr(self.gout), ptr(self.eseg), E,
+                                           ptr(self.mws), ptr(self.dw), ptr(self.gh0), s), "acn_mlp_train_bwd_dw_pairs")
+        check(L.acn_hashgrid_bwd_pairs_sumsq(ptr(self.x01), ptr(self.pkl), ptr(self.pflag), ptr(self.eseg), E,
+                                             ptr(self.gh0), self._gtables, self._res, len(enc._res_host),
+                                             enc.log2_hashmap_size, enc._interp_code,
+                                             ptr(self.table_sumsq) if self.tele else None, s),
+              "acn_hashgrid_bwd_pairs_sumsq")
+        from . import routed_train as RT
+        self.adam.step(self.eseg, self.grad_clip, self.table_sumsq if self.tele else None,
+                       hook=RT.EVENT_HOOK if self.graph is None else None,
+                       allreduce=comm.all_reduce if self.W > 1 else None)
+        self.loss_global.copy_(self.loss.view(1))
+        comm.all_reduce(self.loss_global)
+
+    def _capture(self) -> None:
+        dev = self.device
+        torch.cuda.synchronize(dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._step(self.N)
+        torch.cuda.synchronize(dev)
+        self.graph = g
+
+    def __call__(self, rays: Tensor, rgbs: Tensor, jitter_u: Optional[Tensor] = None) -> Tensor:
+        """One update on this rank's ``rays`` / ``rgbs`` (n <= n_rays); collective over the group.  Returns the
+        global loss (device, 1 element)."""
+        from ._lib import AcnError
+        from .optim import bump_versions
+        n = int(rays.shape[0])
+        if rays.dim() != 2 or rays.shape[1] != 8 or tuple(rgbs.shape) != (n, 3) or not 0 < n <= self.N:
+            raise AcnError(f"ExpertParallelAdaptStep was built for up to {self.N} rays per rank; got "
+                           f"{tuple(rays.shape)}, {tuple(rgbs.shape)}")
+        if self.adam.step0 + self.steps_done + 1 > self.adam.table_steps:
+            raise AcnError("ExpertParallelAdaptStep: the Adam constant table is exhausted; build a new step object")
+        self.rays[:n].copy_(rays, non_blocking=True)
+        self.rgbs[:n].copy_(rgbs, non_blocking=True)
+        if self.jitter_mode == "given":
+            if jitter_u is None or tuple(jitter_u.shape) != (n, self.S):
+                raise AcnError(f"ExpertParallelAdaptStep(jitter='given') needs jitter_u of shape ({n}, {self.S})")
+            self.u[:n].copy_(jitter_u, non_blocking=True)
+        if n == self.N and self.graph is not None:
+            self.graph.replay()
+            self.replays += 1
+        else:
+            self._step(n)
+            if n == self.N and self._eager_left > 0:
+                self._eager_left -= 1
+                if self._eager_left == 0:
+                    self._capture()
+        self.steps_done += 1
+        bump_versions(self._params)
+        return self.loss_global
+
+    @property
+    def last_norm(self) -> Tensor:
+        return self.adam.scale
+
+    def sync_state(self) -> None:
+        self.adam.sync_state()

@@ -457,12 +457,6 @@ class GraphedMetaStep:
         torch.cuda.synchronize(self.device)
         dev = self.device
         self.static = {}
-        for cid in self.cids:
-            ns, nq = self.shapes[cid]
-            self.static[cid] = {"support": {"rays": torch.zeros(ns, 8, device=dev), "rgbs": torch.zeros(ns, 3, device=dev)},
-                                "query": {"rays": torch.zeros(nq, 8, device=dev), "rgbs": torch.zeros(nq, 3, device=dev)},
-                                "wq": torch.zeros((), device=dev)}
-            self._load(cid, next(t for t in task_data[cid] if _task_shapes(t) == self.shapes[cid]))
         self.inner_acc = torch.zeros((), device=dev)
         self.q_acc = torch.zeros((), device=dev)
         K = len(model.submodules)
@@ -482,19 +476,32 @@ class GraphedMetaStep:
         # activity of the outer update: seg[K + 1 + k] > 0 <=> region k processed a task (SlottedAdam)
         self.act = torch.zeros(2 * K + 1, dtype=torch.int64, device=dev)
         self.act_host = torch.zeros(2 * K + 1, dtype=torch.int64).pin_memory()
-        pool = torch.cuda.graph_pool_handle()
+        self.pool = torch.cuda.graph_pool_handle()
         self.graphs = {}
         for cid in self.cids:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool):
-                self._task(cid)
-            self.graphs[cid] = g
+            self._add_region(cid, next(t for t in task_data[cid] if _task_shapes(t) == self.shapes[cid]))
         self.outer = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.outer, pool=pool):
+        with torch.cuda.graph(self.outer, pool=self.pool):
             self.adam.step(self.act, getattr(P, "grad_clip", 1.0))
         self.replays = 0
         self.eager_steps = 0
         torch._foreach_zero_(self.grads)
+
+    def _add_region(self, cid, task) -> None:
+        """Static buffers + the captured task graph of region ``cid`` at the shapes of ``task`` (capture runs
+        nothing; a region first seen after construction is added the same way)."""
+        dev = self.device
+        ns, nq = _task_shapes(task)
+        self.shapes[cid] = (ns, nq)
+        self.static[cid] = {"support": {"rays": torch.zeros(ns, 8, device=dev), "rgbs": torch.zeros(ns, 3, device=dev)},
+                            "query": {"rays": torch.zeros(nq, 8, device=dev), "rgbs": torch.zeros(nq, 3, device=dev)},
+                            "wq": torch.zeros((), device=dev)}
+        self._load(cid, task)
+        torch.cuda.synchronize(dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, pool=self.pool):
+            self._task(cid)
+        self.graphs[cid] = g
 
     def _load(self, cid, task) -> None:
         sup, qry = (task.support, task.query) if hasattr(task, "support") else (task["support"], task["query"])
@@ -526,13 +533,22 @@ class GraphedMetaStep:
         self.q_acc.add_(loss_q.detach() * nq)
 
     def _covers(self, task_data) -> bool:
+        """Every non-empty task has its region's captured shapes; a region seen for the first time (with one
+        task shape, of an expert of the container) gets its graph captured here."""
+        new_shape, new_task = {}, {}
         for cid, tasks in task_data.items():
             for t in tasks:
                 sh = _task_shapes(t)
                 if sh[0] == 0 or sh[1] == 0:
                     continue   # skipped, as the reference skips empty tasks
-                if self.shapes.get(cid) != sh:
+                want = self.shapes.get(cid, new_shape.get(cid))
+                if want is None and isinstance(cid, int) and 0 <= cid < self.K:
+                    new_shape[cid], new_task[cid] = sh, t
+                    want = sh
+                if want != sh:
                     return False
+        for cid, t in new_task.items():
+            self._add_region(cid, t)
         return True
 
     def _eager(self, step, task_data):

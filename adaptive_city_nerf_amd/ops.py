@@ -7,6 +7,7 @@ No CPU path exists: CPU tensors raise.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Dict, Optional, Sequence
 
 import torch
@@ -56,31 +57,41 @@ def hashgrid_fwd(x01: torch.Tensor, table: torch.Tensor, resolutions: Sequence[i
     return out.view(*x01.shape[:-1], L * F)
 
 
+# workspace cap of the deterministic hash-grid backward (~24 B x 8 x L per point, 3 GB at 1M points)
+DET_WS_CAP = 1 << 30
+
+
 def hashgrid_bwd(x01: torch.Tensor, grad_out: torch.Tensor, resolutions: Sequence[int], log2T: int, F: int,
                  interp: int, deterministic: Optional[bool] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Table gradient (scatter-add).  ``deterministic`` (default: torch.are_deterministic_algorithms_enabled())
     selects the sort-based backward (acn_hashgrid_bwd_det: bitwise reproducible, every row summed in point
     order) over the float-atomic one.  ``out``: an existing (L * 2^log2T, F) fp32 buffer the float-atomic
-    scatter adds into (accumulation; not with the deterministic backward)."""
+    scatter adds into (accumulation; the deterministic backward accumulates into it too, each row continuing
+    its serial sum).  The deterministic workspace (records + sort buffers, ~3 KB per point at L = 16) is
+    bounded by processing the points in chunks of at most DET_WS_CAP bytes: the kernel adds every row's
+    contributions, in point order, onto the row's current value, so consecutive chunks give exactly the
+    serial sum of one pass."""
     L = len(resolutions)
     x = _f32(x01).view(-1, 3)
     g = _f32(grad_out).view(-1, L * F)
     if out is not None:
-        if deterministic:
-            raise ValueError("hashgrid_bwd: out= accumulates with atomics; not available in deterministic mode")
         if tuple(out.shape) != (L << log2T, F) or out.dtype != torch.float32 or not out.is_contiguous():
             raise ValueError("hashgrid_bwd: out must be a contiguous fp32 (L * 2^log2T, F) buffer")
-        deterministic = False
     gt = out if out is not None else torch.zeros(L << log2T, F, device=x.device, dtype=torch.float32)
     res = (C.c_int32 * L)(*[int(r) for r in resolutions])
     if deterministic is None:
         deterministic = torch.are_deterministic_algorithms_enabled()
     if deterministic and F == 2:
         L_ = _lib.lib()
-        ws = torch.empty(max(int(L_.acn_hashgrid_bwd_det_workspace_bytes(x.shape[0], L, log2T, interp)), 1),
+        M = x.shape[0]
+        per = max(1, int(L_.acn_hashgrid_bwd_det_workspace_bytes(1 << 16, L, log2T, interp)) >> 16)
+        chunk = max(1, min(M, DET_WS_CAP // per))
+        ws = torch.empty(max(int(L_.acn_hashgrid_bwd_det_workspace_bytes(chunk, L, log2T, interp)), 1),
                          dtype=torch.uint8, device=x.device)
-        check(L_.acn_hashgrid_bwd_det(ptr(x), x.shape[0], ptr(g), res, L, log2T, F, interp, ptr(gt), ptr(ws), ws.numel(),
-                                      stream_of(x)), "acn_hashgrid_bwd_det")
+        for m0 in range(0, M, chunk):
+            n = min(chunk, M - m0)
+            check(L_.acn_hashgrid_bwd_det(ptr(x[m0:m0 + n]), n, ptr(g[m0:m0 + n]), res, L, log2T, F, interp, ptr(gt),
+                                          ptr(ws), ws.numel(), stream_of(x)), "acn_hashgrid_bwd_det")
         return gt
     check(_lib.lib().acn_hashgrid_bwd(ptr(x), x.shape[0], ptr(g), res, L, log2T, F, interp, ptr(gt),
                                       stream_of(x)), "acn_hashgrid_bwd")
@@ -499,7 +510,7 @@ MLP_GROUP = 2048
 
 
 def _mlp_ws(device):
-    return torch.empty(int(_lib.lib().acn_mlp_workspace_bytes()), dtype=torch.uint8, device=device)
+    return torch.empty(int(mlp_fn("acn_mlp_workspace_bytes")()), dtype=torch.uint8, device=device)
 
 
 def _fm_zeros(M: int, cols: int, device) -> torch.Tensor:
@@ -518,7 +529,7 @@ def mlp_train_fwd(h0: torch.Tensor, sh: torch.Tensor, ws: Sequence[torch.Tensor]
     out = torch.empty(M, 4, device=h0.device, dtype=torch.float32)
     sv = _fm_zeros(M, MLP_SAVE_COLS, h0.device) if save else None
     w = _mlp_struct(ws)
-    check(_lib.lib().acn_mlp_train_fwd(ptr(h0), ptr(sh), M, C.byref(w), ptr(out), ptr(sv) if save else None,
+    check(mlp_fn("acn_mlp_train_fwd")(ptr(h0), ptr(sh), M, C.byref(w), ptr(out), ptr(sv) if save else None,
                                        ptr(_mlp_ws(h0.device)), stream_of(h0)), "acn_mlp_train_fwd")
     return out, sv
 
@@ -529,7 +540,7 @@ def mlp_train_bwd(save: torch.Tensor, out: torch.Tensor, gout: torch.Tensor, ws:
     gs = _fm_zeros(M, MLP_GRAD_COLS, out.device)
     gh = torch.empty(M, 32, device=out.device, dtype=torch.float32) if want_h0 else None
     w = _mlp_struct(ws)
-    check(_lib.lib().acn_mlp_train_bwd(ptr(save), ptr(out), ptr(gout), M, C.byref(w), ptr(gs),
+    check(mlp_fn("acn_mlp_train_bwd")(ptr(save), ptr(out), ptr(gout), M, C.byref(w), ptr(gs),
                                        ptr(gh) if want_h0 else None, ptr(_mlp_ws(out.device)), stream_of(out)),
           "acn_mlp_train_bwd")
     return gs, gh
@@ -539,6 +550,24 @@ def mlp_train_bwd(save: torch.Tensor, out: torch.Tensor, gout: torch.Tensor, ws:
 MLP_DW_SHAPES = ((64, 32), (64,), (64, 64), (64,), (1, 64), (1,), (15, 64), (15,), (64, 31), (64,), (64, 64), (64,),
                  (3, 64), (3,))
 MLP_DW_FLOATS = 13715
+# Precision of the training MLP's layer products: "fp16x3" (default: the fp32-accurate 3-term fp16 split on
+# v_mfma_f32_32x32x16_f16) or "fp32" (exact fp32 MFMA, the acn_mlp_*_exact entry points).  Env ACN_TRAIN_MLP.
+TRAIN_MLP_PRECISION = os.environ.get("ACN_TRAIN_MLP", "fp16x3")
+
+
+def set_train_mlp_precision(mode: str) -> None:
+    """Select the training MLP kernels ("fp16x3" or "fp32") for later calls; step objects (RoutedAdaptStep,
+    ExpertParallelAdaptStep) keep the precision they were built with."""
+    global TRAIN_MLP_PRECISION
+    if mode not in ("fp16x3", "fp32"):
+        raise ValueError(f"train MLP precision must be 'fp16x3' or 'fp32', got {mode!r}")
+    TRAIN_MLP_PRECISION = mode
+
+
+def mlp_fn(name: str, precision: Optional[str] = None):
+    """The training-MLP entry point ``name`` of the selected precision."""
+    exact = (precision or TRAIN_MLP_PRECISION) == "fp32"
+    return getattr(_lib.lib(), name + ("_exact" if exact else ""))
 # Optional timing hook (bench.py --workload meta): when set to a list, every acn_mlp_train_bwd_dw call appends
 # (start event, end event, M, want_h0) recorded on the current stream around the call (weight pack +
 # mlp_bwd_dw_kernel + mlp_dw_reduce_kernel)
@@ -563,13 +592,13 @@ def mlp_train_bwd_dw(h0: torch.Tensor, sh: torch.Tensor, out: torch.Tensor, gout
     M = out.shape[0]
     dw = torch.empty(MLP_DW_FLOATS, device=out.device, dtype=torch.float32)
     gh = torch.empty(M, 32, device=out.device, dtype=torch.float32) if want_h0 else None
-    wsp = torch.empty(int(_lib.lib().acn_mlp_dw_workspace_bytes()), dtype=torch.uint8, device=out.device)
+    wsp = torch.empty(int(mlp_fn("acn_mlp_dw_workspace_bytes")()), dtype=torch.uint8, device=out.device)
     w = _mlp_struct(ws)
     hook = DW_HOOK
     if hook is not None:
         e0 = torch.cuda.Event(enable_timing=True)
         e0.record()
-    check(_lib.lib().acn_mlp_train_bwd_dw(ptr(h0), ptr(sh), ptr(out), ptr(gout), M, C.byref(w), ptr(dw),
+    check(mlp_fn("acn_mlp_train_bwd_dw")(ptr(h0), ptr(sh), ptr(out), ptr(gout), M, C.byref(w), ptr(dw),
                                           ptr(gh) if want_h0 else None, ptr(wsp), stream_of(out)),
           "acn_mlp_train_bwd_dw")
     if hook is not None:

@@ -300,7 +300,7 @@ class SlottedAdam:
     addresses)."""
 
     def __init__(self, optimizer: FusedAdam, slot_of, grads, K: int, nslots: int, flags=None,
-                 max_steps: int = 1 << 16):
+                 max_steps: int = 1 << 16, split_norm: bool = False, segmaps=None):
         L = _lib.lib()
         self.opt, self.K, self.nslots = optimizer, int(K), int(nslots)
         flags = flags or {}
@@ -348,6 +348,40 @@ class SlottedAdam:
                                  device=dev)
         self._hparams = None
         self.refresh()
+        # segment maps (acn_adam_step_slots_segmap): id(p) -> (now, ever) uint8 device maps of p's 64-B
+        # segments; only for tensors whose group has weight_decay 0 (the skipped update is then exact)
+        self.segmaps = None
+        if segmaps:
+            ptrs = []
+            for (p, g, m, v, gi) in rows:
+                mp = segmaps.get(id(p))
+                ok = mp is not None and float(optimizer.param_groups[gi]["weight_decay"]) == 0.0 and p.numel() % 16 == 0
+                ptrs += [mp[0].data_ptr(), mp[1].data_ptr()] if ok else [0, 0]
+            if any(ptrs):
+                self.segmaps = torch.tensor(ptrs, dtype=torch.int64).to(dev)
+        # split_norm (expert parallel): the clip norm's sum of squares in two passes, the per-rank slots
+        # (< K) first -- all-reduced over the group by the caller's function -- then the replicated shared
+        # slots (>= K) once, added on top (the reference's clip_grad_norm_ over the whole container)
+        self.split = bool(split_norm)
+        if self.split:
+            own_flags = [f | (NORM_ELSEWHERE_FLAG if (f & 0xffff) >= self.K else 0) for f in fl]
+            self.flags_own = torch.tensor(own_flags, device=dev, dtype=torch.int32)
+            sh = [(r, f) for r, f in zip(rows, fl) if (f & 0xffff) >= self.K]
+            arr = (_lib.acn_param_desc * max(1, len(sh)))()
+            first = 0
+            for t, ((p, g, m, v, gi), f) in enumerate(sh):
+                arr[t] = _lib.acn_param_desc(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(), gi,
+                                             first)
+                first += (p.numel() + ACN_OPTIM_CHUNK - 1) // ACN_OPTIM_CHUNK
+            if first == 0:
+                raise AcnError("SlottedAdam(split_norm): no shared parameter")
+            self.nchunks_sh = first
+            self.descs_sh = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(dev)
+            self.chunk_sh = torch.cat([torch.full(((r[0].numel() + ACN_OPTIM_CHUNK - 1) // ACN_OPTIM_CHUNK,), t,
+                                                  dtype=torch.int32) for t, (r, f) in enumerate(sh)]).to(dev)
+            self.flags_sh = torch.tensor([f & ~NORM_ELSEWHERE_FLAG for r, f in sh], device=dev, dtype=torch.int32)
+            self.partials_sh = torch.empty(first, device=dev, dtype=torch.float64)
+            self.total_own = torch.empty(1, device=dev, dtype=torch.float64)
 
     def _group_hparams(self):
         return tuple((float(g["lr"]), tuple(float(b) for b in g["betas"]), float(g["eps"]), float(g["weight_decay"]))
@@ -370,26 +404,44 @@ class SlottedAdam:
         self._hparams = hp
 
     def step(self, seg: torch.Tensor, max_norm: Optional[float], table_sumsq: Optional[torch.Tensor] = None,
-             hook=None) -> None:
+             hook=None, allreduce=None) -> None:
         """Clip norm over the active slots' gradients (+ ``table_sumsq``, a device double some kernel
         accumulated for NORM_ELSEWHERE tensors; reset by the norm pass), clip coefficient, then Adam over
-        the active slots; per-slot step counters advance on the device."""
+        the active slots; per-slot step counters advance on the device.  ``allreduce`` (split_norm):
+        in-place sum of a device double over the expert-parallel group, applied to the per-rank part."""
         L = _lib.lib()
         s = _stream(self.device)
         from ._lib import ptr
         scale = None
         if max_norm is not None:
-            check(L.acn_grad_sumsq_slots_ex(ptr(self.descs), ptr(self.chunk_tensor), self.nchunks, ptr(self.flags),
-                                            ptr(seg), self.K, ptr(self.partials), ptr(self.total),
-                                            ptr(table_sumsq), s), "acn_grad_sumsq_slots_ex")
+            if allreduce is not None:
+                if not self.split:
+                    raise AcnError("SlottedAdam.step(allreduce=...) needs split_norm=True")
+                check(L.acn_grad_sumsq_slots_ex(ptr(self.descs), ptr(self.chunk_tensor), self.nchunks,
+                                                ptr(self.flags_own), ptr(seg), self.K, ptr(self.partials),
+                                                ptr(self.total_own), ptr(table_sumsq), s), "acn_grad_sumsq_slots_ex")
+                allreduce(self.total_own)
+                check(L.acn_grad_sumsq_slots_ex(ptr(self.descs_sh), ptr(self.chunk_sh), self.nchunks_sh,
+                                                ptr(self.flags_sh), ptr(seg), self.K, ptr(self.partials_sh),
+                                                ptr(self.total), ptr(self.total_own), s), "acn_grad_sumsq_slots_ex")
+            else:
+                check(L.acn_grad_sumsq_slots_ex(ptr(self.descs), ptr(self.chunk_tensor), self.nchunks,
+                                                ptr(self.flags), ptr(seg), self.K, ptr(self.partials), ptr(self.total),
+                                                ptr(table_sumsq), s), "acn_grad_sumsq_slots_ex")
             check(L.acn_clip_coef(ptr(self.total), float(max_norm), ptr(self.scale), s), "acn_clip_coef")
             scale = self.scale
         if hook is not None:
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record()
-        check(L.acn_adam_step_slots(ptr(self.descs), ptr(self.chunk_tensor), self.nchunks, ptr(self.flags),
-                                    ptr(self.table), self.ngroups, self.table_steps, ptr(self.step_dev), self.nslots,
-                                    ptr(seg), self.K, ptr(scale), s), "acn_adam_step_slots")
+        if self.segmaps is not None:
+            check(L.acn_adam_step_slots_segmap(ptr(self.descs), ptr(self.chunk_tensor), self.nchunks, ptr(self.flags),
+                                               ptr(self.table), self.ngroups, self.table_steps, ptr(self.step_dev),
+                                               self.nslots, ptr(seg), self.K, ptr(scale), ptr(self.segmaps), s),
+                  "acn_adam_step_slots_segmap")
+        else:
+            check(L.acn_adam_step_slots(ptr(self.descs), ptr(self.chunk_tensor), self.nchunks, ptr(self.flags),
+                                        ptr(self.table), self.ngroups, self.table_steps, ptr(self.step_dev),
+                                        self.nslots, ptr(seg), self.K, ptr(scale), s), "acn_adam_step_slots")
         if hook is not None:
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record()

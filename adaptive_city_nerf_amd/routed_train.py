@@ -54,6 +54,10 @@ TELESCOPED_TABLE_NORM = os.environ.get("ACN_TELE_NORM", "1") != "0"
 # The background head's forward / backward as two HIP launches (acn_background_fwd / _bwd) instead of the
 # ~15 torch launches of its autograd graph
 FUSED_BACKGROUND = os.environ.get("ACN_FUSED_BG", "1") != "0"
+# Segment maps of the table gradients: the scatter marks the 64-B segments it adds into, and the Adam pass skips
+# segments never touched (m = v = g = 0: bit-identical under torch's Adam with weight_decay 0) and reads no
+# gradient for segments not touched this step
+ADAM_SEGMAP = os.environ.get("ACN_ADAM_SEGMAP", "1") != "0"
 
 
 def draw_jitter(n: int, S: int, device) -> torch.Tensor:
@@ -95,6 +99,7 @@ class RoutedAdaptStep:
                or e._interp_code != e0._interp_code for e in encs) or e0._interp_code == 0:
             raise AcnError("RoutedAdaptStep: experts must share one Linear/Smoothstep hash-grid configuration")
         self.P, self.model, self.opt = P, model, optimizer
+        self.mlp_precision = ops.TRAIN_MLP_PRECISION   # training MLP kernels (ops.set_train_mlp_precision)
         self.grad_clip = grad_clip
         self.jitter_mode = jitter
         # clear_in_adam=False keeps the gradients readable after the step (tests): the table gradients
@@ -128,7 +133,8 @@ class RoutedAdaptStep:
         self.h0 = torch.empty(cap, 32, **f32)
         self.out = torch.empty(cap, 4, **f32)
         self.gh0 = torch.empty(cap, 32, **f32)
-        self.mws = torch.empty(int(L.acn_mlp_pairs_workspace_bytes(K)), device=dev, dtype=torch.uint8)
+        self.mws = torch.empty(int(ops.mlp_fn("acn_mlp_pairs_workspace_bytes", self.mlp_precision)(K)), device=dev,
+                               dtype=torch.uint8)
         self.dw = torch.zeros(K, ops.MLP_DW_FLOATS, **f32)
         self.loss = torch.zeros((), **f32)
         # ---- persistent gradients (every parameter's .grad is one of these buffers)
@@ -172,7 +178,20 @@ class RoutedAdaptStep:
         flags = {}
         for i in zero_of:
             flags[i] = (ZERO_GRAD_FLAG if self.clear_in_adam else 0) | (NORM_ELSEWHERE_FLAG if self.tele else 0)
-        self.adam = SlottedAdam(optimizer, slot_of, grads, K, K + 1, flags, max_steps=max_steps)
+        # segment maps: (K, 2, segments) bytes -- [k, 0] touched this step, [k, 1] touched before.  A table whose
+        # moments may already be non-zero (optimizer state from earlier steps) starts all "touched before".
+        self.segmaps = None
+        smap = {}
+        if ADAM_SEGMAP:
+            nseg = encs[0].hash_table.numel() // 16
+            self.segmaps = torch.zeros(K, 2, nseg, device=dev, dtype=torch.uint8)
+            for k, e in enumerate(encs):
+                st = optimizer.state.get(e.hash_table)
+                if st and float(st.get("step", 0)) > 0:
+                    self.segmaps[k, 1].fill_(1)
+                smap[id(e.hash_table)] = (self.segmaps[k, 0], self.segmaps[k, 1])
+            self._segnow = (C.c_void_p * K)(*[self.segmaps[k, 0].data_ptr() for k in range(K)])
+        self.adam = SlottedAdam(optimizer, slot_of, grads, K, K + 1, flags, max_steps=max_steps, segmaps=smap)
         self.rows, self.flags, self.step_dev = self.adam.rows, self.adam.flags, self.adam.step_dev
         self.nslots, self.table_steps, self._step0 = self.adam.nslots, self.adam.table_steps, self.adam.step0
         self.scale = self.adam.scale
@@ -217,8 +236,9 @@ class RoutedAdaptStep:
         check(L.acn_hashgrid_fwd_pairs(ptr(self.x01), ptr(self.pk), ptr(self.seg), K, self._tables, self._res,
                                        len(enc._res_host), enc.log2_hashmap_size, enc._interp_code, ptr(self.h0), s),
               "acn_hashgrid_fwd_pairs")
-        check(L.acn_mlp_pack_pairs(self._mlp_ptrs, K, ptr(self.mws), s), "acn_mlp_pack_pairs")
-        check(L.acn_mlp_train_fwd_pairs(ptr(self.h0), ptr(self.sh), ptr(self.seg), K, ptr(self.mws), ptr(self.out), s),
+        mfn = lambda name: ops.mlp_fn(name, self.mlp_precision)  # noqa: E731
+        check(mfn("acn_mlp_pack_pairs")(self._mlp_ptrs, K, ptr(self.mws), s), "acn_mlp_pack_pairs")
+        check(mfn("acn_mlp_train_fwd_pairs")(ptr(self.h0), ptr(self.sh), ptr(self.seg), K, ptr(self.mws), ptr(self.out), s),
               "acn_mlp_train_fwd_pairs")
         rs = ops.routed_blend_fwd(self.out, self.pw, self.pmap[:M]).view(N, S, 4).requires_grad_(True)
         rays, rgbs, dirs = self.rays[:N], self.rgbs[:N], self.dirs[:N]
@@ -245,23 +265,52 @@ class RoutedAdaptStep:
                 buf.copy_(g)
         self.loss.copy_(loss.detach())
         gout = ops.routed_blend_bwd(g_rs.reshape(M, 4).contiguous(), self.pidx, self.pw, live=self.seg[K:K + 1])
-        check(L.acn_mlp_train_bwd_dw_pairs(ptr(self.h0), ptr(self.sh), ptr(self.out), ptr(gout), ptr(self.seg), K,
+        check(mfn("acn_mlp_train_bwd_dw_pairs")(ptr(self.h0), ptr(self.sh), ptr(self.out), ptr(gout), ptr(self.seg), K,
                                            ptr(self.mws), ptr(self.dw), ptr(self.gh0), s), "acn_mlp_train_bwd_dw_pairs")
         bhook = BWD_HOOK if self.graph is None else None
         if bhook is not None:
             b0 = torch.cuda.Event(enable_timing=True)
             b0.record()
-        check(L.acn_hashgrid_bwd_pairs_sumsq(ptr(self.x01), ptr(self.pk), ptr(self.pidx), ptr(self.seg), K,
-                                             ptr(self.gh0), self._gtables, self._res, len(enc._res_host),
-                                             enc.log2_hashmap_size, enc._interp_code,
-                                             ptr(self.table_sumsq) if self.tele else None, s),
-              "acn_hashgrid_bwd_pairs_sumsq")
+        if torch.are_deterministic_algorithms_enabled():
+            self._table_bwd_deterministic(enc)
+            if self.segmaps is not None:   # the sort-based backward marks no segments: the marks on their own
+                check(L.acn_hashgrid_pairs_mark(ptr(self.x01), ptr(self.pk), ptr(self.pidx), ptr(self.seg), K,
+                                                self._res, len(enc._res_host), enc.log2_hashmap_size,
+                                                enc._interp_code, self._segnow, s), "acn_hashgrid_pairs_mark")
+        else:
+            check(L.acn_hashgrid_bwd_pairs_segmap(ptr(self.x01), ptr(self.pk), ptr(self.pidx), ptr(self.seg), K,
+                                                  ptr(self.gh0), self._gtables, self._res, len(enc._res_host),
+                                                  enc.log2_hashmap_size, enc._interp_code,
+                                                  ptr(self.table_sumsq) if self.tele else None,
+                                                  self._segnow if self.segmaps is not None else None, s),
+                  "acn_hashgrid_bwd_pairs_segmap")
         if bhook is not None:
             b1 = torch.cuda.Event(enable_timing=True)
             b1.record()
             bhook.append((b0, b1))
         self.adam.step(self.seg, self.grad_clip, self.table_sumsq if self.tele else None,
                        hook=EVENT_HOOK if self.graph is None else None)
+
+    def _table_bwd_deterministic(self, enc) -> None:
+        """Under torch.use_deterministic_algorithms(True): every expert's table gradient by the sort-based
+        backward over its live pairs (acn_hashgrid_bwd_det: each row the serial fp32 sum of its contributions
+        in pair order = sample order, bitwise reproducible) instead of float atomics, and the tables' share of
+        the clip norm by a deterministic double reduction.  Reads the segment table to the host: eager only
+        (a graph-replayed step runs this eagerly instead, __call__)."""
+        if torch.cuda.is_current_stream_capturing():
+            raise AcnError("RoutedAdaptStep: deterministic mode cannot be captured (it reads the pair counts)")
+        K = self.K
+        seg = self.seg.cpu().tolist()
+        for k in range(K):
+            s0, n = int(seg[k]), int(seg[K + 1 + k])
+            if n:
+                ops.hashgrid_bwd(self.x01[s0:s0 + n], self.gh0[s0:s0 + n], enc._res_host, enc.log2_hashmap_size, 2,
+                                 enc._interp_code, deterministic=True, out=self.gtables[k])
+        if self.tele:
+            tot = torch.zeros((), device=self.device, dtype=torch.float64)
+            for g in self.gtables:
+                tot = tot + (g.double() ** 2).sum()
+            self.table_sumsq.copy_(tot.view(1))
 
     def __call__(self, rays: torch.Tensor, rgbs: torch.Tensor, jitter_u: Optional[torch.Tensor] = None) -> torch.Tensor:
         n = int(rays.shape[0])
@@ -278,12 +327,13 @@ class RoutedAdaptStep:
             if jitter_u is None or tuple(jitter_u.shape) != (n, self.S):
                 raise AcnError(f"RoutedAdaptStep(jitter='given') needs jitter_u of shape ({n}, {self.S}) per call")
             self.u[:n].copy_(jitter_u, non_blocking=True)
-        if n == self.N and self.graph is not None:
+        det = torch.are_deterministic_algorithms_enabled()   # eager: the deterministic table backward
+        if n == self.N and self.graph is not None and not det:
             self.graph.replay()
             self.replays += 1
         else:
             self._step(n)
-            if n == self.N and self._eager_left > 0:
+            if n == self.N and self._eager_left > 0 and not det:
                 self._eager_left -= 1
                 if self._eager_left == 0:
                     self._capture()
@@ -296,6 +346,14 @@ class RoutedAdaptStep:
         """(total_norm, clip coefficient) of the last step (device), as FusedAdam.last_norm."""
         return self.scale
 
+    def segment_stats(self):
+        """(segments touched by the last step's scatter, segments ever updated, segments in all tables), from
+        the maps after a step (the last step's marks are in 'ever' once its Adam pass ran).  Host read."""
+        if self.segmaps is None:
+            return None
+        ever = int(self.segmaps[:, 1].sum())
+        return ever, int(self.segmaps[:, 1].numel())
+
     def sync_state(self) -> None:
         """Host state['step'] of every parameter from the per-slot device counters (state_dict, or before
         an eager FusedAdam step on the same optimizer)."""
@@ -307,4 +365,6 @@ class RoutedAdaptStep:
         group hyper-parameters."""
         top = self.adam.load_state()
         self.adam.refresh()
+        if self.segmaps is not None and top > self._step0 + self.steps_done:
+            self.segmaps[:, 1].fill_(1)   # eager steps may have moved any row: treat every segment as touched
         self._step0 = top - self.steps_done   # keeps the exhaustion guard exact

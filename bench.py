@@ -54,7 +54,6 @@ FLOP_PER_SAMPLE = 26880          # MLP MACs x 2: 32*64+64*64+64+
 BYTES_PER_SAMPLE = 1024.2        # algorithmic hash-table reads + amortised ray I/O
 FP32_MFMA_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 matrix = vector peak (spec)
 HBM_PEAK_GBS = 8000.0
-IC_GATHER_GBS = 8600.0         # Infinity-Cache random-row gather rate (MI355X_MICROARCH.md 'Indexed rows')
 ATOMIC_REQ_PEAK = 1.3e12 / 64   # memory-side float-atomic requests/s (MI355X_MICROARCH.md 'Global float atomics')
 
 
@@ -353,6 +352,16 @@ def load_traffic(name: str = "render", rnd: str = "r01"):
     return None
 
 
+def load_gather_ceiling():
+    """Committed gather-only ceiling of the render's hash access (tools/micro/hash_gather.py on the GPU box:
+    profiles/r03_hash_gather_ceiling.json)."""
+    p = REPO / "profiles" / "r03_hash_gather_ceiling.json"
+    try:
+        return json.loads(p.read_text())
+    except Exception:
+        return None
+
+
 def free_port() -> int:
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
@@ -407,6 +416,11 @@ def main():
     ap.add_argument("--query-rays", type=int, default=2000, help="meta: query rays per task")
     ap.add_argument("--data-rays", type=int, default=1 << 22, help="data: rays in the region table")
     ap.add_argument("--no-graph", action="store_true", help="c5: eager steps instead of the HIP-graph replay")
+    ap.add_argument("--c5-scaling", choices=["weak", "strong"], default="weak",
+                    help="c5, N > 1: every rank streams its own 1000-ray batches (weak), or the ranks split each "
+                         "1000-ray batch (strong: the reference's exact runtime_adapt update)")
+    ap.add_argument("--ep-graph", action="store_true",
+                    help="c5, N > 1: capture the expert-parallel step, RCCL collectives included, in a HIP graph")
     ap.add_argument("--driver", choices=["step", "runtime_adapt"], default="step",
                     help="c5: time RoutedAdaptStep calls (step), or the drop-in train.runtime_adapt(steps=K) over a "
                          "loader-like list of device batches (what a reference caller of runtime_adapt gets)")
@@ -621,7 +635,10 @@ def main():
         P = SimpleNamespace(ray_samples=S, chunk_points=4000000, color_space="linear", optimizer="adam", lr=1e-4,
                             encoding_lr=0.01, sigma_lr=0.002, color_lr=0.002, bg_lr=0.001, weight_decay=0.0)
         nb, bsz = 32, 1000
-        pool = make_rays_multi(gbox, device, nb * bsz, 4321 + rank).view(nb, bsz, 8)
+        strong = a.c5_scaling == "strong" and world > 1
+        # weak: every rank streams its own 1000-ray batches (global batch W x 1000); strong: the ranks split
+        # each 1000-ray runtime_adapt batch (the reference's exact update), so they share one pool
+        pool = make_rays_multi(gbox, device, nb * bsz, 4321 + (0 if strong else rank)).view(nb, bsz, 8)
         val_rays = make_rays_multi(gbox, device, 4096, 97)
         teacher, _, _, _ = build_model(device, K, seed=1, table_seed=900)
         with torch.no_grad():
@@ -641,12 +658,19 @@ def main():
         psnr_before = val_psnr()
         model.train()
         opt = aoptim.build_optimizer(P, model)
-        samples_per_step = world * bsz * S
+        samples_per_step = (1 if strong else world) * bsz * S
         it = [0]
         graphed = None
         expert = None
         routed = None
+        ep = None
         pg = dist.group.WORLD if world > 1 else None
+        shard = slice(bsz * rank // world, bsz * (rank + 1) // world) if strong else slice(0, bsz)
+        if world > 1:   # one expert block per GPU, fixed-capacity exchanges, no host synchronisation
+            from adaptive_city_nerf_amd.expert_parallel import ExpertParallelAdaptStep
+            ep = ExpertParallelAdaptStep(P, model, shard.stop - shard.start, opt,
+                                         n_rays_global=bsz if strong else world * bsz, grad_clip=1.0, group=pg,
+                                         graph=a.ep_graph, warmup=2)
         loader = [(pool[i], gtp[i]) for i in range(nb)]   # a runtime_adapt data loader's batches (device)
         if world == 1 and a.driver == "step":  # the whole routed step (no host sync), one HIP graph (eager: --no-graph)
             from adaptive_city_nerf_amd.routed_train import RoutedAdaptStep
@@ -667,6 +691,8 @@ def main():
             it[0] += 1
             if routed is not None:
                 return routed(pool[i], gtp[i])
+            if ep is not None:
+                return ep(pool[i][shard], gtp[i][shard])
             return adapt_step(P, model, pool[i], gtp[i], opt, grad_clip=1.0, group=pg)
         sample_rays = pool[0]
         aoptim.EVENT_HOOK = []
@@ -777,6 +803,15 @@ def main():
         hash_bwd_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in RT.BWD_HOOK]))
         hash_segments = hash_bwd_segments(routed)
         RT.EVENT_HOOK = RT.BWD_HOOK = None
+    if a.workload == "c5" and ep is not None:
+        # the Adam launch of the expert-parallel step, timed by eager steps (collective: every rank runs them)
+        from adaptive_city_nerf_amd import routed_train as RT
+        ep.graph = None
+        RT.EVENT_HOOK = aoptim.EVENT_HOOK = []
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize()
+        RT.EVENT_HOOK = None
     if a.workload == "meta":
         # graph replays run no Python: the fused MLP backward (the step's dominant kernel) and the outer Adam
         # launch are timed by eager steps afterwards
@@ -835,6 +870,11 @@ def main():
             experts_hit = sum(1 for c in counts if c > 0)
             nparam = sum(r[0].numel() for r, f in zip(routed.rows, routed.flags.cpu().tolist())
                          if (f & 0xffff) >= K or counts[f & 0xffff] > 0)
+        elif ep is not None:   # this rank's Adam: its owned experts that received pairs + the head
+            counts = ep.eseg[ep.E + 1: 2 * ep.E + 1].cpu().tolist()
+            experts_hit = sum(1 for c in counts if c > 0)
+            nparam = sum(r[0].numel() for r, f in zip(ep.adam.rows, ep.adam.flags.cpu().tolist())
+                         if (f & 0xffff) >= ep.E or counts[f & 0xffff] > 0)
         else:
             nparam = sum(p.numel() for p in model.parameters() if p.grad is not None)
             experts_hit = sum(1 for sub in model.submodules if sub.xyz_encoder.hash_table.grad is not None)
@@ -892,19 +932,31 @@ def main():
                               "flop_per_sample": FLOP_PER_SAMPLE,
                               "mlp_arith": "fp32-accurate 3-term fp16 split (hi*hi + hi*lo + lo*hi) on "
                                            "v_mfma_f32_32x32x16_f16, fp32 accumulate (DESIGN.md 4)"}}
+    gc = load_gather_ceiling() if a.workload == "c2" else None
+    if gc:
+        # calibrated ceiling of THIS access shape: the render's hash gathers alone, same sample
+        # points, table and lane mapping (tools/micro/hash_gather.hip), best of a sweep over levels in flight x
+        # waves per CU x XCD bands; same algorithmic bytes, so frac = ceiling time / render time
+        c = gc["ceiling"]
+        roofline["gather_ceiling"] = {
+            "what": "gather-only kernel issuing the fused render's exact hash-table access (8-B corner rows, 16 "
+                    "levels x 8 corners, 128 MiB fp32 table, 32-sample tiles, half-wave per 8 levels, XCD bands) "
+                    "over the C2 sample points, no MLP / compositing; best of levels-in-flight 1-4 x 4-16 waves/CU "
+                    "x bands on/off",
+            "ceiling_ms": c["config"]["ms"], "ceiling_alg_gbs": c["alg_gbs"], "best_config": c["config"],
+            "achieved_alg_gbs": round(hash_gbs, 1), "frac": round(hash_gbs / c["alg_gbs"], 4),
+            "uniform_random_points_alg_gbs": gc["uniform_best"]["alg_gbs"],
+            "source": "profiles/r03_hash_gather_ceiling.json (+ r03_rocprof_hash_gather_kernel_stats.csv)"}
     if tr:
         d = tr.get("derived", {})
         miss_bytes = d.get("l2_miss_bytes_per_launch_at_128B")
-        lg = {"what": "hash-table lines served from beyond the XCD L2 (TCC_MISS x 128-B line) per launch, "
-                      "against the Infinity-Cache random-row gather rate (MI355X_MICROARCH.md 'Indexed rows': "
-                      "38 MB table, uniformly random rows, 8.6 TB/s chip-wide)",
+        lg = {"what": "hash-table lines served from beyond the XCD L2 (TCC_MISS x 128-B line) per launch",
               "l2_misses_per_sample": round(d.get("l2_misses_per_sample", 0.0), 2),
               "l2_hit_rate": round(d.get("l2_hit_rate", 0.0), 3),
               "line_bytes_per_launch": int(miss_bytes) if miss_bytes else None,
-              "ceiling_gbs": IC_GATHER_GBS, "source": f"profiles/pmc_render_r02.json ({tr.get('round')})"}
+              "source": f"profiles/pmc_render_r02.json ({tr.get('round')})"}
         if miss_bytes and tr.get("rocprof_avg_ns"):
             lg["achieved_gbs"] = round(miss_bytes / tr["rocprof_avg_ns"], 1)
-            lg["frac"] = round(lg["achieved_gbs"] / IC_GATHER_GBS, 4)
         roofline["line_gather"] = lg
     if a.workload in ("c5", "c5a", "meta"):
         roofline = {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -1012,7 +1064,14 @@ def main():
                                   f"train render + MSE + backward + fused clip/Adam over every expert hit"
                                   + ("; timed as ONE drop-in train.runtime_adapt(steps=K) call over a loader-like "
                                      "list of device batches" if a.driver == "runtime_adapt" else ""),
-                      "rays_per_step_per_gpu": 1000, "experts": 8, "driver": a.driver},
+                      "rays_per_step_per_gpu": 1000 // world if (a.c5_scaling == "strong" and world > 1) else 1000,
+                      "experts": 8, "driver": a.driver,
+                      "layout": ("one expert block per GPU: fixed-capacity all-to-alls of pair records, no host "
+                                 "synchronisation (expert_parallel.ExpertParallelAdaptStep)"
+                                 + (", captured with its RCCL collectives" if a.ep_graph else "")) if world > 1
+                      else "single GPU: routed_train.RoutedAdaptStep"
+                      + ("" if a.no_graph else " replayed as one HIP graph"),
+                      "scaling_mode": a.c5_scaling if world > 1 else None},
                "c5a": {"workload": f"C5a (placement variant, not a reference configuration): rank r adapts expert r "
                                   f"alone (active_module) on its own 1000-ray x {S}-sample batches, no collective "
                                   f"(train render + MSE + backward + fused clip/Adam); the step replayed as one HIP graph"
@@ -1046,7 +1105,8 @@ def main():
             "metric": "ray-samples/sec + PSNR, 4096 rays×256 samples, 1/2/4/8 MI355X",
             "value": round(value, 1), "unit": "rays/s" if a.workload == "data" else "ray-samples/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "strong" if a.workload == "c4" else "weak", "vs_baseline": None,
+            "scaling": "strong" if (a.workload == "c4" or (a.workload == "c5" and a.c5_scaling == "strong"))
+                       else "weak", "vs_baseline": None,
             "dtype": "f32", "data": "synthetic (formula-filled hash table, seeded MLP init; rays from the "
                                     "reference's validation camera geometry)",
             "config": cfg,

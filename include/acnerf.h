@@ -509,6 +509,35 @@ int acn_routed_scatter_xd(const float* rays, int64_t N, int S, int K, const floa
 int acn_xd_unit_sh(const float* xd, int64_t P, const float* aabb_min, const float* aabb_extent, float lo, float hi,
                    float* x01, float* sh, void* stream);
 
+/* Sync-free expert-parallel exchange (expert_parallel.ExpertParallelAdaptStep, SURVEY §8(e) C5 with one
+ * expert block per GPU; replaces the per-expert nonzero / index_select dispatch of meta_container.py:300-337
+ * across ranks).  Every buffer has a host-known fixed capacity, so the all-to-alls use constant split
+ * sizes and nothing is read back to the host:
+ *   acn_routed_count_fixed -> as acn_routed_count, but expert k's segment is [k cap, (k+1) cap) (cap >= N*S:
+ *                             never overflows); seg[K+1+k] = live count.  With experts numbered by owner
+ *                             (contiguous blocks) the pair buffer IS the send buffer of the all-to-all.
+ *   acn_routed_pad_pairs   -> pidx -1, pw 0 on every segment's slots past its live count (max_pad: a bound
+ *                             on one segment's padding, e.g. cap).
+ *   acn_ep_gather          -> owner side: records received as [src][local expert j][cap] (W x E x cap xd
+ *                             records, live counts recv_cnt (W, E) int64, device) -> compact pair slots per
+ *                             local expert in (src, index) order, segments padded to `align`: seg[2E+1]
+ *                             (device), x01 (HOST aabb_min / extent (E,3), clamped to [lo, hi]), SH-4, pk (local
+ *                             expert), pflag (0 pair / -1 padding, the pidx of the pair kernels), back (index
+ *                             into the received layout or -1).  Slot buffers hold W*E*cap + E*align slots.
+ *                             workspace: acn_ep_workspace_bytes(W, E).
+ *   acn_ep_scatter_back    -> ret[back[p]] = out[p] (float4 per slot): field outputs to the received layout
+ *   acn_ep_gather_grad     -> gout[p] = gy[back[p]] (0 on padding): the senders' dL/d(rgb, sigma) to the slots */
+int acn_routed_count_fixed(const float* rays, int64_t N, int S, const float* jitter, const acn_routing* routing,
+                           int64_t cap, float* t_vals, int64_t* seg, void* workspace, size_t workspace_bytes,
+                           void* stream);
+int acn_routed_pad_pairs(const int64_t* seg, int K, int64_t max_pad, int32_t* pidx, float* pw, void* stream);
+size_t acn_ep_workspace_bytes(int W, int E);
+int acn_ep_gather(const float* recv_xd, const int64_t* recv_cnt, int W, int E, int64_t cap, int align,
+                  const float* aabb_min, const float* aabb_extent, float lo, float hi, int64_t* seg, void* workspace,
+                  float* x01, float* sh, int32_t* pk, int32_t* pflag, int64_t* back, void* stream);
+int acn_ep_scatter_back(const float* out, const int64_t* back, const int64_t* seg, int E, float* ret, void* stream);
+int acn_ep_gather_grad(const float* gy, const int64_t* back, const int64_t* seg, int E, float* gout, void* stream);
+
 /* Per-expert kernels over routed pair slots (segments padded to multiples of 128, slot count seg[K] on the
  * device; fixed grids that stride to it, so a whole step is capturable in a hipGraph):
  *   acn_hashgrid_fwd_pairs : h0 (slots, L*2) of every slot through its expert's table (tables: HOST array
@@ -555,6 +584,49 @@ int acn_mse_linear_fwd_ws(const float* pred, const float* gt, int64_t n, float* 
                           size_t workspace_bytes, void* stream);
 int acn_mse_linear_bwd(const float* pred, const float* gt, int64_t n, const float* g_loss, float* g_pred,
                        void* stream);
+
+
+/* The training MLP in exact fp32 (v_mfma_f32_32x32x2_f32 layer products instead of the fp32-accurate fp16x3
+ * split): the same nine entry points, suffixed _exact, same arguments and semantics; workspaces must come
+ * from the _exact size functions (the weight image layout differs).  mlp_train.hip compiled a second time
+ * with -DACN_TRAIN_F16X3=0 (a runtime precision switch for parity studies: DESIGN.md 4). */
+size_t acn_mlp_workspace_bytes_exact(void);
+int acn_mlp_train_fwd_exact(const float* h0, const float* sh, int64_t M, const acn_mlp* w, float* out, float* save,
+                      void* workspace, void* stream);
+int acn_mlp_train_bwd_exact(const float* save, const float* out, const float* gout, int64_t M, const acn_mlp* w,
+                      float* gsave, float* gh0, void* workspace, void* stream);
+size_t acn_mlp_dw_workspace_bytes_exact(void);
+int acn_mlp_train_bwd_dw_exact(const float* h0, const float* sh, const float* out, const float* gout, int64_t M,
+                         const acn_mlp* w, float* dw, float* gh0, void* workspace, void* stream);
+size_t acn_mlp_pairs_workspace_bytes_exact(int K);
+int acn_mlp_pack_pairs_exact(const acn_mlp* const* w, int K, void* workspace, void* stream);
+int acn_mlp_train_fwd_pairs_exact(const float* h0, const float* sh, const int64_t* seg, int K, const void* workspace,
+                            float* out, void* stream);
+int acn_mlp_train_bwd_dw_pairs_exact(const float* h0, const float* sh, const float* out, const float* gout,
+                               const int64_t* seg, int K, void* workspace, float* dw, float* gh0, void* stream);
+
+/* Segment maps of the hash-table gradients (routed step): per expert table two byte maps over
+ * its 64-B segments (8 rows of 2 features): now[s] = the scatter added into segment s this step, ever[s] = it
+ * was updated by an earlier step.
+ *   acn_hashgrid_bwd_pairs_segmap -> acn_hashgrid_bwd_pairs_sumsq that also sets now[] of every segment it adds
+ *                                   into (seg_now: HOST array of K device byte maps, nullable).
+ *   acn_adam_step_slots_segmap    -> acn_adam_step_slots where tensor t with segmaps[2t] != NULL (device array
+ *                                   of 2 * ntensors byte-map pointers: now, ever) skips segments never touched
+ *                                   (m = v = g = 0: torch's Adam with weight_decay 0 leaves them bit-identical),
+ *                                   reads no gradient for segments not touched this step (g = 0 there), then
+ *                                   sets ever |= now and clears now.  Mapped tensors: numel a multiple of 16,
+ *                                   group weight_decay 0, 16-B aligned.  Exact: bitwise the dense update. */
+int acn_hashgrid_bwd_pairs_segmap(const float* x01, const int32_t* pk, const int32_t* pidx, const int64_t* seg, int K,
+                                  const float* grad_out, float* const* grad_tables, const int32_t* res, int L,
+                                  int log2T, int interp, double* table_sumsq, uint8_t* const* seg_now, void* stream);
+/* acn_hashgrid_pairs_mark -> only the now[] marks of acn_hashgrid_bwd_pairs_segmap (no gradient written): the
+ * segment maps of a step whose table gradients came from the deterministic sort-based backward. */
+int acn_hashgrid_pairs_mark(const float* x01, const int32_t* pk, const int32_t* pidx, const int64_t* seg, int K,
+                            const int32_t* res, int L, int log2T, int interp, uint8_t* const* seg_now, void* stream);
+int acn_adam_step_slots_segmap(const acn_param_desc* descs, const int32_t* chunk_tensor, int64_t nchunks,
+                               const int32_t* flags, const void* table, int ngroups, int table_steps, int32_t* step_dev,
+                               int nslots, const int64_t* seg, int K, const float* grad_scale, uint8_t* const* segmaps,
+                               void* stream);
 
 #ifdef __cplusplus
 }

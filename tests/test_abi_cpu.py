@@ -31,7 +31,11 @@ def test_library_loads_and_exports_every_declared_symbol():
     assert set(_lib.exported_symbols()) == set(declared_symbols())
     assert L.acn_workspace_bytes(1) > 50_000 and L.acn_workspace_bytes(4) == 4 * L.acn_workspace_bytes(1)
     # ray-order scratch: 4 B per ray for the re-ordered batch sizes (1..8192), none otherwise
-    assert [L.acn_render_order_bytes(n) for n in (0, 1, 4096, 8192, 8193)] == [0, 4, 16384, 32768, 0]
+    # the scratch of acn_render_stratified_fwd_ordered: the ray order (n <= 8192 rays, 4 B each) and the split
+    # routed render's ray lists (code[n], list[n + 16 kMaxK], multi[n], hdr[kMaxK + 2] int32)
+    split = lambda n: 4 * (3 * n + 16 * 16 + 16 + 2)  # noqa: E731
+    assert [L.acn_render_order_bytes(n) for n in (0, 1, 4096, 8192, 8193)] == [0] + [split(n) for n in (1, 4096, 8192,
+                                                                                                        8193)]
 
 
 def test_argument_errors_are_reported_without_a_gpu():

@@ -222,3 +222,163 @@ def test_hip_backend_adapt_step_matches_reference_fixture():
         return adapt_step_expert_parallel(Pk, HipBackend(m), rays, rgbs, opt, len(m.submodules), rays.shape[0],
                                           shared, grad_clip=1.0, u=u)
     check_adapt_fixture("k8", fn)
+
+
+# ------------------------------------------------------------------------------- sync-free step (GPU)
+def _ep_step_fn(graph, n_global=None):
+    """check_adapt_fixture step through ExpertParallelAdaptStep at world size 1 (the exchanges are copies):
+    built on the first call; graph=True: one eager real step, then the captured step replayed."""
+    def fn(Pk, m, rays, rgbs, opt, u):
+        from adaptive_city_nerf_amd.expert_parallel import ExpertParallelAdaptStep
+        st = getattr(opt, "_ep_step", None)
+        if st is None:
+            st = opt._ep_step = ExpertParallelAdaptStep(Pk, m, rays.shape[0], opt, grad_clip=1.0, graph=graph,
+                                                        warmup=1, jitter="given", clear_in_adam=False)
+        loss = st(rays, rgbs, jitter_u=u)
+        opt.last_norm = st.last_norm
+        return loss
+    return fn
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graph", [False, True])
+def test_ep_step_world1_matches_reference_fixture(graph):
+    """ExpertParallelAdaptStep (fixed-capacity exchange, no host read, slotted Adam) at world size 1 replays
+    the reference's K=8 runtime_adapt steps, eagerly and as a replayed HIP graph (steps 2-3)."""
+    from test_train import check_adapt_fixture
+    m, opt = check_adapt_fixture("k8", _ep_step_fn(graph))
+    st = opt._ep_step
+    assert st.steps_done == 3 and st.replays == (2 if graph else 0)
+
+
+def _ep_gpu_worker(rank, world, port, out):
+    """World-2 gloo group on ONE GPU: the product's exchange code (_Comm staged through host copies) with the
+    HIP kernels; strong mode -- the fixture's 1000-ray batch split over the ranks, loss over all 1000."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        from test_module_api import build_model, reference_state_dict
+        from adaptive_city_nerf_amd.expert_parallel import ExpertParallelAdaptStep
+        from adaptive_city_nerf_amd.optim import build_optimizer
+        d = G.load("train_k8")
+        Pk = SimpleNamespace(ray_samples=96, chunk_points=4_000_000, color_space="linear", optimizer="adam", lr=1e-4,
+                             encoding_lr=0.01, sigma_lr=0.002, color_lr=0.002, bg_lr=0.001, weight_decay=0.0)
+        m, _ = build_model("k8")
+        m.load_state_dict(reference_state_dict(d, 8, "w:"))
+        m = m.cuda().train()
+        opt = build_optimizer(Pk, m)
+        rays = torch.from_numpy(d["train0:rays"]).cuda()
+        sl = _shard(rays.shape[0], world, rank)
+        n_loc = sl.stop - sl.start
+        st = ExpertParallelAdaptStep(Pk, m, n_loc, opt, n_rays_global=rays.shape[0], grad_clip=1.0,
+                                     group=dist.group.WORLD, jitter="given", clear_in_adam=False)
+        res = {"loss": [], "norm": [], "grads": {}, "params": {}}
+        owner = expert_owner(8, world)
+        for step in range(3):
+            pre = f"train{step}:"
+            r = torch.from_numpy(d[pre + "rays"]).cuda()[sl]
+            c = torch.from_numpy(d[pre + "rgbs"]).cuda()[sl]
+            u = torch.from_numpy(d[pre + "u"]).cuda()[sl]
+            loss = st(r, c, jitter_u=u)
+            torch.cuda.synchronize()
+            res["loss"].append(float(loss[0]))
+            res["norm"].append(float(st.last_norm[0]))
+            if step == 0:
+                for name, p in m.named_parameters():
+                    if name.startswith("submodules.") and owner[int(name.split(".")[1])] == rank \
+                            and not name.endswith("hash_table") and p.grad is not None:
+                        res["grads"][name] = p.grad.cpu().numpy().copy()
+                    if name.startswith("bg_mlp"):
+                        res["grads"][name] = p.grad.cpu().numpy().copy()
+                res["table_rows"] = {k: m.submodules[k].xyz_encoder.hash_table.detach()[
+                    torch.from_numpy(d["train:rows"][k]).cuda()].cpu().numpy() for k in range(8) if owner[k] == rank}
+        for name, p in m.named_parameters():
+            if name.startswith("bg_mlp") or (name.startswith("submodules.") and owner[int(name.split(".")[1])] == rank
+                                             and not name.endswith("hash_table")):
+                res["params"][name] = p.detach().cpu().numpy().copy()
+        out[rank] = res
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_ep_step_world2_gloo_on_gpu_matches_reference():
+    """Two ranks on one GPU over gloo (staged exchange), each holding half of the reference batch and 4 of
+    the 8 experts: every step's global loss and clip norm, the owned experts' gradients and step-0 table rows,
+    and after 3 steps the owned experts' MLPs and the replicated background head equal the reference's
+    single-process runtime_adapt (train_k8.npz) -- strong scaling of one 1000-ray update."""
+    d = G.load("train_k8")
+    world = 2
+    with mp.Manager() as man:
+        out = man.dict()
+        mp.spawn(_ep_gpu_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+        res = dict(out)
+    for step in range(3):
+        ref = float(d[f"train{step}:loss"])
+        for r in range(world):
+            assert abs(res[r]["loss"][step] - ref) <= 1e-5 * ref, (step, r, res[r]["loss"][step], ref)
+            nref = float(d[f"train{step}:total_norm"])
+            assert abs(res[r]["norm"][step] - nref) <= 1e-4 * nref, (step, r)
+    owner = expert_owner(8, world)
+    for r in range(world):
+        for name, v in res[r]["grads"].items():
+            ref = d["train0:grad:" + name]
+            np.testing.assert_allclose(v, ref, rtol=0, atol=1e-4 * (np.abs(ref).max() + 1e-12), err_msg=name)
+        for k, rows in res[r]["table_rows"].items():
+            if f"train0:table_rows:{k}" in d:   # Adam's first step: ~lr * sign(g) per touched row
+                ref = d[f"train0:table_rows:{k}"]
+                close = np.mean(np.abs(rows.astype(np.float64) - ref) <= 1e-3 * 0.01 + 1e-6 * np.abs(ref))
+                assert close >= 0.99, (k, close)
+        for name, v in res[r]["params"].items():
+            key = "train2:param:" + name
+            if key in d:
+                lr = 0.001 if name.startswith("bg_mlp") else 0.002
+                close = np.mean(np.abs(v.astype(np.float64) - d[key]) <= 1e-3 * lr + 1e-6 * np.abs(d[key]))
+                assert close >= 0.95, (name, close)
+    for name, v in res[0]["params"].items():   # the replicated head: identical on both ranks
+        if name.startswith("bg_mlp"):
+            np.testing.assert_array_equal(v, res[1]["params"][name])
+
+
+def _comm_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from adaptive_city_nerf_amd.expert_parallel import _Comm
+        comm = _Comm(dist.group.WORLD)
+        K, C = 8, 5
+        owner = expert_owner(K, world)
+        eo = [owner.count(o) for o in range(world)]
+        E = eo[rank]
+        # sender layout [expert k][C] rows tagged (rank, k, i); the owner receives [src][local j][C]
+        send = torch.tensor([[rank, k, i] for k in range(K) for i in range(C)], dtype=torch.float32)
+        recv = torch.empty(world * E * C, 3)
+        comm.all_to_all(recv, send, [E * C] * world, [e * C for e in eo])
+        cnt = torch.arange(K, dtype=torch.int64) + 10 * rank
+        rc = torch.empty(world * E, dtype=torch.int64)
+        comm.all_to_all(rc, cnt, [E] * world, eo)
+        t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+        comm.all_reduce(t)
+        out[rank] = (recv.numpy(), rc.numpy(), float(t[0]), comm.staged)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ep_comm_fixed_splits_gloo_world2():
+    """The sync-free step's exchange helper (_Comm) on gloo: constant split sizes route sender segment
+    [expert k] of every rank to k's owner as [src][local expert][C]; counts likewise; sums all-reduced."""
+    world = 2
+    with mp.Manager() as man:
+        out = man.dict()
+        mp.spawn(_comm_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+        res = dict(out)
+    owner = expert_owner(8, world)
+    for r in range(world):
+        recv, rc, tot, staged = res[r]
+        assert staged and tot == 3.0
+        mine = [k for k in range(8) if owner[k] == r]
+        exp = np.array([[s, k, i] for s in range(world) for k in mine for i in range(5)], np.float32)
+        np.testing.assert_array_equal(recv, exp)
+        np.testing.assert_array_equal(rc, np.array([k + 10 * s for s in range(world) for k in mine]))

@@ -4,7 +4,7 @@ set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r03b
 mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests/test_train.py tests/test_meta_gpu.py tests/test_graph_gpu.py tests/test_loss_gpu.py -m gpu -x -v \
+timeout -k 10 900 python -u -m pytest tests/test_train.py tests/test_meta_gpu.py tests/test_graph_gpu.py tests/test_loss_gpu.py tests/test_expert_parallel.py -m gpu -x -v \
   --timeout 240 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || { echo "pytest failed"; grep -E "FAIL|Error|error" $O/pytest.log | head -30; tail -40 $O/pytest.log; exit 1; }
 tail -3 $O/pytest.log
 timeout -k 10 300 python -u bench.py --workload c5 --no-cpu-baseline > $O/bench_c5.json 2> $O/bench_c5.err || { echo "bench c5 failed"; tail $O/bench_c5.err; exit 3; }
