@@ -6,6 +6,7 @@ CPU fallback: if the library or a HIP device is missing, calls raise.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import os
 import threading
@@ -222,3 +223,21 @@ def require_hip(t: torch.Tensor, what: str) -> None:
     if not (isinstance(t, torch.Tensor) and t.is_cuda):
         raise AcnError(f"{what}: the HIP implementation needs tensors on a HIP device (got "
                        f"{getattr(t, 'device', type(t))}); there is no CPU fallback")
+
+
+@contextlib.contextmanager
+def graph_capture(graph, pool=None):
+    """torch.cuda.graph(graph, pool) with Python's cyclic garbage collector held off: a collection inside the
+    capture frees tensors of earlier, uncaptured work from within the capturing thread, which aborted the
+    process on this stack (round 3, tests/test_meta_gpu.py region-without-tasks).  Garbage is collected just
+    before the capture instead."""
+    import gc
+    gc.collect()
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        with torch.cuda.graph(graph, pool=pool):
+            yield
+    finally:
+        if was:
+            gc.enable()

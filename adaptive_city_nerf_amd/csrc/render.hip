@@ -1048,7 +1048,10 @@ __global__ void __launch_bounds__(1024, 4) render_kernel(FieldCfg cfg, BgArgs bg
 // the same one or two experts, so staging is rare).  A sample whose expert is not resident is
 // evaluated from the packed image in global memory (L2), without the SH fold.
 #ifndef ACN_SPLIT_ROUTED
-#define ACN_SPLIT_ROUTED 1  // K > 2: single-expert rays through render_single_kernel, the rest through render_slots_kernel
+// K > 2: single-expert rays through render_single_kernel, the rest through render_slots_kernel.  Off: measured
+// slower than the one slots launch on C3 and C4 (round 3, DESIGN.md 4: the single-expert kernel runs ~2x
+// render_kernel's per-ray time, the multi-expert remainder is latency-bound, plus two list passes)
+#define ACN_SPLIT_ROUTED 0
 #endif
 #ifndef ACN_SLOTS_SINGLE
 #define ACN_SLOTS_SINGLE 1  // single-expert rays (kSingleRay) skip the per-sample routing and blend
@@ -1320,60 +1323,91 @@ __global__ void __launch_bounds__(1024) ray_lists_kernel(const int32_t* __restri
 }
 
 #ifndef ACN_SINGLE_DBG
-#define ACN_SINGLE_DBG 0  // diagnostic builds: 1 no SH fold, 2 a workgroup barrier after every round
+#define ACN_SINGLE_DBG 0  // diagnostic builds: 1 no SH fold, 3 weights read from global memory (no LDS image)
+#endif
+#ifndef ACN_SINGLE_THREADS
+#define ACN_SINGLE_THREADS 1024  // rays per round = ACN_SINGLE_THREADS / 64 (divides the 16-ray segment padding)
+#endif
+// The block's expert metadata is selected from cfg.ex[] by compile-time indices.  Indexing the by-value
+// kernel argument with the runtime k inside the ray loop (ACN_SINGLE_EXSEL=0) gave run-to-run differences
+// in a few rays per launch (~1e-4 in RGB) on the MI355X -- only with the weights in LDS, never with the
+// same code reading them from global memory (tools/dbg/split_dbg5.py).
+#ifndef ACN_SINGLE_EXSEL
+#define ACN_SINGLE_EXSEL 1
 #endif
 template <int INTERP>
-__global__ void __launch_bounds__(1024, 4) render_single_kernel(FieldCfg cfg, BgArgs bg, RenderParams p,
+__global__ void __launch_bounds__(ACN_SINGLE_THREADS, ACN_SINGLE_THREADS / 256) render_single_kernel(FieldCfg cfg, BgArgs bg, RenderParams p,
                                                                 const int32_t* __restrict__ list,
                                                                 const int32_t* __restrict__ hdr) {
-    constexpr bool FOLD = ACN_SHFOLD != 0 && ACN_SINGLE_DBG != 1;
-    __shared__ __attribute__((aligned(16))) float smem[PK_FLOATS];
-    __shared__ __attribute__((aligned(16))) float cbuf[FOLD ? 16 * 64 : 4];
+    constexpr bool FOLD = ACN_SHFOLD != 0 && ACN_SINGLE_DBG != 1 && ACN_SINGLE_DBG != 3;
+    __shared__ __attribute__((aligned(16))) float smem[ACN_SINGLE_DBG == 3 ? 4 : PK_FLOATS];
+    __shared__ __attribute__((aligned(16))) float cbuf[FOLD ? (ACN_SINGLE_THREADS / 64) * 64 : 4];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     float* cb = FOLD ? cbuf + wave * 64 : nullptr;
     const float step = 1.0f / (float)(p.S - 1);
     const int K = cfg.K;
-    const int64_t G = (int64_t)hdr[K] >> 4;   // workgroup rounds of 16 rays
-    // contiguous round ranges per workgroup (the expert changes at most a few times per workgroup), in XCD
-    // bands: with the grid a multiple of 8, XCD x (blocks b = x mod 8) takes the x-th eighth of the rounds
-    int64_t g0, g1;
-    if ((gridDim.x & 7) == 0) {
-        const int64_t x = blockIdx.x & 7, slot = blockIdx.x >> 3, nx = gridDim.x >> 3;
-        const int64_t lo = G * x / 8, hi = G * (x + 1) / 8;
-        g0 = lo + (hi - lo) * slot / nx;
-        g1 = lo + (hi - lo) * (slot + 1) / nx;
-    } else {
-        g0 = G * blockIdx.x / gridDim.x;
-        g1 = G * (blockIdx.x + 1) / gridDim.x;
+    constexpr int WPR = ACN_SINGLE_THREADS / 64;   // rays (waves) per workgroup round
+    auto ld = [](const int32_t* a) -> int32_t { return *a; };
+    // Every workgroup renders rounds of ONE expert, whose image it stages into LDS once, before its loop
+    // (render_kernel's shape: no restaging inside the loop).
+    // Blocks are dealt to the experts in proportion to their rounds (at least one each), every block
+    // computing the same deal from hdr; virtual block ids keep consecutive ids on one XCD (block b runs on
+    // XCD b mod 8), so an XCD walks a contiguous stretch of the sorted list.
+    const int B = gridDim.x;
+    const int vb = (B & 7) == 0 ? (int)(blockIdx.x & 7) * (B >> 3) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+    int nz = 0;
+    int64_t G = 0;
+    for (int e = 0; e < K; ++e) {
+        const int64_t r = (int64_t)(ld(hdr + e + 1) - ld(hdr + e)) / WPR;
+        G += r;
+        nz += r > 0 ? 1 : 0;
     }
-    int cur = -1;
-    for (int64_t g = g0; g < g1; ++g) {
-        int k = 0;
-        while (k + 1 < K && hdr[k + 1] <= 16 * g) ++k;
-        k = __builtin_amdgcn_readfirstlane(k);
-        if (k != cur) {   // uniform over the workgroup: every wave walks the same rounds
-            __syncthreads();
-            const f32x4* src = reinterpret_cast<const f32x4*>(p.packed + (size_t)k * PK_FLOATS);
-            f32x4* dst = reinterpret_cast<f32x4*>(smem);
-            for (int i = threadIdx.x; i < PK_FLOATS / 4; i += blockDim.x) dst[i] = src[i];
-            __syncthreads();
-            cur = k;
+    const int64_t avail = B > nz ? B - nz : 0;
+    int k = -1, first = 0, nb = 0;
+    for (int e = 0, acc = 0; e < K; ++e) {
+        const int64_t r = (int64_t)(ld(hdr + e + 1) - ld(hdr + e)) / WPR;
+        const int n = r > 0 ? 1 + (int)(avail * r / (G > 0 ? G : 1)) : 0;
+        if (k < 0 && vb < acc + n) {
+            k = e;
+            first = acc;
+            nb = n;
         }
-        const int32_t ray = __builtin_amdgcn_readfirstlane(list[16 * g + wave]);
-#if ACN_SINGLE_DBG == 2
-        __syncthreads();
+        acc += n;
+    }
+    k = __builtin_amdgcn_readfirstlane(k);
+    if (k < 0) return;   // whole workgroup: more blocks than the deal uses
+    const int64_t base_k = ld(hdr + k) / WPR, rk = (ld(hdr + k + 1) - ld(hdr + k)) / WPR, j = vb - first;
+    // rounds j, j + nb, j + 2 nb, ... of the expert's segment: at any time its blocks work on a contiguous
+    // window of the (spatially ordered) list, as render_kernel's grid-stride loop does
+    const int64_t g0 = base_k + j, g1 = base_k + rk;
+#if ACN_SINGLE_EXSEL   // the expert's metadata selected by compile-time indices (no dynamic kernarg index)
+    ExpertMeta em = cfg.ex[0];
+#pragma unroll
+    for (int e = 1; e < kMaxK; ++e)
+        if (k == e) em = cfg.ex[e];
+#else
+    const ExpertMeta& em = cfg.ex[k];
 #endif
+    if (ACN_SINGLE_DBG != 3) {
+        const f32x4* src = reinterpret_cast<const f32x4*>(p.packed + (size_t)k * PK_FLOATS);
+        f32x4* dst = reinterpret_cast<f32x4*>(smem);
+        for (int i = threadIdx.x; i < PK_FLOATS / 4; i += blockDim.x) dst[i] = src[i];
+        __syncthreads();
+    }
+    for (int64_t g = g0; g < g1; g += nb) {
+        const int32_t ray = __builtin_amdgcn_readfirstlane(ld(list + WPR * g + wave));
         if (ray < 0) continue;   // padding of expert k's segment
         render_ray(p, bg, ray, lane, step,
                    [&](float px, float py, float pz, const float (&shv)[8], uint32_t& folded, float& yr, float& yg,
                        float& yb, float& ys) {
+                       const float* Wk = ACN_SINGLE_DBG == 3 ? p.packed + (size_t)k * PK_FLOATS : smem;
                        if (FOLD && !(folded & 1u)) {
-                           fold_sh_bias(smem, shv, lane, cb);
+                           fold_sh_bias(Wk, shv, lane, cb);
                            folded |= 1u;
                        }
                        float sg;
-                       field_tile<INTERP, FOLD>(smem, cfg.ex[k], cfg.log2T, px, py, pz, shv, cb, lane, yr, yg, yb, sg);
+                       field_tile<INTERP, FOLD>(Wk, em, cfg.log2T, px, py, pz, shv, cb, lane, yr, yg, yb, sg);
                        ys = trunc_exp(sg);
                    });
     }
@@ -1994,12 +2028,17 @@ extern "C" int acn_render_stratified_fwd_ordered(const float* rays, int64_t N, i
         if (cfg.routing == 1) hipLaunchKernelGGL((ray_class_kernel<1>), cgrid, dim3(256), 0, s, cfg, p, code);
         else hipLaunchKernelGGL((ray_class_kernel<2>), cgrid, dim3(256), 0, s, cfg, p, code);
         hipLaunchKernelGGL(ray_lists_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)code, N, K, list, multi, hdr);
-        int64_t swgs = (N + 15) / 16;
+
+        int64_t swgs = (N + ACN_SINGLE_THREADS / 64 - 1) / (ACN_SINGLE_THREADS / 64);
         if ((num_cus() & 7) == 0) swgs = (swgs + 7) & ~(int64_t)7;
-        const dim3 sgrid((unsigned)(swgs < num_cus() ? swgs : num_cus()));
-        if (interp == 1) hipLaunchKernelGGL(render_single_kernel<1>, sgrid, block, 0, s, cfg, b, p, list, hdr);
-        else if (interp == 0) hipLaunchKernelGGL(render_single_kernel<0>, sgrid, block, 0, s, cfg, b, p, list, hdr);
-        else hipLaunchKernelGGL(render_single_kernel<2>, sgrid, block, 0, s, cfg, b, p, list, hdr);
+        const int64_t scap = (int64_t)num_cus() * (1024 / ACN_SINGLE_THREADS);
+        int64_t sg_n = swgs < scap ? swgs : scap;
+        if (sg_n < K) sg_n = K;   // render_single_kernel deals at least one block to every expert
+        const dim3 sgrid((unsigned)sg_n);
+        const dim3 sblock(ACN_SINGLE_THREADS);
+        if (interp == 1) hipLaunchKernelGGL(render_single_kernel<1>, sgrid, sblock, 0, s, cfg, b, p, list, hdr);
+        else if (interp == 0) hipLaunchKernelGGL(render_single_kernel<0>, sgrid, sblock, 0, s, cfg, b, p, list, hdr);
+        else hipLaunchKernelGGL(render_single_kernel<2>, sgrid, sblock, 0, s, cfg, b, p, list, hdr);
         RenderParams pm = p;
         pm.order = multi;
         pm.norder = hdr + K + 1;

@@ -31,6 +31,7 @@ import torch
 import torch.distributed as dist
 from torch import Tensor
 
+from ._lib import graph_capture
 from .color_space import color_space_transformer
 
 
@@ -545,7 +546,7 @@ class ExpertParallelAdaptStep:
         dev = self.device
         torch.cuda.synchronize(dev)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with graph_capture(g):
             self._step(self.N)
         torch.cuda.synchronize(dev)
         self.graph = g

@@ -40,6 +40,7 @@ from typing import Dict, List, Mapping, Optional
 import torch
 import torch.distributed as dist
 
+from ._lib import graph_capture
 from .expert_parallel import expert_owner, global_clip_grad_norm_
 from .encodings import accumulate_table_grad
 from .optim import FusedAdam
@@ -481,7 +482,7 @@ class GraphedMetaStep:
         for cid in self.cids:
             self._add_region(cid, next(t for t in task_data[cid] if _task_shapes(t) == self.shapes[cid]))
         self.outer = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.outer, pool=self.pool):
+        with graph_capture(self.outer, pool=self.pool):
             self.adam.step(self.act, getattr(P, "grad_clip", 1.0))
         self.replays = 0
         self.eager_steps = 0
@@ -499,7 +500,7 @@ class GraphedMetaStep:
         self._load(cid, task)
         torch.cuda.synchronize(dev)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, pool=self.pool):
+        with graph_capture(g, pool=self.pool):
             self._task(cid)
         self.graphs[cid] = g
 

@@ -37,7 +37,7 @@ import numpy as np
 import torch
 
 from . import _lib, ops
-from ._lib import AcnError, acn_mlp, check, ptr
+from ._lib import AcnError, acn_mlp, check, graph_capture, ptr
 from .optim import NORM_ELSEWHERE_FLAG, ZERO_GRAD_FLAG, FusedAdam, SlottedAdam, bump_versions
 from .train import mse_color_loss
 
@@ -208,7 +208,7 @@ class RoutedAdaptStep:
         dev = self.device
         torch.cuda.synchronize(dev)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with graph_capture(g):
             self._step(self.N)
         torch.cuda.synchronize(dev)
         self.graph = g

@@ -24,6 +24,7 @@ import torch
 import torch.nn.functional as F
 
 from . import ops
+from ._lib import graph_capture
 from .color_space import color_space_transformer
 from .optim import FusedAdam
 from .ray_rendering import render_rays
@@ -129,7 +130,7 @@ class GraphedAdaptStep:
         optimizer.graph_begin(max_steps)
         optimizer.zero_grad(set_to_none=True)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        with graph_capture(self.graph):
             self.static_loss = adapt_step(P, base, self.static_rays, self.static_rgbs, optimizer,
                                           active_module=active_module, grad_clip=grad_clip, **render_kwargs)
         optimizer.graph_end_capture()

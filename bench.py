@@ -879,6 +879,24 @@ def main():
             nparam = sum(p.numel() for p in model.parameters() if p.grad is not None)
             experts_hit = sum(1 for sub in model.submodules if sub.xyz_encoder.hash_table.grad is not None)
         adam_bytes = 28 * nparam            # read p, g, m, v + write p, m, v (fp32)
+        adam_bytes_dense = adam_bytes
+        segmap = None
+        if routed is not None and getattr(routed, "segmaps", None) is not None:
+            # segment-mapped Adam (optim.hip adam_chunk_seg): a 64-B table segment never touched is skipped;
+            # one touched before but not this step reads + writes p, m, v (384 B); one touched this step also
+            # reads g and clears it (+128 B); both byte maps are read for every segment of a hit table
+            ever, total = routed.segment_stats()
+            ntab = sum(sub.xyz_encoder.hash_table.numel() for k_, sub in enumerate(model.submodules)
+                       if counts[k_] > 0)
+            nseg = ntab // 16
+            now = hash_segments
+            adam_bytes = 28 * (nparam - ntab) + 384 * ever + 128 * now + 2 * nseg
+            segmap = {"table_segments_hit_experts": nseg, "ever_touched_segments": ever,
+                      "ever_touched_fraction": round(ever / max(total, 1), 4),
+                      "segments_touched_this_step": now, "adam_bytes_dense": adam_bytes_dense,
+                      "adam_bytes_segmap": adam_bytes,
+                      "note": "ever-touched counted after the timed steps (it only grows); this-step segments = "
+                              "the distinct 64-B segments of one step's table scatter (hash_bwd_segments)"}
         achieved_gbs = adam_bytes / (kernel_ms * 1e-3) / 1e9
     if a.workload == "c5a":
         nparam = sum(p.numel() for p in model.submodules[expert].parameters()) + sum(p.numel() for p in shared)
@@ -966,8 +984,11 @@ def main():
         if a.workload == "c5":
             pmc = load_traffic("c5", "r02") or {}
             ad = pmc.get("adam_slots_kernel", {})
-            if ad.get("params") == int(nparam):   # counters of this exact workload (all 8 experts hit)
+            if ad.get("params") == int(nparam) and segmap is None:   # counters of this exact workload (dense Adam)
                 roofline["traffic"] = ad["hbm_bytes_per_launch"]
+            if segmap is not None:
+                roofline["bytes_per_param"] = "28 dense (MLP, head); table segments per segmap"
+                roofline["segmap"] = segmap
             hb = pmc.get("hashgrid_bwd_pairs", {})
             roofline["secondary"] = {
                 "kernel": "hashgrid_bwd_pairs (table-gradient scatter-add, returning float atomics that also telescope the tables share of the clip norm)",

@@ -324,6 +324,9 @@ def test_ep_step_world2_gloo_on_gpu_matches_reference():
     owner = expert_owner(8, world)
     for r in range(world):
         for name, v in res[r]["grads"].items():
+            if "train0:grad:" + name not in d:   # an expert the batch does not reach: grad None in the reference
+                assert not np.any(v), name
+                continue
             ref = d["train0:grad:" + name]
             np.testing.assert_allclose(v, ref, rtol=0, atol=1e-4 * (np.abs(ref).max() + 1e-12), err_msg=name)
         for k, rows in res[r]["table_rows"].items():
