@@ -359,7 +359,46 @@ __device__ __forceinline__ void adam_chunk_seg(float* p, float* g, float* m, flo
     f4* v4 = reinterpret_cast<f4*>(v);
     const int64_t n4 = n >> 2;   // n is a multiple of 16 (checked by the host)
     const f4 zero = 0.0f;
-    for (int64_t i = threadIdx.x; i < n4; i += kThreads) {
+    int64_t i = threadIdx.x;
+    // kUnroll vectors per thread per iteration: every map byte first, then all their p / m / v / g loads in
+    // flight together (the one-vector loop waited on the map load before each data load: 4.7 TB/s)
+    for (; i + (kUnroll - 1) * kThreads < n4; i += kUnroll * kThreads) {
+        uint8_t nw[kUnroll], ev[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const int64_t sgi = (i + u * kThreads) >> 2;
+            nw[u] = now[sgi];
+            ev[u] = ever[sgi];
+        }
+        f4 pp[kUnroll], mm[kUnroll], vv[kUnroll], gg[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const int64_t iv = i + u * kThreads;
+            if (nw[u] | ev[u]) {
+                pp[u] = ldv(&p4[iv]);
+                mm[u] = ldv(&m4[iv]);
+                vv[u] = ldv(&v4[iv]);
+                gg[u] = nw[u] ? ldv(&g4[iv]) : zero;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const int64_t iv = i + u * kThreads;
+            if (nw[u] | ev[u]) {
+                adam_vec(pp[u], gg[u], mm[u], vv[u], scale, k);
+                stv(&p4[iv], pp[u]);
+                stv(&m4[iv], mm[u]);
+                stv(&v4[iv], vv[u]);
+                if (clear && nw[u] && (gg[u][0] != 0.0f || gg[u][1] != 0.0f || gg[u][2] != 0.0f || gg[u][3] != 0.0f))
+                    stv(&g4[iv], zero);
+            }
+            if ((iv & 3) == 0 && nw[u]) {
+                now[iv >> 2] = 0;
+                if (!ev[u]) ever[iv >> 2] = 1;
+            }
+        }
+    }
+    for (; i < n4; i += kThreads) {
         const int64_t sgi = i >> 2;
         const uint8_t nw = now[sgi], ev = ever[sgi];
         if (nw | ev) {

@@ -108,7 +108,7 @@ class MetaContainer(MetaModule):
             return ops.pack_experts(specs, routing, active_module)
         subs = self.submodules if active_module is None else [self.submodules[active_module]]
         key = (active_module,) + tuple((id(t), t.data_ptr(), t._version) for s in subs
-                                      for t in s.meta_parameters())
+                                      for t in s._mlp_tensors(None).values())
         if not hasattr(self, "_pack_cache"):
             self._pack_cache = ops.PackCache()
         return self._pack_cache.get(specs, routing, active_module, key)
