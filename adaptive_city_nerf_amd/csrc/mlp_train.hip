@@ -838,18 +838,42 @@ __device__ __forceinline__ void dw_zero(DwAcc& a) {
     a.bWC2 = a.bWC1 = a.bWC0 = a.bHD = a.bW1 = a.bW0 = 0.0f;
 }
 
+#ifndef ACN_DW_DIAG
+#define ACN_DW_DIAG 0  // diagnostic builds: shader-clock cycles per phase of mlp_bwd_dw_kernel (acn_mlp_dw_diag)
+#endif
+#if ACN_DW_DIAG
+__device__ unsigned long long g_dw_diag[MAX_DW_BLOCKS * 4][8];
+struct DwClock {
+    uint64_t c[8];
+    uint64_t t;
+};
+#define DW_T0(dc) (dc).t = __builtin_amdgcn_s_memtime()
+#define DW_LAP(dc, i)                                              \
+    do {                                                           \
+        const uint64_t now_ = __builtin_amdgcn_s_memtime();        \
+        (dc).c[i] += now_ - (dc).t;                                \
+        (dc).t = now_;                                             \
+    } while (0)
+#else
+struct DwClock {};
+#define DW_T0(dc) (void)0
+#define DW_LAP(dc, i) (void)0
+#endif
+
 // one round: wave w re-runs the forward of its tile (samples m = tile * 32 + j), runs the backward chain
 // and adds its share of every layer's [dW | db] over the workgroup's 128 samples; barriers inside
 __device__ __forceinline__ void dw_round(const float* W, float* st, const float* __restrict__ h0,
                                          const float* __restrict__ sh, const float* __restrict__ out,
                                          const float* __restrict__ gout, int64_t m, bool ok, int w, int lane,
-                                         float* __restrict__ gh0, DwAcc& a) {
+                                         float* __restrict__ gh0, DwAcc& a, DwClock& dc) {
     const int h = lane >> 5;
     f32x16 A1[2], A2[2], Hd[1], Cin[1], C1[2], C2[2], Rg[1];
+    DW_T0(dc);
     {
         f32x16 X0[1];
         tile_forward(W, h0, sh, m, ok, lane, X0, A1, A2, Hd, Cin, C1, C2, Rg);
     }
+    DW_LAP(dc, 0);
     f32x16 dRg[1], dHd[1];
     dRg[0] = 0.0f;
     float dsig = 0.0f;
@@ -864,27 +888,37 @@ __device__ __forceinline__ void dw_round(const float* W, float* st, const float*
             dsig = gout[m * 4 + 3] * out[m * 4 + 3];
         }
     }
+    DW_LAP(dc, 4);
     // colour head 3 x 64: column block w, rows 0..15 (0..2 live)
     {
         const StageScale sc = stage_layer<1, 2>(st, dRg, C2, w, lane);
+        DW_LAP(dc, 1);
         dw_blocks<1>(st, 0, X_ROW + 16 * w, a.aWC2, a.bWC2, sc, lane);
+        DW_LAP(dc, 2);
     }
     f32x16 G2[2], G1[2], Gc[1];
     bwd_layer<2, 1, 3, 32>(W + L_WC2, S64, dRg, G2, lane);
     relu_mask<2>(G2, C2);
+    DW_LAP(dc, 3);
     // colour layer 1, 64 x 64: row block w
     {
         const StageScale sc = stage_layer<2, 2>(st, G2, C1, w, lane);
+        DW_LAP(dc, 1);
         dw_blocks<4>(st, 16 * w, X_ROW, a.aWC1, a.bWC1, sc, lane);
+        DW_LAP(dc, 2);
     }
     bwd_layer<2, 2, 64, 64>(W + L_WC1, S64, G2, G1, lane);
     relu_mask<2>(G1, C1);
+    DW_LAP(dc, 3);
     // colour layer 0, 64 x 31 (input 31 = zero column): row block w
     {
         const StageScale sc = stage_layer<2, 1>(st, G1, Cin, w, lane);
+        DW_LAP(dc, 1);
         dw_blocks<2>(st, 16 * w, X_ROW, a.aWC0, a.bWC0, sc, lane);
+        DW_LAP(dc, 2);
     }
     bwd_layer<1, 2, 64, 64>(W + L_WC0, S32, G1, Gc, lane);  // d cin: rows 0..14 = d geo (SH rows dropped)
+    DW_LAP(dc, 3);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int f = rho(r, h);
@@ -893,29 +927,38 @@ __device__ __forceinline__ void dw_round(const float* W, float* st, const float*
     // heads [geo 15 | sigma 1] x 64: column block w
     {
         const StageScale sc = stage_layer<1, 2>(st, dHd, A2, w, lane);
+        DW_LAP(dc, 1);
         dw_blocks<1>(st, 0, X_ROW + 16 * w, a.aHD, a.bHD, sc, lane);
+        DW_LAP(dc, 2);
     }
     f32x16 GA2[2], GA1[2], GH[1];
     bwd_layer<2, 1, 16, 32>(W + L_WH, S64, dHd, GA2, lane);
     relu_mask<2>(GA2, A2);
+    DW_LAP(dc, 3);
     // sigma trunk 1, 64 x 64: row block w
     {
         const StageScale sc = stage_layer<2, 2>(st, GA2, A1, w, lane);
+        DW_LAP(dc, 1);
         dw_blocks<4>(st, 16 * w, X_ROW, a.aW1, a.bW1, sc, lane);
+        DW_LAP(dc, 2);
     }
     bwd_layer<2, 2, 64, 64>(W + L_W1, S64, GA2, GA1, lane);
     relu_mask<2>(GA1, A1);
+    DW_LAP(dc, 3);
     // sigma trunk 0, 64 x 32: row block w
     f32x16 X0[1];
     load_tiles<1>(h0, 32, 0, 32, m, ok, h, X0);  // reloaded (L2-hot) rather than kept live
     {
         const StageScale sc = stage_layer<2, 1>(st, GA1, X0, w, lane);
+        DW_LAP(dc, 1);
         dw_blocks<2>(st, 16 * w, X_ROW, a.aW0, a.bW0, sc, lane);
+        DW_LAP(dc, 2);
     }
     if (gh0) {
         bwd_layer<1, 2, 64, 64>(W + L_W0, S32, GA1, GH, lane);
         store_tiles<1>(gh0, 32, 0, 32, m, ok, h, GH);
     }
+    DW_LAP(dc, 5);
 }
 
 // one copy of the 13,715 partial sums: every element has exactly one owner (wave, lane, register)
@@ -985,12 +1028,19 @@ __global__ void __launch_bounds__(256) mlp_bwd_dw_kernel(const float* __restrict
     const int64_t ntiles = (M + 31) / 32;
     DwAcc a;
     dw_zero(a);
+    DwClock dc{};
     // rounds are uniform over the workgroup (barriers inside): tiles past the end have zero gradients
     for (int64_t base = (int64_t)blockIdx.x * 4; base < ntiles; base += (int64_t)gridDim.x * 4) {
         const int64_t m = (base + w) * 32 + j;
-        dw_round(Wl + opaque_s(0), st_base + opaque_s(0), h0, sh, out, gout, m, m < M, w, opaque_v(lane0), gh0, a);
+        dw_round(Wl + opaque_s(0), st_base + opaque_s(0), h0, sh, out, gout, m, m < M, w, opaque_v(lane0), gh0, a, dc);
     }
+    DW_T0(dc);
     dw_flush(a, partial + (int64_t)blockIdx.x * NDW, w, lane0);
+#if ACN_DW_DIAG
+    DW_LAP(dc, 6);
+    if (lane0 == 0)
+        for (int i = 0; i < 8; ++i) g_dw_diag[blockIdx.x * 4 + w][i] = dc.c[i];
+#endif
 }
 
 // Pair-list variant (routed container): workgroup b takes the contiguous rounds [b R / G, (b+1) R / G)
@@ -1027,7 +1077,8 @@ __global__ void __launch_bounds__(256) mlp_bwd_dw_pairs_kernel(const float* __re
             cur = k;
         }
         const int64_t m = (rd * 4 + w) * 32 + j;
-        dw_round(Wl + opaque_s(0), st_base + opaque_s(0), h0, sh, out, gout, m, true, w, opaque_v(lane0), gh0, a);
+        DwClock dcp{};
+        dw_round(Wl + opaque_s(0), st_base + opaque_s(0), h0, sh, out, gout, m, true, w, opaque_v(lane0), gh0, a, dcp);
     }
     if (cur >= 0) dw_flush(a, partial + ((int64_t)blockIdx.x * K + cur) * NDW, w, lane0);
 }
@@ -1165,6 +1216,12 @@ extern "C" int ACN_MLP_API(acn_mlp_train_bwd)(const float* save, const float* ou
                        M, gsave, gh0);
     return acn_check_launch("acn_mlp_train_bwd");
 }
+
+#if ACN_DW_DIAG
+extern "C" int ACN_MLP_API(acn_mlp_dw_diag)(unsigned long long* host, int nblk) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dw_diag), (size_t)nblk * 4 * 8 * sizeof(unsigned long long));
+}
+#endif
 
 extern "C" size_t ACN_MLP_API(acn_mlp_dw_workspace_bytes)(void) {
     return ((size_t)L_FLOATS + (size_t)MAX_DW_BLOCKS * NDW) * sizeof(float);
