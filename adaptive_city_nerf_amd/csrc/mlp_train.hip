@@ -453,7 +453,11 @@ __device__ __forceinline__ void tile_forward(const float* Wl, const float* h0, c
     fwd_layer<1, 2, 32>(Wl + L_WC2, S64, Wl + L_BC2, C2, Rg, lane);
 }
 
-__global__ void __launch_bounds__(256) mlp_fwd_kernel(const float* __restrict__ img, const float* __restrict__ h0,
+// SAVE: write the layer inputs for the split backward (keeps every activation live to the end of the tile:
+// ~250 VGPRs, 4-wave blocks).  The no-save instantiation -- every fused-path call -- needs ~124 registers, so it
+// runs 8-wave blocks: two blocks (the 72 KB weight image each) = four waves per SIMD.
+template <bool SAVE>
+__global__ void __launch_bounds__(SAVE ? 256 : 512) mlp_fwd_kernel(const float* __restrict__ img, const float* __restrict__ h0,
                                                       const float* __restrict__ sh, int64_t M,
                                                       float* __restrict__ out, float* __restrict__ save) {
     __shared__ __attribute__((aligned(16))) float Wl[L_FLOATS];
@@ -467,7 +471,9 @@ __global__ void __launch_bounds__(256) mlp_fwd_kernel(const float* __restrict__ 
         const int64_t m = tile * 32 + j;
         const bool ok = m < M;
         f32x16 X0[1], A1[2], A2[2], Hd[1], Cin[1], C1[2], C2[2], Rg[1];
-        tile_forward(Wl, h0, sh, m, ok, lane, X0, A1, A2, Hd, Cin, C1, C2, Rg);
+        // opaque base: the LDS weight reads are re-issued per tile instead of hoisted out of the loop into
+        // ~240 held registers (one wave per SIMD; with it the no-save form fits two)
+        tile_forward(Wl + opaque_s(0), h0, sh, m, ok, lane, X0, A1, A2, Hd, Cin, C1, C2, Rg);
         if (ok) {
             if (h == 0) {
 #pragma unroll
@@ -475,7 +481,7 @@ __global__ void __launch_bounds__(256) mlp_fwd_kernel(const float* __restrict__ 
             } else {
                 out[m * 4 + 3] = acn::trunc_exp(Hd[0][7]);  // row 15 = sigma head (lane half 1, reg 7)
             }
-            if (save) {
+            if (SAVE) {
                 // layer inputs (+ ones columns for the bias gradient), feature-major
 #pragma unroll
                 for (int r = 0; r < 16; ++r) save[fm_index(m, SS, O_H0 + rho(r, h))] = h0[m * 32 + rho(r, h)];
@@ -1200,8 +1206,14 @@ extern "C" int ACN_MLP_API(acn_mlp_train_fwd)(const float* h0, const float* sh, 
     ACN_REQUIRE(h0 && sh && out, "acn_mlp_train_fwd: NULL pointer");
     hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(mlp_pack_kernel, dim3((L_FLOATS + 255) / 256), dim3(256), 0, s, ptrs(w), (float*)workspace);
-    hipLaunchKernelGGL(mlp_fwd_kernel, dim3(grid_for(M)), dim3(256), 0, s, (const float*)workspace, h0, sh, M, out,
-                       save);
+    if (save)
+        hipLaunchKernelGGL(mlp_fwd_kernel<true>, dim3(grid_for(M)), dim3(256), 0, s, (const float*)workspace, h0, sh, M,
+                           out, save);
+    else {
+        const int64_t blocks = ((M + 31) / 32 + 7) / 8;
+        hipLaunchKernelGGL(mlp_fwd_kernel<false>, dim3((unsigned)(blocks < 512 ? blocks : 512)), dim3(512), 0, s,
+                           (const float*)workspace, h0, sh, M, out, save);
+    }
     return acn_check_launch("acn_mlp_train_fwd");
 }
 
