@@ -1192,6 +1192,10 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
                                ys = trunc_exp(sg);
                                return;
                            }
+#if ACN_DIAG_SLOTS_NOMULTI  // diagnostic build only: the multi-expert blend path removed (register study)
+                           yr = yg = yb = ys = 0.0f;
+                           return;
+#endif
                            const RouteState st = route_prep<ROUTE>(cfg, px, py, pz);
                            yr = yg = yb = ys = 0.0f;
                            for (int k = 0; k < cfg.K; ++k) {
