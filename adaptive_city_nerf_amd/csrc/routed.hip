@@ -142,23 +142,6 @@ __global__ void __launch_bounds__(1024) routed_scan_kernel(int32_t* __restrict__
     }
 }
 
-// padding slots of every segment: pidx -1 (no sample), x01 0.5, sh 0, pk = k
-__global__ void __launch_bounds__(256) routed_pad_kernel(const int64_t* __restrict__ seg, int K, int align,
-                                                         int32_t* __restrict__ pidx, float* __restrict__ pw,
-                                                         float* __restrict__ x01, float* __restrict__ sh,
-                                                         int32_t* __restrict__ pk) {
-    const int k = blockIdx.x;
-    const int64_t p0 = seg[k] + seg[K + 1 + k], p1 = seg[k + 1];
-    for (int64_t p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
-        pidx[p] = -1;
-        pw[p] = 0.0f;
-        x01[3 * p] = x01[3 * p + 1] = x01[3 * p + 2] = 0.5f;
-#pragma unroll
-        for (int q = 0; q < 16; ++q) sh[16 * p + q] = 0.0f;
-        if (pk) pk[p] = k;
-    }
-}
-
 struct BoxCfg {
     float amin[kMaxK][3], ext[kMaxK][3];
     float lo, hi;
@@ -174,9 +157,26 @@ __global__ void __launch_bounds__(kBlk) routed_scatter_kernel(const float* __res
                                                               const int64_t* __restrict__ starts, BoxCfg box,
                                                               int32_t* __restrict__ pidx, float* __restrict__ pw,
                                                               float* __restrict__ x01, float* __restrict__ sh_out,
-                                                              int32_t* __restrict__ pmap, int32_t* __restrict__ pk) {
+                                                              int32_t* __restrict__ pmap, int32_t* __restrict__ pk,
+                                                              int pad) {
     __shared__ int wcnt[kBlk / 64][kMaxK];
     const int64_t M = N * (int64_t)S;
+    if (XD == 0 && pad) {
+        // the padding slots of expert k (segment tail past its live count, ALIGN padding): pidx -1, weight 0,
+        // a neutral point; disjoint from every pair slot this kernel writes (was routed_pad_kernel, a launch
+        // of its own)
+        for (int k = blockIdx.x; k < K; k += gridDim.x) {
+            const int64_t p0 = starts[k] + starts[K + 1 + k], p1 = starts[k + 1];
+            for (int64_t p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
+                pidx[p] = -1;
+                pw[p] = 0.0f;
+                x01[3 * p] = x01[3 * p + 1] = x01[3 * p + 2] = 0.5f;
+#pragma unroll
+                for (int q = 0; q < 16; ++q) sh_out[16 * p + q] = 0.0f;
+                if (pk) pk[p] = k;
+            }
+        }
+    }
     const int64_t m = (int64_t)blockIdx.x * kBlk + threadIdx.x;
     const bool live = m < M;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -470,10 +470,7 @@ extern "C" int acn_routed_scatter(const float* rays, int64_t N, int S, int K, co
     const float* W = (const float*)workspace;
     const int32_t* blk = (const int32_t*)(W + M * K);
     hipLaunchKernelGGL(routed_scatter_kernel<0>, dim3(blocks_for(M, kBlk)), dim3(kBlk), 0, (hipStream_t)stream, rays,
-                       N, S, K, t_vals, W, blk, starts, box, pidx, pw, x01, sh, pmap, pk);
-    if (align > 1)
-        hipLaunchKernelGGL(routed_pad_kernel, dim3(K), dim3(256), 0, (hipStream_t)stream, starts, K, align, pidx, pw, x01,
-                           sh, pk);
+                       N, S, K, t_vals, W, blk, starts, box, pidx, pw, x01, sh, pmap, pk, align > 1 ? 1 : 0);
     return acn_check_launch("acn_routed_scatter");
 }
 
@@ -508,7 +505,7 @@ extern "C" int acn_routed_scatter_xd(const float* rays, int64_t N, int S, int K,
     const float* W = (const float*)workspace;
     const int32_t* blk = (const int32_t*)(W + M * K);
     hipLaunchKernelGGL(routed_scatter_kernel<1>, dim3(blocks_for(M, kBlk)), dim3(kBlk), 0, (hipStream_t)stream, rays,
-                       N, S, K, t_vals, W, blk, seg, box, pidx, pw, xd, (float*)nullptr, pmap, pk);
+                       N, S, K, t_vals, W, blk, seg, box, pidx, pw, xd, (float*)nullptr, pmap, pk, 0);
     return acn_check_launch("acn_routed_scatter_xd");
 }
 

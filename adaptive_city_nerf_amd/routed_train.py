@@ -137,6 +137,7 @@ class RoutedAdaptStep:
                                dtype=torch.uint8)
         self.dw = torch.zeros(K, ops.MLP_DW_FLOATS, **f32)
         self.loss = torch.zeros((), **f32)
+        self._one = torch.ones((), **f32)          # dL/dL of the explicit loss backward
         # ---- persistent gradients (every parameter's .grad is one of these buffers)
         self.gtables = [torch.zeros_like(e.hash_table) for e in encs]
         self.bg_params = list(model.bg_mlp.parameters())
@@ -246,7 +247,18 @@ class RoutedAdaptStep:
         # background head as its fused HIP forward and backward (writing the persistent .grad buffers), or
         # under autograd when the head is not the HIP-supported SH-4 MLP
         from .ray_rendering import volume_render
-        if self.bg_spec is not None:
+        if self.bg_spec is not None and str(self.P.color_space).lower() == "linear":
+            # the kernels autograd would run (compositing, the linear-space MSE and their backwards), called
+            # directly: no ones-fill for the loss gradient, no autograd bookkeeping launches
+            dirs.copy_(rays[:, 3:6])
+            rs_ = rs.detach()
+            bg = ops.background_fwd(dirs, self.bg_spec)
+            rgb = ops.volume_render(rs_, t, bg)[0]
+            loss = ops.mse_linear_fwd(rgb, rgbs)
+            g_rgb = ops.mse_linear_bwd(rgb, rgbs, self._one)
+            g_rs, g_bg = ops.volume_render_bwd(rs_, t, bg, 1.0, g_rgb, None, None, None)
+            ops.background_bwd(dirs, self.bg_spec, g_bg, self.gbg)
+        elif self.bg_spec is not None:
             dirs.copy_(rays[:, 3:6])
             bg = ops.background_fwd(dirs, self.bg_spec).requires_grad_(True)
             with torch.enable_grad():
