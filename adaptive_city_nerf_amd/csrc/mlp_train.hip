@@ -844,6 +844,9 @@ __device__ __forceinline__ void dw_zero(DwAcc& a) {
     a.bWC2 = a.bWC1 = a.bWC0 = a.bHD = a.bW1 = a.bW0 = 0.0f;
 }
 
+#ifndef ACN_DW_PC
+#define ACN_DW_PC 1  // mlp_bwd_dw_pc_kernel (producer / consumer waves) for acn_mlp_train_bwd_dw
+#endif
 #ifndef ACN_DW_DIAG
 #define ACN_DW_DIAG 0  // diagnostic builds: shader-clock cycles per phase of mlp_bwd_dw_kernel (acn_mlp_dw_diag)
 #endif
@@ -1049,6 +1052,146 @@ __global__ void __launch_bounds__(256) mlp_bwd_dw_kernel(const float* __restrict
 #endif
 }
 
+#if !ACN_DW_F16X3
+// Producer / consumer form of the fused backward (8-wave workgroups, two waves per SIMD).  Waves 0-3
+// (producers) run exactly the per-tile work of dw_round -- forward recompute, the dX chain, ReLU masks --
+// and put each layer's dY / X into the shared stage; waves 4-7 (consumers) hold the weight-gradient
+// accumulators of the same row / column blocks wave w - 4 owned in dw_round and contract the stage.  Per
+// layer: producers put -> barrier -> [producers: dX of the layer | consumers: dW of the layer] -> barrier,
+// so the MFMA-bound contraction overlaps the producers' VALU-bound split / ReLU / dX work instead of
+// following it, and neither role carries the other's registers.  Every wave executes the same 12
+// barriers per round and the same rounds; the sums, their order and every output are those of
+// mlp_bwd_dw_kernel bit for bit (same owners, same stage, same k order).
+__device__ __forceinline__ void pc_sync() { __syncthreads(); }
+
+__device__ __forceinline__ void pc_producer_round(const float* W, float* st, const float* __restrict__ h0,
+                                                  const float* __restrict__ sh, const float* __restrict__ out,
+                                                  const float* __restrict__ gout, int64_t m, bool ok, int w, int lane,
+                                                  float* __restrict__ gh0) {
+    const int h = lane >> 5;
+    f32x16 A1[2], A2[2], Hd[1], Cin[1], C1[2], C2[2], Rg[1];
+    {
+        f32x16 X0[1];
+        tile_forward(W, h0, sh, m, ok, lane, X0, A1, A2, Hd, Cin, C1, C2, Rg);
+    }
+    f32x16 dRg[1], dHd[1];
+    dRg[0] = 0.0f;
+    float dsig = 0.0f;
+    if (ok) {
+        if (h == 0) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const float y = out[m * 4 + c];
+                dRg[0][c] = (gout[m * 4 + c] * (1.0f - y)) * y;
+            }
+        } else {
+            dsig = gout[m * 4 + 3] * out[m * 4 + 3];
+        }
+    }
+    // colour head
+    stage_put<1>(st, 0, dRg, w, lane);
+    stage_put<2>(st, X_ROW, C2, w, lane);
+    pc_sync();
+    f32x16 G2[2], G1[2], Gc[1];
+    bwd_layer<2, 1, 3, 32>(W + L_WC2, S64, dRg, G2, lane);
+    relu_mask<2>(G2, C2);
+    pc_sync();
+    // colour layer 1
+    stage_put<2>(st, 0, G2, w, lane);
+    stage_put<2>(st, X_ROW, C1, w, lane);
+    pc_sync();
+    bwd_layer<2, 2, 64, 64>(W + L_WC1, S64, G2, G1, lane);
+    relu_mask<2>(G1, C1);
+    pc_sync();
+    // colour layer 0
+    stage_put<2>(st, 0, G1, w, lane);
+    stage_put<1>(st, X_ROW, Cin, w, lane);
+    pc_sync();
+    bwd_layer<1, 2, 64, 64>(W + L_WC0, S32, G1, Gc, lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int f = rho(r, h);
+        dHd[0][r] = f < 15 ? Gc[0][r] : (f == 15 ? dsig : 0.0f);
+    }
+    pc_sync();
+    // heads
+    stage_put<1>(st, 0, dHd, w, lane);
+    stage_put<2>(st, X_ROW, A2, w, lane);
+    pc_sync();
+    f32x16 GA2[2], GA1[2], GH[1];
+    bwd_layer<2, 1, 16, 32>(W + L_WH, S64, dHd, GA2, lane);
+    relu_mask<2>(GA2, A2);
+    pc_sync();
+    // sigma trunk 1
+    stage_put<2>(st, 0, GA2, w, lane);
+    stage_put<2>(st, X_ROW, A1, w, lane);
+    pc_sync();
+    bwd_layer<2, 2, 64, 64>(W + L_W1, S64, GA2, GA1, lane);
+    relu_mask<2>(GA1, A1);
+    pc_sync();
+    // sigma trunk 0
+    f32x16 X0[1];
+    load_tiles<1>(h0, 32, 0, 32, m, ok, h, X0);
+    stage_put<2>(st, 0, GA1, w, lane);
+    stage_put<1>(st, X_ROW, X0, w, lane);
+    pc_sync();
+    if (gh0) {
+        bwd_layer<1, 2, 64, 64>(W + L_W0, S32, GA1, GH, lane);
+        store_tiles<1>(gh0, 32, 0, 32, m, ok, h, GH);
+    }
+    pc_sync();
+}
+
+__device__ __forceinline__ void pc_consumer_round(const float* st, int w, int lane, DwAcc& a) {
+    const StageScale sc{0, 0};
+    pc_sync();
+    dw_blocks<1>(st, 0, X_ROW + 16 * w, a.aWC2, a.bWC2, sc, lane);
+    pc_sync();
+    pc_sync();
+    dw_blocks<4>(st, 16 * w, X_ROW, a.aWC1, a.bWC1, sc, lane);
+    pc_sync();
+    pc_sync();
+    dw_blocks<2>(st, 16 * w, X_ROW, a.aWC0, a.bWC0, sc, lane);
+    pc_sync();
+    pc_sync();
+    dw_blocks<1>(st, 0, X_ROW + 16 * w, a.aHD, a.bHD, sc, lane);
+    pc_sync();
+    pc_sync();
+    dw_blocks<4>(st, 16 * w, X_ROW, a.aW1, a.bW1, sc, lane);
+    pc_sync();
+    pc_sync();
+    dw_blocks<2>(st, 16 * w, X_ROW, a.aW0, a.bW0, sc, lane);
+    pc_sync();
+}
+
+__global__ void __launch_bounds__(512) mlp_bwd_dw_pc_kernel(const float* __restrict__ img, const float* __restrict__ h0,
+                                                            const float* __restrict__ sh, const float* __restrict__ out,
+                                                            const float* __restrict__ gout, int64_t M,
+                                                            float* __restrict__ gh0, float* __restrict__ partial) {
+    __shared__ __attribute__((aligned(16))) float Wl[L_FLOATS];
+    __shared__ __attribute__((aligned(16))) float st_base[ST_FLOATS];
+    stage_weights(img, Wl);
+    __syncthreads();
+    const int lane0 = threadIdx.x & 63, j = lane0 & 31;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), w = wv & 3;
+    const int64_t ntiles = (M + 31) / 32;
+    // rounds are uniform over the workgroup (the same 12 barriers per round in both roles)
+    if (wv < 4) {
+        for (int64_t base = (int64_t)blockIdx.x * 4; base < ntiles; base += (int64_t)gridDim.x * 4) {
+            const int64_t m = (base + w) * 32 + j;
+            pc_producer_round(Wl + opaque_s(0), st_base + opaque_s(0), h0, sh, out, gout, m, m < M, w,
+                              opaque_v(lane0), gh0);
+        }
+    } else {
+        DwAcc a;
+        dw_zero(a);
+        for (int64_t base = (int64_t)blockIdx.x * 4; base < ntiles; base += (int64_t)gridDim.x * 4)
+            pc_consumer_round(st_base + opaque_s(0), w, opaque_v(lane0), a);
+        dw_flush(a, partial + (int64_t)blockIdx.x * NDW, w, lane0);
+    }
+}
+#endif
+
 // Pair-list variant (routed container): workgroup b takes the contiguous rounds [b R / G, (b+1) R / G)
 // (R = seg[K] / 128 from the device); when the expert of the next round differs, the running sums go
 // to copy (b, expert) and restart, and the new expert's image is staged.  mlp_dw_reduce_pairs_kernel
@@ -1253,8 +1396,13 @@ extern "C" int ACN_MLP_API(acn_mlp_train_bwd_dw)(const float* h0, const float* s
     const int64_t tiles = (M + 31) / 32, want = (tiles + 3) / 4;
     const int nblk = (int)(want < MAX_DW_BLOCKS ? want : MAX_DW_BLOCKS);
     hipLaunchKernelGGL(mlp_pack_kernel, dim3((L_FLOATS + 255) / 256), dim3(256), 0, s, ptrs(w), img);
+#if ACN_DW_PC && !ACN_DW_F16X3
+    hipLaunchKernelGGL(mlp_bwd_dw_pc_kernel, dim3(nblk), dim3(512), 0, s, (const float*)img, h0, sh, out, gout, M, gh0,
+                       partial);
+#else
     hipLaunchKernelGGL(mlp_bwd_dw_kernel, dim3(nblk), dim3(256), 0, s, (const float*)img, h0, sh, out, gout, M, gh0,
                        partial);
+#endif
     hipLaunchKernelGGL(mlp_dw_reduce_kernel, dim3((NDW + 31) / 32), dim3(256), 0, s, (const float*)partial, nblk,
                        dw);
     return acn_check_launch("acn_mlp_train_bwd_dw");
