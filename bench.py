@@ -1008,16 +1008,17 @@ def main():
                     sec["requests_over_distinct_segments"] = round(sec["atomic_requests_per_launch"] / hash_segments, 3)
                     sec["achieved_requests_per_s"] = round(sec["atomic_requests_per_launch"] / (hash_bwd_ms * 1e-3), 1)
     if a.workload == "meta":
-        # dominant kernel: the fused MLP backward (mlp_bwd_dw_kernel, ~40% of the step); FLOP roofline on the
+        # dominant kernel: the fused MLP backward (mlp_bwd_dw_pc_kernel, ~40% of the step); FLOP roofline on the
         # algorithmic dW + dX MACs x 2 (ops.mlp_bwd_flops) against the fp32 matrix peak (the products are
         # fp32-accurate: fp16x3 split for dX, fp32 MFMA for dW); the forward recompute is stated beside it
         dw_tf = dw_flop / (dw_ms * 1e-3) / 1e12
         adam = roofline
         roofline = {"bound": "mfma", "achieved": round(dw_tf, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(dw_tf / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
-                    "kernel": "mlp_bwd_dw_kernel (fused MLP backward: forward recompute in registers, dX chain on the "
-                              "fp16x3 split, dW + db on fp32 MFMA; kernel_ms = HIP events around the "
-                              "acn_mlp_train_bwd_dw call = weight pack + mlp_bwd_dw_kernel + mlp_dw_reduce_kernel)",
+                    "kernel": "mlp_bwd_dw_pc_kernel (fused MLP backward, producer / consumer waves: forward recompute "
+                              "+ dX chain on the fp16x3 split in waves 0-3, dW + db on fp32 MFMA in waves 4-7; "
+                              "kernel_ms = HIP events around the acn_mlp_train_bwd_dw call = weight pack + "
+                              "mlp_bwd_dw_pc_kernel + mlp_dw_reduce_kernel)",
                     "kernel_ms": round(dw_ms, 4), "launches_per_step": dw_launches,
                     "share_of_step": round(dw_ms * dw_launches / ms_per_step, 4),
                     "samples_per_launch": int(dw_samples), "flop_per_launch": int(dw_flop),
