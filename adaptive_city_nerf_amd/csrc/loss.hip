@@ -76,12 +76,20 @@ __global__ void __launch_bounds__(kWsThreads) mse_linear_fwd_ws_kernel(const flo
         last = atomicAdd(counter, 1u) == gridDim.x - 1;
     }
     __syncthreads();
-    if (last && threadIdx.x == 0) {
+    // last workgroup: wave 0's lanes load the G <= 64 partials at once (one round trip to the coherent
+    // level instead of G dependent ones), then every lane adds them in index order through the
+    // cross-lane shuffle -- the same summation order as a serial loop over partials[0..G)
+    if (last && threadIdx.x < 64) {
         __threadfence();
+        const double v = threadIdx.x < gridDim.x
+                             ? __hip_atomic_load(&partials[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                             : 0.0;
         double t = 0.0;
-        for (unsigned int b = 0; b < gridDim.x; ++b) t += __hip_atomic_load(&partials[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        loss[0] = (float)(t / (double)n);
-        counter[0] = 0u;
+        for (unsigned int b = 0; b < gridDim.x; ++b) t += __shfl(v, (int)b);
+        if (threadIdx.x == 0) {
+            loss[0] = (float)(t / (double)n);
+            counter[0] = 0u;
+        }
     }
 }
 
