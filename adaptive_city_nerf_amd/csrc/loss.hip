@@ -44,12 +44,17 @@ __global__ void __launch_bounds__(kThreads) mse_linear_fwd_kernel(const float* _
     }
 }
 
-// Multi-workgroup form (acn_mse_linear_fwd_ws): G workgroups of 256 threads, thread i of workgroup b
-// sums elements b*256 + i, + G*256, ... in double; the workgroup sums in a fixed order into partials[b];
-// the last workgroup to finish (ticket counter) adds partials[0..G) in order, writes the loss and resets
-// the counter.  Deterministic (fixed assignment and order for a given n).
+// Multi-workgroup form (acn_mse_linear_fwd_ws): G workgroups of 256 threads (G sized for ~2 elements per
+// thread, at most 256), thread i of workgroup b sums elements b*256 + i, + G*256, ... in double; the
+// workgroup sums in a fixed order into partials[b]; the last workgroup to finish (ticket counter) adds
+// partials[0..G) in order, writes the loss and resets the counter.  Deterministic (fixed assignment and
+// order for a given n).  The time of this launch is memory latency, not arithmetic: a thread's loads are
+// issued 4 at a time ahead of the sums (same per-thread order), and the grid is wide enough that a thread
+// has one or two such rounds (8 dependent rounds per thread measured 11 us at n = 12000,
+// tools/micro/loss_micro.py).
 constexpr int kWsThreads = 256;
-constexpr int kWsMaxBlocks = 64;
+constexpr int kWsMaxBlocks = 256;
+constexpr int kWsPerThread = 2;
 __global__ void __launch_bounds__(kWsThreads) mse_linear_fwd_ws_kernel(const float* __restrict__ pred,
                                                                        const float* __restrict__ gt, int64_t n,
                                                                        double* __restrict__ partials,
@@ -59,10 +64,21 @@ __global__ void __launch_bounds__(kWsThreads) mse_linear_fwd_ws_kernel(const flo
     __shared__ bool last;
     double acc = 0.0;
     const int64_t stride = (int64_t)gridDim.x * kWsThreads;
-#pragma unroll 8
-    for (int64_t e = (int64_t)blockIdx.x * kWsThreads + threadIdx.x; e < n; e += stride) {
-        const float d = clamp01(pred[e]) - gt_linear(gt[e]);
-        acc += (double)(d * d);
+    for (int64_t e = (int64_t)blockIdx.x * kWsThreads + threadIdx.x; e < n; e += 4 * stride) {
+        float p[4], q[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t i = e + u * stride;
+            p[u] = i < n ? pred[i] : 0.0f;
+            q[u] = i < n ? gt[i] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (e + u * stride < n) {
+                const float d = clamp01(p[u]) - gt_linear(q[u]);
+                acc += (double)(d * d);
+            }
+        }
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off);
@@ -76,16 +92,22 @@ __global__ void __launch_bounds__(kWsThreads) mse_linear_fwd_ws_kernel(const flo
         last = atomicAdd(counter, 1u) == gridDim.x - 1;
     }
     __syncthreads();
-    // last workgroup: wave 0's lanes load the G <= 64 partials at once (one round trip to the coherent
-    // level instead of G dependent ones), then every lane adds them in index order through the
-    // cross-lane shuffle -- the same summation order as a serial loop over partials[0..G)
+    // last workgroup: wave 0's lanes load the G <= 256 partials at once (lane l: partials[l + 64 j]), then
+    // every lane adds them in index order through the cross-lane shuffle -- the same summation order as a
+    // serial loop over partials[0..G)
     if (last && threadIdx.x < 64) {
         __threadfence();
-        const double v = threadIdx.x < gridDim.x
-                             ? __hip_atomic_load(&partials[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                             : 0.0;
+        const unsigned int G = gridDim.x;
+        double v[kWsMaxBlocks / 64];
+#pragma unroll
+        for (int j = 0; j < kWsMaxBlocks / 64; ++j) {
+            const unsigned int b = threadIdx.x + 64u * j;
+            v[j] = b < G ? __hip_atomic_load(&partials[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+        }
         double t = 0.0;
-        for (unsigned int b = 0; b < gridDim.x; ++b) t += __shfl(v, (int)b);
+#pragma unroll
+        for (int j = 0; j < kWsMaxBlocks / 64; ++j)
+            for (unsigned int b = 0; b < 64u && 64u * j + b < G; ++b) t += __shfl(v[j], (int)b);
         if (threadIdx.x == 0) {
             loss[0] = (float)(t / (double)n);
             counter[0] = 0u;
@@ -120,7 +142,7 @@ extern "C" int acn_mse_linear_fwd_ws(const float* pred, const float* gt, int64_t
                                      size_t workspace_bytes, void* stream) {
     ACN_REQUIRE(n >= 1 && pred && gt && loss && workspace, "acn_mse_linear_fwd_ws: bad arguments");
     ACN_REQUIRE(workspace_bytes >= acn_mse_linear_workspace_bytes(), "acn_mse_linear_fwd_ws: workspace too small");
-    int64_t g = (n + kWsThreads * 8 - 1) / (kWsThreads * 8);
+    int64_t g = (n + kWsThreads * kWsPerThread - 1) / (kWsThreads * kWsPerThread);
     g = g < 1 ? 1 : (g > kWsMaxBlocks ? kWsMaxBlocks : g);
     double* partials = (double*)workspace;
     unsigned int* counter = (unsigned int*)((char*)workspace + kWsMaxBlocks * sizeof(double));

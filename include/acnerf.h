@@ -575,7 +575,7 @@ int acn_mlp_train_bwd_dw_pairs(const float* h0, const float* sh, const float* ou
  * bwd: g_pred = 2/n * (clamp(pred) - gt_lin) * g_loss[0] where 0 <= pred <= 1, else 0 (mse_loss_backward
  * through clamp's backward).  g_loss is a DEVICE scalar (graph-replayable). */
 int acn_mse_linear_fwd(const float* pred, const float* gt, int64_t n, float* loss, void* stream);
-/* The same loss over up to 64 workgroups (deterministic: fixed per-thread assignment and reduction order
+/* The same loss over up to 256 workgroups (deterministic: fixed per-thread assignment and reduction order
  * for a given n; a last-workgroup ticket adds the workgroup sums in order).  workspace: a device buffer of
  * acn_mse_linear_workspace_bytes(), ZEROED once before first use (the call leaves its counter at 0 again);
  * one workspace per stream. */
