@@ -359,6 +359,25 @@ class SlottedAdam:
                 ptrs += [mp[0].data_ptr(), mp[1].data_ptr()] if ok else [0, 0]
             if any(ptrs):
                 self.segmaps = torch.tensor(ptrs, dtype=torch.int64).to(dev)
+        # the clip norm's own pass visits only the tensors whose sum of squares it computes: rows flagged
+        # NORM_ELSEWHERE (the routed step's tables: their share is telescoped from the scatter) would launch
+        # one empty workgroup per 256 KiB chunk -- ~4,100 of them against ~120 live ones in C5 -- and the
+        # reduction would then read ~4,100 partials (zeros) per step
+        self.norm_plan = None
+        keep = [t for t, f in enumerate(fl) if not f & NORM_ELSEWHERE_FLAG]
+        if keep and len(keep) < len(rows):
+            arr = (_lib.acn_param_desc * len(keep))()
+            first = 0
+            for j, t in enumerate(keep):
+                p, g, m, v, gi = rows[t]
+                arr[j] = _lib.acn_param_desc(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), p.numel(), gi,
+                                             first)
+                first += (p.numel() + ACN_OPTIM_CHUNK - 1) // ACN_OPTIM_CHUNK
+            self.norm_plan = (torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(dev),
+                              torch.cat([torch.full(((rows[t][0].numel() + ACN_OPTIM_CHUNK - 1) // ACN_OPTIM_CHUNK,),
+                                                    j, dtype=torch.int32) for j, t in enumerate(keep)]).to(dev),
+                              first, torch.tensor([fl[t] for t in keep], device=dev, dtype=torch.int32),
+                              torch.empty(first, device=dev, dtype=torch.float64))
         # split_norm (expert parallel): the clip norm's sum of squares in two passes, the per-rank slots
         # (< K) first -- all-reduced over the group by the caller's function -- then the replicated shared
         # slots (>= K) once, added on top (the reference's clip_grad_norm_ over the whole container)
@@ -424,6 +443,11 @@ class SlottedAdam:
                 check(L.acn_grad_sumsq_slots_ex(ptr(self.descs_sh), ptr(self.chunk_sh), self.nchunks_sh,
                                                 ptr(self.flags_sh), ptr(seg), self.K, ptr(self.partials_sh),
                                                 ptr(self.total), ptr(self.total_own), s), "acn_grad_sumsq_slots_ex")
+            elif self.norm_plan is not None:
+                descs, chunks, nch, flags, partials = self.norm_plan
+                check(L.acn_grad_sumsq_slots_ex(ptr(descs), ptr(chunks), nch, ptr(flags), ptr(seg), self.K,
+                                                ptr(partials), ptr(self.total), ptr(table_sumsq), s),
+                      "acn_grad_sumsq_slots_ex")
             else:
                 check(L.acn_grad_sumsq_slots_ex(ptr(self.descs), ptr(self.chunk_tensor), self.nchunks,
                                                 ptr(self.flags), ptr(seg), self.K, ptr(self.partials), ptr(self.total),
