@@ -44,7 +44,7 @@ from ._lib import graph_capture
 from .expert_parallel import expert_owner, global_clip_grad_norm_
 from .encodings import accumulate_table_grad
 from .optim import FusedAdam
-from .ray_rendering import encoding_frozen, second_order
+from .ray_rendering import encoding_frozen, inner_loop_background_cache, second_order
 from .train import compute_mse_loss
 
 
@@ -110,6 +110,12 @@ def task_adapt(P, model, support, inner_lr, iterations, active_module=None):
     base = model.submodules[active_module] if active_module is not None else model
     fast = extract_module_params(base, copy=(algo == "reptile"))
     inner_losses = []
+    with inner_loop_background_cache() if first_order else contextlib.nullcontext():
+        return _inner_steps(P, model, support, inner_lr, iterations, active_module, first_order, fast, inner_losses)
+
+
+def _inner_steps(P, model, support, inner_lr, iterations, active_module, first_order, fast, inner_losses):
+    """task_adapt's inner gradient steps (meta_core.py:30-64)."""
     for _ in range(int(iterations)):
         with second_order(not first_order), encoding_frozen(first_order):
             loss = compute_loss(P, model, support, params=fast, active_module=active_module, grad_buffer={},

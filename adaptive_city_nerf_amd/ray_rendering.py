@@ -67,6 +67,36 @@ def encoding_frozen(enabled: bool = True):
         _GRAPH_MODE.frozen_encoding = prev
 
 
+@contextmanager
+def inner_loop_background_cache():
+    """Within this context (one first-order task_adapt call), frozen-encoding renders reuse the background
+    head's output for rays they have already rendered: the head is not a fast weight and the support rays do
+    not change between inner steps, so steps 2..n would recompute the same values (a strided-directions
+    copy and a background launch per step).  Entries hold their rays tensor (compared by identity) and end
+    with the context.  Only the model's background head is cached ('random' backgrounds are re-drawn per
+    render, as in the reference).  Thread-local."""
+    prev = getattr(_GRAPH_MODE, "bg_cache", None)
+    _GRAPH_MODE.bg_cache = {}
+    try:
+        yield
+    finally:
+        _GRAPH_MODE.bg_cache = prev
+
+
+def _frozen_background(model, rays, params, rgb_sigma, N, bg_color_default):
+    """The background of a frozen-encoding render (no autograd), through the inner-loop cache when open."""
+    cache = getattr(_GRAPH_MODE, "bg_cache", None)
+    if cache is None or not getattr(model, "use_bg_nerf", False):
+        return _get_bg_rgb(model, rays[:, 3:6], params, rgb_sigma, N=N, bg_color_default=bg_color_default)
+    key = (id(model), id(rays))
+    hit = cache.get(key)
+    if hit is not None and hit[0] is rays and hit[1] == rays._version:
+        return hit[2]
+    bg = _get_bg_rgb(model, rays[:, 3:6], params, rgb_sigma, N=N, bg_color_default=bg_color_default)
+    cache[key] = (rays, rays._version, bg)
+    return bg
+
+
 # ============================== BG helpers ===============================
 def _get_bg_rgb(model, dirs: Tensor, params, rgb_sigma_or_map, N: int, bg_color_default: str) -> Optional[Tensor]:
     """Background RGB: the model's background head if it has one, else a default colour (:23-45)."""
@@ -337,7 +367,7 @@ def render_rays_stratified(model, rays: Tensor, ray_samples: int, params=None, a
         rgb_sigma = _FusedMLPFn.apply(h0.contiguous(), sh, *ws).view(N, ray_samples, 4)
         if getattr(_GRAPH_MODE, "frozen_encoding", False):
             with torch.no_grad():  # nor is the shared background head a fast weight: one fused HIP launch
-                bg_rgb = _get_bg_rgb(model, rays[:, 3:6], params, rgb_sigma, N=N, bg_color_default=bg_color_default)
+                bg_rgb = _frozen_background(model, rays, params, rgb_sigma, N, bg_color_default)
         else:
             bg_rgb = _get_bg_rgb(model, rays[:, 3:6], params, rgb_sigma, N=N, bg_color_default=bg_color_default)
         return volume_render(rgb_sigma, t_vals, bg_rgb=bg_rgb, raw_rgb=False, raw_sigma=False,
