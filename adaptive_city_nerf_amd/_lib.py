@@ -140,6 +140,7 @@ SIGNATURES = {
     "acn_mlp_dw_workspace_bytes": ([], C.c_size_t),
     "acn_sample_stratified": ([vp, i64, C.c_int, vp, vp, vp, C.c_float, C.c_float, vp, vp, vp, vp], C.c_int),
     "acn_mlp_train_bwd_dw": ([vp, vp, vp, vp, i64, vp, vp, vp, vp, vp], C.c_int),
+    "acn_mlp_train_bwd_dw_img": ([vp, vp, vp, vp, i64, vp, vp, vp, vp, vp], C.c_int),
     # routed.hip
     "acn_routed_workspace_bytes": ([i64, i32], C.c_size_t),
     "acn_routed_count": ([vp, i64, i32, vp, vp, i32, vp, vp, vp, sz, vp], C.c_int),
@@ -173,9 +174,9 @@ SIGNATURES = {
     # clusters.hip
     "acn_voronoi_route": ([vp, i64, i32, vp, i32, i32, C.c_double, i32, i32, vp, vp, vp, vp, vp, vp], C.c_int),
 }
-# the exact-fp32 training MLP: the same nine entry points, suffixed _exact (mlp_train.hip built twice)
+# the exact-fp32 training MLP: the same ten entry points, suffixed _exact (mlp_train.hip built twice)
 MLP_ENTRY_POINTS = ("acn_mlp_workspace_bytes", "acn_mlp_train_fwd", "acn_mlp_train_bwd", "acn_mlp_dw_workspace_bytes",
-                    "acn_mlp_train_bwd_dw", "acn_mlp_pairs_workspace_bytes", "acn_mlp_pack_pairs",
+                    "acn_mlp_train_bwd_dw", "acn_mlp_train_bwd_dw_img", "acn_mlp_pairs_workspace_bytes", "acn_mlp_pack_pairs",
                     "acn_mlp_train_fwd_pairs", "acn_mlp_train_bwd_dw_pairs")
 SIGNATURES.update({n + "_exact": SIGNATURES[n] for n in MLP_ENTRY_POINTS})
 

@@ -1382,6 +1382,23 @@ extern "C" size_t ACN_MLP_API(acn_mlp_dw_workspace_bytes)(void) {
     return ((size_t)L_FLOATS + (size_t)MAX_DW_BLOCKS * NDW) * sizeof(float);
 }
 
+namespace {
+// the fused backward + the copy reduction, on a packed weight image
+int bwd_dw_launch(const float* h0, const float* sh, const float* out, const float* gout, int64_t M, const float* img,
+                  float* dw, float* gh0, float* partial, hipStream_t s) {
+    const int64_t tiles = (M + 31) / 32, want = (tiles + 3) / 4;
+    const int nblk = (int)(want < MAX_DW_BLOCKS ? want : MAX_DW_BLOCKS);
+#if ACN_DW_PC && !ACN_DW_F16X3
+    hipLaunchKernelGGL(mlp_bwd_dw_pc_kernel, dim3(nblk), dim3(512), 0, s, img, h0, sh, out, gout, M, gh0, partial);
+#else
+    hipLaunchKernelGGL(mlp_bwd_dw_kernel, dim3(nblk), dim3(256), 0, s, img, h0, sh, out, gout, M, gh0, partial);
+#endif
+    hipLaunchKernelGGL(mlp_dw_reduce_kernel, dim3((NDW + 31) / 32), dim3(256), 0, s, (const float*)partial, nblk,
+                       dw);
+    return acn_check_launch("acn_mlp_train_bwd_dw");
+}
+}  // namespace
+
 extern "C" int ACN_MLP_API(acn_mlp_train_bwd_dw)(const float* h0, const float* sh, const float* out, const float* gout, int64_t M,
                                     const acn_mlp* w, float* dw, float* gh0, void* workspace, void* stream) {
     ACN_REQUIRE(M >= 0 && w && workspace && dw, "acn_mlp_train_bwd_dw: bad arguments");
@@ -1393,19 +1410,23 @@ extern "C" int ACN_MLP_API(acn_mlp_train_bwd_dw)(const float* h0, const float* s
     ACN_REQUIRE(h0 && sh && out && gout, "acn_mlp_train_bwd_dw: NULL pointer");
     float* img = (float*)workspace;
     float* partial = img + L_FLOATS;  // L_FLOATS is a multiple of 4: 16-B aligned
-    const int64_t tiles = (M + 31) / 32, want = (tiles + 3) / 4;
-    const int nblk = (int)(want < MAX_DW_BLOCKS ? want : MAX_DW_BLOCKS);
     hipLaunchKernelGGL(mlp_pack_kernel, dim3((L_FLOATS + 255) / 256), dim3(256), 0, s, ptrs(w), img);
-#if ACN_DW_PC && !ACN_DW_F16X3
-    hipLaunchKernelGGL(mlp_bwd_dw_pc_kernel, dim3(nblk), dim3(512), 0, s, (const float*)img, h0, sh, out, gout, M, gh0,
-                       partial);
-#else
-    hipLaunchKernelGGL(mlp_bwd_dw_kernel, dim3(nblk), dim3(256), 0, s, (const float*)img, h0, sh, out, gout, M, gh0,
-                       partial);
-#endif
-    hipLaunchKernelGGL(mlp_dw_reduce_kernel, dim3((NDW + 31) / 32), dim3(256), 0, s, (const float*)partial, nblk,
-                       dw);
-    return acn_check_launch("acn_mlp_train_bwd_dw");
+    return bwd_dw_launch(h0, sh, out, gout, M, img, dw, gh0, partial, s);
+}
+
+// the same backward on the image acn_mlp_train_fwd packed into ITS workspace for the same weights (one
+// pack per forward + backward pair instead of two); workspace: acn_mlp_dw_workspace_bytes() as above
+extern "C" int ACN_MLP_API(acn_mlp_train_bwd_dw_img)(const float* h0, const float* sh, const float* out, const float* gout,
+                                        int64_t M, const float* img, float* dw, float* gh0, void* workspace,
+                                        void* stream) {
+    ACN_REQUIRE(M >= 0 && img && workspace && dw, "acn_mlp_train_bwd_dw_img: bad arguments");
+    hipStream_t s = (hipStream_t)stream;
+    if (M == 0) {
+        const hipError_t e = hipMemsetAsync(dw, 0, (size_t)NDW * sizeof(float), s);
+        return e == hipSuccess ? ACN_OK : acn_set_error((int)e, "acn_mlp_train_bwd_dw_img: memset failed");
+    }
+    ACN_REQUIRE(h0 && sh && out && gout, "acn_mlp_train_bwd_dw_img: NULL pointer");
+    return bwd_dw_launch(h0, sh, out, gout, M, img, dw, gh0, (float*)workspace + L_FLOATS, s);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -389,8 +389,13 @@ class _FusedMLPFn(torch.autograd.Function):
     def forward(ctx, h0, sh, *ws):
         need = any(ctx.needs_input_grad)
         fused = _FusedMLPFn.DW_FUSED
-        out, save = ops.mlp_train_fwd(h0, sh, ws, save=need and not fused)
+        # the forward's packed weight image is kept for the fused backward (same weights: autograd's saved-
+        # tensor version check rejects an in-place change in between), which then packs nothing itself
+        prec = ops.TRAIN_MLP_PRECISION
+        out, save, img = ops.mlp_train_fwd(h0, sh, ws, save=need and not fused, precision=prec, return_img=True)
         ctx.fused = fused
+        ctx.prec = prec
+        ctx.img = img if need and fused else None
         if need:
             if fused:
                 ctx.save_for_backward(h0, sh, out, *ws)
@@ -403,7 +408,9 @@ class _FusedMLPFn(torch.autograd.Function):
         need = ctx.needs_input_grad[2:]
         if ctx.fused:
             h0, sh, out, *ws = ctx.saved_tensors
-            grads, gh = ops.mlp_train_bwd_dw(h0, sh, out, g.contiguous(), ws, want_h0=ctx.needs_input_grad[0])
+            grads, gh = ops.mlp_train_bwd_dw(h0, sh, out, g.contiguous(), ws, want_h0=ctx.needs_input_grad[0],
+                                             img=ctx.img, precision=ctx.prec)
+            ctx.img = None
             return (gh, None, *[gr if n else None for gr, n in zip(grads, need)])
         save, out, *ws = ctx.saved_tensors
         gs, gh = ops.mlp_train_bwd(save, out, g.contiguous(), ws, want_h0=ctx.needs_input_grad[0])

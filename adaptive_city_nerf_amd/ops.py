@@ -522,15 +522,21 @@ def _fm_zeros(M: int, cols: int, device) -> torch.Tensor:
     return t
 
 
-def mlp_train_fwd(h0: torch.Tensor, sh: torch.Tensor, ws: Sequence[torch.Tensor], save: bool = True):
-    """(M,32) hash features + (M,16) SH -> out (M,4) and the feature-major saved layer inputs (or None)."""
+def mlp_train_fwd(h0: torch.Tensor, sh: torch.Tensor, ws: Sequence[torch.Tensor], save: bool = True,
+                  precision: Optional[str] = None, return_img: bool = False):
+    """(M,32) hash features + (M,16) SH -> out (M,4) and the feature-major saved layer inputs (or None);
+    with ``return_img`` also the call's packed weight image (for mlp_train_bwd_dw(img=...))."""
     require_hip(h0, "MetaNGP MLP (training)")
     M = h0.shape[0]
     out = torch.empty(M, 4, device=h0.device, dtype=torch.float32)
     sv = _fm_zeros(M, MLP_SAVE_COLS, h0.device) if save else None
     w = _mlp_struct(ws)
-    check(mlp_fn("acn_mlp_train_fwd")(ptr(h0), ptr(sh), M, C.byref(w), ptr(out), ptr(sv) if save else None,
-                                       ptr(_mlp_ws(h0.device)), stream_of(h0)), "acn_mlp_train_fwd")
+    img = torch.empty(int(mlp_fn("acn_mlp_workspace_bytes", precision)()), dtype=torch.uint8, device=h0.device)
+    check(mlp_fn("acn_mlp_train_fwd", precision)(ptr(h0), ptr(sh), M, C.byref(w), ptr(out),
+                                                  ptr(sv) if save else None, ptr(img), stream_of(h0)),
+          "acn_mlp_train_fwd")
+    if return_img:
+        return out, sv, (img if M > 0 else None)
     return out, sv
 
 
@@ -585,22 +591,30 @@ def mlp_bwd_flops(M: int, want_h0: bool) -> int:
 
 
 def mlp_train_bwd_dw(h0: torch.Tensor, sh: torch.Tensor, out: torch.Tensor, gout: torch.Tensor,
-                     ws: Sequence[torch.Tensor], want_h0: bool = True):
+                     ws: Sequence[torch.Tensor], want_h0: bool = True, img: Optional[torch.Tensor] = None,
+                     precision: Optional[str] = None):
     """Fused backward: the 14 weight / bias gradients (views of one flat buffer, nn.Linear shapes) and
-    dL/dh0 (M, 32) or None, from h0 / sh (the forward is re-run in registers) and dL/dout."""
+    dL/dh0 (M, 32) or None, from h0 / sh (the forward is re-run in registers) and dL/dout.  ``img``: the
+    packed image mlp_train_fwd(return_img=True) returned for the same weights and precision (the
+    backward then skips its own pack)."""
     require_hip(h0, "MetaNGP MLP (training)")
     M = out.shape[0]
     dw = torch.empty(MLP_DW_FLOATS, device=out.device, dtype=torch.float32)
     gh = torch.empty(M, 32, device=out.device, dtype=torch.float32) if want_h0 else None
-    wsp = torch.empty(int(mlp_fn("acn_mlp_dw_workspace_bytes")()), dtype=torch.uint8, device=out.device)
-    w = _mlp_struct(ws)
+    wsp = torch.empty(int(mlp_fn("acn_mlp_dw_workspace_bytes", precision)()), dtype=torch.uint8, device=out.device)
     hook = DW_HOOK
     if hook is not None:
         e0 = torch.cuda.Event(enable_timing=True)
         e0.record()
-    check(mlp_fn("acn_mlp_train_bwd_dw")(ptr(h0), ptr(sh), ptr(out), ptr(gout), M, C.byref(w), ptr(dw),
-                                          ptr(gh) if want_h0 else None, ptr(wsp), stream_of(out)),
-          "acn_mlp_train_bwd_dw")
+    if img is not None:
+        check(mlp_fn("acn_mlp_train_bwd_dw_img", precision)(ptr(h0), ptr(sh), ptr(out), ptr(gout), M, ptr(img),
+                                                             ptr(dw), ptr(gh) if want_h0 else None, ptr(wsp),
+                                                             stream_of(out)), "acn_mlp_train_bwd_dw_img")
+    else:
+        w = _mlp_struct(ws)
+        check(mlp_fn("acn_mlp_train_bwd_dw", precision)(ptr(h0), ptr(sh), ptr(out), ptr(gout), M, C.byref(w),
+                                                         ptr(dw), ptr(gh) if want_h0 else None, ptr(wsp),
+                                                         stream_of(out)), "acn_mlp_train_bwd_dw")
     if hook is not None:
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()

@@ -418,6 +418,11 @@ int acn_mlp_train_bwd(const float* save, const float* out, const float* gout, in
 size_t acn_mlp_dw_workspace_bytes(void);
 int acn_mlp_train_bwd_dw(const float* h0, const float* sh, const float* out, const float* gout, int64_t M,
                          const acn_mlp* w, float* dw, float* gh0, void* workspace, void* stream);
+/* acn_mlp_train_bwd_dw on a packed weight image instead of acn_mlp pointers: img = the workspace of the
+ * acn_mlp_train_fwd call for the same weights (that call packs them there; reusing it saves the backward's
+ * own pack launch).  The weights must not have changed since that forward.                          */
+int acn_mlp_train_bwd_dw_img(const float* h0, const float* sh, const float* out, const float* gout, int64_t M,
+                             const float* img, float* dw, float* gh0, void* workspace, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Episodic task routing (data.hip).  Replaces TaskDataset's region clip + micro-cell assignment
@@ -587,7 +592,7 @@ int acn_mse_linear_bwd(const float* pred, const float* gt, int64_t n, const floa
 
 
 /* The training MLP in exact fp32 (v_mfma_f32_32x32x2_f32 layer products instead of the fp32-accurate fp16x3
- * split): the same nine entry points, suffixed _exact, same arguments and semantics; workspaces must come
+ * split): the same ten entry points, suffixed _exact, same arguments and semantics; workspaces must come
  * from the _exact size functions (the weight image layout differs).  mlp_train.hip compiled a second time
  * with -DACN_TRAIN_F16X3=0 (a runtime precision switch for parity studies: DESIGN.md 4). */
 size_t acn_mlp_workspace_bytes_exact(void);
@@ -598,6 +603,8 @@ int acn_mlp_train_bwd_exact(const float* save, const float* out, const float* go
 size_t acn_mlp_dw_workspace_bytes_exact(void);
 int acn_mlp_train_bwd_dw_exact(const float* h0, const float* sh, const float* out, const float* gout, int64_t M,
                          const acn_mlp* w, float* dw, float* gh0, void* workspace, void* stream);
+int acn_mlp_train_bwd_dw_img_exact(const float* h0, const float* sh, const float* out, const float* gout, int64_t M,
+                             const float* img, float* dw, float* gh0, void* workspace, void* stream);
 size_t acn_mlp_pairs_workspace_bytes_exact(int K);
 int acn_mlp_pack_pairs_exact(const acn_mlp* const* w, int K, void* workspace, void* stream);
 int acn_mlp_train_fwd_pairs_exact(const float* h0, const float* sh, const int64_t* seg, int K, const void* workspace,

@@ -96,6 +96,32 @@ def test_fused_dw_matches_split_path(n):
         assert np.abs(a - b).max() <= 2e-5 * scale + 1e-9, (k, np.abs(a - b).max(), scale)
 
 
+@pytest.mark.parametrize("precision", ["fp16x3", "fp32"])
+def test_fused_dw_on_forward_image(precision):
+    """acn_mlp_train_bwd_dw_img (the backward on the image the forward packed, no pack of its own) against
+    acn_mlp_train_bwd_dw (its own pack of the same weights): the same kernels on the same image."""
+    from adaptive_city_nerf_amd import ops
+    n = 4113
+    g = torch.Generator(device="cuda").manual_seed(11)
+    sub = _expert()
+    ws = [t.detach().contiguous() for t in (
+        sub.sigma_trunk[0].linear.weight, sub.sigma_trunk[0].linear.bias, sub.sigma_trunk[1].linear.weight,
+        sub.sigma_trunk[1].linear.bias, sub.sigma_head.weight, sub.sigma_head.bias, sub.geo_head.weight,
+        sub.geo_head.bias, sub.color_mlp[0].linear.weight, sub.color_mlp[0].linear.bias,
+        sub.color_mlp[1].linear.weight, sub.color_mlp[1].linear.bias, sub.color_mlp[2].weight,
+        sub.color_mlp[2].bias)]
+    h0 = (torch.rand(n, 32, device="cuda", generator=g) - 0.5) * 2
+    sh = (torch.rand(n, 16, device="cuda", generator=g) - 0.5) * 2
+    gout = torch.randn(n, 4, device="cuda", generator=g)
+    out, _, img = ops.mlp_train_fwd(h0, sh, ws, save=False, precision=precision, return_img=True)
+    a, gha = ops.mlp_train_bwd_dw(h0, sh, out, gout, ws, want_h0=True, precision=precision)
+    b, ghb = ops.mlp_train_bwd_dw(h0, sh, out, gout, ws, want_h0=True, img=img, precision=precision)
+    assert torch.equal(gha, ghb)
+    for x, y in zip(a, b):
+        scale = max(float(x.abs().max()), 1e-12)
+        assert float((x - y).abs().max()) <= 1e-6 * scale
+
+
 def test_fused_dw_empty_batch():
     from adaptive_city_nerf_amd import ops
     z = torch.zeros(0, 32, device="cuda")
