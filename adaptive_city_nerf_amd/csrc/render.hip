@@ -1104,12 +1104,16 @@ template <int INTERP, int ROUTE>
 __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) render_slots_kernel(FieldCfg cfg, BgArgs bg, RenderParams p) {
     constexpr bool FOLD = ACN_SHFOLD != 0;
     __shared__ __attribute__((aligned(16))) float smem[2 * PK_FLOATS];
-    __shared__ __attribute__((aligned(16))) float cbuf[FOLD ? 16 * 2 * 64 : 4];
+    // per wave: the folded SH bias of the two LDS slots and of the expert read from L2 (every expert's
+    // colour layer 0 runs folded, wherever its weights are read from: a ray's arithmetic must not depend on
+    // which experts its workgroup round keeps in LDS -- that choice depends on the other rays of the batch)
+    __shared__ __attribute__((aligned(16))) float cbuf[FOLD ? 16 * 3 * 64 : 4];
     __shared__ int cnt[kMaxK];
     __shared__ int slot_k[2], restage[2];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    float* cb = FOLD ? cbuf + wave * 2 * 64 : nullptr;
+    float* cb = FOLD ? cbuf + wave * 3 * 64 : nullptr;
+    float* cbg = FOLD ? cb + 2 * 64 : nullptr;
     const float step = 1.0f / (float)(p.S - 1);
     if (threadIdx.x < kMaxK) cnt[threadIdx.x] = 0;
     if (threadIdx.x < 2) slot_k[threadIdx.x] = -1;
@@ -1186,8 +1190,10 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
                                    field_tile<INTERP, FOLD>(Wk, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbk, lane, yr,
                                                             yg, yb, sg);
                                } else {
-                                   field_tile<INTERP, false>(p.packed + (size_t)k * PK_FLOATS, cfg.ex[k], cfg.log2T,
-                                                             px, py, pz, shv, nullptr, lane, yr, yg, yb, sg);
+                                   const float* Wg = p.packed + (size_t)k * PK_FLOATS;
+                                   if (FOLD) fold_sh_bias(Wg, shv, lane, cbg);
+                                   field_tile<INTERP, FOLD>(Wg, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbg, lane, yr,
+                                                            yg, yb, sg);
                                }
                                ys = trunc_exp(sg);
                                return;
@@ -1217,8 +1223,10 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
 #if ACN_SLOTS_NOFALLBACK  // diagnostic only: non-resident experts skipped
                                    r = g = b = sg = 0.0f;
 #else
-                                   field_tile<INTERP, false>(p.packed + (size_t)k * PK_FLOATS, cfg.ex[k], cfg.log2T,
-                                                             px, py, pz, shv, nullptr, lane, r, g, b, sg);
+                                   const float* Wg = p.packed + (size_t)k * PK_FLOATS;
+                                   if (FOLD) fold_sh_bias(Wg, shv, lane, cbg);
+                                   field_tile<INTERP, FOLD>(Wg, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbg, lane, r, g,
+                                                            b, sg);
 #endif
                                }
                                sg = trunc_exp(sg);
