@@ -251,15 +251,38 @@ __device__ __forceinline__ void split_acc2(const f32x16& a0, const f32x16& a1, f
 }
 
 // out[T] = bias + W . X over NK k-steps of 16, three fp16 products per k-step (small terms first)
-template <int NT, int NK>
+// Wait states between the operand split (VALU: v_cvt_pk_f16_f32 writes the B fragments) and the layer's first
+// MFMA.  hipcc (ROCm 7.2) separates them by the 2 wait states of its gfx950 VALU -> MFMA rule; in the routed
+// render's schedule that left rare, timing-dependent wrong B operands: 16 consecutive columns of a tile off by
+// ~1e-4 relative, different run to run (a self-check build that evaluated every tile twice in a row saw ~57
+// mismatching rays per 10 K=8 renders; with this pad, none).  0: compiler only, 1: s_nop 2,
+// 2: 16 wait states, 3: scheduling barrier only.
+#ifndef ACN_X3_NOP
+#define ACN_X3_NOP 2
+#endif
+// REV: k-steps in reverse order (colour layer 0 with per-lane SH: the SH k-step first, the order the per-ray
+// fold accumulates in, so the result is bit-identical to fold_sh_bias + the folded layer)
+template <int NT, int NK, bool REV = false>
 __device__ __forceinline__ void layer_x3(const float* W, int seg, const float* bias_base, int bt, int lane, int h,
                                          const f16x8 (&bh)[NK], const f16x8 (&bl)[NK], f32x16 (&out)[NT],
                                          int nk_used = NK) {
 #pragma unroll
     for (int T = 0; T < NT; ++T) out[T] = bias_frag_at(bias_base, bt + T, h);
+#if ACN_X3_NOP == 1
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 2" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#elif ACN_X3_NOP == 2
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#elif ACN_X3_NOP == 3
+    __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
-    for (int s = 0; s < NK; ++s) {
-        if (s >= nk_used) break;
+    for (int si = 0; si < NK; ++si) {
+        if (si >= nk_used) break;
+        const int s = REV ? NK - 1 - si : si;
 #pragma unroll
         for (int T = 0; T < NT; ++T) {
             const float* fp = W + seg + (((T * NK + s) * 2) * 64 + lane) * 4;
@@ -422,7 +445,10 @@ __device__ __forceinline__ void hash_levels8(const ExpertMeta& em, int log2T, in
 // Returns rgb (after sigmoid) on every lane and sigma_raw on every lane.
 // FOLD: the colour MLP's SH columns + bias were folded per ray into cb (LDS, [tile][h][16],
 // see fold_sh_bias): colour layer 0 then only runs the 8 k-steps of the [sigma_raw, geo] rows.
-template <int INTERP, bool FOLD>
+// SHFIRST (with FOLD false): colour layer 0 runs unfolded on per-lane SH rows, the SH k-step before the
+// [sigma_raw, geo] one -- bit for bit the folded result of a ray whose lanes all carry its SH (the render of
+// compacted samples of several rays, render_routed_kernel)
+template <int INTERP, bool FOLD, bool SHFIRST = false>
 __device__ __forceinline__ void field_tile(const float* W, const ExpertMeta& em, int log2T, float px, float py,
                                            float pz, const float (&shv)[8], const float* cb, int lane, float& rr,
                                            float& rg, float& rb, float& sraw) {
@@ -501,6 +527,7 @@ __device__ __forceinline__ void field_tile(const float* W, const ExpertMeta& em,
         }
         f32x16 c[2];
         if (FOLD) layer_x3<2, 2>(W, PK_WC1, cb, 0, lane, h, ch, cl, c, 1);   // per-ray folded bias
+        else if (SHFIRST) layer_x3<2, 2, true>(W, PK_WC1, W + PK_B, BT_C1, lane, h, ch, cl, c);
         else layer_x3<2, 2>(W, PK_WC1, W + PK_B, BT_C1, lane, h, ch, cl, c);
         relu16(c[0]);
         relu16(c[1]);
@@ -573,14 +600,17 @@ __device__ __forceinline__ void field_tile(const float* W, const ExpertMeta& em,
     }
     {
         constexpr int NG = FOLD ? 2 : 4;
-        f32x4 n0 = ld4(W + PK_WC1 + ((0 * 4 + 0) * 64 + lane) * 4);
-        f32x4 n1 = ld4(W + PK_WC1 + ((1 * 4 + 0) * 64 + lane) * 4);
+        constexpr bool RV = SHFIRST && !FOLD;   // groups 2, 3 (SH rows) first: the fold's order
+        auto gq = [](int i) { return RV ? (i + 2) & 3 : i; };
+        f32x4 n0 = ld4(W + PK_WC1 + ((0 * 4 + gq(0)) * 64 + lane) * 4);
+        f32x4 n1 = ld4(W + PK_WC1 + ((1 * 4 + gq(0)) * 64 + lane) * 4);
 #pragma unroll
-        for (int g = 0; g < NG; ++g) {
+        for (int gi = 0; gi < NG; ++gi) {
+            const int g = gq(gi);
             const f32x4 w0 = n0, w1 = n1;
-            if (g < NG - 1) {
-                n0 = ld4(W + PK_WC1 + ((0 * 4 + g + 1) * 64 + lane) * 4);
-                n1 = ld4(W + PK_WC1 + ((1 * 4 + g + 1) * 64 + lane) * 4);
+            if (gi < NG - 1) {
+                n0 = ld4(W + PK_WC1 + ((0 * 4 + gq(gi + 1)) * 64 + lane) * 4);
+                n1 = ld4(W + PK_WC1 + ((1 * 4 + gq(gi + 1)) * 64 + lane) * 4);
             }
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -945,7 +975,7 @@ __device__ __forceinline__ void render_ray(const RenderParams& p, const BgArgs& 
 #if ACN_DIAG_PHASE
         const uint64_t dA = __builtin_amdgcn_s_memtime();
 #endif
-        field(px, py, pz, shv, folded, yr, yg, yb, ys);
+        field(sc, px, py, pz, shv, folded, yr, yg, yb, ys);
 #if ACN_DIAG_PHASE
         const uint64_t dB = __builtin_amdgcn_s_memtime();
         const uint32_t dS = __builtin_amdgcn_readfirstlane((uint32_t)g_diag_stamp[wave]);
@@ -1033,7 +1063,7 @@ __global__ void __launch_bounds__(1024, 4) render_kernel(FieldCfg cfg, BgArgs bg
     for (; pos < hi; pos += stride) {
         const int64_t ray = p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[pos]) : pos;
         render_ray(p, bg, ray, lane, step,
-                   [&](float px, float py, float pz, const float (&shv)[8], uint32_t& folded, float& yr, float& yg,
+                   [&](int, float px, float py, float pz, const float (&shv)[8], uint32_t& folded, float& yr, float& yg,
                        float& yb, float& ys) {
                        container_tile<INTERP, ROUTE, FOLD>(cfg, W, px, py, pz, shv, cb, &folded, lane, yr, yg, yb, ys);
                    });
@@ -1174,7 +1204,7 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
             const bool single = (m & kSingleRay) != 0u;
             const int k_single = __builtin_ctz(m | kSingleRay);
             render_ray(p, bg, ray, lane, step,
-                       [&](float px, float py, float pz, const float (&shv)[8], uint32_t& folded, float& yr, float& yg,
+                       [&](int, float px, float py, float pz, const float (&shv)[8], uint32_t& folded, float& yr, float& yg,
                            float& yb, float& ys) {
                            if (single) {  // wave-uniform: one expert, weight 1.0f on every sample
                                const int k = k_single;
@@ -1243,6 +1273,395 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
                            }
                        });
         }
+    }
+}
+
+// inclusive scan over the 64 lanes of a wave on DPP: row_shr 1/2/4/8 inside each 16-lane row, then
+// row_bcast:15 / :31 carry the row totals upward (gfx9-family DPP)
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);
+    return v;
+}
+// lanes of this wave (among `valid`) holding the same 6-bit digit, and how many of them sit below this lane
+__device__ __forceinline__ uint64_t same_digit_lanes(bool valid, int dig) {
+    uint64_t m = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+        const uint64_t bb = __ballot(valid && ((dig >> b) & 1));
+        m &= ((dig >> b) & 1) ? bb : ~bb;
+    }
+    return m;
+}
+__device__ __forceinline__ int lanes_below(uint64_t m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+// ------------------------------------------------------------------------------------------
+// Routed render, expert-major chunks (C3 / C4: K > 2 experts, soft or hard routing; round 4).
+//
+// The reference evaluates the container expert by expert over the samples each one owns
+// (meta_container.py:300-337: index_select of the routed samples, MetaNGP.forward, index_add_ of y_k * w_k
+// in expert order) and then composites every ray (ray_rendering.py:114-165).  This kernel does the same
+// per CHUNK of rays, with every expert's MLP image read from LDS:
+//   A  route: every sample of the chunk's rays -> its expert mask (bit k: w_k > 0) in LDS;
+//   B  for each expert k the chunk needs, in ascending k: stage expert k's packed image (58 KB) into the
+//      workgroup's one LDS slot (skipped when it is already there), compact the
+//      chunk's samples that need k into a list, and evaluate them 32 per wave-tile (hash grid + MLP on
+//      per-lane SH: lanes may belong to different rays); each result y_k * w_k is added into the
+//      sample's accumulator in LDS -- 0 + y_a w_a + y_b w_b ... in ascending k, the reference's order;
+//   C  composite: one wave per ray reads its samples' accumulated (rgb, sigma) from LDS and runs the
+//      same compositing / background / output code as render_kernel.
+// Every sample is evaluated once per expert it needs (the per-ray kernels evaluate a whole 32-sample
+// tile for every expert any of its samples needs, and read non-resident experts' weights from L2).
+// Arithmetic per sample and expert is the one render_kernel / render_slots_kernel use (the SH k-step of
+// colour layer 0 first = the per-ray fold's order), so a ray's outputs do not depend on its batch.
+// 512 threads, two workgroups per CU (16 waves), <= 80 KB of LDS each.
+#ifndef ACN_ROUTED
+#define ACN_ROUTED 1
+#endif
+#ifndef ACN_ROUTED_CHUNK
+#define ACN_ROUTED_CHUNK 1024  // samples per chunk (rays per chunk = ACN_ROUTED_CHUNK / S)
+#endif
+constexpr int kRtThreads = 512;
+constexpr int kRtWaves = kRtThreads / 64;
+static_assert(ACN_ROUTED_CHUNK == 2 * kRtThreads, "phase-B list build: two samples per thread");
+
+template <int INTERP, int ROUTE>
+__global__ void __launch_bounds__(kRtThreads, 4) render_routed_kernel(FieldCfg cfg, BgArgs bg, RenderParams p,
+                                                                       int R) {
+#if ACN_RT_ACCFIRST  // diagnostic: LDS layout with the accumulators first
+    __shared__ __attribute__((aligned(16))) f32x4 accs[ACN_ROUTED_CHUNK];  // per-sample container output
+    __shared__ __attribute__((aligned(16))) float Wsl[PK_FLOATS];     // the staged expert's packed image
+#else
+    __shared__ __attribute__((aligned(16))) float Wsl[PK_FLOATS];     // the staged expert's packed image
+    __shared__ __attribute__((aligned(16))) f32x4 accs[ACN_ROUTED_CHUNK];  // per-sample container output
+#endif
+#if ACN_RT_PAD  // diagnostic: > 80 KB of LDS, one workgroup per CU
+    __shared__ int pad_lds[1024];
+    if (threadIdx.x == 1023) pad_lds[0] = 0;
+#endif
+    __shared__ uint16_t emask[ACN_ROUTED_CHUNK];                         // per-sample expert mask
+    __shared__ uint16_t elist[ACN_ROUTED_CHUNK];                         // samples of the current expert
+    __shared__ int wsum[kRtWaves];
+    __shared__ uint32_t uni;
+    __shared__ int tctr;
+#if ACN_RT_DEBUG  // diagnostic build: per-sample count of expert evaluations
+    __shared__ uint8_t dvis[ACN_ROUTED_CHUNK];
+#endif
+#if ACN_RT_CHECK  // diagnostic build: per-sample self-check flags
+    __shared__ uint8_t dflag[ACN_ROUTED_CHUNK];
+#endif
+    const int tid = threadIdx.x, lane = tid & 63, j = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int S = p.S;
+    const float step = 1.0f / (float)(S - 1);
+    const int64_t nchunks = (p.N + R - 1) / R;
+    // chunk range of this workgroup: with the grid a multiple of 8 (blocks dealt round-robin over the XCDs),
+    // XCD x owns the x-th contiguous eighth of the chunks, each of its workgroups a contiguous piece of it
+    int64_t c_lo, c_hi;
+    {
+        int64_t band_lo = 0, band_n = nchunks, q = blockIdx.x, Q = gridDim.x;
+        if ((gridDim.x & 7) == 0) {
+            const int x = blockIdx.x & 7;
+            band_lo = nchunks * x / 8;
+            band_n = nchunks * (x + 1) / 8 - band_lo;
+            q = blockIdx.x >> 3;
+            Q = gridDim.x >> 3;
+        }
+        c_lo = band_lo + band_n * q / Q;
+        c_hi = band_lo + band_n * (q + 1) / Q;
+    }
+    auto ray_at = [&](int64_t pos) -> int64_t {
+        return p.order ? (int64_t)p.order[pos] : pos;
+    };
+    int slot = -1;  // expert in the LDS slot (workgroup-uniform)
+    if (tid == 0) uni = 0u;
+    __syncthreads();
+    for (int64_t c = c_lo; c < c_hi; ++c) {
+        const int64_t r0 = c * R;
+        const int nr = (int)min((int64_t)R, p.N - r0);
+        const int ns = nr * S;
+        // ---- A: expert mask of every sample (meta_container.py:97-134)
+        for (int sl = tid; sl < ns; sl += kRtThreads) {
+            const int rl = sl / S, i = sl - rl * S;
+            const float* rp = p.rays + ray_at(r0 + rl) * 8;
+            const float near = rp[6], far = rp[7];
+            const float t = p.jitter ? tval(near, far, i, S, p.jitter + ray_at(r0 + rl) * S) : tlin_sel(near, far, i, S, step);
+            const float px = rp[0] + rp[3] * t, py = rp[1] + rp[4] * t, pz = rp[2] + rp[5] * t;
+            uint32_t m = 0u;
+            if (ROUTE == 1) {
+                const RouteState st = route_prep<1>(cfg, px, py, pz);
+                for (int k = 0; k < cfg.K; ++k)
+                    if (route_weight(cfg, st, k, px, py, pz) > 0.0f) m |= 1u << k;
+            } else {
+                m = 1u << route_prep<2>(cfg, px, py, pz).hard;
+            }
+            emask[sl] = (uint16_t)m;
+#if ACN_RT_CHECK
+            dflag[sl] = 0;
+#endif
+#if ACN_RT_DEBUG
+            dvis[sl] = 0;
+#endif
+            if (m == 0u) accs[sl] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};   // no expert: the container output is 0
+            uint32_t any = 0u;
+            for (int k = 0; k < cfg.K; ++k)
+                if (__ballot((m >> k) & 1u) != 0ull) any |= 1u << k;
+            if (lane == 0 && any) atomicOr(&uni, any);
+        }
+        __syncthreads();
+        const uint32_t U = (uint32_t)__builtin_amdgcn_readfirstlane((int)uni);
+        // ---- B: expert by expert, ascending
+        for (uint32_t rem = U; rem != 0u; rem &= rem - 1u) {
+            const int k = __builtin_ctz(rem);
+            if (k != slot) {
+                const f32x4* src = reinterpret_cast<const f32x4*>(p.packed + (size_t)k * PK_FLOATS);
+                f32x4* dst = reinterpret_cast<f32x4*>(Wsl);
+                for (int i = tid; i < PK_FLOATS / 4; i += kRtThreads) dst[i] = src[i];
+                slot = k;
+            }
+            // compact the chunk's samples that need k (two per thread, in sample order)
+            const int s0 = 2 * tid;
+            const bool f0 = s0 < ns && ((emask[s0] >> k) & 1u);
+            const bool f1 = s0 + 1 < ns && ((emask[s0 + 1] >> k) & 1u);
+            const int cnt2 = (int)f0 + (int)f1;
+            const int incl = wave_incl_scan(cnt2);
+            if (lane == 63) wsum[wave] = incl;
+            if (tid == 0) tctr = 0;
+            __syncthreads();
+            int base = incl - cnt2, total = 0;
+            for (int w = 0; w < kRtWaves; ++w) {
+                const int v = wsum[w];
+                base += w < wave ? v : 0;
+                total += v;
+            }
+            if (f0) elist[base] = (uint16_t)s0;
+            if (f1) elist[base + (int)f0] = (uint16_t)(s0 + 1);
+            __syncthreads();
+            // wave-tiles of 32 listed samples, pulled from a workgroup counter
+            const int ntiles = (total + 31) >> 5;
+#if ACN_RT_STATIC  // diagnostic: static tile assignment
+            for (int tile = wave; tile < ntiles; tile += kRtWaves) {
+#else
+            for (;;) {
+                int tile = 0;
+                if (lane == 0) tile = atomicAdd(&tctr, 1);
+                tile = __builtin_amdgcn_readfirstlane(tile);
+                if (tile >= ntiles) break;
+#endif
+#if ACN_RT_SYNC  // diagnostic: drain every counter at the start of a tile
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+#endif
+                const int e = tile * 32 + j;
+                const bool valid = e < total;
+                const int sl = elist[valid ? e : total - 1];
+                const int rl = sl / S, i = sl - rl * S;
+                const int64_t ray = ray_at(r0 + rl);
+                const float* rp = p.rays + ray * 8;
+                const float ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
+                const float near = rp[6], far = rp[7];
+                const float t = p.jitter ? tval(near, far, i, S, p.jitter + ray * S) : tlin_sel(near, far, i, S, step);
+                const float px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;
+                float sh[16], shv[8];
+                dir_sh(dx, dy, dz, sh);
+                sh_rows_for_half(sh, h, shv);
+                float wk = 1.0f;
+                if (ROUTE == 1) wk = route_weight(cfg, route_prep<1>(cfg, px, py, pz), k, px, py, pz);
+                float r, g, b, sg;
+                // metadata straight from the kernel arguments (k is wave-uniform): the table pointer stays a
+                // global-address-space pointer (global_load gathers, not flat)
+#if ACN_RT_EXSEL  // diagnostic: the expert's metadata selected by compile-time indices
+                switch (k) {
+#define ACN_RT_CASE(Q) case Q: field_tile<INTERP, false, true>(Wsl, cfg.ex[Q], cfg.log2T, px, py, pz, shv, nullptr, lane, r, g, b, sg); break;
+                    ACN_RT_CASE(0) ACN_RT_CASE(1) ACN_RT_CASE(2) ACN_RT_CASE(3) ACN_RT_CASE(4) ACN_RT_CASE(5)
+                    ACN_RT_CASE(6) default: ACN_RT_CASE(7)
+#undef ACN_RT_CASE
+                }
+#else
+                field_tile<INTERP, false, true>(Wsl, cfg.ex[k], cfg.log2T, px, py, pz, shv, nullptr, lane, r, g, b, sg);
+#endif
+                sg = trunc_exp(sg);
+#if ACN_RT_CHECK
+                uint32_t fl = 0u;
+                {
+                    __builtin_amdgcn_sched_barrier(0);
+                    const float* rq = p.rays + ray * 8;
+                    if (rq[0] != ox || rq[1] != oy || rq[2] != oz || rq[3] != dx || rq[4] != dy || rq[5] != dz ||
+                        rq[6] != near || rq[7] != far) fl |= 1u;
+                    float r2, g2, b2, s2;
+                    field_tile<INTERP, false, true>(Wsl, cfg.ex[k], cfg.log2T, px, py, pz, shv, nullptr, lane, r2, g2, b2, s2);
+                    s2 = trunc_exp(s2);
+                    if (__float_as_uint(r2) != __float_as_uint(r) || __float_as_uint(s2) != __float_as_uint(sg)) fl |= 2u;
+                }
+#endif
+                if (valid && h == 0) {
+#if ACN_RT_CHECK
+                    dflag[sl] = (uint8_t)(dflag[sl] | fl);
+#endif
+                    f32x4 a;
+                    if (ROUTE == 1) {
+                        const bool first = (emask[sl] & ((1u << k) - 1u)) == 0u;
+                        a = first ? f32x4{0.0f, 0.0f, 0.0f, 0.0f} : accs[sl];
+                        a[0] = a[0] + r * wk;
+                        a[1] = a[1] + g * wk;
+                        a[2] = a[2] + b * wk;
+                        a[3] = a[3] + sg * wk;
+                    } else {
+                        a = f32x4{r, g, b, sg};
+                    }
+                    accs[sl] = a;
+#if ACN_RT_DEBUG
+                    dvis[sl] = dvis[sl] + 1;
+#endif
+                }
+            }
+            __syncthreads();
+        }
+        // ---- C: composite one ray per wave (ray_rendering.py:114-165, 23-45)
+        for (int rl = wave; rl < nr; rl += kRtWaves) {
+            const int rb = rl * S;
+            render_ray(p, bg, ray_at(r0 + rl), lane, step,
+                       [&](int sc, float, float, float, const float (&)[8], uint32_t&, float& yr, float& yg, float& yb,
+                           float& ys) {
+                           const f32x4 a = accs[rb + sc];
+                           yr = a[0];
+                           yg = a[1];
+                           yb = a[2];
+                           ys = a[3];
+                       });
+#if ACN_RT_DEBUG2  // diagnostic: weights <- the container's sigma per sample (the accumulated field output)
+            if (p.weights)
+                for (int i = lane; i < S; i += 64) p.weights[ray_at(r0 + rl) * S + i] = accs[rb + i][3];
+#endif
+#if ACN_RT_CHECK  // depth <- OR of the ray's samples' self-check flags
+            {
+                uint32_t f = 0u;
+                for (int i = lane; i < S; i += 64) f |= dflag[rb + i];
+                for (int off = 32; off >= 1; off >>= 1) f |= (uint32_t)__shfl_xor((int)f, off);
+                if (lane == 0) p.depth[ray_at(r0 + rl)] = (float)f;
+            }
+#endif
+#if ACN_RT_DEBUG  // depth <- samples of the ray whose evaluation count differs from their expert count
+            {
+                int bad = 0;
+                for (int i = lane; i < S; i += 64)
+                    bad += (__builtin_popcount((uint32_t)emask[rb + i]) != (int)dvis[rb + i]) ? 1 : 0;
+                for (int off = 32; off >= 1; off >>= 1) bad += __shfl_xor(bad, off);
+                int multi = 0;
+                for (int i = lane; i < S; i += 64) multi += __builtin_popcount((uint32_t)emask[rb + i]) > 1 ? 1 : 0;
+                for (int off = 32; off >= 1; off >>= 1) multi += __shfl_xor(multi, off);
+                if (lane == 0) {
+                    p.depth[ray_at(r0 + rl)] = (float)bad;
+                    p.acc[ray_at(r0 + rl)] = (float)multi;
+                }
+            }
+#endif
+        }
+        if (tid == 0) uni = 0u;
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// One expert per GPU, render (expert_parallel.ExpertParallelRenderer).  The routed render of
+// render_routed_kernel split at its expert boundary: the senders' (sample, expert) pairs travel to the
+// experts' owners as 24-B [world point, direction] records in the fixed layout of acn_routed_count_fixed.
+//   ep_field_kernel     owner: each owned expert's field on the records received from every sender, in the
+//                       received layout [sender][local expert][cap] -> (rgb, sigma) per record, the same
+//                       per-(sample, expert) arithmetic as render_routed_kernel (LDS-staged image, SH-first
+//                       colour layer 0 on per-lane SH), so a ray renders bit for bit as on one GPU;
+//   ep_composite_kernel sender: the blend sum_k y_k w_k in ascending k from zero (meta_container.py:320-337)
+//                       read from the returned pair slots, then render_kernel's compositing / background /
+//                       outputs (ray_rendering.py:114-165): no (N,S,4) field tensor.
+template <int INTERP>
+__global__ void __launch_bounds__(kRtThreads, 4) ep_field_kernel(FieldCfg cfg, const float* __restrict__ xd,
+                                                                  const int64_t* __restrict__ cnt, int W, int E,
+                                                                  int64_t cap, const float* __restrict__ packed,
+                                                                  float* __restrict__ ret) {
+    __shared__ __attribute__((aligned(16))) float Wsl[PK_FLOATS];
+    const int tid = threadIdx.x, lane = tid & 63, j = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t G = (int64_t)gridDim.x * kRtWaves;
+    int slot = -1;
+    for (int e = 0; e < E; ++e) {
+        int64_t T = 0;   // wave-tiles of local expert e over all senders (records past cap were not sent)
+        for (int w = 0; w < W; ++w) {
+            const int64_t c = min(cnt[(int64_t)w * E + e], cap);
+            T += (c + 31) >> 5;
+        }
+        if ((int64_t)blockIdx.x * kRtWaves >= T) continue;   // no tile of this expert for this workgroup
+        if (slot != e) {
+            __syncthreads();   // every wave is done with the previous expert's image
+            const f32x4* src = reinterpret_cast<const f32x4*>(packed + (size_t)e * PK_FLOATS);
+            f32x4* dst = reinterpret_cast<f32x4*>(Wsl);
+            for (int i = tid; i < PK_FLOATS / 4; i += kRtThreads) dst[i] = src[i];
+            __syncthreads();
+            slot = e;
+        }
+        for (int64_t g = (int64_t)blockIdx.x * kRtWaves + wave; g < T; g += G) {
+            int64_t tl = g, c = 0;
+            int w = 0;
+            for (; w < W; ++w) {   // sender of wave-tile g
+                c = min(cnt[(int64_t)w * E + e], cap);
+                const int64_t nt = (c + 31) >> 5;
+                if (tl < nt) break;
+                tl -= nt;
+            }
+            const int64_t i = tl * 32 + j;
+            const bool valid = i < c;
+            const int64_t rec = ((int64_t)w * E + e) * cap + (valid ? i : c - 1);
+            const float* r = xd + rec * 6;
+            const float px = r[0], py = r[1], pz = r[2];
+            float sh[16], shv[8];
+            dir_sh(r[3], r[4], r[5], sh);
+            sh_rows_for_half(sh, h, shv);
+            float rr, rg, rb, sg;
+            field_tile<INTERP, false, true>(Wsl, cfg.ex[e], cfg.log2T, px, py, pz, shv, nullptr, lane, rr, rg, rb, sg);
+            sg = trunc_exp(sg);
+            if (valid && h == 0)
+                *reinterpret_cast<f32x4*>(ret + 4 * (((int64_t)w * E + e) * cap + i)) = f32x4{rr, rg, rb, sg};
+        }
+    }
+}
+
+template <int ROUTE>
+__global__ void __launch_bounds__(1024) ep_composite_kernel(BgArgs bg, RenderParams p, const float* __restrict__ yr,
+                                                            const float* __restrict__ pw,
+                                                            const int32_t* __restrict__ pmap, int K) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const float step = 1.0f / (float)(p.S - 1);
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t ray = (int64_t)blockIdx.x * (blockDim.x >> 6) + wave; ray < p.N; ray += nw) {
+        render_ray(p, bg, ray, lane, step,
+                   [&](int sc, float, float, float, const float (&)[8], uint32_t&, float& yr_, float& yg, float& yb,
+                       float& ys) {
+                       const int64_t m = ray * p.S + sc;
+                       f32x4 a = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+                       for (int k = 0; k < K; ++k) {
+                           const int32_t q = pmap[m * K + k];
+                           if (q < 0) continue;
+                           const f32x4 y = *reinterpret_cast<const f32x4*>(yr + 4 * (int64_t)q);
+                           if (ROUTE == 1) {
+                               const float wk = pw[q];
+                               a[0] = a[0] + y[0] * wk;
+                               a[1] = a[1] + y[1] * wk;
+                               a[2] = a[2] + y[2] * wk;
+                               a[3] = a[3] + y[3] * wk;
+                           } else {
+                               a = y;
+                           }
+                       }
+                       yr_ = a[0];
+                       yg = a[1];
+                       yb = a[2];
+                       ys = a[3];
+                   });
     }
 }
 
@@ -1411,7 +1830,7 @@ __global__ void __launch_bounds__(ACN_SINGLE_THREADS, ACN_SINGLE_THREADS / 256) 
         const int32_t ray = __builtin_amdgcn_readfirstlane(ld(list + WPR * g + wave));
         if (ray < 0) continue;   // padding of expert k's segment
         render_ray(p, bg, ray, lane, step,
-                   [&](float px, float py, float pz, const float (&shv)[8], uint32_t& folded, float& yr, float& yg,
+                   [&](int, float px, float py, float pz, const float (&shv)[8], uint32_t& folded, float& yr, float& yg,
                        float& yb, float& ys) {
                        const float* Wk = ACN_SINGLE_DBG == 3 ? p.packed + (size_t)k * PK_FLOATS : smem;
                        if (FOLD && !(folded & 1u)) {
@@ -1796,8 +2215,9 @@ __global__ void __launch_bounds__(256) sample_train_kernel(const float* __restri
 // XCD's samples over the whole frame and its 4 MB L2 serves the hash cells of all of it).  One
 // workgroup: the batch's mean direction m and an orthonormal pair (e1, e2) perpendicular to it; every
 // ray's gnomonic coordinates (d.e1 / d.m, d.e2 / d.m) (for one camera: its image-plane position),
-// quantised to a 64 x 64 grid over the batch's bounding box and Z-ordered; a counting sort over the
-// 4096 cells with LDS atomics (the order inside a cell is arbitrary -- it does not matter, see below).
+// quantised to a 64 x 64 grid over the batch's bounding box and Z-ordered; a STABLE sort of the rays by
+// cell (two 6-bit LSD radix passes, rank inside a wave by ballot multisplit, so rays of one cell keep
+// their index order and the visiting order is reproducible run to run).
 // Only the order changes: each ray is still rendered alone and its outputs written at its own index,
 // so results are bit-identical to the given order.  Rays with a non-finite direction or d.m <= 0
 // go to the last cell.
@@ -1850,16 +2270,66 @@ __device__ __forceinline__ bool dir_ok(float x, float y, float z) {
     const float n2 = x * x + y * y + z * z;
     return n2 > 0.0f && n2 < 3.0e38f;  // finite, non-zero
 }
+// One stable LSD radix pass over N <= ACN_ORDER_MAX 16-bit keys by digit (key >> shift) & 63, 1024 threads.
+// Wave w owns the contiguous input block [w B, (w + 1) B); per (digit, wave) counts cnt[digit * 16 + w]
+// are scanned digit-major, so the output keeps every digit's elements in input order: within a wave
+// chunk by the lanes below with the same digit, across chunks by the wave's running offset, across
+// waves by the scan.  iin == NULL: the input indices are the positions.  FINAL: write idx to order[].
+template <bool FINAL>
+__device__ __forceinline__ void radix_pass6(const uint16_t* kin, const uint16_t* iin, int shift, int N, int* cnt,
+                                            int* wsum, uint16_t* kout, uint16_t* iout, int32_t* __restrict__ order) {
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int B = (((N + 15) >> 4) + 63) & ~63;
+    const int lo = w * B, hi = min(N, lo + B);
+    cnt[tid] = 0;
+    __syncthreads();
+    for (int p0 = lo; p0 < hi; p0 += 64) {
+        const int pos = p0 + lane;
+        const bool v = pos < hi;
+        const int dig = v ? (kin[pos] >> shift) & 63 : 0;
+        const uint64_t m = same_digit_lanes(v, dig);
+        if (v && lanes_below(m) == 0) cnt[dig * 16 + w] += __popcll(m);
+    }
+    __syncthreads();
+    const int val = cnt[tid];
+    const int incl = wave_incl_scan(val);
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    int base = incl - val;
+    for (int k = 0; k < w; ++k) base += wsum[k];
+    cnt[tid] = base;
+    __syncthreads();
+    for (int p0 = lo; p0 < hi; p0 += 64) {
+        const int pos = p0 + lane;
+        const bool v = pos < hi;
+        const uint16_t key = v ? kin[pos] : (uint16_t)0;
+        const int dig = (key >> shift) & 63;
+        const uint64_t m = same_digit_lanes(v, dig);
+        const int below = lanes_below(m);
+        const int run = v ? cnt[dig * 16 + w] : 0;
+        if (v) {
+            const int dst = run + below;
+            const int idx = iin ? (int)iin[pos] : pos;
+            if (FINAL) {
+                order[dst] = idx;
+            } else {
+                kout[dst] = key;
+                iout[dst] = (uint16_t)idx;
+            }
+        }
+        if (v && below == 0) cnt[dig * 16 + w] = run + __popcll(m);
+    }
+    __syncthreads();
+}
 __global__ void __launch_bounds__(1024) ray_order_kernel(const float* __restrict__ rays, int N,
                                                          int32_t* __restrict__ order) {
     constexpr int PER = ACN_ORDER_MAX / 1024;
-    __shared__ int hist[ACN_ORDER_BINS];
-    __shared__ float dir[3][ACN_ORDER_MAX];
-    __shared__ uint16_t cell_of[ACN_ORDER_MAX], rank_of[ACN_ORDER_MAX];
+    __shared__ int cnt[1024];
+    __shared__ __attribute__((aligned(16))) float dir[3][ACN_ORDER_MAX];
+    __shared__ uint16_t cell_of[ACN_ORDER_MAX];
     __shared__ int wsum[16];
     __shared__ float red[16 * 4];
     const int tid = threadIdx.x;
-    for (int c = tid; c < ACN_ORDER_BINS; c += 1024) hist[c] = 0;
     // one pass over global memory, every load of the thread in flight at once
     float sx = 0.0f, sy = 0.0f, sz = 0.0f;
 #pragma unroll
@@ -1928,32 +2398,12 @@ __global__ void __launch_bounds__(1024) ray_order_kernel(const float* __restrict
             c = (int)(spread6(qu) | (spread6(qv) << 1));
         }
         cell_of[i] = (uint16_t)c;
-        rank_of[i] = (uint16_t)atomicAdd(&hist[c], 1);
     }
-    __syncthreads();
-    // exclusive scan of hist: 4 cells per thread, wave scan of the thread sums, then the wave totals
-    constexpr int CPT = ACN_ORDER_BINS / 1024;
-    int h[CPT], run = 0;
-#pragma unroll
-    for (int c = 0; c < CPT; ++c) h[c] = hist[tid * CPT + c], run += h[c];
-    const int lane = tid & 63;
-    // inclusive wave scan on DPP: row_shr 1/2/4/8 inside each 16-lane row, then row_bcast:15 / :31 carry
-    // the row totals upward (gfx9-family DPP)
-    int incl = run;
-    incl += __builtin_amdgcn_update_dpp(0, incl, 0x111, 0xF, 0xF, true);
-    incl += __builtin_amdgcn_update_dpp(0, incl, 0x112, 0xF, 0xF, true);
-    incl += __builtin_amdgcn_update_dpp(0, incl, 0x114, 0xF, 0xF, true);
-    incl += __builtin_amdgcn_update_dpp(0, incl, 0x118, 0xF, 0xF, true);
-    incl += __builtin_amdgcn_update_dpp(0, incl, 0x142, 0xA, 0xF, false);
-    incl += __builtin_amdgcn_update_dpp(0, incl, 0x143, 0xC, 0xF, false);
-    if (lane == 63) wsum[tid >> 6] = incl;
-    __syncthreads();
-    int base = incl - run;
-    for (int w = 0; w < (tid >> 6); ++w) base += wsum[w];
-#pragma unroll
-    for (int c = 0; c < CPT; ++c) hist[tid * CPT + c] = base, base += h[c];
-    __syncthreads();
-    for (int i = tid; i < N; i += 1024) order[hist[cell_of[i]] + rank_of[i]] = i;
+    __syncthreads();  // dir[] is free from here on: it holds the first pass's output
+    uint16_t* key1 = reinterpret_cast<uint16_t*>(&dir[0][0]);
+    uint16_t* idx1 = reinterpret_cast<uint16_t*>(&dir[1][0]);
+    radix_pass6<false>(cell_of, nullptr, 0, N, cnt, wsum, key1, idx1, nullptr);
+    radix_pass6<true>(key1, idx1, 6, N, cnt, wsum, nullptr, nullptr, order);
 }
 
 extern "C" size_t acn_workspace_bytes(int K) { return (size_t)(K < 1 ? 1 : K) * PK_BYTES; }
@@ -1966,6 +2416,14 @@ extern "C" size_t acn_render_order_bytes(int64_t N) {
     const size_t ord = N <= ACN_ORDER_MAX ? (size_t)N * sizeof(int32_t) : 0;
     const size_t spl = ACN_SPLIT_ROUTED ? split_bytes(N) : 0;
     return ord > spl ? ord : spl;
+}
+
+extern "C" int acn_ray_order(const float* rays, int64_t N, int32_t* order, void* stream) {
+    ACN_REQUIRE(N >= 1 && N <= ACN_ORDER_MAX, "acn_ray_order: N must be in [1, %d], got %lld", ACN_ORDER_MAX,
+                (long long)N);
+    ACN_REQUIRE(rays && order, "acn_ray_order: NULL pointer");
+    hipLaunchKernelGGL(ray_order_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, rays, (int)N, order);
+    return acn_check_launch("acn_ray_order");
 }
 
 extern "C" int acn_pack_experts(const acn_expert* experts, const acn_routing* routing, int active_module,
@@ -2035,6 +2493,26 @@ extern "C" int acn_render_stratified_fwd_ordered(const float* rays, int64_t N, i
     if (order_scratch && !slots && N <= ACN_ORDER_MAX && order_bytes >= (size_t)N * sizeof(int32_t)) {
         hipLaunchKernelGGL(ray_order_kernel, dim3(1), dim3(1024), 0, s, rays, (int)N, (int32_t*)order_scratch);
         p.order = (const int32_t*)order_scratch;
+    }
+    if (slots && ACN_ROUTED && S <= ACN_ROUTED_CHUNK) {
+        // expert-major chunks (render_routed_kernel): R rays per chunk, two workgroups per CU
+#if ACN_RT_R1  // diagnostic: one ray per chunk
+        const int R = 1;
+#else
+        const int R = ACN_ROUTED_CHUNK / S;
+#endif
+        const int64_t nch = (N + R - 1) / R;
+        int64_t g = 2 * (int64_t)num_cus();
+        if (nch < g) g = nch;
+        const dim3 rgrid((unsigned)g), rblock(kRtThreads);
+#define ACN_RT_LAUNCH(I, RT) hipLaunchKernelGGL((render_routed_kernel<I, RT>), rgrid, rblock, 0, s, cfg, b, p, R)
+        if (cfg.routing == 1) {
+            if (interp == 1) ACN_RT_LAUNCH(1, 1); else if (interp == 0) ACN_RT_LAUNCH(0, 1); else ACN_RT_LAUNCH(2, 1);
+        } else {
+            if (interp == 1) ACN_RT_LAUNCH(1, 2); else if (interp == 0) ACN_RT_LAUNCH(0, 2); else ACN_RT_LAUNCH(2, 2);
+        }
+#undef ACN_RT_LAUNCH
+        return acn_check_launch("acn_render_stratified_fwd");
     }
     if (slots && ACN_SPLIT_ROUTED && order_scratch && order_bytes >= split_bytes(N)) {
         // split: single-expert rays through render_single_kernel, the rest through render_slots_kernel
@@ -2348,4 +2826,52 @@ extern "C" int acn_sample_stratified(const float* rays, int64_t N, int S, const 
     hipLaunchKernelGGL(sample_train_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                        rays, N, S, jitter, mn, ex, lo, hi, t_vals, x01, sh);
     return acn_check_launch("acn_sample_stratified");
+}
+
+extern "C" int acn_ep_field_fwd(const float* recv_xd, const int64_t* recv_cnt, int W, int E, int64_t cap,
+                                const acn_expert* experts, const void* packed, size_t packed_bytes, float* ret,
+                                void* stream) {
+    ACN_REQUIRE(W >= 1 && E >= 1 && E <= kMaxK && cap >= 1, "acn_ep_field_fwd: bad arguments");
+    ACN_REQUIRE(recv_xd && recv_cnt && experts && packed && ret, "acn_ep_field_fwd: NULL pointer");
+    acn_routing rt{};
+    rt.K = E;
+    rt.boundary_margin = 1.0f;
+    FieldCfg cfg{};
+    int interp, K;
+    int st = prepare(experts, &rt, -1, (void*)packed, packed_bytes, (hipStream_t)stream, cfg, interp, K, false);
+    if (st) return st;
+    int64_t g = 2 * (int64_t)num_cus();
+    const int64_t tiles = (int64_t)W * E * ((cap + 31) / 32);
+    const int64_t need = (tiles + kRtWaves - 1) / kRtWaves;
+    if (need < g) g = need < 1 ? 1 : need;
+    const dim3 grid((unsigned)g), block(kRtThreads);
+    hipStream_t s = (hipStream_t)stream;
+    if (interp == 1)
+        hipLaunchKernelGGL(ep_field_kernel<1>, grid, block, 0, s, cfg, recv_xd, recv_cnt, W, E, cap, (const float*)packed, ret);
+    else if (interp == 0)
+        hipLaunchKernelGGL(ep_field_kernel<0>, grid, block, 0, s, cfg, recv_xd, recv_cnt, W, E, cap, (const float*)packed, ret);
+    else
+        hipLaunchKernelGGL(ep_field_kernel<2>, grid, block, 0, s, cfg, recv_xd, recv_cnt, W, E, cap, (const float*)packed, ret);
+    return acn_check_launch("acn_ep_field_fwd");
+}
+
+extern "C" int acn_ep_composite(const float* rays, int64_t N, int S, const float* jitter, const float* yr, const float* pw,
+                                const int32_t* pmap, int K, int hard, const acn_background* bg, float sigma_scale,
+                                float tau, float* rgb, float* depth, float* weights, float* acc, void* stream) {
+    ACN_REQUIRE(N >= 0 && S >= 2 && K >= 1 && K <= kMaxK, "acn_ep_composite: bad arguments");
+    if (N == 0) return ACN_OK;
+    ACN_REQUIRE(rays && yr && pw && pmap && bg && rgb && depth && acc, "acn_ep_composite: NULL pointer");
+    if (bg->mode == ACN_BG_MLP) {
+        ACN_REQUIRE(bg->w1 && bg->b1 && bg->w2 && bg->b2, "background MLP pointers are NULL");
+        ACN_REQUIRE(bg->hidden >= 1 && bg->hidden <= 64, "bg_hidden must be in [1, 64], got %d", bg->hidden);
+    }
+    BgArgs b{bg->mode, bg->hidden, {bg->color[0], bg->color[1], bg->color[2]}, bg->w1, bg->b1, bg->w2, bg->b2};
+    RenderParams p{rays, N, S, jitter, nullptr, sigma_scale, tau, rgb, depth, weights, acc, nullptr};
+    int64_t wgs = (N + 15) / 16;
+    const int64_t cap_g = 4 * (int64_t)num_cus();
+    const dim3 grid((unsigned)(wgs < cap_g ? wgs : cap_g)), block(1024);
+    hipStream_t s = (hipStream_t)stream;
+    if (hard) hipLaunchKernelGGL(ep_composite_kernel<2>, grid, block, 0, s, b, p, yr, pw, pmap, K);
+    else hipLaunchKernelGGL(ep_composite_kernel<1>, grid, block, 0, s, b, p, yr, pw, pmap, K);
+    return acn_check_launch("acn_ep_composite");
 }

@@ -211,6 +211,10 @@ __global__ void __launch_bounds__(kBlk) routed_scatter_kernel(const float* __res
         }
         int64_t pos = starts[k] + blk_off[(int64_t)blockIdx.x * K + k] + __popcll(b & below);
         for (int q = 0; q < wave; ++q) pos += wcnt[q][k];
+        if (pos >= starts[k + 1]) {   // fixed layout below the expert's count (capacity-bounded exchange):
+            pmap[m * K + k] = -1;      // the pair is dropped; the caller sees the count exceed the capacity
+            continue;
+        }
         pmap[m * K + k] = (int32_t)pos;
         pidx[pos] = (int32_t)m;
         if (pk) pk[pos] = k;
@@ -299,15 +303,16 @@ __global__ void __launch_bounds__(256) pad_pairs_kernel(const int64_t* __restric
 // Owner: the received layout is [src s][local expert j][cap] records with live counts cnt[s][j]; the compact
 // pair list holds local expert j's records in (s, i) order in a segment padded to `align`.  One thread:
 // off[s][j] = sum_{s' < s} cnt[s'][j], seg[j] (padded starts), seg[E] = slots, seg[E + 1 + j] = live count.
-__global__ void ep_seg_kernel(const int64_t* __restrict__ cnt, int W, int E, int align, int64_t* __restrict__ off,
-                              int64_t* __restrict__ seg) {
+__global__ void ep_seg_kernel(const int64_t* __restrict__ cnt, int W, int E, int align, int64_t cap,
+                              int64_t* __restrict__ off, int64_t* __restrict__ seg) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     int64_t base = 0;
     for (int j = 0; j < E; ++j) {
         int64_t run = 0;
         for (int s = 0; s < W; ++s) {
             off[(int64_t)s * E + j] = run;
-            run += cnt[(int64_t)s * E + j];
+            const int64_t c = cnt[(int64_t)s * E + j];
+            run += c < cap ? c : cap;   // a sender's count past the capacity: only cap records were sent
         }
         seg[j] = base;
         seg[E + 1 + j] = run;
@@ -425,8 +430,7 @@ extern "C" int acn_routed_count_fixed(const float* rays, int64_t N, int S, const
     const int K = routing->K;
     ACN_REQUIRE(K >= 1 && K <= kMaxK, "acn_routed_count_fixed: K = %d outside [1, %d]", K, kMaxK);
     const int64_t M = N * (int64_t)S;
-    ACN_REQUIRE(cap >= M && cap >= 1, "acn_routed_count_fixed: capacity %lld below the %lld samples (a segment could "
-                "overflow)", (long long)cap, (long long)M);
+    ACN_REQUIRE(cap >= 1, "acn_routed_count_fixed: capacity must be >= 1, got %lld", (long long)cap);
     ACN_REQUIRE(workspace && workspace_bytes >= acn_routed_workspace_bytes(M, K),
                 "acn_routed_count_fixed: workspace too small");
     hipStream_t s = (hipStream_t)stream;
@@ -548,7 +552,7 @@ extern "C" int acn_ep_gather(const float* recv_xd, const int64_t* recv_cnt, int 
     box.hi = hi;
     hipStream_t s = (hipStream_t)stream;
     int64_t* off = (int64_t*)workspace;
-    hipLaunchKernelGGL(ep_seg_kernel, dim3(1), dim3(64), 0, s, recv_cnt, W, E, align, off, seg);
+    hipLaunchKernelGGL(ep_seg_kernel, dim3(1), dim3(64), 0, s, recv_cnt, W, E, align, cap, off, seg);
     hipLaunchKernelGGL(ep_gather_kernel, dim3(kEpBlocks), dim3(256), 0, s, recv_xd, recv_cnt, (const int64_t*)off,
                        (const int64_t*)seg, W, E, cap, box, x01, sh, pk, pflag, back);
     return acn_check_launch("acn_ep_gather");

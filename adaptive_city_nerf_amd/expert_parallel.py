@@ -227,11 +227,209 @@ class HipBackend:
         return volume_render(rs, t, bg_rgb=bg, raw_rgb=False, raw_sigma=False)
 
 
+class ExpertParallelRenderer:
+    """render_rays (ray_rendering.py:290-345, eval) of this rank's rays through the routed container with the
+    experts distributed -- expert k on rank expert_owner(K, W)[k] -- and no host synchronisation: every
+    exchange has a constant size, so one call is a fixed sequence of launches and collectives (at world size 1
+    the exchanges are copies and ``graph=True`` replays the whole call as one HIP graph).
+
+    Per call, on every rank (batches of up to ``n_rays`` rays):
+      sender  t values, routing and (sample, expert) pairs in the fixed layout of acn_routed_count_fixed:
+              expert k's pairs at [k C, k C + min(count, C)), 24-B [world point, direction] records -- grouped
+              by owner, the pair buffer is the all-to-all send buffer
+      a2a #0  the per-expert live counts (int64) to the owners;  a2a #1 the records (constant splits)
+      owner   acn_ep_field_fwd: the field of its experts on every received record, written in the received
+              layout (no compaction, no scatter-back)
+      a2a #2  (rgb, sigma) back to the senders' pair slots
+      sender  acn_ep_composite: blend in expert order + background + compositing in one launch -> rgb, depth,
+              acc (+ weights): the (N, S, 4) field tensor is never materialised.
+    The per-sample arithmetic is render_routed_kernel's, so each ray renders bit for bit as in the fused
+    single-process routed render.  ``capacity`` C per (sender, expert) segment: n_rays * S (default, never
+    overflows) or smaller to shrink the exchange; ``overflowed()`` reads the counts back (one host read, to be
+    called lazily, e.g. once per frame) and a caller re-renders an overflowed batch at full capacity.
+    Reference: models/inr/meta_container.py:300-337, nerfs/ray_rendering.py:577-627."""
+
+    def __init__(self, model, n_rays: int, ray_samples: int, group=None, capacity: Optional[int] = None,
+                 graph: bool = False, bg_color_default: str = "white", want_weights: bool = False):
+        from . import _lib, ops
+        from ._lib import AcnError
+        from .meta_container import MetaContainer
+        from .ray_rendering import _fused_background
+        if not isinstance(model, MetaContainer) or not all(s._fusable for s in model.submodules):
+            raise AcnError("ExpertParallelRenderer: a MetaContainer of reference-configuration experts is required")
+        self.comm = comm = _Comm(group)
+        W, rank = comm.world, comm.rank
+        self.model, self.group = model, group
+        K = len(model.submodules)
+        owner = expert_owner(K, W)
+        own = [k for k in range(K) if owner[k] == rank]
+        if not own:
+            raise AcnError(f"ExpertParallelRenderer: rank {rank} owns no expert (K = {K} < W = {W})")
+        E = len(own)
+        eo = [owner.count(o) for o in range(W)]
+        N, S = int(n_rays), int(ray_samples)
+        M = N * S
+        Cc = int(capacity) if capacity is not None else M
+        if Cc < 1:
+            raise AcnError("ExpertParallelRenderer: capacity must be >= 1")
+        self.K, self.E, self.W, self.N, self.S, self.M, self.C = K, E, W, N, S, M, Cc
+        self.own, self.eo = own, eo
+        self.split_send = [e * Cc for e in eo]
+        self.split_recv = [E * Cc] * W
+        self.split_cnt_send, self.split_cnt_recv = list(eo), [E] * W
+        dev = model.submodules[0].xyz_encoder.hash_table.device
+        self.device = dev
+        f32 = dict(device=dev, dtype=torch.float32)
+        i32 = dict(device=dev, dtype=torch.int32)
+        L = _lib.lib()
+        self.rays = torch.zeros(N, 8, **f32)
+        self.t = torch.empty(N, S, **f32)
+        self.seg = torch.zeros(2 * K + 1, device=dev, dtype=torch.int64)
+        self.rws = torch.empty(int(L.acn_routed_workspace_bytes(M, K)), device=dev, dtype=torch.uint8)
+        self.pidx = torch.empty(K * Cc, **i32)
+        self.pw = torch.empty(K * Cc, **f32)
+        self.pk = torch.empty(K * Cc, **i32)
+        self.xd = torch.zeros(K * Cc, 6, **f32)
+        self.pmap = torch.empty(M, K, **i32)
+        self.yr = torch.zeros(K * Cc, 4, **f32)
+        R = W * E * Cc
+        self.recv_cnt = torch.zeros(W * E, device=dev, dtype=torch.int64)
+        self.recv_xd = torch.zeros(R, 6, **f32)
+        self.ret = torch.zeros(R, 4, **f32)
+        self.rgb = torch.empty(N, 3, **f32)
+        self.depth = torch.empty(N, **f32)
+        self.acc = torch.empty(N, **f32)
+        self.weights = torch.empty(N, S, **f32) if want_weights else None
+        self.routing = model.routing_spec()
+        self.hard = 0 if self.routing.boundary_margin > 1.0 else 1
+        self.bg = _fused_background(model, bg_color_default, N, dev)
+        if self.bg is None:
+            raise AcnError(f"ExpertParallelRenderer: background policy {bg_color_default!r} needs the composed path")
+        self.bg_spec, self._bg_keep = self.bg if isinstance(self.bg, tuple) else (self.bg, None)
+        # the owned experts' packed images (acn_pack_experts with a routing of K = E): packed per call from the
+        # live parameters, so a captured call renders the current weights
+        self.own_specs = [model.submodules[k].expert_spec(None) for k in own]
+        self.own_routing = ops.make_routing(torch.zeros(E, 3), E, True, 1.0)
+        self.packed = torch.empty(E * int(L.acn_workspace_bytes(1)) // 4, **f32)
+        self._own_arr = ops._experts_array(self.own_specs)
+        self.graph = None
+        self._graph_wanted = bool(graph)
+        self.replays = 0
+
+    def _run(self, n: int) -> None:
+        import ctypes as C
+        from . import _lib
+        from ._lib import check, ptr
+        L = _lib.lib()
+        s = int(torch.cuda.current_stream(self.device).cuda_stream)
+        K, E, S, Cc, comm = self.K, self.E, self.S, self.C, self.comm
+        check(L.acn_routed_count_fixed(ptr(self.rays), n, S, None, C.byref(self.routing), Cc, ptr(self.t),
+                                       ptr(self.seg), ptr(self.rws), self.rws.numel(), s), "acn_routed_count_fixed")
+        check(L.acn_routed_scatter_xd(ptr(self.rays), n, S, K, ptr(self.t), ptr(self.seg), ptr(self.rws),
+                                      ptr(self.pidx), ptr(self.pw), ptr(self.xd), ptr(self.pmap), ptr(self.pk), s),
+              "acn_routed_scatter_xd")
+        comm.all_to_all(self.recv_cnt, self.seg[K + 1:], self.split_cnt_recv, self.split_cnt_send)
+        comm.all_to_all(self.recv_xd, self.xd, self.split_recv, self.split_send)
+        check(L.acn_pack_experts(self._own_arr, C.byref(self.own_routing), -1, ptr(self.packed),
+                                 self.packed.numel() * 4, s), "acn_pack_experts")
+        check(L.acn_ep_field_fwd(ptr(self.recv_xd), ptr(self.recv_cnt), self.W, E, Cc, self._own_arr,
+                                 ptr(self.packed), self.packed.numel() * 4, ptr(self.ret), s), "acn_ep_field_fwd")
+        comm.all_to_all(self.yr, self.ret, self.split_send, self.split_recv)
+        check(L.acn_ep_composite(ptr(self.rays), n, S, None, ptr(self.yr), ptr(self.pw), ptr(self.pmap), K, self.hard,
+                                 C.byref(self.bg_spec), 1.0, 0.0, ptr(self.rgb), ptr(self.depth), ptr(self.weights),
+                                 ptr(self.acc), s), "acn_ep_composite")
+
+    def __call__(self, rays: Tensor):
+        """(rgb (n,3), depth (n,), weights (n,S) or None, acc (n,)) of this rank's ``rays`` (n <= n_rays): views
+        of persistent buffers, valid until the next call.  Collective over the group."""
+        from ._lib import AcnError
+        n = int(rays.shape[0])
+        if rays.dim() != 2 or rays.shape[1] != 8 or not 0 < n <= self.N:
+            raise AcnError(f"ExpertParallelRenderer was built for up to {self.N} rays per rank; got {tuple(rays.shape)}")
+        self.rays[:n].copy_(rays, non_blocking=True)
+        if n == self.N and self.graph is not None:
+            self.graph.replay()
+            self.replays += 1
+        else:
+            self._run(n)
+            if n == self.N and self._graph_wanted and self.graph is None:
+                torch.cuda.synchronize(self.device)
+                g = torch.cuda.CUDAGraph()
+                with graph_capture(g):
+                    self._run(self.N)
+                torch.cuda.synchronize(self.device)
+                self.graph = g
+        w = self.weights[:n] if self.weights is not None else None
+        return self.rgb[:n], self.depth[:n], w, self.acc[:n]
+
+    def overflowed(self) -> bool:
+        """True when the last call's pairs of some expert exceeded the capacity (host read of the counts)."""
+        return bool(int(self.seg[self.K + 1: 2 * self.K + 1].max()) > self.C)
+
+
+def _renderer_for(model, n: int, S: int, group, cap: Optional[int]) -> ExpertParallelRenderer:
+    """The ExpertParallelRenderer cached on ``model`` for (batch, samples, group, capacity)."""
+    cache = model.__dict__.setdefault("_acn_ep_renderers", {})
+    key = (n, S, id(group), cap)
+    r = cache.get(key)
+    if r is None:
+        r = cache[key] = ExpertParallelRenderer(model, n, S, group=group, capacity=cap)
+    return r
+
+
+@torch.no_grad()
+def render_rays_ep_batched(model, rays: Tensor, ray_samples: int, group=None, batch: int = 32768,
+                           capacity_frac: float = 1.0):
+    """(rgb, depth, acc) of this rank's ``rays`` through ExpertParallelRenderer in batches of ``batch`` rays.
+    Every rank must make the same number of calls: the batch count is agreed on with one all-reduce (MAX) of
+    the rank's batch count.  ``capacity_frac`` < 1 sizes each (sender, expert) exchange segment to that share
+    of a batch's samples; the counts of all batches are read back once at the end and any overflowed batch is
+    re-rendered at full capacity (collectively)."""
+    world, _ = world_rank(group)
+    n, S = int(rays.shape[0]), int(ray_samples)
+    dev = rays.device
+    nb = (n + batch - 1) // batch
+    if world > 1:
+        t = torch.tensor([nb], dtype=torch.int64, device=dev)
+        _Comm(group).all_reduce_max(t)
+        nb = int(t)
+    M = batch * S
+    cap = None if capacity_frac >= 1.0 else max(1, int(M * capacity_frac))
+    r = _renderer_for(model, batch, S, group, cap)
+    rgb = torch.empty(n, 3, device=dev)
+    depth = torch.empty(n, device=dev)
+    acc = torch.empty(n, device=dev)
+    K = r.K
+    counts = torch.zeros(nb, K, device=dev, dtype=torch.int64)
+    dummy = rays[:1] if n else torch.zeros(1, 8, device=dev)
+    for b in range(nb):
+        lo, hi = b * batch, min(n, (b + 1) * batch)
+        sub = rays[lo:hi] if hi > lo else dummy       # a rank with fewer rays still joins the collectives
+        o = r(sub)
+        if hi > lo:
+            rgb[lo:hi], depth[lo:hi], acc[lo:hi] = o[0], o[1], o[3]
+        counts[b] = r.seg[K + 1: 2 * K + 1]
+    if cap is not None:
+        over = (counts.max(dim=1).values > cap).to(torch.int64)
+        if world > 1:
+            _Comm(group).all_reduce_max(over)
+        redo = [b for b in range(nb) if int(over[b])]       # the one host read of the frame
+        if redo:
+            full = _renderer_for(model, batch, S, group, None)
+            for b in redo:
+                lo, hi = b * batch, min(n, (b + 1) * batch)
+                o = full(rays[lo:hi] if hi > lo else dummy)
+                if hi > lo:
+                    rgb[lo:hi], depth[lo:hi], acc[lo:hi] = o[0], o[1], o[3]
+    return rgb, depth, acc
+
+
 @torch.no_grad()
 def render_image_expert_parallel(model, *, H: int, W: int, fx: float, fy: float, cx: float, cy: float, c2w: Tensor,
                                  scene_box, ray_samples: int = 64, center_pixels: bool = True,
                                  gt_srgb: Optional[Tensor] = None, metrics_space: str = "linear", group=None,
-                                 backend=None, rays: Optional[Tensor] = None):
+                                 backend=None, rays: Optional[Tensor] = None, batch: int = 32768,
+                                 capacity_frac: float = 1.0):
     """render_image (ray_rendering.py:577-627) with the experts distributed: rank r renders a contiguous
     band of the frame's pixels through render_rays_expert_parallel (its samples' records go to the
     experts' owners), then the rendered rows are all-gathered and the PSNR all-reduced (parallel.py).
@@ -243,11 +441,14 @@ def render_image_expert_parallel(model, *, H: int, W: int, fx: float, fy: float,
         device = next(model.parameters()).device
         rays, _ = ops.get_rays_image(H, W, fx, fy, cx, cy, c2w, scene_box.aabb, device, center_pixels=center_pixels,
                                      near_far_override=(None, None), apply_clamp=True)
-    backend = backend or HipBackend(model)
     plan = contiguous_plan(rays.shape[0], world, rays.device)
     idx = plan.indices(rank).to(rays.device)
-    rgb, depth, _, acc = render_rays_expert_parallel(backend, rays[idx].contiguous(), ray_samples,
-                                                     len(model.submodules), group)
+    if backend is not None:   # a compute backend (tests: the CPU restatement) through the eager exchange
+        rgb, depth, _, acc = render_rays_expert_parallel(backend, rays[idx].contiguous(), ray_samples,
+                                                         len(model.submodules), group)
+    else:
+        rgb, depth, acc = render_rays_ep_batched(model, rays[idx].contiguous(), ray_samples, group=group,
+                                                 batch=batch, capacity_frac=capacity_frac)
     local = torch.cat([rgb.float().view(-1, 3), depth.float().view(-1, 1), acc.float().view(-1, 1)], dim=1)
     full = gather_rendered(local, plan, group)
     rgb_img = full[:, :3].reshape(H, W, 3).clamp_(0, 1)
@@ -288,6 +489,16 @@ class _Comm:
             t.copy_(c)
         else:
             dist.all_reduce(t, group=self.group)
+
+    def all_reduce_max(self, t: Tensor) -> None:
+        if self.world == 1:
+            return
+        if self.staged:
+            c = t.cpu()
+            dist.all_reduce(c, op=dist.ReduceOp.MAX, group=self.group)
+            t.copy_(c)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
 
 
 class ExpertParallelAdaptStep:

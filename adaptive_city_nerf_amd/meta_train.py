@@ -292,10 +292,20 @@ def train_step(P, step, model, optimizer, task_data, metric_logger=None, logger=
             g = optimizer._acn_meta_graph = False   # shapes the graphs cannot cover: stay eager
     if isinstance(g, GraphedMetaStep):
         out = g(step, task_data)
+        # host state['step'] (and the first-updated experts' state entries) current after every replayed step:
+        # optimizer.state_dict() -- the reference's checkpoint (utils.py:290) -- sees the real counts
+        g.sync_state()
         if out is not None and scheduler is not None:
             scheduler.step()
     else:
+        g_prev = optimizer.__dict__.get("_acn_meta_graph")
+        if isinstance(g_prev, GraphedMetaStep):
+            # an ineligible call (a GradScaler, MAML ...) on an optimizer a graphed step also updates: hand the
+            # state over both ways, as GraphedMetaStep._eager does
+            g_prev.adam.sync_state(extra_slots=set(range(g_prev.adam.nslots)))
         out = _train_step_eager(P, step, model, optimizer, task_data, scheduler, grad_scaler, group, logger)
+        if isinstance(g_prev, GraphedMetaStep):
+            g_prev.adam.load_state()
         if g is None:
             optimizer._acn_meta_graph = "pending"
     if out is None:

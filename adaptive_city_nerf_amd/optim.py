@@ -489,11 +489,29 @@ class SlottedAdam:
 
     def load_state(self) -> int:
         """Per-slot device step counters from the optimizer's host state['step'] (after eager FusedAdam
-        steps on the same optimizer); returns the highest step."""
+        steps on the same optimizer, or a load_state_dict); returns the highest step.
+
+        A captured step reads and writes the moment tensors it was built on (``rows``).  When an eager step
+        or a load_state_dict gave a parameter other state tensors -- a pending parameter whose first update
+        happened eagerly, or replaced tensors -- their values are copied into the row tensors and
+        optimizer.state is pointed back at them, so the graph and the optimizer share one state."""
         steps = [0] * self.nslots
         for (p, g, m, v, gi), f in zip(self.rows, self._flags_host):
-            st = self._pending.get(p) or self.opt.state[p]
-            steps[f & 0xffff] = max(steps[f & 0xffff], int(st["step"].item()))
+            st = self.opt.state.get(p)
+            if st and p in self._pending:
+                self._pending.pop(p)        # its first update ran eagerly: adopt that state below
+            elif not st:
+                st = self._pending[p]
+            if st["exp_avg"] is not m:
+                m.copy_(st["exp_avg"])
+                st["exp_avg"] = m
+            if st["exp_avg_sq"] is not v:
+                v.copy_(st["exp_avg_sq"])
+                st["exp_avg_sq"] = v
+            n = int(st["step"].item())
+            if n == 0 and self.opt.state.get(p) is st:
+                self._pending[p] = self.opt.state.pop(p)   # never updated: no state entry, as in torch
+            steps[f & 0xffff] = max(steps[f & 0xffff], n)
         if max(steps) + 1 > self.table_steps:
             raise AcnError("SlottedAdam: the Adam constant table is exhausted; build a new step object")
         self.step_dev.copy_(torch.tensor(steps, dtype=torch.int32))

@@ -375,8 +375,15 @@ class RoutedAdaptStep:
         """Per-slot device step counters from the optimizer's host state['step'] (after eager FusedAdam
         steps taken on the same optimizer outside this object), and the Adam constants from the current
         group hyper-parameters."""
+        before = self.adam.step_dev.cpu().tolist()
         top = self.adam.load_state()
         self.adam.refresh()
-        if self.segmaps is not None and top > self._step0 + self.steps_done:
-            self.segmaps[:, 1].fill_(1)   # eager steps may have moved any row: treat every segment as touched
+        if self.segmaps is not None:
+            # an eager step on slot k (runtime_adapt(active_module=k), or the eager routed step) may have moved
+            # any row of table k: every segment of a table whose slot counter changed counts as touched, so the
+            # segment-mapped Adam keeps decaying its moments (ADVICE r03)
+            after = self.adam.step_dev.cpu().tolist()
+            for k in range(self.K):
+                if after[k] != before[k]:
+                    self.segmaps[k, 1].fill_(1)
         self._step0 = top - self.steps_done   # keeps the exhaustion guard exact

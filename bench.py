@@ -352,6 +352,25 @@ def load_traffic(name: str = "render", rnd: str = "r01"):
     return None
 
 
+def render_traffic_profile(workload: str, S: int, layout: str):
+    """Round-4 counter summary of the render line's dominant kernel (tools/pmc_r04.sh + tools/pmc_fold_r04.py:
+    separate rocprofv3 --pmc passes, FETCH_SIZE doubled per the gfx950 correction of MI355X_MICROARCH.md
+    'HBM', plus WRITE_SIZE), or None when no profile of this exact configuration is committed."""
+    name = {("c2", 256, "replicated"): "r04_pmc_c2_render.json",
+            ("c3", 256, "replicated"): "r04_pmc_c3_routed.json",
+            ("c4", 96, "replicated"): "r04_pmc_c4s96_routed.json",
+            ("c4", 256, "replicated"): "r04_pmc_c4_routed.json"}.get((workload, S, layout))
+    if name is None:
+        return None
+    p = REPO / "profiles" / name
+    try:
+        d = json.loads(p.read_text())
+    except Exception:
+        return None
+    d["_source"] = f"profiles/{name}"
+    return d
+
+
 def load_gather_ceiling():
     """Committed gather-only ceiling of the render's hash access (tools/micro/hash_gather.py on the GPU box:
     profiles/r03_hash_gather_ceiling.json)."""
@@ -916,7 +935,7 @@ def main():
     # samples one launch of the dominant kernel processes on this rank
     launch_samples = samples_per_step // world // max(kernel_launches, 1)
     achieved = FLOP_PER_SAMPLE * launch_samples / (kernel_ms * 1e-3) / 1e12
-    tr = load_traffic("render", "r02") if a.workload == "c2" else None
+    tr = render_traffic_profile(a.workload, S, a.layout) if a.workload in ("c2", "c3", "c4") else None
     kname = {"c5": "adam_slots_kernel (Adam over every expert with routed samples + background head, clip coefficient "
                    "folded in, table gradients cleared in the same pass)",
              "c5a": "adam_kernel (fused clip + Adam over the adapted expert + background head)",
@@ -941,7 +960,8 @@ def main():
     hash_gbs = BYTES_PER_SAMPLE * launch_samples / (kernel_ms * 1e-3) / 1e9
     roofline = {"bound": "hbm", "achieved": round(hash_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(hash_gbs / HBM_PEAK_GBS, 4),
-                "traffic": (tr or {}).get("hbm_bytes_per_launch"),
+                "traffic": (tr or {}).get("hbm_bytes_per_launch")
+                if tr and tr.get("samples_per_launch") == int(launch_samples) else None,
                 "kernel": kname, "kernel_ms": round(kernel_ms, 4), "samples_per_launch": int(launch_samples),
                 "bytes_per_sample": BYTES_PER_SAMPLE,
                 "bytes_algorithmic_per_launch": int(BYTES_PER_SAMPLE * launch_samples),
@@ -965,17 +985,28 @@ def main():
             "achieved_alg_gbs": round(hash_gbs, 1), "frac": round(hash_gbs / c["alg_gbs"], 4),
             "uniform_random_points_alg_gbs": gc["uniform_best"]["alg_gbs"],
             "source": "profiles/r03_hash_gather_ceiling.json (+ r03_rocprof_hash_gather_kernel_stats.csv)"}
-    if tr:
+    if tr and tr.get("samples_per_launch") == int(launch_samples):
         d = tr.get("derived", {})
         miss_bytes = d.get("l2_miss_bytes_per_launch_at_128B")
-        lg = {"what": "hash-table lines served from beyond the XCD L2 (TCC_MISS x 128-B line) per launch",
-              "l2_misses_per_sample": round(d.get("l2_misses_per_sample", 0.0), 2),
-              "l2_hit_rate": round(d.get("l2_hit_rate", 0.0), 3),
-              "line_bytes_per_launch": int(miss_bytes) if miss_bytes else None,
-              "source": f"profiles/pmc_render_r02.json ({tr.get('round')})"}
-        if miss_bytes and tr.get("rocprof_avg_ns"):
-            lg["achieved_gbs"] = round(miss_bytes / tr["rocprof_avg_ns"], 1)
-        roofline["line_gather"] = lg
+        prof_ms = (tr.get("rocprof_avg_ns") or 0.0) / 1e6
+        roofline["traffic_detail"] = {
+            "what": "bytes beyond the XCD L2s per launch: 2 x FETCH_SIZE (gfx950 read correction, "
+                    "MI355X_MICROARCH.md 'HBM') + WRITE_SIZE, Infinity-Cache hits included; cross-checked by "
+                    "TCC_MISS x 128 B",
+            "source": f"{tr['_source']} ({tr.get('round')}, kernel {tr.get('kernel_match')})",
+            "traffic_over_algorithmic": round(d.get("traffic_over_algorithmic", 0.0), 3),
+            "fetch_over_tcc_miss_lines": round(d.get("fetch_corrected_over_tcc_miss_lines") or 0.0, 3),
+            "l2_misses_per_sample": round(d.get("l2_misses_per_sample", 0.0), 2),
+            "l2_requests_per_sample": round(d.get("l2_requests_per_sample", 0.0), 2),
+            "l2_hit_rate": round(d.get("l2_hit_rate") or 0.0, 3),
+            "td_busy_frac": round(d.get("td_busy_frac") or 0.0, 3),
+            "td_stalled_on_tc_frac": round(d.get("td_stalled_on_tc_frac") or 0.0, 3),
+            "mfma_busy_frac_per_simd": round(d.get("mfma_busy_frac_per_simd") or 0.0, 3),
+            "mean_waves_per_cu": round(d.get("mean_waves_per_cu") or 0.0, 2),
+            "profiled_kernel_ms": round(prof_ms, 4),
+            "traffic_gbs_at_profiled_time": round(tr["hbm_bytes_per_launch"] / (prof_ms * 1e-3) / 1e9, 1)
+            if prof_ms else None,
+            "line_bytes_per_launch": int(miss_bytes) if miss_bytes else None}
     if a.workload in ("c5", "c5a", "meta"):
         roofline = {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kname,

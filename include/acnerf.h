@@ -156,6 +156,13 @@ int acn_render_stratified_fwd(const float* rays, int64_t N, int S, const float* 
  * (0 when N is outside the re-ordered range 1..8192: the call then renders in the given order). */
 size_t acn_render_order_bytes(int64_t N);
 
+/* The visiting order acn_render_stratified_fwd_ordered uses for a batch of 1 <= N <= 8192 rays (the
+ * reference renders rays independently, ray_rendering.py:290-345, so only the order of the work
+ * changes): order[0..N) is a permutation of 0..N-1 grouping the rays by a Z-ordered 64 x 64 cell of
+ * their direction about the batch mean; the sort is stable, so rays of one cell stay in index order
+ * and the order is the same on every call.  Exposed for tests and tools.                         */
+int acn_ray_order(const float* rays, int64_t N, int32_t* order, void* stream);
+
 /* acn_render_stratified_fwd with a caller-owned scratch of acn_render_order_bytes(N) bytes (NULL /
  * too small = no re-ordering).  Small batches are first sorted by ray direction (Z-order) so that
  * each XCD renders one compact image region and its L2 serves that region's hash cells; every ray
@@ -518,9 +525,12 @@ int acn_xd_unit_sh(const float* xd, int64_t P, const float* aabb_min, const floa
  * expert block per GPU; replaces the per-expert nonzero / index_select dispatch of meta_container.py:300-337
  * across ranks).  Every buffer has a host-known fixed capacity, so the all-to-alls use constant split
  * sizes and nothing is read back to the host:
- *   acn_routed_count_fixed -> as acn_routed_count, but expert k's segment is [k cap, (k+1) cap) (cap >= N*S:
- *                             never overflows); seg[K+1+k] = live count.  With experts numbered by owner
- *                             (contiguous blocks) the pair buffer IS the send buffer of the all-to-all.
+ *   acn_routed_count_fixed -> as acn_routed_count, but expert k's segment is [k cap, (k+1) cap); seg[K+1+k] =
+ *                             live count.  cap >= N*S never overflows; a smaller cap (an exchange sized to the
+ *                             live records) keeps the first cap pairs of an expert in sample order, the scatter
+ *                             drops the rest (pmap -1) and seg[K+1+k] > cap tells the caller to redo the batch
+ *                             with a larger cap.  With experts numbered by owner (contiguous blocks) the pair
+ *                             buffer IS the send buffer of the all-to-all.  Consumers clamp counts to cap.
  *   acn_routed_pad_pairs   -> pidx -1, pw 0 on every segment's slots past its live count (max_pad: a bound
  *                             on one segment's padding, e.g. cap).
  *   acn_ep_gather          -> owner side: records received as [src][local expert j][cap] (W x E x cap xd
@@ -542,6 +552,23 @@ int acn_ep_gather(const float* recv_xd, const int64_t* recv_cnt, int W, int E, i
                   float* x01, float* sh, int32_t* pk, int32_t* pflag, int64_t* back, void* stream);
 int acn_ep_scatter_back(const float* out, const int64_t* back, const int64_t* seg, int E, float* ret, void* stream);
 int acn_ep_gather_grad(const float* gy, const int64_t* back, const int64_t* seg, int E, float* gout, void* stream);
+
+/* One expert per GPU, render (expert_parallel.ExpertParallelRenderer): the fused routed render split at its
+ * expert boundary (render_rays_stratified ray_rendering.py:290-345 with MetaContainer.forward's per-expert
+ * loop meta_container.py:300-337 distributed over the ranks).
+ *   acn_ep_field_fwd -> owner: the field of its E experts (`experts`, packed by acn_pack_experts with a routing
+ *                       of K = E, active_module -1) on the records received as [src][local expert][cap] with live
+ *                       counts recv_cnt (W, E) (clamped to cap) -> ret (W*E*cap, 4) (rgb, sigma) in the same
+ *                       layout; per record the arithmetic of the fused routed render.
+ *   acn_ep_composite -> sender: per sample y = 0 + sum_k y_k w_k over its pairs in ascending k (pmap (N*S, K)
+ *                       pair index or -1, yr (pairs, 4) the returned field outputs, pw the weights; hard != 0:
+ *                       y = y_k, index_copy_), then compositing, background and outputs as
+ *                       acn_render_stratified_fwd (weights may be NULL).                                   */
+int acn_ep_field_fwd(const float* recv_xd, const int64_t* recv_cnt, int W, int E, int64_t cap,
+                     const acn_expert* experts, const void* packed, size_t packed_bytes, float* ret, void* stream);
+int acn_ep_composite(const float* rays, int64_t N, int S, const float* jitter, const float* yr, const float* pw,
+                     const int32_t* pmap, int K, int hard, const acn_background* bg, float sigma_scale, float tau,
+                     float* rgb, float* depth, float* weights, float* acc, void* stream);
 
 /* Per-expert kernels over routed pair slots (segments padded to multiples of 128, slot count seg[K] on the
  * device; fixed grids that stride to it, so a whole step is capturable in a hipGraph):

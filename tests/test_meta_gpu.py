@@ -199,3 +199,37 @@ def test_graphed_meta_step_refuses_second_order():
     m, tasks = _model_and_tasks(d)
     with pytest.raises(ValueError):
         MT.GraphedMetaStep(_P("maml"), m, build_optimizer(_P("maml"), m), tasks)
+
+
+def test_drop_in_train_step_state_dict_current_without_sync(monkeypatch):
+    """the drop-in train_step leaves optimizer.state current after every replayed step, so the
+    reference's checkpoint (optimizer.state_dict(), utils.py:290) is right without an explicit sync: step
+    counts equal the eager run's, and an expert whose region first gets a task after the graphs were built
+    (its state was pending inside the graph) appears with its real count."""
+    from adaptive_city_nerf_amd import meta_train as MT
+    from adaptive_city_nerf_amd.optim import build_optimizer
+    d = G.load("meta_fomaml")
+    P = _P("fomaml")
+    ma, tasks = _model_and_tasks(d)
+    mb, _ = _model_and_tasks(d)
+    oa, ob = build_optimizer(P, ma), build_optimizer(P, mb)
+    cids = sorted(tasks)
+    drop = cids[-1]
+    partial = {c: (tasks[c] if c != drop else []) for c in cids}
+    seq = [partial, partial, tasks, tasks, partial]
+    results = []
+    for fast, m, o in ((False, ma, oa), (True, mb, ob)):
+        monkeypatch.setattr(MT, "FAST_META_STEP", fast)
+        torch.manual_seed(5)
+        with contextlib.redirect_stdout(None):
+            for step, td in enumerate(seq):
+                r = MT.train_step(P, step, m, o, td)
+        results.append(r)
+    g = ob._acn_meta_graph
+    assert isinstance(g, MT.GraphedMetaStep) and g.replays == 3
+    sa, sb = oa.state_dict()["state"], ob.state_dict()["state"]
+    assert sorted(sa) == sorted(sb)
+    for i in sa:
+        assert float(sa[i]["step"]) == float(sb[i]["step"]), i
+    _compare_meta_runs(ma, oa, mb, ob, results[0], results[1],
+                       lambda n: 2 if n.startswith(f"submodules.{drop}.") else len(seq))

@@ -620,3 +620,64 @@ def test_adam_segment_maps_bitwise_equal_dense_over_10_steps(monkeypatch):
                 assert torch.equal(a, b), n
     finally:
         torch.use_deterministic_algorithms(False)
+
+
+@pytest.mark.gpu
+def test_runtime_adapt_alternating_active_module_keeps_adam_state(monkeypatch):
+    """an eager single-expert update (runtime_adapt's active_module path) between routed
+    runtime_adapt calls on the same optimizer.  The cached RoutedAdaptStep must pick up that update: the
+    expert's step counter, its moments (first-updated parameters included) and -- with the segment-mapped
+    Adam -- every table segment the eager step touched, whose moments keep decaying in later routed steps.
+    Parameters, moments and step counts equal the all-eager sequence: in particular on the table rows the
+    eager step moved (a missed 'ever' mark would leave them un-updated, an lr-sized difference)."""
+    from test_module_api import build_model, reference_state_dict
+    from adaptive_city_nerf_amd import routed_train as RT
+    from adaptive_city_nerf_amd import train as T
+    from adaptive_city_nerf_amd.optim import build_optimizer
+    d = G.load("train_k8")
+    Pk = SimpleNamespace(**{**vars(P), "ray_samples": 96, "chunk_points": 4_000_000})
+    rays = torch.from_numpy(d["train0:rays"]).cuda()
+    rgbs = torch.from_numpy(d["train0:rgbs"]).cuda()
+    g = torch.Generator(device="cuda").manual_seed(11)
+    batches = []
+    for _ in range(4):
+        sel = torch.randperm(1000, device="cuda", generator=g)
+        batches.append((rays[sel].contiguous(), rgbs[sel].contiguous(), torch.rand(1000, 96, device="cuda", generator=g)))
+    K_EAGER = 3
+    results, moved = [], None
+    for fast in (True, False):
+        m, _ = build_model("k8")
+        m.load_state_dict(reference_state_dict(d, 8, "w:"))
+        m = m.cuda().train()
+        opt = build_optimizer(Pk, m)
+        ustat = torch.zeros(1000, 96, device="cuda")
+        monkeypatch.setattr(RT, "JITTER", lambda n, S, dev: ustat[:n])
+        tab = m.submodules[K_EAGER].xyz_encoder.hash_table
+        for i, (r, c, u) in enumerate(batches):
+            if i == 1:      # the eager single-expert update (runtime_adapt.py with active_module)
+                before = tab.detach().clone()
+                T.adapt_step(Pk, m.submodules[K_EAGER], r, c, opt, active_module=K_EAGER, grad_clip=1.0, jitter_u=u)
+                if not fast:
+                    moved = (tab.detach() != before).any(dim=1)
+            elif fast:
+                ustat.copy_(u)
+                T.runtime_adapt(P=Pk, model=m, data_loader=[(r, c)], optimizer=opt, steps=1)
+            else:
+                T.adapt_step(Pk, m, r, c, opt, grad_clip=1.0, jitter_u=u)
+        torch.cuda.synchronize()
+        if fast:
+            assert next(iter(opt._acn_routed_steps.values())).steps_done == 3
+        results.append(({n: p.detach().clone() for n, p in m.named_parameters()},
+                        {n: float(opt.state[p]["step"]) for n, p in m.named_parameters() if p in opt.state},
+                        {n: opt.state[p]["exp_avg"].clone() for n, p in m.named_parameters() if p in opt.state}))
+    (pa, sa, ma), (pb, sb, mb) = results
+    assert sa == sb
+    assert int(moved.sum()) > 1000
+    for n in pa:
+        lr = 0.01 if n.endswith("hash_table") else 0.001 if n.startswith("bg_mlp") else 0.002
+        assert _close_frac(pa[n].cpu().numpy(), pb[n].cpu().numpy(), 1e-3 * lr, 1e-6) >= 0.95, n
+    key = f"submodules.{K_EAGER}.xyz_encoder.hash_table"
+    a, b = pa[key][moved].cpu().numpy(), pb[key][moved].cpu().numpy()
+    assert _close_frac(a, b, 1e-3 * 0.01, 1e-6) >= 0.99, "rows the eager step moved diverge after routed steps"
+    a, b = ma[key][moved].cpu().numpy(), mb[key][moved].cpu().numpy()
+    assert _close_frac(a, b, 1e-3 * float(np.abs(b).max()), 1e-3) >= 0.99

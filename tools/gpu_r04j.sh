@@ -1,0 +1,5 @@
+#!/bin/bash
+set -o pipefail
+export TMPDIR=/tmp
+export ACNERF_LIB=$PWD/build_variants/libacnerf_check.so
+timeout -k 10 200 python -u tools/dbg/rt_check.py 2>&1 | grep -v -i 'warning\|amdgpu.ids'
