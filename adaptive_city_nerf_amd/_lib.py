@@ -90,6 +90,8 @@ SIGNATURES = {
                                   C.c_int),
     "acn_render_order_bytes": ([i64], sz),
     "acn_ray_order": ([vp, i64, vp, vp], C.c_int),
+    "acn_routed_count_caps": ([vp, i64, i32, vp, vp, vp, vp, vp, vp, sz, vp], C.c_int),
+    "acn_ep_gather_caps": ([vp, vp, i32, i32, vp, i32, vp, vp, f32, f32, vp, vp, vp, vp, vp, vp, vp, vp], C.c_int),
     "acn_ep_field_fwd": ([vp, vp, i32, i32, i64, vp, vp, sz, vp, vp], C.c_int),
     "acn_ep_composite": ([vp, i64, i32, vp, vp, vp, vp, i32, i32, vp, f32, f32, vp, vp, vp, vp, vp], C.c_int),
     "acn_render_stratified_fwd_ordered": ([vp, i64, i32, vp, vp, vp, i32, vp, f32, f32, vp, sz, vp, vp, vp, vp,

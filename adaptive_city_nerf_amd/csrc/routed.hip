@@ -34,6 +34,14 @@ struct RouteCfg {
     float cent[kMaxK][3];
 };
 
+// Fixed pair layout of the expert-parallel exchange: expert k's segment is [off[k], off[k] + cap[k]) (uniform
+// capacity: off[k] = k cap); fixed = 0: the compact layout of acn_routed_count (segments padded to `align`)
+struct Caps {
+    int32_t fixed;
+    int64_t cap[kMaxK];
+    int64_t off[kMaxK + 1];
+};
+
 // weight of expert k for a sample at p (the reference's rule; hard routing as weight 1 of the argmin:
 // 0 + y * 1 == y, identical to index_copy_)
 __device__ __forceinline__ void route_row(const RouteCfg& cfg, float px, float py, float pz, float (&w)[kMaxK]) {
@@ -91,7 +99,7 @@ __global__ void __launch_bounds__(kBlk) routed_count_kernel(const float* __restr
 // cap > 0: fixed layout -- expert k's segment is [k cap, (k + 1) cap) whatever the counts (cap >= M, so no
 // segment can overflow): the expert-parallel send buffer, grouped by owner, with host-known split sizes
 __global__ void __launch_bounds__(1024) routed_scan_kernel(int32_t* __restrict__ blk_cnt, int64_t nblk, int K,
-                                                           int align, int64_t cap, int64_t* __restrict__ starts) {
+                                                           int align, Caps caps, int64_t* __restrict__ starts) {
     // all K experts' scans at once: per-thread chunk sums, an inclusive wave scan (shuffles, no
     // barriers), then the 16 wave totals through LDS (one barrier) -- integer sums, so the result equals
     // the serial prefix sums exactly (a Hillis-Steele pass per expert cost 20 barriers each)
@@ -134,11 +142,11 @@ __global__ void __launch_bounds__(1024) routed_scan_kernel(int32_t* __restrict__
         for (int k = 0; k < K; ++k) {
             int64_t total = 0;
             for (int i = 0; i < 16; ++i) total += wtot[i][k];
-            starts[k] = cap > 0 ? k * cap : base;
+            starts[k] = caps.fixed ? caps.off[k] : base;
             starts[K + 1 + k] = total;                        // real pair count of expert k
             base += (total + align - 1) / align * align;      // segment padded to a multiple of align
         }
-        starts[K] = cap > 0 ? K * cap : base;
+        starts[K] = caps.fixed ? caps.off[K] : base;
     }
 }
 
@@ -303,7 +311,15 @@ __global__ void __launch_bounds__(256) pad_pairs_kernel(const int64_t* __restric
 // Owner: the received layout is [src s][local expert j][cap] records with live counts cnt[s][j]; the compact
 // pair list holds local expert j's records in (s, i) order in a segment padded to `align`.  One thread:
 // off[s][j] = sum_{s' < s} cnt[s'][j], seg[j] (padded starts), seg[E] = slots, seg[E + 1 + j] = live count.
-__global__ void ep_seg_kernel(const int64_t* __restrict__ cnt, int W, int E, int align, int64_t cap,
+// the received layout of a capacity-bounded exchange: sender s's segment of local expert j starts at
+// s * row + off[j] and holds at most cap[j] records (uniform: off[j] = j cap, row = E cap)
+struct OwnCaps {
+    int64_t row;
+    int64_t cap[kMaxK];
+    int64_t off[kMaxK];
+};
+
+__global__ void ep_seg_kernel(const int64_t* __restrict__ cnt, int W, int E, int align, OwnCaps oc,
                               int64_t* __restrict__ off, int64_t* __restrict__ seg) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     int64_t base = 0;
@@ -312,7 +328,7 @@ __global__ void ep_seg_kernel(const int64_t* __restrict__ cnt, int W, int E, int
         for (int s = 0; s < W; ++s) {
             off[(int64_t)s * E + j] = run;
             const int64_t c = cnt[(int64_t)s * E + j];
-            run += c < cap ? c : cap;   // a sender's count past the capacity: only cap records were sent
+            run += c < oc.cap[j] ? c : oc.cap[j];   // a count past the capacity: only cap records were sent
         }
         seg[j] = base;
         seg[E + 1 + j] = run;
@@ -325,7 +341,7 @@ __global__ void ep_seg_kernel(const int64_t* __restrict__ cnt, int W, int E, int
 // routed_scatter_kernel<0>), pk = j, pflag = 0 (pair) / -1 (padding), back = received-layout index or -1
 __global__ void __launch_bounds__(256) ep_gather_kernel(const float* __restrict__ xd, const int64_t* __restrict__ cnt,
                                                         const int64_t* __restrict__ off, const int64_t* __restrict__ seg,
-                                                        int W, int E, int64_t cap, BoxCfg box, float* __restrict__ x01,
+                                                        int W, int E, OwnCaps oc, BoxCfg box, float* __restrict__ x01,
                                                         float* __restrict__ sh_out, int32_t* __restrict__ pk,
                                                         int32_t* __restrict__ pflag, int64_t* __restrict__ back) {
     const int64_t total = seg[E];
@@ -346,7 +362,7 @@ __global__ void __launch_bounds__(256) ep_gather_kernel(const float* __restrict_
         int s = 0;
         while (s + 1 < W && off[(int64_t)(s + 1) * E + j] <= q) ++s;
         const int64_t i = q - off[(int64_t)s * E + j];
-        const int64_t src = ((int64_t)s * E + j) * cap + i;
+        const int64_t src = (int64_t)s * oc.row + oc.off[j] + i;
         const float* r = xd + src * 6;
         pflag[p] = 0;
         back[p] = src;
@@ -419,20 +435,36 @@ extern "C" int acn_routed_count(const float* rays, int64_t N, int S, const float
     const int64_t nblk = (M + kBlk - 1) / kBlk;
     hipLaunchKernelGGL(routed_count_kernel, dim3(blocks_for(M, kBlk)), dim3(kBlk), 0, s, rays, N, S, jitter, cfg, t_vals,
                        W, blk);
-    hipLaunchKernelGGL(routed_scan_kernel, dim3(1), dim3(1024), 0, s, blk, nblk, K, align, (int64_t)0, starts);
+    Caps caps{};
+    hipLaunchKernelGGL(routed_scan_kernel, dim3(1), dim3(1024), 0, s, blk, nblk, K, align, caps, starts);
     return acn_check_launch("acn_routed_count");
 }
 
 extern "C" int acn_routed_count_fixed(const float* rays, int64_t N, int S, const float* jitter,
                                       const acn_routing* routing, int64_t cap, float* t_vals, int64_t* starts,
                                       void* workspace, size_t workspace_bytes, void* stream) {
-    ACN_REQUIRE(N >= 0 && S >= 1 && routing && starts, "acn_routed_count_fixed: bad arguments");
+    ACN_REQUIRE(routing && routing->K >= 1 && routing->K <= kMaxK, "acn_routed_count_fixed: bad routing");
+    int64_t caps[kMaxK];
+    for (int k = 0; k < routing->K; ++k) caps[k] = cap;
+    return acn_routed_count_caps(rays, N, S, jitter, routing, caps, t_vals, starts, workspace, workspace_bytes, stream);
+}
+
+extern "C" int acn_routed_count_caps(const float* rays, int64_t N, int S, const float* jitter,
+                                     const acn_routing* routing, const int64_t* caps_host, float* t_vals,
+                                     int64_t* starts, void* workspace, size_t workspace_bytes, void* stream) {
+    ACN_REQUIRE(N >= 0 && S >= 1 && routing && starts && caps_host, "acn_routed_count_caps: bad arguments");
     const int K = routing->K;
-    ACN_REQUIRE(K >= 1 && K <= kMaxK, "acn_routed_count_fixed: K = %d outside [1, %d]", K, kMaxK);
+    ACN_REQUIRE(K >= 1 && K <= kMaxK, "acn_routed_count_caps: K = %d outside [1, %d]", K, kMaxK);
     const int64_t M = N * (int64_t)S;
-    ACN_REQUIRE(cap >= 1, "acn_routed_count_fixed: capacity must be >= 1, got %lld", (long long)cap);
+    Caps caps{};
+    caps.fixed = 1;
+    for (int k = 0; k < K; ++k) {
+        ACN_REQUIRE(caps_host[k] >= 1, "acn_routed_count_caps: capacity of expert %d must be >= 1", k);
+        caps.cap[k] = caps_host[k];
+        caps.off[k + 1] = caps.off[k] + caps_host[k];
+    }
     ACN_REQUIRE(workspace && workspace_bytes >= acn_routed_workspace_bytes(M, K),
-                "acn_routed_count_fixed: workspace too small");
+                "acn_routed_count_caps: workspace too small");
     hipStream_t s = (hipStream_t)stream;
     RouteCfg cfg{};
     cfg.K = K;
@@ -445,12 +477,12 @@ extern "C" int acn_routed_count_fixed(const float* rays, int64_t N, int S, const
     int32_t* blk = (int32_t*)(W + M * K);
     const int64_t nblk = (M + kBlk - 1) / kBlk;
     if (M > 0) {
-        ACN_REQUIRE(rays && t_vals, "acn_routed_count_fixed: NULL pointer");
+        ACN_REQUIRE(rays && t_vals, "acn_routed_count_caps: NULL pointer");
         hipLaunchKernelGGL(routed_count_kernel, dim3(blocks_for(M, kBlk)), dim3(kBlk), 0, s, rays, N, S, jitter, cfg,
                            t_vals, W, blk);
     }
-    hipLaunchKernelGGL(routed_scan_kernel, dim3(1), dim3(1024), 0, s, blk, nblk, K, 1, cap, starts);
-    return acn_check_launch("acn_routed_count_fixed");
+    hipLaunchKernelGGL(routed_scan_kernel, dim3(1), dim3(1024), 0, s, blk, nblk, K, 1, caps, starts);
+    return acn_check_launch("acn_routed_count_caps");
 }
 
 extern "C" int acn_routed_scatter(const float* rays, int64_t N, int S, int K, const float* t_vals,
@@ -538,8 +570,26 @@ extern "C" int acn_ep_gather(const float* recv_xd, const int64_t* recv_cnt, int 
                              const float* aabb_min, const float* aabb_extent, float lo, float hi, int64_t* seg,
                              void* workspace, float* x01, float* sh, int32_t* pk, int32_t* pflag, int64_t* back,
                              void* stream) {
-    ACN_REQUIRE(W >= 1 && E >= 1 && E <= kMaxK && cap >= 1 && align >= 1 && aabb_min && aabb_extent,
+    ACN_REQUIRE(E >= 1 && E <= kMaxK && cap >= 1, "acn_ep_gather: bad arguments");
+    int64_t caps[kMaxK];
+    for (int j = 0; j < E; ++j) caps[j] = cap;
+    return acn_ep_gather_caps(recv_xd, recv_cnt, W, E, caps, align, aabb_min, aabb_extent, lo, hi, seg, workspace, x01,
+                              sh, pk, pflag, back, stream);
+}
+
+extern "C" int acn_ep_gather_caps(const float* recv_xd, const int64_t* recv_cnt, int W, int E, const int64_t* caps_host,
+                                  int align, const float* aabb_min, const float* aabb_extent, float lo, float hi,
+                                  int64_t* seg, void* workspace, float* x01, float* sh, int32_t* pk, int32_t* pflag,
+                                  int64_t* back, void* stream) {
+    ACN_REQUIRE(W >= 1 && E >= 1 && E <= kMaxK && caps_host && align >= 1 && aabb_min && aabb_extent,
                 "acn_ep_gather: bad arguments");
+    OwnCaps oc{};
+    for (int j = 0; j < E; ++j) {
+        ACN_REQUIRE(caps_host[j] >= 1, "acn_ep_gather: capacity of local expert %d must be >= 1", j);
+        oc.cap[j] = caps_host[j];
+        oc.off[j] = oc.row;
+        oc.row += caps_host[j];
+    }
     ACN_REQUIRE(recv_xd && recv_cnt && seg && workspace && x01 && sh && pk && pflag && back,
                 "acn_ep_gather: NULL pointer");
     BoxCfg box{};
@@ -552,9 +602,9 @@ extern "C" int acn_ep_gather(const float* recv_xd, const int64_t* recv_cnt, int 
     box.hi = hi;
     hipStream_t s = (hipStream_t)stream;
     int64_t* off = (int64_t*)workspace;
-    hipLaunchKernelGGL(ep_seg_kernel, dim3(1), dim3(64), 0, s, recv_cnt, W, E, align, cap, off, seg);
+    hipLaunchKernelGGL(ep_seg_kernel, dim3(1), dim3(64), 0, s, recv_cnt, W, E, align, oc, off, seg);
     hipLaunchKernelGGL(ep_gather_kernel, dim3(kEpBlocks), dim3(256), 0, s, recv_xd, recv_cnt, (const int64_t*)off,
-                       (const int64_t*)seg, W, E, cap, box, x01, sh, pk, pflag, back);
+                       (const int64_t*)seg, W, E, oc, box, x01, sh, pk, pflag, back);
     return acn_check_launch("acn_ep_gather");
 }
 

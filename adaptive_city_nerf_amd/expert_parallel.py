@@ -528,7 +528,8 @@ class ExpertParallelAdaptStep:
 
     def __init__(self, P, model, n_rays: int, optimizer: FusedAdam, n_rays_global: Optional[int] = None,
                  grad_clip: Optional[float] = 1.0, group=None, graph: bool = False, warmup: int = 1,
-                 jitter: str = "draw", clear_in_adam: bool = True, max_steps: int = 1 << 16):
+                 jitter: str = "draw", clear_in_adam: bool = True, max_steps: int = 1 << 16,
+                 capacity: Optional[int] = None):
         import ctypes as C
         import numpy as np
         from . import _lib, ops
@@ -565,14 +566,24 @@ class ExpertParallelAdaptStep:
         eo = [owner.count(o) for o in range(W)]      # experts per owner (contiguous blocks)
         S, N = int(P.ray_samples), int(n_rays)
         M = N * S
-        Cc = M                                          # capacity of one (sender, expert) segment
+        # capacity of one (sender, expert) segment of the exchange: M (never overflows) or smaller, sized to the
+        # live records -- then a step whose pairs overflow on any rank is gated off on the device (zero upstream
+        # gradients, no slot active in Adam: no update, no step count) and re-run at full capacity at the next
+        # call (one small host read of the flag per step)
+        # capacity="adaptive": full capacity for the warm-up steps, then per expert ~1.5x the largest count any rank
+        # routed to it (all-reduced), regrown after an overflow (the graph is then captured again)
+        self.adaptive = capacity == "adaptive"
+        Cc = M if capacity is None or self.adaptive else max(1, min(M, int(capacity)))
         self.K, self.E, self.W, self.N, self.S, self.M, self.C = K, E, W, N, S, M, Cc
         self.own, self.eo = own, eo
         self.n_global = int(n_rays_global) if n_rays_global is not None else N * W
-        # splits (rows): sender -> owner o: its experts' segments; owner <- every sender: E segments
-        self.split_send = [e * Cc for e in eo]
-        self.split_recv = [E * Cc] * W
         self.split_cnt_send, self.split_cnt_recv = list(eo), [E] * W
+        self.overflows = 0
+        self.recaptures = 0
+        self._check = None     # (event, n) of the last capacity-bounded step
+        self.caps_dev = torch.full((K,), Cc, device=dev, dtype=torch.int64)
+        self._set_caps([Cc] * K)
+        Cc = M                 # buffers: full capacity (the re-run layout); a bounded layout uses their prefix
         f32 = dict(device=dev, dtype=torch.float32)
         i32 = dict(device=dev, dtype=torch.int32)
         i64 = dict(device=dev, dtype=torch.int64)
@@ -614,6 +625,10 @@ class ExpertParallelAdaptStep:
         self.dw = torch.zeros(E, ops.MLP_DW_FLOATS, **f32)
         self.loss = torch.zeros((), **f32)
         self.loss_global = torch.zeros(1, **f32)
+        self.ovf = torch.zeros(1, **i64)                # global overflow flag of the last step (device)
+        self.ovf_host = torch.zeros(1, dtype=torch.int64, pin_memory=True)
+        self.keep = torch.ones((), **f32)               # 1 - overflow: gates the upstream gradients
+        self.ovf_b = torch.zeros(1, device=dev, dtype=torch.bool)
         # ---- persistent gradients of the owned experts and the (replicated) background head
         self.gtables = [torch.zeros_like(encs[k].hash_table) for k in own]
         self.bg_params = list(model.bg_mlp.parameters())
@@ -669,7 +684,26 @@ class ExpertParallelAdaptStep:
         self.graph = None
         self._eager_left = max(1, int(warmup)) if graph else 0
 
-    def _step(self, n: int) -> None:
+    def _set_caps(self, caps) -> None:
+        """Per-expert segment capacities (identical on every rank) and the layouts / split sizes they imply."""
+        import ctypes as C
+        self.caps = [int(max(1, min(self.M, c))) for c in caps]
+        self.caps_dev.copy_(torch.tensor(self.caps, dtype=torch.int64))
+        self._caps_c = (C.c_int64 * self.K)(*self.caps)
+        self._own_caps_c = (C.c_int64 * self.E)(*[self.caps[k] for k in self.own])
+        owner = expert_owner(self.K, self.W)
+        self.split_send = [sum(self.caps[k] for k in range(self.K) if owner[k] == o) for o in range(self.W)]
+        self.split_recv = [sum(self.caps[k] for k in self.own)] * self.W
+        self.slots_send, self.slots_recv = sum(self.split_send), sum(self.split_recv)
+        self.bounded = any(c < self.M for c in self.caps)
+
+    def exchange_bytes(self) -> int:
+        """Bytes this rank sends per step over the four all-to-alls at the current capacities: the counts (8 B
+        per expert), then per pair slot the record (24 B), the (rgb, sigma) result (16 B) and its gradient
+        (16 B) -- the sends of this rank's records and results summed with those of its gradients."""
+        return 8 * self.K + 24 * self.slots_send + 16 * self.slots_recv + 16 * self.slots_send
+
+    def _step(self, n: int, full: bool = False) -> None:
         import ctypes as C
         from . import _lib, ops
         from ._lib import check, ptr
@@ -677,7 +711,13 @@ class ExpertParallelAdaptStep:
         from .routed_train import ALIGN, JITTER
         from .train import mse_color_loss
         L = _lib.lib()
-        dev, K, E, S, Cc, comm = self.device, self.K, self.E, self.S, self.C, self.comm
+        saved = None
+        if full and self.bounded:      # the full-capacity re-run of an overflowed step
+            saved = list(self.caps)
+            self._set_caps([self.M] * self.K)
+        bounded = self.bounded
+        Cc = self.C
+        dev, K, E, S, comm = self.device, self.K, self.E, self.S, self.comm
         s = int(torch.cuda.current_stream(dev).cuda_stream)
         M = n * S
         if not self.clear_in_adam:
@@ -687,16 +727,22 @@ class ExpertParallelAdaptStep:
         if self.jitter_mode == "draw":
             u.copy_(JITTER(n, S, dev))   # the reference's rand_like(low) draw
         # sender: pairs in the fixed owner-grouped layout
-        check(L.acn_routed_count_fixed(ptr(self.rays), n, S, ptr(u), C.byref(self.routing), Cc, ptr(t), ptr(self.seg),
-                                       ptr(self.rws), self.rws.numel(), s), "acn_routed_count_fixed")
+        check(L.acn_routed_count_caps(ptr(self.rays), n, S, ptr(u), C.byref(self.routing), self._caps_c, ptr(t),
+                                      ptr(self.seg), ptr(self.rws), self.rws.numel(), s), "acn_routed_count_caps")
         check(L.acn_routed_scatter_xd(ptr(self.rays), n, S, K, ptr(t), ptr(self.seg), ptr(self.rws), ptr(self.pidx),
                                       ptr(self.pw), ptr(self.xd), ptr(self.pmap), ptr(self.pk), s),
               "acn_routed_scatter_xd")
-        check(L.acn_routed_pad_pairs(ptr(self.seg), K, Cc, ptr(self.pidx), ptr(self.pw), s), "acn_routed_pad_pairs")
+        check(L.acn_routed_pad_pairs(ptr(self.seg), K, max(self.caps), ptr(self.pidx), ptr(self.pw), s),
+              "acn_routed_pad_pairs")
+        if bounded:   # any rank's expert past its capacity: the whole step is gated off (device flag, all-reduced)
+            torch.any(torch.gt(self.seg[K + 1: 2 * K + 1], self.caps_dev), dim=0, keepdim=True, out=self.ovf_b)
+            self.ovf.copy_(self.ovf_b)
+            comm.all_reduce_max(self.ovf)
+            self.keep.copy_(1.0 - self.ovf.to(torch.float32).view(()))
         comm.all_to_all(self.recv_cnt, self.seg[K + 1:], self.split_cnt_recv, self.split_cnt_send)
-        comm.all_to_all(self.recv_xd, self.xd, self.split_recv, self.split_send)
+        comm.all_to_all(self.recv_xd[:self.slots_recv], self.xd[:self.slots_send], self.split_recv, self.split_send)
         # owner: compact pair lists of the owned experts, field, results back into the received layout
-        check(L.acn_ep_gather(ptr(self.recv_xd), ptr(self.recv_cnt), self.W, E, Cc, ALIGN,
+        check(L.acn_ep_gather_caps(ptr(self.recv_xd), ptr(self.recv_cnt), self.W, E, self._own_caps_c, ALIGN,
                               C.cast(self._mins, C.c_void_p), C.cast(self._exts, C.c_void_p), self._lo, self._hi,
                               ptr(self.eseg), ptr(self.ews), ptr(self.x01), ptr(self.sh), ptr(self.pkl),
                               ptr(self.pflag), ptr(self.back), s), "acn_ep_gather")
@@ -710,11 +756,13 @@ class ExpertParallelAdaptStep:
               "acn_mlp_train_fwd_pairs")
         check(L.acn_ep_scatter_back(ptr(self.out), ptr(self.back), ptr(self.eseg), E, ptr(self.ret), s),
               "acn_ep_scatter_back")
-        comm.all_to_all(self.yr, self.ret, self.split_send, self.split_recv)
+        comm.all_to_all(self.yr[:self.slots_send], self.ret[:self.slots_recv], self.split_send, self.split_recv)
         # sender: blend, background, compositing, loss (the global batch mean), their gradients
         rs = ops.routed_blend_fwd(self.yr, self.pw, self.pmap[:M]).view(n, S, 4).requires_grad_(True)
         rays, rgbs, dirs = self.rays[:n], self.rgbs[:n], self.rgbs_dirs[:n]
-        frac = float(n) / float(self.n_global)
+        # the loss averages over the global batch: a full batch is n_global / W rays per rank (weak) or the
+        # configured share (strong); a ragged batch (n < n_rays, world size 1 only) averages over its own n rays
+        frac = float(n) / float(self.n_global) if n == self.N else 1.0
         if self.bg_spec is not None:
             dirs.copy_(rays[:, 3:6])
             bg = ops.background_fwd(dirs, self.bg_spec).requires_grad_(True)
@@ -722,6 +770,8 @@ class ExpertParallelAdaptStep:
                 rgb = volume_render(rs, t, bg_rgb=bg)[0]
                 loss = mse_color_loss(rgb, rgbs, self.P.color_space) * frac
                 g_rs, g_bg = torch.autograd.grad(loss, [rs, bg])
+            if bounded:
+                g_rs, g_bg = g_rs * self.keep, g_bg * self.keep
             ops.background_bwd(dirs, self.bg_spec, g_bg, self.gbg)
         else:
             with torch.enable_grad():
@@ -729,13 +779,13 @@ class ExpertParallelAdaptStep:
                 rgb = volume_render(rs, t, bg_rgb=bg)[0]
                 loss = mse_color_loss(rgb, rgbs, self.P.color_space) * frac
                 grads = torch.autograd.grad(loss, [rs] + self.bg_params)
-            g_rs = grads[0]
+            g_rs = grads[0] * self.keep if bounded else grads[0]
             for g, buf in zip(grads[1:], self.gbg):
-                buf.copy_(g)
+                buf.copy_(g * self.keep if bounded else g)
         self.loss.copy_(loss.detach())
         comm.all_reduce(self.gbg_flat)
-        gy = ops.routed_blend_bwd(g_rs.reshape(M, 4).contiguous(), self.pidx, self.pw)
-        comm.all_to_all(self.recv_gy, gy, self.split_recv, self.split_send)
+        gy = ops.routed_blend_bwd(g_rs.reshape(M, 4).contiguous(), self.pidx[:self.slots_send], self.pw[:self.slots_send])
+        comm.all_to_all(self.recv_gy[:self.slots_recv], gy, self.split_recv, self.split_send)
         # owner: backward of the owned experts
         check(L.acn_ep_gather_grad(ptr(self.recv_gy), ptr(self.back), ptr(self.eseg), E, ptr(self.gout), s),
               "acn_ep_gather_grad")
@@ -747,14 +797,37 @@ class ExpertParallelAdaptStep:
                                              ptr(self.table_sumsq) if self.tele else None, s),
               "acn_hashgrid_bwd_pairs_sumsq")
         from . import routed_train as RT
+        if bounded:   # an overflowed step activates no slot: no moment decay, no step count (seg[E] < 0)
+            self.eseg[E:E + 1].copy_(torch.where(self.ovf > 0, torch.full_like(self.ovf, -1), self.eseg[E:E + 1]))
         self.adam.step(self.eseg, self.grad_clip, self.table_sumsq if self.tele else None,
-                       hook=RT.EVENT_HOOK if self.graph is None else None,
+                       hook=RT.EVENT_HOOK if self.graph is None and not torch.cuda.is_current_stream_capturing()
+                       else None,
                        allreduce=comm.all_reduce if self.W > 1 else None)
         self.loss_global.copy_(self.loss.view(1))
         comm.all_reduce(self.loss_global)
+        if saved is not None:
+            self._set_caps(saved)
+
+    def _adapt_caps(self, grow: float = 1.5) -> None:
+        """Capacities from the last step's per-expert counts, all-reduced (MAX) so every rank agrees: ~grow x the
+        largest count (at least 256 slots), never below the current capacity after a regrow; drops the graph
+        (the split sizes changed) so the next full step is captured again."""
+        c = self.seg[self.K + 1: 2 * self.K + 1].clone()
+        self.comm.all_reduce_max(c)
+        counts = [int(v) for v in c.cpu().tolist()]
+        new = [max(256, int(grow * v) + 1) for v in counts]
+        if grow > 1.5:
+            new = [max(a, b) for a, b in zip(new, self.caps)]
+        self._set_caps(new)
+        if self.graph is not None:
+            self.graph = None
+            self._eager_left = 1
+            self.recaptures += 1
 
     def _capture(self) -> None:
         dev = self.device
+        if self.adaptive and not self.bounded:
+            self._adapt_caps()
         torch.cuda.synchronize(dev)
         g = torch.cuda.CUDAGraph()
         with graph_capture(g):
@@ -773,6 +846,12 @@ class ExpertParallelAdaptStep:
                            f"{tuple(rays.shape)}, {tuple(rgbs.shape)}")
         if self.adam.step0 + self.steps_done + 1 > self.adam.table_steps:
             raise AcnError("ExpertParallelAdaptStep: the Adam constant table is exhausted; build a new step object")
+        if n != self.N and self.W > 1:
+            # the global mean over a ragged global batch needs every rank's n: not known without a host exchange
+            # on a path the ranks may not all take -- feed full batches (drop_last) at W > 1
+            raise AcnError(f"ExpertParallelAdaptStep: ragged batch ({n} of {self.N} rays) at world size {self.W}; "
+                           "use full batches (drop_last=True) with more than one rank")
+        self.flush()    # the previous bounded step, re-run at full capacity if it overflowed
         self.rays[:n].copy_(rays, non_blocking=True)
         self.rgbs[:n].copy_(rgbs, non_blocking=True)
         if self.jitter_mode == "given":
@@ -788,13 +867,34 @@ class ExpertParallelAdaptStep:
                 self._eager_left -= 1
                 if self._eager_left == 0:
                     self._capture()
+        if self.bounded:
+            self.ovf_host.copy_(self.ovf, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._check = (ev, n)
         self.steps_done += 1
         bump_versions(self._params)
         return self.loss_global
+
+    def flush(self) -> None:
+        """Settle the last capacity-bounded step: read its (global) overflow flag and, when set, redo that step
+        at full capacity from the batch still in the static buffers (the overflowed attempt changed nothing).
+        Called at the start of every step and by sync_state()."""
+        if self._check is None:
+            return
+        ev, n = self._check
+        self._check = None
+        ev.synchronize()
+        if int(self.ovf_host[0]):
+            self.overflows += 1
+            self._step(n, full=True)
+            if self.adaptive:   # regrow from the true counts of the re-run, then capture again
+                self._adapt_caps(grow=2.0)
 
     @property
     def last_norm(self) -> Tensor:
         return self.adam.scale
 
     def sync_state(self) -> None:
+        self.flush()
         self.adam.sync_state()

@@ -279,7 +279,8 @@ class RoutedAdaptStep:
         gout = ops.routed_blend_bwd(g_rs.reshape(M, 4).contiguous(), self.pidx, self.pw, live=self.seg[K:K + 1])
         check(mfn("acn_mlp_train_bwd_dw_pairs")(ptr(self.h0), ptr(self.sh), ptr(self.out), ptr(gout), ptr(self.seg), K,
                                            ptr(self.mws), ptr(self.dw), ptr(self.gh0), s), "acn_mlp_train_bwd_dw_pairs")
-        bhook = BWD_HOOK if self.graph is None else None
+        capturing = torch.cuda.is_current_stream_capturing()   # no timing events inside a capture
+        bhook = BWD_HOOK if self.graph is None and not capturing else None
         if bhook is not None:
             b0 = torch.cuda.Event(enable_timing=True)
             b0.record()
@@ -301,7 +302,7 @@ class RoutedAdaptStep:
             b1.record()
             bhook.append((b0, b1))
         self.adam.step(self.seg, self.grad_clip, self.table_sumsq if self.tele else None,
-                       hook=EVENT_HOOK if self.graph is None else None)
+                       hook=EVENT_HOOK if self.graph is None and not capturing else None)
 
     def _table_bwd_deterministic(self, enc) -> None:
         """Under torch.use_deterministic_algorithms(True): every expert's table gradient by the sort-based

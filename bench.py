@@ -438,6 +438,9 @@ def main():
     ap.add_argument("--c5-scaling", choices=["weak", "strong"], default="weak",
                     help="c5, N > 1: every rank streams its own 1000-ray batches (weak), or the ranks split each "
                          "1000-ray batch (strong: the reference's exact runtime_adapt update)")
+    ap.add_argument("--ep-capacity", choices=["adaptive", "full"], default="adaptive",
+                    help="c5, N > 1: exchange segments sized per expert to ~1.5x the live pairs (overflowed steps "
+                         "re-run at full capacity), or every (sender, expert) segment at the full n x S")
     ap.add_argument("--ep-graph", action="store_true",
                     help="c5, N > 1: capture the expert-parallel step, RCCL collectives included, in a HIP graph")
     ap.add_argument("--driver", choices=["step", "runtime_adapt"], default="step",
@@ -689,7 +692,8 @@ def main():
             from adaptive_city_nerf_amd.expert_parallel import ExpertParallelAdaptStep
             ep = ExpertParallelAdaptStep(P, model, shard.stop - shard.start, opt,
                                          n_rays_global=bsz if strong else world * bsz, grad_clip=1.0, group=pg,
-                                         graph=a.ep_graph, warmup=2)
+                                         graph=a.ep_graph, warmup=2,
+                                         capacity=None if a.ep_capacity == "full" else "adaptive")
         loader = [(pool[i], gtp[i]) for i in range(nb)]   # a runtime_adapt data loader's batches (device)
         if world == 1 and a.driver == "step":  # the whole routed step (no host sync), one HIP graph (eager: --no-graph)
             from adaptive_city_nerf_amd.routed_train import RoutedAdaptStep
@@ -1182,6 +1186,15 @@ def main():
                                    "note": "linear-space PSNR (runtime_adapt.py:152-157) on held-out rays against a "
                                            "different 8-expert model's render (synthetic target)"}
             line["experts_hit_per_step"] = experts_hit
+            if ep is not None:
+                ep.flush()
+                live = int(ep.seg[ep.K + 1: 2 * ep.K + 1].sum())
+                line["exchange"] = {"bytes_sent_per_step_per_rank": ep.exchange_bytes(),
+                                    "live_pair_bytes_per_step_per_rank": 56 * live + 8 * ep.K,
+                                    "capacity_per_expert": ep.caps, "overflow_reruns": ep.overflows,
+                                    "recaptures": ep.recaptures,
+                                    "note": "sent = 8 B counts + 24 B record + 16 B result + 16 B gradient per pair "
+                                            "slot at the step's capacities; live = the same for the routed pairs"}
         if a.workload == "c4":
             line["psnr_vs_synthetic_gt_db"] = round(float(out[3]), 4)
         print(json.dumps(line))

@@ -546,6 +546,17 @@ int acn_routed_count_fixed(const float* rays, int64_t N, int S, const float* jit
                            int64_t cap, float* t_vals, int64_t* seg, void* workspace, size_t workspace_bytes,
                            void* stream);
 int acn_routed_pad_pairs(const int64_t* seg, int K, int64_t max_pad, int32_t* pidx, float* pw, void* stream);
+/* Per-expert capacities (HOST arrays): acn_routed_count_caps lays expert k's pairs at [sum_{j<k} caps[j], + caps[k]);
+ * acn_ep_gather_caps reads sender s's records of local expert j at s * sum(caps) + sum_{i<j} caps[i].  The
+ * uniform-capacity forms above are these with every capacity equal (an exchange sized per expert to the
+ * live records: expert_parallel.ExpertParallelAdaptStep(capacity="adaptive")).                             */
+int acn_routed_count_caps(const float* rays, int64_t N, int S, const float* jitter, const acn_routing* routing,
+                          const int64_t* caps, float* t_vals, int64_t* seg, void* workspace, size_t workspace_bytes,
+                          void* stream);
+int acn_ep_gather_caps(const float* recv_xd, const int64_t* recv_cnt, int W, int E, const int64_t* caps, int align,
+                       const float* aabb_min, const float* aabb_extent, float lo, float hi, int64_t* seg,
+                       void* workspace, float* x01, float* sh, int32_t* pk, int32_t* pflag, int64_t* back,
+                       void* stream);
 size_t acn_ep_workspace_bytes(int W, int E);
 int acn_ep_gather(const float* recv_xd, const int64_t* recv_cnt, int W, int E, int64_t cap, int align,
                   const float* aabb_min, const float* aabb_extent, float lo, float hi, int64_t* seg, void* workspace,
