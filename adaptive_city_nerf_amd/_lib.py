@@ -176,14 +176,16 @@ SIGNATURES = {
     "acn_adam_step_slots_segmap": ([vp, vp, i64, vp, vp, i32, i32, vp, i32, vp, i32, vp, vp, vp], C.c_int),
     "acn_hashgrid_bwd_pairs_segmap": ([vp, vp, vp, vp, i32, vp, vp, vp, i32, i32, i32, vp, vp, vp], C.c_int),
     "acn_hashgrid_pairs_mark": ([vp, vp, vp, vp, i32, vp, i32, i32, i32, vp, vp], C.c_int),
+    "acn_amp_unscale_coef": ([vp, f32, vp, f32, f32, i32, vp, vp, i32, vp], C.c_int),
     # clusters.hip
     "acn_voronoi_route": ([vp, i64, i32, vp, i32, i32, C.c_double, i32, i32, vp, vp, vp, vp, vp, vp], C.c_int),
 }
-# the exact-fp32 training MLP: the same ten entry points, suffixed _exact (mlp_train.hip built twice)
+# the exact-fp32 training MLP (suffix _exact) and the reference's use_amp arithmetic (suffix _amp): the same ten
+# entry points (mlp_train.hip built three times)
 MLP_ENTRY_POINTS = ("acn_mlp_workspace_bytes", "acn_mlp_train_fwd", "acn_mlp_train_bwd", "acn_mlp_dw_workspace_bytes",
                     "acn_mlp_train_bwd_dw", "acn_mlp_train_bwd_dw_img", "acn_mlp_pairs_workspace_bytes", "acn_mlp_pack_pairs",
                     "acn_mlp_train_fwd_pairs", "acn_mlp_train_bwd_dw_pairs")
-SIGNATURES.update({n + "_exact": SIGNATURES[n] for n in MLP_ENTRY_POINTS})
+SIGNATURES.update({n + sfx: SIGNATURES[n] for n in MLP_ENTRY_POINTS for sfx in ("_exact", "_amp")})
 
 
 def lib():

@@ -47,6 +47,27 @@ constexpr int G_A1 = 0, G_A2 = 64, G_HD = 128, G_C1 = 144, G_C2 = 208, G_RGB = 2
 #ifndef ACN_TRAIN_F16X3
 #define ACN_TRAIN_F16X3 1  // layer products as the fp32-accurate 3-term fp16 split (0: exact fp32 MFMA)
 #endif
+// ACN_TRAIN_AMP (third object, acn_mlp_*_amp): the reference's use_amp arithmetic -- the chain run under
+// torch.autocast(float16) (runtime_adapt.py:249-259, meta_core.py:38, configs/train.json:37).  F.linear casts
+// its input and weights to fp16 and addmm returns fp16 (one fp16 x fp16 product per term, fp32 accumulation,
+// the bias added, one rounding to fp16); ReLU / sigmoid / trunc_exp (custom_fwd without cast_inputs) run on
+// the fp16 tensors and round their results to fp16; the backward mirrors it (the output gradient cast to
+// fp16, each dX and [dW | db] rounded to fp16 once).  No per-wave rescaling: values past fp16's range
+// overflow / underflow exactly as under autocast -- the loss scale (GradScaler) is the caller's.
+#ifndef ACN_TRAIN_AMP
+#define ACN_TRAIN_AMP 0
+#endif
+#if ACN_TRAIN_AMP && !ACN_TRAIN_F16X3
+#error "ACN_TRAIN_AMP builds on the fp16 weight image (ACN_TRAIN_F16X3=1)"
+#endif
+// round to fp16 and back (the identity outside the AMP build)
+__device__ __forceinline__ float amp_r(float x) {
+#if ACN_TRAIN_AMP
+    return (float)(_Float16)x;
+#else
+    return x;
+#endif
+}
 
 // LDS weight image: row-major, W0 64x32, W1 64x64, Whead 32x64 (geo rows 0..14, sigma row 15, rows
 // 16..31 zero), Wc0 64x31 (col 31 = 0), Wc1 64x64, Wc2 32x64 (rows 3..31 zero), then the biases
@@ -79,6 +100,25 @@ __device__ __forceinline__ int opaque_v(int v) {
     asm volatile("" : "+v"(v));
     return v;
 }
+
+// the heads' activations and the first backward step (torch's derivative chain: sigmoid_backward
+// g * (1 - y) * y; trunc_exp backward g * exp(xc) = g * y; threshold_backward (ReLU) g where the output > 0).
+// AMP: sigmoid / exp of the fp16 pre-activations rounded to fp16; trunc_exp clamps at fp16(11.089866488) =
+// 11.09375 (clamp's scalar is cast to the tensor's dtype; exp(11.09375) > 65504, so the clamped maximum is
+// inf, as in the reference); the incoming gradient is cast to fp16 and each product rounded once.
+__device__ __forceinline__ float out_rgb(float x) { return amp_r(acn::sigmoidf_(x)); }
+__device__ __forceinline__ float out_sigma(float x) {
+#if ACN_TRAIN_AMP
+    const float m = 11.09375f;
+    x = x < -m ? -m : x;
+    x = x > m ? m : x;
+    return amp_r(expf(x));
+#else
+    return acn::trunc_exp(x);
+#endif
+}
+__device__ __forceinline__ float grad_rgb(float g, float y) { return amp_r((amp_r(g) * (1.0f - y)) * y); }
+__device__ __forceinline__ float grad_sigma(float g, float y) { return amp_r(amp_r(g) * y); }
 
 __device__ __forceinline__ int64_t fm_index(int64_t m, int nfeat, int f) {
     return (m / GS) * ((int64_t)nfeat * GS) + (int64_t)f * GS + (m % GS);
@@ -226,6 +266,21 @@ __device__ __forceinline__ void split_tiles(const f32x16 (&X)[KT], int k, f16x8 
     }
 }
 
+// AMP: the layer input cast to fp16 as F.linear under autocast does (B operand layout as split_tiles)
+template <int KT>
+__device__ __forceinline__ void cvt_tiles(const f32x16 (&X)[KT], f16x8 (&bh)[2 * KT]) {
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int s = 0; s < 2 * KT; ++s)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const f16x2 h = __builtin_convertvector(((f32x2){X[s >> 1][8 * (s & 1) + 2 * q], X[s >> 1][8 * (s & 1) + 2 * q + 1]}), f16x2);
+            bh[s][2 * q] = h[0];
+            bh[s][2 * q + 1] = h[1];
+        }
+}
+
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f16x8 cat44(const f16x4& a, const f16x4& b) {
     return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
@@ -237,6 +292,25 @@ template <int NT, int KT, int ROWS>
 __device__ __forceinline__ void fwd_layer(const float* W, int ld, const float* b, const f32x16 (&X)[KT],
                                           f32x16 (&Y)[NT], int lane) {
     const int i = lane & 31, h = lane >> 5;
+#if ACN_TRAIN_AMP
+    (void)ROWS;
+    f16x8 bh[2 * KT];
+    cvt_tiles<KT>(X, bh);
+    const _Float16* Wh = reinterpret_cast<const _Float16*>(W);
+#pragma unroll
+    for (int to = 0; to < NT; ++to) {
+        const int ro = (32 * to + i) * ld;
+        f32x16 acc = 0.0f;
+#pragma unroll
+        for (int s = 0; s < 2 * KT; ++s) {
+            const int c0 = ro + 32 * (s >> 1) + 16 * (s & 1) + 4 * h;
+            const f16x8 ahi = cat44(*reinterpret_cast<const f16x4*>(Wh + c0), *reinterpret_cast<const f16x4*>(Wh + c0 + 8));
+            acc = mfma_h(ahi, bh[s], acc);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) Y[to][r] = amp_r(acc[r] + amp_r(b[32 * to + rho(r, h)]));
+    }
+#else
     const int k = tile_scale_exp<KT>(X);
     const float usc = ldexpf(1.0f, -k);
     f16x8 bh[2 * KT], bl[2 * KT];
@@ -260,6 +334,7 @@ __device__ __forceinline__ void fwd_layer(const float* W, int ld, const float* b
 #pragma unroll
         for (int r = 0; r < 16; ++r) Y[to][r] = __builtin_fmaf(acc[r], usc, b[32 * to + rho(r, h)]);
     }
+#endif
 }
 
 #ifndef ACN_BWD_TR16
@@ -283,10 +358,15 @@ template <int NT, int KT, int NROW, int ROWS>
 __device__ __forceinline__ void bwd_layer(const float* W, int ld, const f32x16 (&dY)[KT], f32x16 (&dX)[NT],
                                           int lane) {
     const int i = lane & 31, h = lane >> 5;
+#if ACN_TRAIN_AMP
+    f16x8 bh[2 * KT];
+    cvt_tiles<KT>(dY, bh);
+#else
     const int k = tile_scale_exp<KT>(dY);
     const float usc = ldexpf(1.0f, -k);
     f16x8 bh[2 * KT], bl[2 * KT];
     split_tiles<KT>(dY, k, bh, bl);
+#endif
     const _Float16* Wh = reinterpret_cast<const _Float16*>(W);
     const _Float16* Wlo = Wh + ROWS * ld;
 #if ACN_BWD_TR16
@@ -303,7 +383,9 @@ __device__ __forceinline__ void bwd_layer(const float* W, int ld, const f32x16 (
             {
                 const int o = (32 * (s >> 1) + 16 * (s & 1) + trow) * ld + 32 * ti + tcol;
                 ahi = cat44(ds_read_tr16(Wh + o), ds_read_tr16(Wh + o + 8 * ld));
+#if !ACN_TRAIN_AMP
                 alo = cat44(ds_read_tr16(Wlo + o), ds_read_tr16(Wlo + o + 8 * ld));
+#endif
             }
 #else
 #pragma unroll
@@ -313,12 +395,22 @@ __device__ __forceinline__ void bwd_layer(const float* W, int ld, const f32x16 (
                 alo[e] = Wlo[o];
             }
 #endif
+#if ACN_TRAIN_AMP
+            (void)alo;
+            acc = mfma_h(ahi, bh[s], acc);
+#else
             acc = mfma_h(alo, bh[s], acc);
             acc = mfma_h(ahi, bl[s], acc);
             acc = mfma_h(ahi, bh[s], acc);
+#endif
         }
+#if ACN_TRAIN_AMP
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dX[ti][r] = amp_r(acc[r]);
+#else
 #pragma unroll
         for (int r = 0; r < 16; ++r) dX[ti][r] = acc[r] * usc;
+#endif
     }
 }
 #else
@@ -399,7 +491,7 @@ __device__ __forceinline__ void store_fm(float* dst, int nall, int off, int nfea
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int f = 32 * t + rho(r, h);
-            if (f < nfeat) dst[fm_index(m, nall, off + f)] = X[t][r];
+            if (f < nfeat) dst[fm_index(m, nall, off + f)] = amp_r(X[t][r]);
         }
 }
 
@@ -477,14 +569,14 @@ __global__ void __launch_bounds__(SAVE ? 256 : 512) mlp_fwd_kernel(const float* 
         if (ok) {
             if (h == 0) {
 #pragma unroll
-                for (int c = 0; c < 3; ++c) out[m * 4 + c] = acn::sigmoidf_(Rg[0][c]);
+                for (int c = 0; c < 3; ++c) out[m * 4 + c] = out_rgb(Rg[0][c]);
             } else {
-                out[m * 4 + 3] = acn::trunc_exp(Hd[0][7]);  // row 15 = sigma head (lane half 1, reg 7)
+                out[m * 4 + 3] = out_sigma(Hd[0][7]);  // row 15 = sigma head (lane half 1, reg 7)
             }
             if (SAVE) {
                 // layer inputs (+ ones columns for the bias gradient), feature-major
 #pragma unroll
-                for (int r = 0; r < 16; ++r) save[fm_index(m, SS, O_H0 + rho(r, h))] = h0[m * 32 + rho(r, h)];
+                for (int r = 0; r < 16; ++r) save[fm_index(m, SS, O_H0 + rho(r, h))] = amp_r(h0[m * 32 + rho(r, h)]);
                 store_fm<2>(save, SS, O_A1, 64, m, ok, h, A1);
                 store_fm<2>(save, SS, O_A2, 64, m, ok, h, A2);
                 store_fm<1>(save, SS, O_CIN, 31, m, ok, h, Cin);
@@ -530,10 +622,10 @@ __global__ void __launch_bounds__(256) mlp_bwd_kernel(const float* __restrict__ 
 #pragma unroll
                 for (int c = 0; c < 3; ++c) {
                     const float y = out[m * 4 + c];
-                    dRg[0][c] = (gout[m * 4 + c] * (1.0f - y)) * y;
+                    dRg[0][c] = grad_rgb(gout[m * 4 + c], y);
                 }
             } else {
-                dsig = gout[m * 4 + 3] * out[m * 4 + 3];
+                dsig = grad_sigma(gout[m * 4 + 3], out[m * 4 + 3]);
             }
         }
         store_fm<1>(gsave, DS, G_RGB, 3, m, ok, h, dRg);
@@ -773,7 +865,7 @@ __device__ __forceinline__ void stage_put(float* st, int row0, const f32x16 (&T)
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) st[(row0 + 32 * t + rho(r, h)) * SW + 32 * w + j] = T[t][r];
+        for (int r = 0; r < 16; ++r) st[(row0 + 32 * t + rho(r, h)) * SW + 32 * w + j] = amp_r(T[t][r]);  // AMP: fp16 X
 }
 
 // acc[n] += dY[16 rows from arow] . X[16 features from xrow + 16 n]^T over the 128 staged samples;
@@ -891,10 +983,10 @@ __device__ __forceinline__ void dw_round(const float* W, float* st, const float*
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
                 const float y = out[m * 4 + c];
-                dRg[0][c] = (gout[m * 4 + c] * (1.0f - y)) * y;
+                dRg[0][c] = grad_rgb(gout[m * 4 + c], y);
             }
         } else {
-            dsig = gout[m * 4 + 3] * out[m * 4 + 3];
+            dsig = grad_sigma(gout[m * 4 + 3], out[m * 4 + 3]);
         }
     }
     DW_LAP(dc, 4);
@@ -1082,10 +1174,10 @@ __device__ __forceinline__ void pc_producer_round(const float* W, float* st, con
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
                 const float y = out[m * 4 + c];
-                dRg[0][c] = (gout[m * 4 + c] * (1.0f - y)) * y;
+                dRg[0][c] = grad_rgb(gout[m * 4 + c], y);
             }
         } else {
-            dsig = gout[m * 4 + 3] * out[m * 4 + 3];
+            dsig = grad_sigma(gout[m * 4 + 3], out[m * 4 + 3]);
         }
     }
     // colour head
@@ -1252,7 +1344,7 @@ __global__ void __launch_bounds__(256) mlp_dw_reduce_kernel(const float* __restr
         float t = red[0][c];
 #pragma unroll
         for (int k = 1; k < 8; ++k) t += red[k][c];
-        dw[e] = t;
+        dw[e] = amp_r(t);  // AMP: the fp16 GEMM output rounding of [dW | db]
     }
 }
 
@@ -1284,9 +1376,9 @@ __global__ void __launch_bounds__(256) mlp_fwd_pairs_kernel(const float* __restr
         tile_forward(Wl, h0, sh, m, true, lane, X0, A1, A2, Hd, Cin, C1, C2, Rg);
         if (h == 0) {
 #pragma unroll
-            for (int c = 0; c < 3; ++c) out[m * 4 + c] = acn::sigmoidf_(Rg[0][c]);
+            for (int c = 0; c < 3; ++c) out[m * 4 + c] = out_rgb(Rg[0][c]);
         } else {
-            out[m * 4 + 3] = acn::trunc_exp(Hd[0][7]);
+            out[m * 4 + 3] = out_sigma(Hd[0][7]);
         }
     }
 }
@@ -1324,7 +1416,7 @@ __global__ void __launch_bounds__(256) mlp_dw_reduce_pairs_kernel(const float* _
         float t = red[0][c];
 #pragma unroll
         for (int q = 1; q < 8; ++q) t += red[q][c];
-        dw[(int64_t)k * NDW + e] = t;
+        dw[(int64_t)k * NDW + e] = amp_r(t);
     }
 }
 

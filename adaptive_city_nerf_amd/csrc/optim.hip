@@ -113,6 +113,40 @@ __global__ void clip_coef_kernel(const double* __restrict__ total_sumsq, float m
     out[1] = coef;
 }
 
+// GradScaler (torch/amp/grad_scaler.py: _unscale_grads_ + _amp_update_scale_) folded into the clip
+// coefficient: the gradients stay scaled in memory and Adam multiplies by clip_coef / scale (exact: the scale
+// is a power of two); a non-finite norm skips the step through seg[K] = -1.
+__global__ void amp_unscale_coef_kernel(const double* __restrict__ total_sumsq, float max_norm, float* __restrict__ amp,
+                                        float growth, float backoff, int growth_interval, float* __restrict__ out,
+                                        int64_t* __restrict__ seg, int K) {
+    const float scale = amp[0];
+    const float inv = (float)(1.0 / (double)scale);  // scale.double().reciprocal().float(), as GradScaler
+    const float norm = (float)sqrt(total_sumsq[0]) * inv;
+    const bool found_inf = !(norm == norm) || norm == INFINITY;
+    float coef = 1.0f;
+    if (max_norm > 0.0f) {
+        coef = max_norm / (norm + 1e-6f);
+        coef = coef > 1.0f ? 1.0f : coef;
+    }
+    out[0] = norm;
+    out[1] = coef * inv;
+    amp[2] = found_inf ? 1.0f : 0.0f;
+    if (found_inf) {
+        if (seg) seg[K] = -1;
+        amp[0] = scale * backoff;
+        amp[1] = 0.0f;
+    } else {
+        const float t = amp[1] + 1.0f;
+        if (t >= (float)growth_interval) {
+            const float g = scale * growth;
+            amp[0] = (g == g && g != INFINITY) ? g : scale;  // _amp_update_scale_: only a finite grown scale
+            amp[1] = 0.0f;
+        } else {
+            amp[1] = t;
+        }
+    }
+}
+
 struct GroupK {
     float lr_neg_step, w1, beta2, one_m_beta2, bc2s, eps, wd;
 };
@@ -241,7 +275,9 @@ constexpr int kSlotZero = 1 << 16;
 constexpr int kSlotNormElsewhere = 1 << 17;  // sum of squares supplied by acn_hashgrid_bwd_pairs_sumsq
 
 __device__ __forceinline__ bool slot_active(const int64_t* __restrict__ seg, int K, int slot) {
-    return slot >= K || seg == nullptr || seg[K + 1 + slot] > 0;
+    if (seg == nullptr) return true;
+    if (seg[K] < 0) return false;  // an overflowed bounded exchange step (expert_parallel.py): no slot steps
+    return slot >= K || seg[K + 1 + slot] > 0;
 }
 
 __global__ void bump_slots_kernel(int32_t* __restrict__ step_dev, const int64_t* __restrict__ seg, int K, int nslots) {
@@ -428,7 +464,25 @@ __global__ void __launch_bounds__(kThreads) adam_slots_kernel(const acn_param_de
     const int t = chunk_tensor[blockIdx.x];
     const acn_param_desc d = descs[t];
     const int f = flags[t], slot = f & 0xffff;
-    if (d.grad == nullptr || !slot_active(seg, K, slot)) return;
+    if (d.grad == nullptr) return;
+    if (seg != nullptr && seg[K] < 0) {
+        // a skipped step (AMP found_inf, an overflowed bounded exchange): parameters and moments stay, but the
+        // gradients this pass would have cleared are cleared (and the segment marks reset) so the next step
+        // starts from zero as after an update
+        if (f & kSlotZero) {
+            const int64_t base = (int64_t)(blockIdx.x - d.first_chunk) * ACN_OPTIM_CHUNK;
+            const int64_t n = d.numel - base < ACN_OPTIM_CHUNK ? d.numel - base : ACN_OPTIM_CHUNK;
+            float* g = const_cast<float*>(d.grad) + base;
+            uint8_t* now = segmaps ? segmaps[2 * t] : nullptr;
+            for (int64_t i = threadIdx.x; i < n; i += kThreads)
+                if ((now == nullptr || now[(base + i) >> 4]) && g[i] != 0.0f) g[i] = 0.0f;
+            __syncthreads();
+            if (now)
+                for (int64_t sg = threadIdx.x; sg < (n + 15) >> 4; sg += kThreads) now[(base >> 4) + sg] = 0;
+        }
+        return;
+    }
+    if (!slot_active(seg, K, slot)) return;
     const int row = step_dev[slot] - 1;
     if (row < 0 || row >= table_steps) return;  // outside the uploaded table: the host refills first
     const GroupK k = table[(int64_t)row * ngroups + d.group];
@@ -555,6 +609,16 @@ extern "C" int acn_clip_coef(const double* total_sumsq, float max_norm, float* o
     ACN_REQUIRE(total_sumsq && out, "acn_clip_coef: NULL pointer");
     hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, total_sumsq, max_norm, out);
     return acn_check_launch("acn_clip_coef");
+}
+
+extern "C" int acn_amp_unscale_coef(const double* total_sumsq, float max_norm, float* amp, float growth,
+                                    float backoff, int growth_interval, float* out, int64_t* seg, int K,
+                                    void* stream) {
+    ACN_REQUIRE(total_sumsq && amp && out && growth_interval >= 1 && (seg == nullptr || K >= 0),
+                "acn_amp_unscale_coef: bad arguments");
+    hipLaunchKernelGGL(amp_unscale_coef_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, total_sumsq, max_norm, amp,
+                       growth, backoff, growth_interval, out, seg, K);
+    return acn_check_launch("acn_amp_unscale_coef");
 }
 
 extern "C" int acn_adam_step(const acn_param_desc* descs, const int32_t* chunk_tensor, int64_t nchunks,

@@ -557,23 +557,25 @@ MLP_DW_SHAPES = ((64, 32), (64,), (64, 64), (64,), (1, 64), (1,), (15, 64), (15,
                  (3, 64), (3,))
 MLP_DW_FLOATS = 13715
 # Precision of the training MLP's layer products: "fp16x3" (default: the fp32-accurate 3-term fp16 split on
-# v_mfma_f32_32x32x16_f16) or "fp32" (exact fp32 MFMA, the acn_mlp_*_exact entry points).  Env ACN_TRAIN_MLP.
+# v_mfma_f32_32x32x16_f16), "fp32" (exact fp32 MFMA, the acn_mlp_*_exact entry points) or "amp" (the
+# reference's use_amp=True arithmetic: torch.autocast(float16) -- one fp16 product per term, fp16 layer outputs
+# and gradients; the acn_mlp_*_amp entry points; pair it with a loss scale, see optim.AmpScaler).  Env ACN_TRAIN_MLP.
 TRAIN_MLP_PRECISION = os.environ.get("ACN_TRAIN_MLP", "fp16x3")
+_MLP_SUFFIX = {"fp16x3": "", "fp32": "_exact", "amp": "_amp"}
 
 
 def set_train_mlp_precision(mode: str) -> None:
-    """Select the training MLP kernels ("fp16x3" or "fp32") for later calls; step objects (RoutedAdaptStep,
-    ExpertParallelAdaptStep) keep the precision they were built with."""
+    """Select the training MLP kernels ("fp16x3", "fp32" or "amp") for later calls; step objects
+    (RoutedAdaptStep, ExpertParallelAdaptStep) keep the precision they were built with."""
     global TRAIN_MLP_PRECISION
-    if mode not in ("fp16x3", "fp32"):
-        raise ValueError(f"train MLP precision must be 'fp16x3' or 'fp32', got {mode!r}")
+    if mode not in _MLP_SUFFIX:
+        raise ValueError(f"train MLP precision must be one of {sorted(_MLP_SUFFIX)}, got {mode!r}")
     TRAIN_MLP_PRECISION = mode
 
 
 def mlp_fn(name: str, precision: Optional[str] = None):
     """The training-MLP entry point ``name`` of the selected precision."""
-    exact = (precision or TRAIN_MLP_PRECISION) == "fp32"
-    return getattr(_lib.lib(), name + ("_exact" if exact else ""))
+    return getattr(_lib.lib(), name + _MLP_SUFFIX[precision or TRAIN_MLP_PRECISION])
 # Optional timing hook (bench.py --workload meta): when set to a list, every acn_mlp_train_bwd_dw call appends
 # (start event, end event, M, want_h0) recorded on the current stream around the call (weight pack +
 # mlp_bwd_dw_kernel + mlp_dw_reduce_kernel)

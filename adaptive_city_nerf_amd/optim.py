@@ -281,6 +281,51 @@ class FusedAdam(torch.optim.Optimizer):
         return loss
 
 
+class AmpScaler:
+    """torch.cuda.amp.GradScaler for the fused training steps (use_amp: runtime_adapt.py:237-268,
+    meta_core.py:123-136), its state on the device so a captured step replays it: ``state`` = float32
+    [scale, growth tracker, found_inf, 0].  The step multiplies its loss gradient by ``scale`` (scaler.scale),
+    and SlottedAdam.step(amp=...) folds unscale_ + clip_grad_norm_ + the found_inf skip + update() into
+    acn_amp_unscale_coef.  Defaults are GradScaler's."""
+
+    def __init__(self, device, init_scale: float = 2.0 ** 16, growth_factor: float = 2.0,
+                 backoff_factor: float = 0.5, growth_interval: int = 2000):
+        self.growth_factor, self.backoff_factor = float(growth_factor), float(backoff_factor)
+        self.growth_interval = int(growth_interval)
+        self.state = torch.tensor([float(init_scale), 0.0, 0.0, 0.0], device=device, dtype=torch.float32)
+
+    @property
+    def scale(self) -> torch.Tensor:
+        """The current loss scale (device, 0-dim view)."""
+        return self.state[0]
+
+    def get_scale(self) -> float:
+        return float(self.state[0])
+
+    def found_inf(self) -> bool:
+        """Whether the last step was skipped for a non-finite gradient (host read)."""
+        return bool(self.state[2] != 0)
+
+    def state_dict(self) -> dict:
+        """GradScaler.state_dict()'s keys."""
+        st = self.state.cpu().tolist()
+        return {"scale": st[0], "growth_factor": self.growth_factor, "backoff_factor": self.backoff_factor,
+                "growth_interval": self.growth_interval, "_growth_tracker": int(st[1])}
+
+    def load_state_dict(self, d: dict) -> None:
+        self.growth_factor, self.backoff_factor = float(d["growth_factor"]), float(d["backoff_factor"])
+        self.growth_interval = int(d["growth_interval"])
+        self.state.copy_(torch.tensor([float(d["scale"]), float(d["_growth_tracker"]), 0.0, 0.0]))
+
+    def unscale_coef(self, total_sumsq: torch.Tensor, max_norm: Optional[float], out: torch.Tensor,
+                     seg: Optional[torch.Tensor], K: int) -> None:
+        from ._lib import ptr
+        check(_lib.lib().acn_amp_unscale_coef(ptr(total_sumsq), float(max_norm or 0.0), ptr(self.state),
+                                              self.growth_factor, self.backoff_factor, self.growth_interval,
+                                              ptr(out), ptr(seg) if seg is not None else None, int(K),
+                                              _stream(out.device)), "acn_amp_unscale_coef")
+
+
 ZERO_GRAD_FLAG = 1 << 16       # adam_step_slots: clear the gradient after reading it
 NORM_ELSEWHERE_FLAG = 1 << 17  # grad_sumsq_slots_ex: this tensor's sum of squares comes from elsewhere
 
@@ -423,16 +468,18 @@ class SlottedAdam:
         self._hparams = hp
 
     def step(self, seg: torch.Tensor, max_norm: Optional[float], table_sumsq: Optional[torch.Tensor] = None,
-             hook=None, allreduce=None) -> None:
+             hook=None, allreduce=None, amp: Optional[AmpScaler] = None) -> None:
         """Clip norm over the active slots' gradients (+ ``table_sumsq``, a device double some kernel
         accumulated for NORM_ELSEWHERE tensors; reset by the norm pass), clip coefficient, then Adam over
         the active slots; per-slot step counters advance on the device.  ``allreduce`` (split_norm):
-        in-place sum of a device double over the expert-parallel group, applied to the per-rank part."""
+        in-place sum of a device double over the expert-parallel group, applied to the per-rank part.
+        ``amp``: the gradients carry the AmpScaler's loss scale -- unscaled inside the Adam multiplier, the
+        step skipped (seg[K] = -1) on a non-finite norm, the scale updated (GradScaler semantics)."""
         L = _lib.lib()
         s = _stream(self.device)
         from ._lib import ptr
         scale = None
-        if max_norm is not None:
+        if max_norm is not None or amp is not None:
             if allreduce is not None:
                 if not self.split:
                     raise AcnError("SlottedAdam.step(allreduce=...) needs split_norm=True")
@@ -452,7 +499,10 @@ class SlottedAdam:
                 check(L.acn_grad_sumsq_slots_ex(ptr(self.descs), ptr(self.chunk_tensor), self.nchunks,
                                                 ptr(self.flags), ptr(seg), self.K, ptr(self.partials), ptr(self.total),
                                                 ptr(table_sumsq), s), "acn_grad_sumsq_slots_ex")
-            check(L.acn_clip_coef(ptr(self.total), float(max_norm), ptr(self.scale), s), "acn_clip_coef")
+            if amp is not None:
+                amp.unscale_coef(self.total, max_norm, self.scale, seg, self.K)
+            else:
+                check(L.acn_clip_coef(ptr(self.total), float(max_norm), ptr(self.scale), s), "acn_clip_coef")
             scale = self.scale
         if hook is not None:
             e0 = torch.cuda.Event(enable_timing=True)

@@ -38,7 +38,7 @@ import torch
 
 from . import _lib, ops
 from ._lib import AcnError, acn_mlp, check, graph_capture, ptr
-from .optim import NORM_ELSEWHERE_FLAG, ZERO_GRAD_FLAG, FusedAdam, SlottedAdam, bump_versions
+from .optim import NORM_ELSEWHERE_FLAG, ZERO_GRAD_FLAG, AmpScaler, FusedAdam, SlottedAdam, bump_versions
 from .train import mse_color_loss
 
 # Optional timing hook (bench.py): when set to a list, an eager step appends recorded HIP events
@@ -100,6 +100,9 @@ class RoutedAdaptStep:
             raise AcnError("RoutedAdaptStep: experts must share one Linear/Smoothstep hash-grid configuration")
         self.P, self.model, self.opt = P, model, optimizer
         self.mlp_precision = ops.TRAIN_MLP_PRECISION   # training MLP kernels (ops.set_train_mlp_precision)
+        # use_amp (ops.set_train_mlp_precision("amp")): the autocast(fp16) MLP arithmetic plus GradScaler --
+        # the loss gradient enters the backward multiplied by the device loss scale, Adam unscales / skips
+        self.amp = AmpScaler(model.submodules[0].xyz_encoder.hash_table.device) if self.mlp_precision == "amp" else None
         self.grad_clip = grad_clip
         self.jitter_mode = jitter
         # clear_in_adam=False keeps the gradients readable after the step (tests): the table gradients
@@ -255,7 +258,7 @@ class RoutedAdaptStep:
             bg = ops.background_fwd(dirs, self.bg_spec)
             rgb = ops.volume_render(rs_, t, bg)[0]
             loss = ops.mse_linear_fwd(rgb, rgbs)
-            g_rgb = ops.mse_linear_bwd(rgb, rgbs, self._one)
+            g_rgb = ops.mse_linear_bwd(rgb, rgbs, self._one if self.amp is None else self.amp.scale)
             g_rs, g_bg = ops.volume_render_bwd(rs_, t, bg, 1.0, g_rgb, None, None, None)
             ops.background_bwd(dirs, self.bg_spec, g_bg, self.gbg)
         elif self.bg_spec is not None:
@@ -264,14 +267,14 @@ class RoutedAdaptStep:
             with torch.enable_grad():
                 rgb = volume_render(rs, t, bg_rgb=bg)[0]
                 loss = mse_color_loss(rgb, rgbs, self.P.color_space)
-                g_rs, g_bg = torch.autograd.grad(loss, [rs, bg])
+                g_rs, g_bg = torch.autograd.grad(loss if self.amp is None else loss * self.amp.scale, [rs, bg])
             ops.background_bwd(dirs, self.bg_spec, g_bg, self.gbg)
         else:
             with torch.enable_grad():
                 bg = self.model.background_color(rays[:, 3:6])
                 rgb = volume_render(rs, t, bg_rgb=bg)[0]
                 loss = mse_color_loss(rgb, rgbs, self.P.color_space)
-                grads = torch.autograd.grad(loss, [rs] + self.bg_params)
+                grads = torch.autograd.grad(loss if self.amp is None else loss * self.amp.scale, [rs] + self.bg_params)
             g_rs = grads[0]
             for g, buf in zip(grads[1:], self.gbg):
                 buf.copy_(g)
@@ -302,7 +305,7 @@ class RoutedAdaptStep:
             b1.record()
             bhook.append((b0, b1))
         self.adam.step(self.seg, self.grad_clip, self.table_sumsq if self.tele else None,
-                       hook=EVENT_HOOK if self.graph is None and not capturing else None)
+                       hook=EVENT_HOOK if self.graph is None and not capturing else None, amp=self.amp)
 
     def _table_bwd_deterministic(self, enc) -> None:
         """Under torch.use_deterministic_algorithms(True): every expert's table gradient by the sort-based

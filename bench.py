@@ -454,6 +454,9 @@ def main():
                          "expert sort")
     ap.add_argument("--diag-expert-only-order", action="store_true",
                     help="diagnostic (c3): sort the batch by owning expert only (no direction-cell secondary key)")
+    ap.add_argument("--mlp-precision", choices=["fp16x3", "fp32", "amp"], default="fp16x3",
+                    help="c5 / meta: training-MLP arithmetic -- fp16x3 (default, fp32-accurate), fp32 (exact), or "
+                         "amp (the reference's use_amp=True: autocast(float16) products + GradScaler)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check: every rank reports (rank, world) over gloo and exits before any GPU call")
     a = ap.parse_args()
@@ -488,6 +491,9 @@ def main():
     torch.cuda.set_device(device)
 
     from adaptive_city_nerf_amd import ops, parallel, render_rays
+    if a.mlp_precision == "amp" and a.workload != "c5":
+        raise SystemExit("bench.py: --mlp-precision amp is measured on c5 (RoutedAdaptStep with its GradScaler)")
+    ops.set_train_mlp_precision(a.mlp_precision)
     S = a.samples
     K = {"c2": 1, "c3": 4, "c4": 8, "c5": 8, "c5a": 8, "occ": 1, "meta": 4, "data": 1, "clusters": 1}[a.workload]
     occ_conf = None
@@ -1197,6 +1203,13 @@ def main():
                                             "slot at the step's capacities; live = the same for the routed pairs"}
         if a.workload == "c4":
             line["psnr_vs_synthetic_gt_db"] = round(float(out[3]), 4)
+        if a.workload in ("c5", "meta"):
+            line["mlp_precision"] = a.mlp_precision
+            if a.mlp_precision == "amp":
+                line["dtype"] = "f16 MLP products / f32 accumulate (use_amp), f32 elsewhere"
+                amp = getattr(routed, "amp", None) if a.workload == "c5" else None
+                if amp is not None:
+                    line["amp_scaler"] = amp.state_dict()
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()

@@ -650,6 +650,42 @@ int acn_mlp_train_fwd_pairs_exact(const float* h0, const float* sh, const int64_
 int acn_mlp_train_bwd_dw_pairs_exact(const float* h0, const float* sh, const float* out, const float* gout,
                                const int64_t* seg, int K, void* workspace, float* dw, float* gh0, void* stream);
 
+/* The training MLP in the reference's use_amp arithmetic (the MetaLinear chain under torch.autocast(float16):
+ * pipelines/online_stage/runtime_adapt.py:249-259, pipelines/offline_stage/meta_core.py:38, configs/train.json:37):
+ * one fp16 x fp16 MFMA product per term with fp32 accumulation, every layer output, activation, dX and
+ * [dW | db] rounded to fp16 once, the incoming gradient cast to fp16; no internal rescaling (the caller's
+ * loss scale -- acn_amp_unscale_coef -- keeps the gradients in fp16's range, as GradScaler does).  The same ten
+ * entry points, suffixed _amp; workspaces from the _amp size functions.  mlp_train.hip compiled a third
+ * time with -DACN_TRAIN_AMP=1. */
+size_t acn_mlp_workspace_bytes_amp(void);
+int acn_mlp_train_fwd_amp(const float* h0, const float* sh, int64_t M, const acn_mlp* w, float* out, float* save,
+                          void* workspace, void* stream);
+int acn_mlp_train_bwd_amp(const float* save, const float* out, const float* gout, int64_t M, const acn_mlp* w,
+                          float* gsave, float* gh0, void* workspace, void* stream);
+size_t acn_mlp_dw_workspace_bytes_amp(void);
+int acn_mlp_train_bwd_dw_amp(const float* h0, const float* sh, const float* out, const float* gout, int64_t M,
+                             const acn_mlp* w, float* dw, float* gh0, void* workspace, void* stream);
+int acn_mlp_train_bwd_dw_img_amp(const float* h0, const float* sh, const float* out, const float* gout, int64_t M,
+                                 const float* img, float* dw, float* gh0, void* workspace, void* stream);
+size_t acn_mlp_pairs_workspace_bytes_amp(int K);
+int acn_mlp_pack_pairs_amp(const acn_mlp* const* w, int K, void* workspace, void* stream);
+int acn_mlp_train_fwd_pairs_amp(const float* h0, const float* sh, const int64_t* seg, int K, const void* workspace,
+                                float* out, void* stream);
+int acn_mlp_train_bwd_dw_pairs_amp(const float* h0, const float* sh, const float* out, const float* gout,
+                                   const int64_t* seg, int K, void* workspace, float* dw, float* gh0, void* stream);
+
+/* torch.cuda.amp.GradScaler's unscale_ + clip_grad_norm_ + step-skip + update in one device launch
+ * (replaces scaler.unscale_(optimizer); clip_grad_norm_(params, max_norm); scaler.step(optimizer);
+ * scaler.update() of runtime_adapt.py:261-268 for the fused Adam paths).  total_sumsq = sum of squares of the
+ * SCALED gradients (acn_grad_sumsq*), amp = {scale, growth tracker, found_inf, 0} (float32, device).  Writes
+ * out[0] = the unscaled total norm, out[1] = the Adam gradient multiplier clip_coef / scale (clip_coef = 1
+ * when max_norm <= 0); when the norm is not finite (an inf / NaN gradient: GradScaler's found_inf) the step
+ * is skipped -- seg[K] = -1 (the slotted Adam's no-step gate; seg may be NULL for callers that test amp[2]) --
+ * and the scale backs off (x backoff, tracker 0); otherwise tracker += 1 and, at growth_interval, the scale
+ * grows (x growth, tracker 0).  Powers of two keep the unscaling exact. */
+int acn_amp_unscale_coef(const double* total_sumsq, float max_norm, float* amp, float growth, float backoff,
+                         int growth_interval, float* out, int64_t* seg, int K, void* stream);
+
 /* Segment maps of the hash-table gradients (routed step): per expert table two byte maps over
  * its 64-B segments (8 rows of 2 features): now[s] = the scatter added into segment s this step, ever[s] = it
  * was updated by an earlier step.
