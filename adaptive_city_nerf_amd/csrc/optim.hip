@@ -116,10 +116,11 @@ __global__ void clip_coef_kernel(const double* __restrict__ total_sumsq, float m
 // GradScaler (torch/amp/grad_scaler.py: _unscale_grads_ + _amp_update_scale_) folded into the clip
 // coefficient: the gradients stay scaled in memory and Adam multiplies by clip_coef / scale (exact: the scale
 // is a power of two); a non-finite norm skips the step through seg[K] = -1.
-__global__ void amp_unscale_coef_kernel(const double* __restrict__ total_sumsq, float max_norm, float* __restrict__ amp,
-                                        float growth, float backoff, int growth_interval, float* __restrict__ out,
+__global__ void amp_unscale_coef_kernel(const double* __restrict__ total_sumsq, float max_norm, float* __restrict__ scale_p,
+                                        int32_t* __restrict__ tracker, float* __restrict__ found_inf_p, float growth,
+                                        float backoff, int growth_interval, float* __restrict__ out,
                                         int64_t* __restrict__ seg, int K) {
-    const float scale = amp[0];
+    const float scale = scale_p[0];
     const float inv = (float)(1.0 / (double)scale);  // scale.double().reciprocal().float(), as GradScaler
     const float norm = (float)sqrt(total_sumsq[0]) * inv;
     const bool found_inf = !(norm == norm) || norm == INFINITY;
@@ -130,19 +131,19 @@ __global__ void amp_unscale_coef_kernel(const double* __restrict__ total_sumsq, 
     }
     out[0] = norm;
     out[1] = coef * inv;
-    amp[2] = found_inf ? 1.0f : 0.0f;
-    if (found_inf) {
+    found_inf_p[0] = found_inf ? 1.0f : 0.0f;
+    if (found_inf) {  // torch._amp_update_scale_
         if (seg) seg[K] = -1;
-        amp[0] = scale * backoff;
-        amp[1] = 0.0f;
+        scale_p[0] = scale * backoff;
+        tracker[0] = 0;
     } else {
-        const float t = amp[1] + 1.0f;
-        if (t >= (float)growth_interval) {
+        const int t = tracker[0] + 1;
+        if (t == growth_interval) {
             const float g = scale * growth;
-            amp[0] = (g == g && g != INFINITY) ? g : scale;  // _amp_update_scale_: only a finite grown scale
-            amp[1] = 0.0f;
+            scale_p[0] = (g == g && g != INFINITY) ? g : scale;  // only a finite grown scale is kept
+            tracker[0] = 0;
         } else {
-            amp[1] = t;
+            tracker[0] = t;
         }
     }
 }
@@ -611,13 +612,14 @@ extern "C" int acn_clip_coef(const double* total_sumsq, float max_norm, float* o
     return acn_check_launch("acn_clip_coef");
 }
 
-extern "C" int acn_amp_unscale_coef(const double* total_sumsq, float max_norm, float* amp, float growth,
-                                    float backoff, int growth_interval, float* out, int64_t* seg, int K,
-                                    void* stream) {
-    ACN_REQUIRE(total_sumsq && amp && out && growth_interval >= 1 && (seg == nullptr || K >= 0),
+extern "C" int acn_amp_unscale_coef(const double* total_sumsq, float max_norm, float* scale, int32_t* growth_tracker,
+                                    float* found_inf, float growth, float backoff, int growth_interval, float* out,
+                                    int64_t* seg, int K, void* stream) {
+    ACN_REQUIRE(total_sumsq && scale && growth_tracker && found_inf && out && growth_interval >= 1 &&
+                    (seg == nullptr || K >= 0),
                 "acn_amp_unscale_coef: bad arguments");
-    hipLaunchKernelGGL(amp_unscale_coef_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, total_sumsq, max_norm, amp,
-                       growth, backoff, growth_interval, out, seg, K);
+    hipLaunchKernelGGL(amp_unscale_coef_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, total_sumsq, max_norm, scale,
+                       growth_tracker, found_inf, growth, backoff, growth_interval, out, seg, K);
     return acn_check_launch("acn_amp_unscale_coef");
 }
 

@@ -302,7 +302,8 @@ class ExpertParallelRenderer:
         self.weights = torch.empty(N, S, **f32) if want_weights else None
         self.routing = model.routing_spec()
         self.hard = 0 if self.routing.boundary_margin > 1.0 else 1
-        self.bg = _fused_background(model, bg_color_default, N, dev)
+        with torch.no_grad():   # an inference renderer: the head's spec, whatever the caller's grad mode
+            self.bg = _fused_background(model, bg_color_default, N, dev)
         if self.bg is None:
             raise AcnError(f"ExpertParallelRenderer: background policy {bg_color_default!r} needs the composed path")
         self.bg_spec, self._bg_keep = self.bg if isinstance(self.bg, tuple) else (self.bg, None)

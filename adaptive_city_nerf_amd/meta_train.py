@@ -40,6 +40,7 @@ from typing import Dict, List, Mapping, Optional
 import torch
 import torch.distributed as dist
 
+from . import ops
 from ._lib import graph_capture
 from .expert_parallel import expert_owner, global_clip_grad_norm_
 from .encodings import accumulate_table_grad
@@ -263,8 +264,9 @@ FAST_META_STEP = os.environ.get("ACN_FAST_META", "1") != "0"
 def _graph_eligible(P, model, optimizer, scheduler, grad_scaler, group) -> bool:
     if not FAST_META_STEP or str(getattr(P, "algo", "")).lower() != "fomaml" or not isinstance(optimizer, FusedAdam):
         return False
-    if grad_scaler is not None and getattr(grad_scaler, "is_enabled", lambda: False)():
-        return False
+    if grad_scaler is not None and getattr(grad_scaler, "is_enabled", lambda: False)() and \
+            ops.TRAIN_MLP_PRECISION != "amp":
+        return False   # a GradScaler is replayed on the device with the use_amp kernels (GraphedMetaStep.amp)
     if group is not None and dist.is_initialized() and dist.get_world_size(group) > 1:
         return False
     return hasattr(model, "submodules") and not getattr(model, "use_occ", False)
@@ -287,7 +289,8 @@ def train_step(P, step, model, optimizer, task_data, metric_logger=None, logger=
                                                                       group) else False
     if g == "pending":   # second eligible call: capture now (the first call's gradients stayed readable)
         try:
-            g = optimizer._acn_meta_graph = GraphedMetaStep(P, model, optimizer, task_data, warmup=0)
+            g = optimizer._acn_meta_graph = GraphedMetaStep(P, model, optimizer, task_data, warmup=0,
+                                                            grad_scaler=grad_scaler)
         except (ValueError, TypeError):
             g = optimizer._acn_meta_graph = False   # shapes the graphs cannot cover: stay eager
     if isinstance(g, GraphedMetaStep):
@@ -447,16 +450,23 @@ class GraphedMetaStep:
     stays on the eager train_step: the create_graph backward does an operation HIP stream capture does not
     permit on this stack."""
 
-    def __init__(self, P, model, optimizer, task_data, warmup: int = 1, max_steps: int = 1 << 16):
+    def __init__(self, P, model, optimizer, task_data, warmup: int = 1, max_steps: int = 1 << 16,
+                 grad_scaler=None):
         algo = str(getattr(P, "algo", "")).lower()
         if algo != "fomaml":
             raise ValueError("GraphedMetaStep: FOMAML only (MAML's second-order backward is not capturable; "
                              "Reptile has no gradient step) -- use train_step")
         if not isinstance(optimizer, FusedAdam):
             raise TypeError("GraphedMetaStep needs FusedAdam (its slotted device step makes the update replayable)")
-        from .optim import SlottedAdam
+        from .optim import AmpScaler, SlottedAdam
         self.P, self.model, self.opt = P, model, optimizer
         self.device = next(model.parameters()).device
+        # use_amp (meta_core.py:123-136 with trainer.py:24's GradScaler): the query loss is scaled by the
+        # scaler's device scale inside the task graphs and the outer graph unscales / skips / updates it, on
+        # the GradScaler's own state tensors (its get_scale() and state_dict() follow the replays)
+        self.amp = AmpScaler.wrap(grad_scaler, self.device) if grad_scaler is not None and \
+            getattr(grad_scaler, "is_enabled", lambda: False)() else None
+        self.grad_scaler = grad_scaler if self.amp is not None else None
         self.shapes = {}
         for cid, tasks in task_data.items():
             for t in tasks:
@@ -470,7 +480,7 @@ class GraphedMetaStep:
             raise ValueError("GraphedMetaStep: no non-empty task to capture")
         for _ in range(max(0, int(warmup))):   # real updates
             with _quiet():
-                _train_step_eager(P, 0, model, optimizer, task_data)
+                _train_step_eager(P, 0, model, optimizer, task_data, grad_scaler=self.grad_scaler)
         torch.cuda.synchronize(self.device)
         dev = self.device
         self.static = {}
@@ -499,7 +509,7 @@ class GraphedMetaStep:
             self._add_region(cid, next(t for t in task_data[cid] if _task_shapes(t) == self.shapes[cid]))
         self.outer = torch.cuda.CUDAGraph()
         with graph_capture(self.outer, pool=self.pool):
-            self.adam.step(self.act, getattr(P, "grad_clip", 1.0))
+            self.adam.step(self.act, getattr(P, "grad_clip", 1.0), amp=self.amp)
         self.replays = 0
         self.eager_steps = 0
         torch._foreach_zero_(self.grads)
@@ -540,7 +550,7 @@ class GraphedMetaStep:
         # add instead of an AccumulateGrad launch each (same sums as .backward())
         targets = self.params   # every optimised tensor (those the task does not reach come back None)
         with accumulate_table_grad():
-            lq = loss_q * st["wq"]
+            lq = loss_q * st["wq"] if self.amp is None else loss_q * st["wq"] * self.amp.scale   # scaler.scale
             gs = torch.autograd.grad(lq, targets, grad_outputs=_ones_like_scalar(lq), allow_unused=True)
         live = [(p.grad, g) for p, g in zip(targets, gs) if g is not None]
         if live:
@@ -575,7 +585,7 @@ class GraphedMetaStep:
         for p in self.params:
             p.grad = None
         with _quiet():
-            out = _train_step_eager(self.P, step, self.model, self.opt, task_data)
+            out = _train_step_eager(self.P, step, self.model, self.opt, task_data, grad_scaler=self.grad_scaler)
         self.adam.load_state()
         for p, g in zip(self.params, self.grads):
             p.grad = g

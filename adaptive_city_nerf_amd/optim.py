@@ -283,46 +283,65 @@ class FusedAdam(torch.optim.Optimizer):
 
 class AmpScaler:
     """torch.cuda.amp.GradScaler for the fused training steps (use_amp: runtime_adapt.py:237-268,
-    meta_core.py:123-136), its state on the device so a captured step replays it: ``state`` = float32
-    [scale, growth tracker, found_inf, 0].  The step multiplies its loss gradient by ``scale`` (scaler.scale),
-    and SlottedAdam.step(amp=...) folds unscale_ + clip_grad_norm_ + the found_inf skip + update() into
-    acn_amp_unscale_coef.  Defaults are GradScaler's."""
+    meta_core.py:123-136, trainer.py:24), its state on the device so a captured step replays it: ``scale``
+    (float32[1]), ``tracker`` (int32[1]) and ``found`` (float32[1]).  The step multiplies its loss gradient by
+    the scale (scaler.scale), and SlottedAdam.step(amp=...) folds unscale_ + clip_grad_norm_ + the found_inf
+    skip + update() into acn_amp_unscale_coef.  ``AmpScaler.wrap(grad_scaler)`` works on a torch GradScaler's
+    own _scale / _growth_tracker tensors, so its get_scale() / state_dict() follow the replayed steps.
+    Defaults are GradScaler's."""
 
     def __init__(self, device, init_scale: float = 2.0 ** 16, growth_factor: float = 2.0,
                  backoff_factor: float = 0.5, growth_interval: int = 2000):
         self.growth_factor, self.backoff_factor = float(growth_factor), float(backoff_factor)
         self.growth_interval = int(growth_interval)
-        self.state = torch.tensor([float(init_scale), 0.0, 0.0, 0.0], device=device, dtype=torch.float32)
+        self.scale_t = torch.full((1,), float(init_scale), device=device, dtype=torch.float32)
+        self.tracker = torch.zeros(1, device=device, dtype=torch.int32)
+        self.found = torch.zeros(1, device=device, dtype=torch.float32)
+        self.torch_scaler = None
+
+    @classmethod
+    def wrap(cls, grad_scaler, device) -> "AmpScaler":
+        """An AmpScaler on a torch.cuda.amp.GradScaler's device state (created lazily, as its scale() does)."""
+        a = cls(device, grad_scaler.get_scale() if grad_scaler._scale is not None else grad_scaler._init_scale,
+                grad_scaler.get_growth_factor(), grad_scaler.get_backoff_factor(), grad_scaler.get_growth_interval())
+        if grad_scaler._scale is None:
+            grad_scaler._lazy_init_scale_growth_tracker(device)
+        if grad_scaler._scale.dtype != torch.float32 or grad_scaler._growth_tracker.dtype != torch.int32:
+            raise AcnError("AmpScaler.wrap: unexpected GradScaler state dtypes")
+        a.scale_t, a.tracker = grad_scaler._scale, grad_scaler._growth_tracker
+        a.torch_scaler = grad_scaler
+        return a
 
     @property
     def scale(self) -> torch.Tensor:
         """The current loss scale (device, 0-dim view)."""
-        return self.state[0]
+        return self.scale_t.view(())
 
     def get_scale(self) -> float:
-        return float(self.state[0])
+        return float(self.scale_t)
 
     def found_inf(self) -> bool:
         """Whether the last step was skipped for a non-finite gradient (host read)."""
-        return bool(self.state[2] != 0)
+        return bool(self.found[0] != 0)
 
     def state_dict(self) -> dict:
         """GradScaler.state_dict()'s keys."""
-        st = self.state.cpu().tolist()
-        return {"scale": st[0], "growth_factor": self.growth_factor, "backoff_factor": self.backoff_factor,
-                "growth_interval": self.growth_interval, "_growth_tracker": int(st[1])}
+        return {"scale": self.get_scale(), "growth_factor": self.growth_factor, "backoff_factor": self.backoff_factor,
+                "growth_interval": self.growth_interval, "_growth_tracker": int(self.tracker[0])}
 
     def load_state_dict(self, d: dict) -> None:
         self.growth_factor, self.backoff_factor = float(d["growth_factor"]), float(d["backoff_factor"])
         self.growth_interval = int(d["growth_interval"])
-        self.state.copy_(torch.tensor([float(d["scale"]), float(d["_growth_tracker"]), 0.0, 0.0]))
+        self.scale_t.fill_(float(d["scale"]))
+        self.tracker.fill_(int(d["_growth_tracker"]))
 
     def unscale_coef(self, total_sumsq: torch.Tensor, max_norm: Optional[float], out: torch.Tensor,
                      seg: Optional[torch.Tensor], K: int) -> None:
         from ._lib import ptr
-        check(_lib.lib().acn_amp_unscale_coef(ptr(total_sumsq), float(max_norm or 0.0), ptr(self.state),
-                                              self.growth_factor, self.backoff_factor, self.growth_interval,
-                                              ptr(out), ptr(seg) if seg is not None else None, int(K),
+        check(_lib.lib().acn_amp_unscale_coef(ptr(total_sumsq), float(max_norm or 0.0), ptr(self.scale_t),
+                                              ptr(self.tracker), ptr(self.found), self.growth_factor,
+                                              self.backoff_factor, self.growth_interval, ptr(out),
+                                              ptr(seg) if seg is not None else None, int(K),
                                               _stream(out.device)), "acn_amp_unscale_coef")
 
 

@@ -491,8 +491,8 @@ def main():
     torch.cuda.set_device(device)
 
     from adaptive_city_nerf_amd import ops, parallel, render_rays
-    if a.mlp_precision == "amp" and a.workload != "c5":
-        raise SystemExit("bench.py: --mlp-precision amp is measured on c5 (RoutedAdaptStep with its GradScaler)")
+    if a.mlp_precision != "fp16x3" and a.workload not in ("c5", "meta"):
+        raise SystemExit("bench.py: --mlp-precision applies to the training workloads (c5, meta)")
     ops.set_train_mlp_precision(a.mlp_precision)
     S = a.samples
     K = {"c2": 1, "c3": 4, "c4": 8, "c5": 8, "c5a": 8, "occ": 1, "meta": 4, "data": 1, "clusters": 1}[a.workload]
@@ -563,8 +563,11 @@ def main():
         S = 96 if a.samples == 256 else a.samples
         P = SimpleNamespace(algo="fomaml", ray_samples=S, chunk_points=4000000, color_space="linear",
                             optimizer="adam", lr=1e-4, encoding_lr=0.01, sigma_lr=0.002, color_lr=0.002, bg_lr=0.001,
-                            weight_decay=0.0, inner_lr=0.015, inner_iter=a.inner_iter, fim=False, use_amp=False,
-                            grad_clip=1.0, seed=0, mixed_precision=False, print_step=10 ** 9)
+                            weight_decay=0.0, inner_lr=0.015, inner_iter=a.inner_iter, fim=False,
+                            use_amp=a.mlp_precision == "amp", grad_clip=1.0, seed=0, mixed_precision=False,
+                            print_step=10 ** 9)
+        # use_amp: trainer.py:24's GradScaler, replayed on the device by the graphed meta step
+        meta_scaler = torch.amp.GradScaler("cuda") if P.use_amp else None
         nsup, nqry, ntask = a.support_rays, a.query_rays, 3
         pool = make_rays(scene, gbox, device, 60000, 4321)
         gen = torch.Generator(device).manual_seed(9)
@@ -592,7 +595,7 @@ def main():
             it[0] += 1
             import contextlib, io
             with contextlib.redirect_stdout(io.StringIO()):  # meta_update's per-region debug prints (eager)
-                return MT.train_step(P, it[0], model, opt, task_data, group=pg)
+                return MT.train_step(P, it[0], model, opt, task_data, group=pg, grad_scaler=meta_scaler)
         sample_rays = pool[:1]
         aoptim.EVENT_HOOK = []
     elif a.workload == "data":
@@ -854,7 +857,7 @@ def main():
         with contextlib.redirect_stdout(io.StringIO()):
             for _ in range(3):
                 it[0] += 1
-                MT.train_step(P, it[0], model, opt, task_data, group=pg)
+                MT.train_step(P, it[0], model, opt, task_data, group=pg, grad_scaler=meta_scaler)
         torch.cuda.synchronize()
         dw_hook, ops.DW_HOOK = ops.DW_HOOK, None
         dw_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1, _, _ in dw_hook]))
@@ -952,10 +955,13 @@ def main():
              "c2": "ray_order_kernel + render_kernel<1,1,0> (one acn_render_stratified_fwd_ordered call: direction "
                    "grouping of the batch, then the fused stratified render, 1 expert; kernel_ms = two HIP events "
                    "bracketing the K timed calls on the launch stream / K)",
-             "c3": "render_slots_kernel (fused stratified render, soft routing over 4 experts, two staged per round)",
-             "c4": ("field_kernel (fused MFMA field of the owned expert over the received per-sample records)"
+             "c3": "render_routed_kernel (fused stratified render, soft routing over 4 experts: expert-major "
+                   "chunks of 1024 ray-samples, one expert image in LDS per chunk pass; + ray_order_kernel)",
+             "c4": ("ep_field_kernel (the owned expert's fused MFMA field over the received per-sample records; "
+                    "+ ep_composite_kernel, one-expert-per-GPU layout)"
                     if a.layout == "expert" else
-                    "render_slots_kernel (fused stratified render, soft routing over 8 experts, two staged per round)"),
+                    "render_routed_kernel (fused stratified render, soft routing over 8 experts: expert-major "
+                    "chunks of 1024 ray-samples, one expert image in LDS per chunk pass; + ray_order_kernel)"),
              "occ": "occ_render_kernel<1,1,0> (fused occupancy render over packed marched samples, 1 expert)",
              "meta": "adam_kernel (fused clip + Adam of the outer meta-update over the region experts + shared head)",
              "data": "route_kernel (TaskDataset region clip + DDA max-overlap micro-cell routing + keep tolerance)",
@@ -1210,6 +1216,8 @@ def main():
                 amp = getattr(routed, "amp", None) if a.workload == "c5" else None
                 if amp is not None:
                     line["amp_scaler"] = amp.state_dict()
+                if a.workload == "meta" and meta_scaler is not None:
+                    line["amp_scaler"] = meta_scaler.state_dict()
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()

@@ -677,14 +677,16 @@ int acn_mlp_train_bwd_dw_pairs_amp(const float* h0, const float* sh, const float
 /* torch.cuda.amp.GradScaler's unscale_ + clip_grad_norm_ + step-skip + update in one device launch
  * (replaces scaler.unscale_(optimizer); clip_grad_norm_(params, max_norm); scaler.step(optimizer);
  * scaler.update() of runtime_adapt.py:261-268 for the fused Adam paths).  total_sumsq = sum of squares of the
- * SCALED gradients (acn_grad_sumsq*), amp = {scale, growth tracker, found_inf, 0} (float32, device).  Writes
- * out[0] = the unscaled total norm, out[1] = the Adam gradient multiplier clip_coef / scale (clip_coef = 1
- * when max_norm <= 0); when the norm is not finite (an inf / NaN gradient: GradScaler's found_inf) the step
- * is skipped -- seg[K] = -1 (the slotted Adam's no-step gate; seg may be NULL for callers that test amp[2]) --
- * and the scale backs off (x backoff, tracker 0); otherwise tracker += 1 and, at growth_interval, the scale
- * grows (x growth, tracker 0).  Powers of two keep the unscaling exact. */
-int acn_amp_unscale_coef(const double* total_sumsq, float max_norm, float* amp, float growth, float backoff,
-                         int growth_interval, float* out, int64_t* seg, int K, void* stream);
+ * SCALED gradients (acn_grad_sumsq*); scale (float32[1]), growth_tracker (int32[1]) and found_inf (float32[1])
+ * are device scalars -- GradScaler's own _scale / _growth_tracker tensors can be passed.  Writes out[0] = the
+ * unscaled total norm, out[1] = the Adam gradient multiplier clip_coef / scale (clip_coef = 1 when max_norm
+ * <= 0); when the norm is not finite (an inf / NaN gradient: GradScaler's found_inf) the step is skipped --
+ * seg[K] = -1 (the slotted Adam's no-step gate; seg may be NULL for callers that test found_inf) -- and the
+ * scale backs off (x backoff, tracker 0); otherwise tracker += 1 and, at growth_interval, the scale grows
+ * (x growth, tracker 0: torch._amp_update_scale_).  Powers of two keep the unscaling exact. */
+int acn_amp_unscale_coef(const double* total_sumsq, float max_norm, float* scale, int32_t* growth_tracker,
+                         float* found_inf, float growth, float backoff, int growth_interval, float* out, int64_t* seg,
+                         int K, void* stream);
 
 /* Segment maps of the hash-table gradients (routed step): per expert table two byte maps over
  * its 64-B segments (8 rows of 2 features): now[s] = the scatter added into segment s this step, ever[s] = it

@@ -100,13 +100,19 @@ def test_amp_mlp_matches_torch_autocast(n):
     # every output of ours is an fp16 value, like autocast's
     assert torch.equal(o_a, o_a.half().float())
     assert torch.isfinite(o_a).all() and torch.isfinite(h_a).all()
-    same = float((o_a == o_t).float().mean())
-    assert same >= 0.9, same                       # the GEMM summation order moves a few roundings only
-    assert _dev(o_a, o_t) <= 4e-3
-    assert _dev(h_a, h_t) <= 1e-2
-    for name, a, b in zip(WNAMES, g_a, g_t):
+    # rgb: most values bit-equal (the GEMM summation order moves a few roundings only); sigma: torch's half
+    # exp on this stack rounds differently from expf-then-round, within an fp16 ulp or two
+    same = float((o_a[:, :3] == o_t[:, :3]).float().mean())
+    assert same >= 0.9, same
+    assert _dev(o_a[:, :3], o_t[:, :3]) <= 4e-3
+    sa, st_ = o_a[:, 3].double(), o_t[:, 3].double()
+    assert float(((sa - st_).abs() / st_.abs().clamp_min(1e-30)).max()) <= 2.0 ** -9
+    # gradients: both sides carry fp16 rounding through the chain; the same error scale as autocast's own
+    _, g64, h64 = _torch(h0.double(), sh.double(), gout.double() * S, [w.double() for w in ws], False)
+    assert _dev(h_a, h_t) <= max(0.25, 2 * _dev(h_t, h64)) and _dev(h_a, h64) <= 2 * _dev(h_t, h64) + 1e-3
+    for name, a, b, r in zip(WNAMES, g_a, g_t, g64):
         assert torch.equal(a, a.half().float()), name       # [dW | db] rounded to fp16 once
-        assert _dev(a, b) <= 1e-2, (name, _dev(a, b))
+        assert _dev(a, r) <= 2 * _dev(b, r) + 1e-3, (name, _dev(a, r), _dev(b, r))
 
 
 def test_amp_mlp_error_against_fp32_oracle():
@@ -117,13 +123,16 @@ def test_amp_mlp_error_against_fp32_oracle():
     S = 2.0 ** 16
     o64, g64, h64 = _torch(h0.double(), sh.double(), gout.double() * S, [w.double() for w in ws], False)
     o_a, g_a, h_a = _ours(h0, sh, gout * S, ws, "amp")
+    o_t, g_t, h_t = _torch(h0, sh, gout * S, ws, True)
     o_x, g_x, h_x = _ours(h0, sh, gout * S, ws, "fp16x3")
-    rep = {"out": (_dev(o_a, o64), _dev(o_x, o64)), "dh0": (_dev(h_a, h64), _dev(h_x, h64))}
-    for name, a, x, r in zip(WNAMES, g_a, g_x, g64):
-        rep[name] = (_dev(a, r), _dev(x, r))
-    print("AMPREPORT", {k: f"amp {v[0]:.2e} fp16x3 {v[1]:.2e}" for k, v in rep.items()})
-    assert max(v[0] for v in rep.values()) <= 3e-2          # fp16 (2^-11) through six layers
-    assert max(v[1] for v in rep.values()) <= 5e-5
+    rep = {"out": (_dev(o_a, o64), _dev(o_t, o64), _dev(o_x, o64)),
+           "dh0": (_dev(h_a, h64), _dev(h_t, h64), _dev(h_x, h64))}
+    for name, a, t, x, r in zip(WNAMES, g_a, g_t, g_x, g64):
+        rep[name] = (_dev(a, r), _dev(t, r), _dev(x, r))
+    print("AMPREPORT", {k: f"amp {v[0]:.2e} torch-autocast {v[1]:.2e} fp16x3 {v[2]:.2e}" for k, v in rep.items()})
+    # the _amp kernels' error is the reference's own autocast error (max |dev| / max |ref| per tensor)
+    assert all(v[0] <= 2 * v[1] + 1e-3 for v in rep.values()), rep
+    assert max(v[2] for v in rep.values()) <= 5e-5
 
 
 def test_amp_underflow_without_loss_scale():
@@ -195,7 +204,7 @@ def test_amp_found_inf_skips_and_backs_off():
     d, m, st = _c5_step(True, clear=True)
     before = {n: p.detach().clone() for n, p in m.named_parameters()}
     steps0 = st.adam.step_dev.clone()
-    st.amp.state[0] = 2.0 ** 40
+    st.amp.scale_t.fill_(2.0 ** 40)
     _run(st, d)
     torch.cuda.synchronize()
     assert st.amp.found_inf()
@@ -209,7 +218,7 @@ def test_amp_found_inf_skips_and_backs_off():
         assert int(st.segmaps[:, 0].sum()) == 0       # no segment left marked "touched now"
     for r in st.adam.rows:
         assert torch.isfinite(r[2]).all() and torch.isfinite(r[3]).all()
-    st.amp.state[0] = 2.0 ** 16
+    st.amp.scale_t.fill_(2.0 ** 16)
     _run(st, d, 1)
     torch.cuda.synchronize()
     assert not st.amp.found_inf()
@@ -230,7 +239,7 @@ def test_amp_scale_growth_interval():
 def test_amp_c5_graph_replay_matches_eager():
     """The captured step replays the GradScaler update on the device: graph-replayed AMP steps track the eager
     ones (same batches, same jitter; the table scatter's float atomics allow last-bit differences) and end
-    with the same scaler state."""
+    with the same scaler state (two growths at interval 2)."""
     d, m1, st1 = _c5_step(True, graph=False)
     d, m2, st2 = _c5_step(True, graph=True)
     st1.amp.growth_interval = st2.amp.growth_interval = 2
@@ -239,4 +248,46 @@ def test_amp_c5_graph_replay_matches_eager():
         assert abs(a - b) <= 1e-4 * abs(a), (i, a, b)
     torch.cuda.synchronize()
     assert st2.replays >= 1
-    assert torch.equal(st1.amp.state, st2.amp.state) and st1.amp.get_scale() == 2.0 ** 17
+    assert st1.amp.state_dict() == st2.amp.state_dict() and st1.amp.get_scale() == 2.0 ** 18   # 4 steps, interval 2
+
+
+def test_amp_graphed_meta_step_matches_eager_gradscaler(monkeypatch):
+    """Offline meta-training with use_amp (trainer.py:24 GradScaler, meta_core.py:123-136): the drop-in
+    train_step replaying the task graphs + the outer graph with the GradScaler's device state, against the
+    eager train_step driving torch's own GradScaler (scale / unscale_ / clip / step / update) with the same
+    _amp kernels: the same updates to fp32 summation order and the same scaler state."""
+    import contextlib
+    import goldens as G
+    from test_meta_gpu import _P, _compare_meta_runs, _model_and_tasks
+    from adaptive_city_nerf_amd import meta_train as MT
+    from adaptive_city_nerf_amd import ops
+    from adaptive_city_nerf_amd.optim import build_optimizer
+    d = G.load("meta_fomaml")
+    P = _P("fomaml")
+    P.use_amp = True
+    was = ops.TRAIN_MLP_PRECISION
+    ops.set_train_mlp_precision("amp")
+    try:
+        ma, tasks = _model_and_tasks(d)
+        mb, _ = _model_and_tasks(d)
+        oa, ob = build_optimizer(P, ma), build_optimizer(P, mb)
+        sa, sb = torch.amp.GradScaler("cuda", growth_interval=2), torch.amp.GradScaler("cuda", growth_interval=2)
+        monkeypatch.setattr(MT, "FAST_META_STEP", False)
+        torch.manual_seed(7)
+        with contextlib.redirect_stdout(None):
+            for step in range(4):
+                ra = MT.train_step(P, step, ma, oa, tasks, grad_scaler=sa)
+        monkeypatch.setattr(MT, "FAST_META_STEP", True)
+        torch.manual_seed(7)
+        with contextlib.redirect_stdout(None):
+            for step in range(4):
+                rb = MT.train_step(P, step, mb, ob, tasks, grad_scaler=sb)
+        g = ob._acn_meta_graph
+        assert isinstance(g, MT.GraphedMetaStep) and g.amp is not None and g.replays == 3
+        torch.cuda.synchronize()
+        g.sync_state()
+        assert sa.get_scale() == sb.get_scale() == 2.0 ** 18        # 4 finite steps at interval 2: two growths
+        assert sa.state_dict()["_growth_tracker"] == sb.state_dict()["_growth_tracker"] == 0
+        _compare_meta_runs(ma, oa, mb, ob, ra, rb, lambda n: 4)
+    finally:
+        ops.set_train_mlp_precision(was)

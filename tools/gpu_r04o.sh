@@ -3,7 +3,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r04o; mkdir -p $O
-for v in nop1 nop3; do
+for v in; do
   export ACNERF_LIB=$PWD/build_variants/libacnerf_$v.so
   echo "== check $v"; timeout -k 10 150 python -u tools/dbg/rt_check.py 2>&1 | grep -v -i 'warning\|amdgpu.ids' || exit 1
 done
