@@ -454,6 +454,99 @@ __device__ __forceinline__ void adam_chunk_seg(float* p, float* g, float* m, flo
     }
 }
 
+#ifndef ACN_ADAM_SEG_LDS
+#define ACN_ADAM_SEG_LDS 1  // segment-mapped chunks through an LDS list of their live segments (0: map-ordered lanes)
+#endif
+// The same update as adam_chunk_seg, with the chunk's live segments (now | ever) first compacted into an LDS
+// list (ascending within each 64-segment ballot group), so that every lane of every wave-instruction moves a
+// live vector: adam_chunk_seg leaves the lanes of dead segments idle (40% at C5's 60% ever-touched tables),
+// which caps the bytes in flight per CU below what HBM needs.  Each vector sees exactly adam_chunk_seg's
+// arithmetic (bitwise the dense update); the lists live in LDS only (nothing kept between steps).
+__device__ __forceinline__ void adam_chunk_seg_lds(float* p, float* g, float* m, float* v, int64_t n, float scale,
+                                                   const GroupK& k, uint8_t* __restrict__ now,
+                                                   uint8_t* __restrict__ ever, bool clear) {
+    __shared__ uint16_t lst[ACN_OPTIM_CHUNK / 16];
+    __shared__ uint8_t flg[ACN_OPTIM_CHUNK / 16];   // bit 0: touched now, bit 1: touched before
+    __shared__ int cnt;
+    const int nseg = (int)(n >> 4);   // n is a multiple of 16 (checked by the host)
+    const int lane = threadIdx.x & 63;
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    for (int s0 = 0; s0 < nseg; s0 += kThreads) {
+        const int sg = s0 + (int)threadIdx.x;
+        uint8_t nw = 0, ev = 0;
+        if (sg < nseg) {
+            nw = now[sg];
+            ev = ever[sg];
+        }
+        const bool live = (nw | ev) != 0;
+        const uint64_t b = __ballot(live);
+        int base = 0;
+        if (lane == 0 && b != 0) base = atomicAdd(&cnt, (int)__popcll(b));
+        base = __shfl(base, 0);
+        if (live) {
+            const int pos = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+            lst[pos] = (uint16_t)sg;
+            flg[pos] = (uint8_t)((nw ? 1 : 0) | (ev ? 2 : 0));
+        }
+    }
+    __syncthreads();
+    const int nv = cnt * 4;   // 4 vectors per segment, consecutive lanes
+    f4* p4 = reinterpret_cast<f4*>(p);
+    f4* g4 = reinterpret_cast<f4*>(g);
+    f4* m4 = reinterpret_cast<f4*>(m);
+    f4* v4 = reinterpret_cast<f4*>(v);
+    const f4 zero = 0.0f;
+    int i = threadIdx.x;
+    for (; i + (kUnroll - 1) * kThreads < nv; i += kUnroll * kThreads) {
+        int64_t iv[kUnroll];
+        uint8_t fl[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const int j = i + u * kThreads;
+            iv[u] = (int64_t)lst[j >> 2] * 4 + (j & 3);
+            fl[u] = flg[j >> 2];
+        }
+        f4 pp[kUnroll], mm[kUnroll], vv[kUnroll], gg[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            pp[u] = ldv(&p4[iv[u]]);
+            mm[u] = ldv(&m4[iv[u]]);
+            vv[u] = ldv(&v4[iv[u]]);
+            gg[u] = (fl[u] & 1) ? ldv(&g4[iv[u]]) : zero;
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            adam_vec(pp[u], gg[u], mm[u], vv[u], scale, k);
+            stv(&p4[iv[u]], pp[u]);
+            stv(&m4[iv[u]], mm[u]);
+            stv(&v4[iv[u]], vv[u]);
+            if (clear && (fl[u] & 1) && (gg[u][0] != 0.0f || gg[u][1] != 0.0f || gg[u][2] != 0.0f || gg[u][3] != 0.0f))
+                stv(&g4[iv[u]], zero);
+            if ((iv[u] & 3) == 0 && (fl[u] & 1)) {
+                now[iv[u] >> 2] = 0;
+                if (!(fl[u] & 2)) ever[iv[u] >> 2] = 1;
+            }
+        }
+    }
+    for (; i < nv; i += kThreads) {
+        const int64_t ivs = (int64_t)lst[i >> 2] * 4 + (i & 3);
+        const uint8_t fs = flg[i >> 2];
+        f4 pp = ldv(&p4[ivs]), mm = ldv(&m4[ivs]), vv = ldv(&v4[ivs]);
+        const f4 gg = (fs & 1) ? ldv(&g4[ivs]) : zero;
+        adam_vec(pp, gg, mm, vv, scale, k);
+        stv(&p4[ivs], pp);
+        stv(&m4[ivs], mm);
+        stv(&v4[ivs], vv);
+        if (clear && (fs & 1) && (gg[0] != 0.0f || gg[1] != 0.0f || gg[2] != 0.0f || gg[3] != 0.0f)) stv(&g4[ivs], zero);
+        if ((ivs & 3) == 0 && (fs & 1)) {
+            now[ivs >> 2] = 0;
+            if (!(fs & 2)) ever[ivs >> 2] = 1;
+        }
+    }
+}
+
 __global__ void __launch_bounds__(kThreads) adam_slots_kernel(const acn_param_desc* __restrict__ descs,
                                                               const int32_t* __restrict__ chunk_tensor,
                                                               const int32_t* __restrict__ flags,
@@ -497,7 +590,11 @@ __global__ void __launch_bounds__(kThreads) adam_slots_kernel(const acn_param_de
     uint8_t* smap = segmaps ? segmaps[2 * t] : nullptr;
     if (smap) {
         const int64_t s0 = base >> 4, nseg = (d.numel + 15) >> 4;
+#if ACN_ADAM_SEG_LDS
+        adam_chunk_seg_lds(p, g, m, v, n, scale, k, smap + s0, segmaps[2 * t + 1] + s0, (f & kSlotZero) != 0);
+#else
         adam_chunk_seg(p, g, m, v, n, scale, k, smap + s0, segmaps[2 * t + 1] + s0, (f & kSlotZero) != 0);
+#endif
         (void)nseg;
     } else if (f & kSlotZero) {
         adam_chunk_zero(p, g, m, v, n, scale, k);
