@@ -174,6 +174,7 @@ SIGNATURES = {
     "acn_grad_sumsq_slots_ex": ([vp, vp, i64, vp, vp, i32, vp, vp, vp, vp], C.c_int),
     "acn_adam_step_slots": ([vp, vp, i64, vp, vp, i32, i32, vp, i32, vp, i32, vp, vp], C.c_int),
     "acn_adam_step_slots_segmap": ([vp, vp, i64, vp, vp, i32, i32, vp, i32, vp, i32, vp, vp, vp], C.c_int),
+    "acn_adam_step_slots_segmap_phase": ([vp, vp, i64, vp, vp, i32, i32, vp, i32, vp, i32, vp, vp, i32, vp], C.c_int),
     "acn_hashgrid_bwd_pairs_segmap": ([vp, vp, vp, vp, i32, vp, vp, vp, i32, i32, i32, vp, vp, vp], C.c_int),
     "acn_hashgrid_pairs_mark": ([vp, vp, vp, vp, i32, vp, i32, i32, i32, vp, vp], C.c_int),
     "acn_amp_unscale_coef": ([vp, f32, vp, vp, vp, f32, f32, i32, vp, vp, i32, vp], C.c_int),

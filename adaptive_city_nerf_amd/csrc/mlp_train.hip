@@ -705,9 +705,15 @@ __device__ __forceinline__ void relu_mask(f32x16 (&G)[NT], const f32x16 (&Y)[NT]
 #ifndef ACN_DW_F16X3
 // weight-gradient contraction on the fp16x3 split as well.  Off: measured slower (fused backward 352 ->
 // 383 us at M = 384k, meta step 79.1 -> 82.8 ms): with one wave per SIMD the dW phase is bound by the
-// staging (split + two f16 planes written per element) and LDS traffic, not by the fp32 MFMAs it saves
-#define ACN_DW_F16X3 0
+// staging (split + two f16 planes written per element) and LDS traffic, not by the fp32 MFMAs it saves.
+// The AMP build always takes the fp16 stage with ONE plane: its dY and X are fp16 values already, so one
+// v_mfma_f32_16x16x16_f16 product per term is exact (fp32 accumulation), as autocast's fp16 GEMM computes it
+#define ACN_DW_F16X3 ACN_TRAIN_AMP
 #endif
+#if ACN_TRAIN_AMP && !ACN_DW_F16X3
+#error "the AMP build contracts [dW | db] on the fp16 stage"
+#endif
+constexpr int kStagePlanes = ACN_TRAIN_AMP ? 1 : 2;   // fp16 stage: hi (+ lo for the fp16x3 split)
 
 struct StageScale {
     int kY, kX;  // power-of-two exponents the staged dY / X carry (0: unscaled fp32 stage)
@@ -724,7 +730,7 @@ struct StageScale {
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 constexpr int SH = 136;                   // stage row stride (halves): 128 samples + 8, 16-B aligned rows
 constexpr int ST_ROWS = 144, ST_ONES = 128;
-constexpr int ST_FLOATS = 2 * ST_ROWS * SH / 2;  // two f16 planes
+constexpr int ST_FLOATS = kStagePlanes * ST_ROWS * SH / 2;  // one or two f16 planes
 __device__ __forceinline__ f32x4 mfma16h(const f16x4& a, const f16x4& b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0);
 }
@@ -735,7 +741,7 @@ __device__ __forceinline__ void stage_init(float* st) {  // the ones row (both p
     _Float16* lp = hp + ST_ROWS * SH;
     for (int e = threadIdx.x; e < (ST_ROWS - ST_ONES) * SH; e += blockDim.x) {
         hp[ST_ONES * SH + e] = (_Float16)(e < SH ? 1.0f : 0.0f);
-        lp[ST_ONES * SH + e] = (_Float16)0.0f;
+        if (kStagePlanes == 2) lp[ST_ONES * SH + e] = (_Float16)0.0f;
     }
 }
 
@@ -779,13 +785,20 @@ __device__ __forceinline__ void stage_put(float* st, int row0, const f32x16 (&T)
         for (int r = 0; r < 16; r += 2) {
             const f32x2 x = (f32x2){T[t][r], T[t][r + 1]} * (f32x2){sc, sc};
             const f16x2 hi = __builtin_convertvector(x, f16x2);
-            const f16x2 lo = __builtin_convertvector(x - __builtin_convertvector(hi, f32x2), f16x2);
             const int o0 = (row0 + 32 * t + rho(r, h)) * SH + 32 * w + j, o1 = (row0 + 32 * t + rho(r + 1, h)) * SH + 32 * w + j;
             hp[o0] = hi[0];
             hp[o1] = hi[1];
-            lp[o0] = lo[0];
-            lp[o1] = lo[1];
+            if (kStagePlanes == 2) {
+                const f16x2 lo = __builtin_convertvector(x - __builtin_convertvector(hi, f32x2), f16x2);
+                lp[o0] = lo[0];
+                lp[o1] = lo[1];
+            }
         }
+}
+// the producer / consumer kernel's put (AMP: unscaled fp16 values)
+template <int NT>
+__device__ __forceinline__ void stage_put(float* st, int row0, const f32x16 (&T)[NT], int w, int lane) {
+    stage_put<NT>(st, row0, T, 0, w, lane);
 }
 
 // acc[n] += dY[16 rows from arow] . X[16 features from xrow + 16 n]^T over the 128 staged samples,
@@ -807,17 +820,26 @@ __device__ __forceinline__ void dw_blocks(const float* st, int arow, int xrow, f
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
         const f16x4 ah = *reinterpret_cast<const f16x4*>(hp + oa + 4 * t);
-        const f16x4 al = *reinterpret_cast<const f16x4*>(lp + oa + 4 * t);
         const f16x4 on = *reinterpret_cast<const f16x4*>(hp + oo + 4 * t);
-        tb = mfma16h(al, on, tb);
-        tb = mfma16h(ah, on, tb);
+        if (kStagePlanes == 2) {
+            const f16x4 al = *reinterpret_cast<const f16x4*>(lp + oa + 4 * t);
+            tb = mfma16h(al, on, tb);
+            tb = mfma16h(ah, on, tb);
 #pragma unroll
-        for (int n = 0; n < NCB; ++n) {
-            const f16x4 bh = *reinterpret_cast<const f16x4*>(hp + ob + 16 * n * SH + 4 * t);
-            const f16x4 bl = *reinterpret_cast<const f16x4*>(lp + ob + 16 * n * SH + 4 * t);
-            tmp[n] = mfma16h(al, bh, tmp[n]);
-            tmp[n] = mfma16h(ah, bl, tmp[n]);
-            tmp[n] = mfma16h(ah, bh, tmp[n]);
+            for (int n = 0; n < NCB; ++n) {
+                const f16x4 bh = *reinterpret_cast<const f16x4*>(hp + ob + 16 * n * SH + 4 * t);
+                const f16x4 bl = *reinterpret_cast<const f16x4*>(lp + ob + 16 * n * SH + 4 * t);
+                tmp[n] = mfma16h(al, bh, tmp[n]);
+                tmp[n] = mfma16h(ah, bl, tmp[n]);
+                tmp[n] = mfma16h(ah, bh, tmp[n]);
+            }
+        } else {   // AMP: dY, X are fp16 values -- one exact product per term
+            tb = mfma16h(ah, on, tb);
+#pragma unroll
+            for (int n = 0; n < NCB; ++n) {
+                const f16x4 bh = *reinterpret_cast<const f16x4*>(hp + ob + 16 * n * SH + 4 * t);
+                tmp[n] = mfma16h(ah, bh, tmp[n]);
+            }
         }
     }
     const float ua = ldexpf(1.0f, -sc.kY), uab = ldexpf(1.0f, -(sc.kY + sc.kX));
@@ -834,6 +856,13 @@ __device__ __forceinline__ void dw_blocks(const float* st, int arow, int xrow, f
 template <int NO, int NI>
 __device__ __forceinline__ StageScale stage_layer(float* st, const f32x16 (&dY)[NO], const f32x16 (&X)[NI], int w,
                                                   int lane) {
+#if ACN_TRAIN_AMP   // fp16 values already: no rescaling (what autocast's GEMM sees)
+    __syncthreads();
+    stage_put<NO>(st, 0, dY, 0, w, lane);
+    stage_put<NI>(st, X_ROW, X, 0, w, lane);
+    __syncthreads();
+    return StageScale{0, 0};
+#endif
     __shared__ uint32_t smax[8];
     const uint32_t my = wave_absmax_bits<NO>(dY), mx = wave_absmax_bits<NI>(X);
     if (lane == 0) {
@@ -1144,7 +1173,7 @@ __global__ void __launch_bounds__(256) mlp_bwd_dw_kernel(const float* __restrict
 #endif
 }
 
-#if !ACN_DW_F16X3
+#if !ACN_DW_F16X3 || ACN_TRAIN_AMP
 // Producer / consumer form of the fused backward (8-wave workgroups, two waves per SIMD).  Waves 0-3
 // (producers) run exactly the per-tile work of dw_round -- forward recompute, the dX chain, ReLU masks --
 // and put each layer's dY / X into the shared stage; waves 4-7 (consumers) hold the weight-gradient
@@ -1263,6 +1292,7 @@ __global__ void __launch_bounds__(512) mlp_bwd_dw_pc_kernel(const float* __restr
     __shared__ __attribute__((aligned(16))) float Wl[L_FLOATS];
     __shared__ __attribute__((aligned(16))) float st_base[ST_FLOATS];
     stage_weights(img, Wl);
+    stage_init(st_base);   // the fp16 stage's ones row (bias sums); nothing for the fp32 stage
     __syncthreads();
     const int lane0 = threadIdx.x & 63, j = lane0 & 31;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), w = wv & 3;
@@ -1480,7 +1510,7 @@ int bwd_dw_launch(const float* h0, const float* sh, const float* out, const floa
                   float* dw, float* gh0, float* partial, hipStream_t s) {
     const int64_t tiles = (M + 31) / 32, want = (tiles + 3) / 4;
     const int nblk = (int)(want < MAX_DW_BLOCKS ? want : MAX_DW_BLOCKS);
-#if ACN_DW_PC && !ACN_DW_F16X3
+#if ACN_DW_PC && (!ACN_DW_F16X3 || ACN_TRAIN_AMP)
     hipLaunchKernelGGL(mlp_bwd_dw_pc_kernel, dim3(nblk), dim3(512), 0, s, img, h0, sh, out, gout, M, gh0, partial);
 #else
     hipLaunchKernelGGL(mlp_bwd_dw_kernel, dim3(nblk), dim3(256), 0, s, img, h0, sh, out, gout, M, gh0, partial);

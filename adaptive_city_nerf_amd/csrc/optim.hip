@@ -387,9 +387,16 @@ __device__ __forceinline__ void adam_chunk_zero(float* p, float* g, float* m, fl
 // s = vector / 4; the 4 vectors of a segment are 4 consecutive lanes of one wave-instruction (the map
 // loads precede the map stores for all of them); the first lane updates the maps.  chunk base is a
 // multiple of ACN_OPTIM_CHUNK floats (segment aligned).
+__device__ __forceinline__ bool seg_live(uint8_t nw, uint8_t ev, int phase) {
+    return phase == 0 ? (nw | ev) != 0 : (phase == 1 ? (ev != 0 && nw == 0) : nw != 0);
+}
+
+// phase 0: every live segment (now | ever); phase 1 (early pass): only segments touched before but not now --
+// their gradient is zero, so the update needs neither the gradient nor the clip coefficient and the maps stay;
+// phase 2 (late pass): only the segments touched now (gradient read and cleared, maps updated).
 __device__ __forceinline__ void adam_chunk_seg(float* p, float* g, float* m, float* v, int64_t n, float scale,
                                                const GroupK& k, uint8_t* __restrict__ now, uint8_t* __restrict__ ever,
-                                               bool clear) {
+                                               bool clear, int phase = 0) {
     f4* p4 = reinterpret_cast<f4*>(p);
     f4* g4 = reinterpret_cast<f4*>(g);
     f4* m4 = reinterpret_cast<f4*>(m);
@@ -411,7 +418,7 @@ __device__ __forceinline__ void adam_chunk_seg(float* p, float* g, float* m, flo
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
             const int64_t iv = i + u * kThreads;
-            if (nw[u] | ev[u]) {
+            if (seg_live(nw[u], ev[u], phase)) {
                 pp[u] = ldv(&p4[iv]);
                 mm[u] = ldv(&m4[iv]);
                 vv[u] = ldv(&v4[iv]);
@@ -421,7 +428,7 @@ __device__ __forceinline__ void adam_chunk_seg(float* p, float* g, float* m, flo
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
             const int64_t iv = i + u * kThreads;
-            if (nw[u] | ev[u]) {
+            if (seg_live(nw[u], ev[u], phase)) {
                 adam_vec(pp[u], gg[u], mm[u], vv[u], scale, k);
                 stv(&p4[iv], pp[u]);
                 stv(&m4[iv], mm[u]);
@@ -429,7 +436,7 @@ __device__ __forceinline__ void adam_chunk_seg(float* p, float* g, float* m, flo
                 if (clear && nw[u] && (gg[u][0] != 0.0f || gg[u][1] != 0.0f || gg[u][2] != 0.0f || gg[u][3] != 0.0f))
                     stv(&g4[iv], zero);
             }
-            if ((iv & 3) == 0 && nw[u]) {
+            if (phase != 1 && (iv & 3) == 0 && nw[u]) {
                 now[iv >> 2] = 0;
                 if (!ev[u]) ever[iv >> 2] = 1;
             }
@@ -438,7 +445,7 @@ __device__ __forceinline__ void adam_chunk_seg(float* p, float* g, float* m, flo
     for (; i < n4; i += kThreads) {
         const int64_t sgi = i >> 2;
         const uint8_t nw = now[sgi], ev = ever[sgi];
-        if (nw | ev) {
+        if (seg_live(nw, ev, phase)) {
             f4 pp = ldv(&p4[i]), mm = ldv(&m4[i]), vv = ldv(&v4[i]);
             const f4 gg = nw ? ldv(&g4[i]) : zero;
             adam_vec(pp, gg, mm, vv, scale, k);
@@ -447,7 +454,7 @@ __device__ __forceinline__ void adam_chunk_seg(float* p, float* g, float* m, flo
             stv(&v4[i], vv);
             if (clear && nw && (gg[0] != 0.0f || gg[1] != 0.0f || gg[2] != 0.0f || gg[3] != 0.0f)) stv(&g4[i], zero);
         }
-        if ((i & 3) == 0 && nw) {
+        if (phase != 1 && (i & 3) == 0 && nw) {
             now[sgi] = 0;
             if (!ev) ever[sgi] = 1;
         }
@@ -455,7 +462,7 @@ __device__ __forceinline__ void adam_chunk_seg(float* p, float* g, float* m, flo
 }
 
 #ifndef ACN_ADAM_SEG_LDS
-#define ACN_ADAM_SEG_LDS 1  // segment-mapped chunks through an LDS list of their live segments (0: map-ordered lanes)
+#define ACN_ADAM_SEG_LDS 0  // 1: segment-mapped chunks through an LDS list of their live segments (measured slower)
 #endif
 // The same update as adam_chunk_seg, with the chunk's live segments (now | ever) first compacted into an LDS
 // list (ascending within each 64-segment ballot group), so that every lane of every wave-instruction moves a
@@ -554,12 +561,15 @@ __global__ void __launch_bounds__(kThreads) adam_slots_kernel(const acn_param_de
                                                               int table_steps, const int32_t* __restrict__ step_dev,
                                                               const int64_t* __restrict__ seg, int K,
                                                               const float* __restrict__ grad_scale,
-                                                              uint8_t* const* __restrict__ segmaps) {
+                                                              uint8_t* const* __restrict__ segmaps, int phase) {
     const int t = chunk_tensor[blockIdx.x];
     const acn_param_desc d = descs[t];
     const int f = flags[t], slot = f & 0xffff;
     if (d.grad == nullptr) return;
+    const bool mapped = segmaps != nullptr && segmaps[2 * t] != nullptr;
+    if (phase == 1 && !mapped) return;   // the early pass touches only the mapped tables' untouched segments
     if (seg != nullptr && seg[K] < 0) {
+        if (phase == 1) return;
         // a skipped step (AMP found_inf, an overflowed bounded exchange): parameters and moments stay, but the
         // gradients this pass would have cleared are cleared (and the segment marks reset) so the next step
         // starts from zero as after an update
@@ -590,10 +600,13 @@ __global__ void __launch_bounds__(kThreads) adam_slots_kernel(const acn_param_de
     uint8_t* smap = segmaps ? segmaps[2 * t] : nullptr;
     if (smap) {
         const int64_t s0 = base >> 4, nseg = (d.numel + 15) >> 4;
-#if ACN_ADAM_SEG_LDS
+#if ACN_ADAM_SEG_LDS  // (phase 0 only)
         adam_chunk_seg_lds(p, g, m, v, n, scale, k, smap + s0, segmaps[2 * t + 1] + s0, (f & kSlotZero) != 0);
 #else
-        adam_chunk_seg(p, g, m, v, n, scale, k, smap + s0, segmaps[2 * t + 1] + s0, (f & kSlotZero) != 0);
+        if (phase != 0)
+            adam_chunk_seg(p, g, m, v, n, scale, k, smap + s0, segmaps[2 * t + 1] + s0, (f & kSlotZero) != 0, phase);
+        else
+            adam_chunk_seg(p, g, m, v, n, scale, k, smap + s0, segmaps[2 * t + 1] + s0, (f & kSlotZero) != 0);
 #endif
         (void)nseg;
     } else if (f & kSlotZero) {
@@ -768,7 +781,7 @@ extern "C" int acn_adam_step_slots(const acn_param_desc* descs, const int32_t* c
     hipLaunchKernelGGL(bump_slots_kernel, dim3(1), dim3(1024), 0, s, step_dev, seg, K, nslots);
     hipLaunchKernelGGL(adam_slots_kernel, dim3((unsigned)nchunks), dim3(kThreads), 0, s, descs, chunk_tensor, flags,
                        reinterpret_cast<const GroupK*>(table), ngroups, table_steps, step_dev, seg, K, grad_scale,
-                       (uint8_t* const*)nullptr);
+                       (uint8_t* const*)nullptr, 0);
     return acn_check_launch("acn_adam_step_slots");
 }
 
@@ -784,6 +797,24 @@ extern "C" int acn_adam_step_slots_segmap(const acn_param_desc* descs, const int
     hipLaunchKernelGGL(bump_slots_kernel, dim3(1), dim3(1024), 0, s, step_dev, seg, K, nslots);
     hipLaunchKernelGGL(adam_slots_kernel, dim3((unsigned)nchunks), dim3(kThreads), 0, s, descs, chunk_tensor, flags,
                        reinterpret_cast<const GroupK*>(table), ngroups, table_steps, step_dev, seg, K, grad_scale,
-                       segmaps);
+                       segmaps, 0);
     return acn_check_launch("acn_adam_step_slots_segmap");
+}
+
+extern "C" int acn_adam_step_slots_segmap_phase(const acn_param_desc* descs, const int32_t* chunk_tensor,
+                                                int64_t nchunks, const int32_t* flags, const void* table, int ngroups,
+                                                int table_steps, int32_t* step_dev, int nslots, const int64_t* seg,
+                                                int K, const float* grad_scale, uint8_t* const* segmaps, int phase,
+                                                void* stream) {
+    ACN_REQUIRE(nchunks >= 1 && nchunks <= 0x7fffffff && descs && chunk_tensor && flags && table && step_dev && segmaps,
+                "acn_adam_step_slots_segmap_phase: bad arguments");
+    ACN_REQUIRE(ngroups >= 1 && ngroups <= ACN_OPTIM_MAX_GROUPS && table_steps >= 1 && nslots >= 1 && nslots <= 1024,
+                "acn_adam_step_slots_segmap_phase: bad ngroups / table_steps / nslots");
+    ACN_REQUIRE(phase == 1 || phase == 2, "acn_adam_step_slots_segmap_phase: phase must be 1 or 2, got %d", phase);
+    hipStream_t s = (hipStream_t)stream;
+    if (phase == 1) hipLaunchKernelGGL(bump_slots_kernel, dim3(1), dim3(1024), 0, s, step_dev, seg, K, nslots);
+    hipLaunchKernelGGL(adam_slots_kernel, dim3((unsigned)nchunks), dim3(kThreads), 0, s, descs, chunk_tensor, flags,
+                       reinterpret_cast<const GroupK*>(table), ngroups, table_steps, step_dev, seg, K, grad_scale,
+                       segmaps, phase);
+    return acn_check_launch("acn_adam_step_slots_segmap_phase");
 }

@@ -1321,7 +1321,7 @@ __device__ __forceinline__ int lanes_below(uint64_t m) {
 // colour layer 0 first = the per-ray fold's order), so a ray's outputs do not depend on its batch.
 // 512 threads, two workgroups per CU (16 waves), <= 80 KB of LDS each.
 #ifndef ACN_ROUTED
-#define ACN_ROUTED 1
+#define ACN_ROUTED 0  // 1: expert-major chunks for K > 2 (measured slower than render_slots_kernel)
 #endif
 #ifndef ACN_ROUTED_CHUNK
 #define ACN_ROUTED_CHUNK 1024  // samples per chunk (rays per chunk = ACN_ROUTED_CHUNK / S)

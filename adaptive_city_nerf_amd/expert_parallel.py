@@ -319,7 +319,7 @@ class ExpertParallelRenderer:
 
     def _run(self, n: int) -> None:
         import ctypes as C
-        from . import _lib
+        from . import _lib, ops
         from ._lib import check, ptr
         L = _lib.lib()
         s = int(torch.cuda.current_stream(self.device).cuda_stream)
@@ -333,8 +333,16 @@ class ExpertParallelRenderer:
         comm.all_to_all(self.recv_xd, self.xd, self.split_recv, self.split_send)
         check(L.acn_pack_experts(self._own_arr, C.byref(self.own_routing), -1, ptr(self.packed),
                                  self.packed.numel() * 4, s), "acn_pack_experts")
+        hook = ops.EVENT_HOOK if not torch.cuda.is_current_stream_capturing() else None   # bench.py timing
+        if hook is not None:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
         check(L.acn_ep_field_fwd(ptr(self.recv_xd), ptr(self.recv_cnt), self.W, E, Cc, self._own_arr,
                                  ptr(self.packed), self.packed.numel() * 4, ptr(self.ret), s), "acn_ep_field_fwd")
+        if hook is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            hook.append((e0, e1))
         comm.all_to_all(self.yr, self.ret, self.split_send, self.split_recv)
         check(L.acn_ep_composite(ptr(self.rays), n, S, None, ptr(self.yr), ptr(self.pw), ptr(self.pmap), K, self.hard,
                                  C.byref(self.bg_spec), 1.0, 0.0, ptr(self.rgb), ptr(self.depth), ptr(self.weights),

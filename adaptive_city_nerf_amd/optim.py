@@ -486,8 +486,29 @@ class SlottedAdam:
         self.table.copy_(host)
         self._hparams = hp
 
+    def step_early(self, seg: torch.Tensor, hook=None) -> None:
+        """Phase 1 of the split segment-mapped update (acn_adam_step_slots_segmap_phase): bump the active slots'
+        step counters and update the table segments touched before but not this step (zero gradient: no clip
+        coefficient needed), on the current stream (a side stream beside the step's forward / backward) -- as soon
+        as the step's now[] marks exist.  step(..., phase=2) finishes the update after the clip coefficient."""
+        if self.segmaps is None:
+            raise AcnError("SlottedAdam.step_early needs segment maps")
+        from ._lib import ptr
+        s = _stream(self.device)
+        if hook is not None:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+        check(_lib.lib().acn_adam_step_slots_segmap_phase(
+            ptr(self.descs), ptr(self.chunk_tensor), self.nchunks, ptr(self.flags), ptr(self.table), self.ngroups,
+            self.table_steps, ptr(self.step_dev), self.nslots, ptr(seg), self.K, None, ptr(self.segmaps), 1, s),
+            "acn_adam_step_slots_segmap_phase")
+        if hook is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            self._early_events = (e0, e1)
+
     def step(self, seg: torch.Tensor, max_norm: Optional[float], table_sumsq: Optional[torch.Tensor] = None,
-             hook=None, allreduce=None, amp: Optional[AmpScaler] = None) -> None:
+             hook=None, allreduce=None, amp: Optional[AmpScaler] = None, phase: int = 0) -> None:
         """Clip norm over the active slots' gradients (+ ``table_sumsq``, a device double some kernel
         accumulated for NORM_ELSEWHERE tensors; reset by the norm pass), clip coefficient, then Adam over
         the active slots; per-slot step counters advance on the device.  ``allreduce`` (split_norm):
@@ -526,7 +547,12 @@ class SlottedAdam:
         if hook is not None:
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record()
-        if self.segmaps is not None:
+        if self.segmaps is not None and phase == 2:    # after step_early: the segments touched now + dense tensors
+            check(L.acn_adam_step_slots_segmap_phase(ptr(self.descs), ptr(self.chunk_tensor), self.nchunks,
+                                                     ptr(self.flags), ptr(self.table), self.ngroups, self.table_steps,
+                                                     ptr(self.step_dev), self.nslots, ptr(seg), self.K, ptr(scale),
+                                                     ptr(self.segmaps), 2, s), "acn_adam_step_slots_segmap_phase")
+        elif self.segmaps is not None:
             check(L.acn_adam_step_slots_segmap(ptr(self.descs), ptr(self.chunk_tensor), self.nchunks, ptr(self.flags),
                                                ptr(self.table), self.ngroups, self.table_steps, ptr(self.step_dev),
                                                self.nslots, ptr(seg), self.K, ptr(scale), ptr(self.segmaps), s),
@@ -538,7 +564,9 @@ class SlottedAdam:
         if hook is not None:
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record()
-            hook.append((e0, e1))
+            early = getattr(self, "_early_events", None) if phase == 2 else None
+            self._early_events = None
+            hook.append((e0, e1) if early is None else (early[0], early[1], e0, e1))   # pairs of events
 
     def sync_state(self, extra_slots=()) -> None:
         """Host state['step'] of every parameter from the per-slot device counters (state_dict, or before

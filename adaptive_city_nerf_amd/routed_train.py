@@ -58,6 +58,9 @@ FUSED_BACKGROUND = os.environ.get("ACN_FUSED_BG", "1") != "0"
 # segments never touched (m = v = g = 0: bit-identical under torch's Adam with weight_decay 0) and reads no
 # gradient for segments not touched this step
 ADAM_SEGMAP = os.environ.get("ACN_ADAM_SEGMAP", "1") != "0"
+# Split segment-mapped Adam: the early pass (segments touched before but not by this step) on a side stream
+# beside the step's forward / backward, the late pass after the clip coefficient
+ADAM_EARLY = os.environ.get("ACN_ADAM_EARLY", "1") != "0"
 
 
 def draw_jitter(n: int, S: int, device) -> torch.Tensor:
@@ -200,6 +203,12 @@ class RoutedAdaptStep:
         self.nslots, self.table_steps, self._step0 = self.adam.nslots, self.adam.table_steps, self.adam.step0
         self.scale = self.adam.scale
         self.table_sumsq = torch.zeros(1, device=dev, dtype=torch.float64)  # reset by grad_sumsq_slots_ex
+        # split Adam (ADAM_EARLY): the table segments a step does not touch but earlier steps did (~40-60% of the
+        # segment-mapped bytes) are updated on a side stream while the step's forward / backward runs -- their
+        # gradient is zero, so they need no clip coefficient; the late pass updates the touched segments and the
+        # dense tensors.  Not with use_amp (a found_inf skip is decided after the backward).
+        self.early = ADAM_EARLY and self.segmaps is not None and self.amp is None
+        self.side = torch.cuda.Stream(dev) if self.early else None
         self.replays = 0          # graph replays
         self.steps_done = 0       # every update this object ran (eager and replayed): Adam table rows used
         self.graph = None
@@ -237,6 +246,23 @@ class RoutedAdaptStep:
                                    ptr(self.pidx), ptr(self.pw), ptr(self.x01), ptr(self.sh), ptr(self.pmap),
                                    ptr(self.pk), s), "acn_routed_scatter")
         enc = self.model.submodules[0].xyz_encoder
+        capturing = torch.cuda.is_current_stream_capturing()   # no timing events inside a capture
+        det = torch.are_deterministic_algorithms_enabled()
+        ev_early = None
+        if self.early and not det:
+            # fork: the step's now[] marks from its pair list, then Adam's early pass, on the side stream
+            main = torch.cuda.current_stream(dev)
+            ev0 = torch.cuda.Event()
+            ev0.record(main)
+            self.side.wait_event(ev0)
+            with torch.cuda.stream(self.side):
+                check(L.acn_hashgrid_pairs_mark(ptr(self.x01), ptr(self.pk), ptr(self.pidx), ptr(self.seg), K,
+                                                self._res, len(enc._res_host), enc.log2_hashmap_size,
+                                                enc._interp_code, self._segnow, int(self.side.cuda_stream)),
+                      "acn_hashgrid_pairs_mark")
+                self.adam.step_early(self.seg, hook=EVENT_HOOK if self.graph is None and not capturing else None)
+                ev_early = torch.cuda.Event()
+                ev_early.record(self.side)
         check(L.acn_hashgrid_fwd_pairs(ptr(self.x01), ptr(self.pk), ptr(self.seg), K, self._tables, self._res,
                                        len(enc._res_host), enc.log2_hashmap_size, enc._interp_code, ptr(self.h0), s),
               "acn_hashgrid_fwd_pairs")
@@ -282,30 +308,36 @@ class RoutedAdaptStep:
         gout = ops.routed_blend_bwd(g_rs.reshape(M, 4).contiguous(), self.pidx, self.pw, live=self.seg[K:K + 1])
         check(mfn("acn_mlp_train_bwd_dw_pairs")(ptr(self.h0), ptr(self.sh), ptr(self.out), ptr(gout), ptr(self.seg), K,
                                            ptr(self.mws), ptr(self.dw), ptr(self.gh0), s), "acn_mlp_train_bwd_dw_pairs")
-        capturing = torch.cuda.is_current_stream_capturing()   # no timing events inside a capture
         bhook = BWD_HOOK if self.graph is None and not capturing else None
         if bhook is not None:
             b0 = torch.cuda.Event(enable_timing=True)
             b0.record()
-        if torch.are_deterministic_algorithms_enabled():
+        if det:
             self._table_bwd_deterministic(enc)
             if self.segmaps is not None:   # the sort-based backward marks no segments: the marks on their own
                 check(L.acn_hashgrid_pairs_mark(ptr(self.x01), ptr(self.pk), ptr(self.pidx), ptr(self.seg), K,
                                                 self._res, len(enc._res_host), enc.log2_hashmap_size,
                                                 enc._interp_code, self._segnow, s), "acn_hashgrid_pairs_mark")
+                if self.early:   # the same two passes, in sequence
+                    self.adam.step_early(self.seg, hook=EVENT_HOOK if self.graph is None and not capturing else None)
         else:
+            # the marks came from the side stream (early) or come with the scatter
             check(L.acn_hashgrid_bwd_pairs_segmap(ptr(self.x01), ptr(self.pk), ptr(self.pidx), ptr(self.seg), K,
                                                   ptr(self.gh0), self._gtables, self._res, len(enc._res_host),
                                                   enc.log2_hashmap_size, enc._interp_code,
                                                   ptr(self.table_sumsq) if self.tele else None,
-                                                  self._segnow if self.segmaps is not None else None, s),
+                                                  self._segnow if self.segmaps is not None and not self.early
+                                                  else None, s),
                   "acn_hashgrid_bwd_pairs_segmap")
         if bhook is not None:
             b1 = torch.cuda.Event(enable_timing=True)
             b1.record()
             bhook.append((b0, b1))
+        if ev_early is not None:
+            torch.cuda.current_stream(dev).wait_event(ev_early)   # join
         self.adam.step(self.seg, self.grad_clip, self.table_sumsq if self.tele else None,
-                       hook=EVENT_HOOK if self.graph is None and not capturing else None, amp=self.amp)
+                       hook=EVENT_HOOK if self.graph is None and not capturing else None, amp=self.amp,
+                       phase=2 if self.early else 0)
 
     def _table_bwd_deterministic(self, enc) -> None:
         """Under torch.use_deterministic_algorithms(True): every expert's table gradient by the sort-based

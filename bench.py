@@ -357,9 +357,8 @@ def render_traffic_profile(workload: str, S: int, layout: str):
     separate rocprofv3 --pmc passes, FETCH_SIZE doubled per the gfx950 correction of MI355X_MICROARCH.md
     'HBM', plus WRITE_SIZE), or None when no profile of this exact configuration is committed."""
     name = {("c2", 256, "replicated"): "r04_pmc_c2_render.json",
-            ("c3", 256, "replicated"): "r04_pmc_c3_routed.json",
-            ("c4", 96, "replicated"): "r04_pmc_c4s96_routed.json",
-            ("c4", 256, "replicated"): "r04_pmc_c4_routed.json"}.get((workload, S, layout))
+            ("c3", 256, "replicated"): "r04_pmc_c3_slots.json",
+            ("c4", 96, "replicated"): "r04_pmc_c4s96_slots.json"}.get((workload, S, layout))
     if name is None:
         return None
     p = REPO / "profiles" / name
@@ -874,7 +873,8 @@ def main():
         hook = [(eb[0], eb[1])] * a.steps     # one launch per step; average = bracketed time / K
     else:
         hook = ops.EVENT_HOOK
-    kernel_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in hook]))
+    # an entry is one or more (start, end) event pairs of one step's launches (the split Adam: early + late pass)
+    kernel_ms = float(np.mean([sum(ev[i].elapsed_time(ev[i + 1]) for i in range(0, len(ev), 2)) for ev in hook]))
     if bracket:
         kernel_ms /= a.steps
     if a.workload == "data":
@@ -955,13 +955,11 @@ def main():
              "c2": "ray_order_kernel + render_kernel<1,1,0> (one acn_render_stratified_fwd_ordered call: direction "
                    "grouping of the batch, then the fused stratified render, 1 expert; kernel_ms = two HIP events "
                    "bracketing the K timed calls on the launch stream / K)",
-             "c3": "render_routed_kernel (fused stratified render, soft routing over 4 experts: expert-major "
-                   "chunks of 1024 ray-samples, one expert image in LDS per chunk pass; + ray_order_kernel)",
+             "c3": "render_slots_kernel (fused stratified render, soft routing over 4 experts, two staged per round)",
              "c4": ("ep_field_kernel (the owned expert's fused MFMA field over the received per-sample records; "
-                    "+ ep_composite_kernel, one-expert-per-GPU layout)"
+                    "one-expert-per-GPU layout, kernel_ms per launch)"
                     if a.layout == "expert" else
-                    "render_routed_kernel (fused stratified render, soft routing over 8 experts: expert-major "
-                    "chunks of 1024 ray-samples, one expert image in LDS per chunk pass; + ray_order_kernel)"),
+                    "render_slots_kernel (fused stratified render, soft routing over 8 experts, two staged per round)"),
              "occ": "occ_render_kernel<1,1,0> (fused occupancy render over packed marched samples, 1 expert)",
              "meta": "adam_kernel (fused clip + Adam of the outer meta-update over the region experts + shared head)",
              "data": "route_kernel (TaskDataset region clip + DDA max-overlap micro-cell routing + keep tolerance)",

@@ -710,6 +710,19 @@ int acn_adam_step_slots_segmap(const acn_param_desc* descs, const int32_t* chunk
                                const int32_t* flags, const void* table, int ngroups, int table_steps, int32_t* step_dev,
                                int nslots, const int64_t* seg, int K, const float* grad_scale, uint8_t* const* segmaps,
                                void* stream);
+/* The same update in two passes, so most of its bytes can run beside the step's forward / backward on a
+ * second stream (routed_train.RoutedAdaptStep):
+ *   phase 1 (early, once the now[] marks of the step are set -- acn_hashgrid_pairs_mark after the pair
+ *            scatter): advances the active slots' step counters and updates the mapped tensors' segments touched
+ *            before but not now -- their gradient is zero, so neither the gradient nor the clip coefficient is
+ *            read; maps unchanged;
+ *   phase 2 (late, after the clip coefficient): the mapped segments touched now and every unmapped tensor
+ *            (maps and gradients updated / cleared as in acn_adam_step_slots_segmap); no counter bump.
+ * Each element sees exactly acn_adam_step_slots_segmap's arithmetic (bitwise the same update). */
+int acn_adam_step_slots_segmap_phase(const acn_param_desc* descs, const int32_t* chunk_tensor, int64_t nchunks,
+                                     const int32_t* flags, const void* table, int ngroups, int table_steps,
+                                     int32_t* step_dev, int nslots, const int64_t* seg, int K, const float* grad_scale,
+                                     uint8_t* const* segmaps, int phase, void* stream);
 
 #ifdef __cplusplus
 }

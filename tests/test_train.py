@@ -584,7 +584,8 @@ def test_adam_segment_maps_bitwise_equal_dense_over_10_steps(monkeypatch):
     """VERDICT r02 "Next" 6: the segment-mapped Adam (never-touched 64-B table segments skipped, no gradient
     read where this step added nothing) leaves parameters and both moments BITWISE equal to the dense update
     over 10 routed runtime_adapt steps (train_k8.npz's three batches cycled; deterministic table backward so
-    the two runs see identical gradients), and it does skip: after step 1 only part of the tables is marked."""
+    the runs see identical gradients), in one pass and split into the early (untouched-now segments, before
+    the clip coefficient) and late passes; and it does skip: after step 1 only part of the tables is marked."""
     from test_module_api import build_model, reference_state_dict
     from adaptive_city_nerf_amd import routed_train as RT
     from adaptive_city_nerf_amd.optim import build_optimizer
@@ -595,14 +596,17 @@ def test_adam_segment_maps_bitwise_equal_dense_over_10_steps(monkeypatch):
     torch.use_deterministic_algorithms(True)
     try:
         out, frac = [], None
-        for seg_on in (True, False):
+        # segment-mapped in one pass, segment-mapped split into the early + late passes (ADAM_EARLY), dense
+        for seg_on, early in ((True, False), (True, True), (False, False)):
             monkeypatch.setattr(RT, "ADAM_SEGMAP", seg_on)
+            monkeypatch.setattr(RT, "ADAM_EARLY", early)
             m, _ = build_model("k8")
             m.load_state_dict(reference_state_dict(d, 8, "w:"))
             m = m.cuda().train()
             opt = build_optimizer(Pk, m)
             st = RT.RoutedAdaptStep(Pk, m, 1000, opt, grad_clip=1.0, graph=False, jitter="given")
             assert (st.segmaps is not None) == seg_on and (st.adam.segmaps is not None) == seg_on
+            assert st.early == early
             for i in range(10):
                 r, c, u = batches[i % 3]
                 st(r, c, jitter_u=u)
@@ -614,10 +618,11 @@ def test_adam_segment_maps_bitwise_equal_dense_over_10_steps(monkeypatch):
             out.append({n: (p.detach().clone(), opt.state[p]["exp_avg"].clone(), opt.state[p]["exp_avg_sq"].clone())
                         for n, p in m.named_parameters() if p in opt.state})
         assert 0.0 < frac < 0.5, frac
-        assert out[0].keys() == out[1].keys()
-        for n in out[0]:
-            for a, b in zip(out[0][n], out[1][n]):
-                assert torch.equal(a, b), n
+        for o in out[:2]:
+            assert o.keys() == out[2].keys()
+            for n in o:
+                for a, b in zip(o[n], out[2][n]):
+                    assert torch.equal(a, b), n
     finally:
         torch.use_deterministic_algorithms(False)
 
