@@ -1173,23 +1173,73 @@ __global__ void __launch_bounds__(256) mlp_bwd_dw_kernel(const float* __restrict
 #endif
 }
 
-#if !ACN_DW_F16X3 || ACN_TRAIN_AMP
 // Producer / consumer form of the fused backward (8-wave workgroups, two waves per SIMD).  Waves 0-3
 // (producers) run exactly the per-tile work of dw_round -- forward recompute, the dX chain, ReLU masks --
 // and put each layer's dY / X into the shared stage; waves 4-7 (consumers) hold the weight-gradient
 // accumulators of the same row / column blocks wave w - 4 owned in dw_round and contract the stage.  Per
 // layer: producers put -> barrier -> [producers: dX of the layer | consumers: dW of the layer] -> barrier,
 // so the MFMA-bound contraction overlaps the producers' VALU-bound split / ReLU / dX work instead of
-// following it, and neither role carries the other's registers.  Every wave executes the same 12
-// barriers per round and the same rounds; the sums, their order and every output are those of
+// following it, and neither role carries the other's registers.  Every wave executes the same barriers per
+// round and the same rounds; with the fp32 stage the sums, their order and every output are those of
 // mlp_bwd_dw_kernel bit for bit (same owners, same stage, same k order).
+//   fp16 stages: the AMP build puts fp16 values unscaled (one plane); the fp16x3 stage (ACN_DW_F16X3 in the
+// default build) scales dY and X by workgroup-uniform powers of two: each producer wave publishes its max
+// |dY| / |X| of the NEXT layer right after computing that layer's dY (before the barrier that ends the
+// current layer), into one of two alternating LDS slots -- so the consumers, which read the current layer's
+// exponents after its put barrier, never race the producers' next publish; one extra barrier per round
+// publishes the first layer's maxima.
 __device__ __forceinline__ void pc_sync() { __syncthreads(); }
+constexpr bool kPcScaled = ACN_DW_F16X3 && !ACN_TRAIN_AMP;
 
-__device__ __forceinline__ void pc_producer_round(const float* W, float* st, const float* __restrict__ h0,
-                                                  const float* __restrict__ sh, const float* __restrict__ out,
-                                                  const float* __restrict__ gout, int64_t m, bool ok, int w, int lane,
-                                                  float* __restrict__ gh0) {
+template <int NO, int NI>
+__device__ __forceinline__ void pc_publish(uint32_t* smax, const f32x16 (&dY)[NO], const f32x16 (&X)[NI], int w,
+                                           int lane) {
+#if ACN_DW_F16X3 && !ACN_TRAIN_AMP
+    const uint32_t my = wave_absmax_bits<NO>(dY), mx = wave_absmax_bits<NI>(X);
+    if (lane == 0) {
+        smax[w] = my;
+        smax[4 + w] = mx;
+    }
+#else
+    (void)smax; (void)dY; (void)X; (void)w; (void)lane;
+#endif
+}
+__device__ __forceinline__ StageScale pc_scale(const uint32_t* smax) {
+#if ACN_DW_F16X3 && !ACN_TRAIN_AMP
+    uint32_t ay = 0u, ax = 0u;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        ay = smax[v] > ay ? smax[v] : ay;
+        ax = smax[4 + v] > ax ? smax[4 + v] : ax;
+    }
+    return StageScale{exp_for_bits(ay), exp_for_bits(ax)};
+#else
+    (void)smax;
+    return StageScale{0, 0};
+#endif
+}
+template <int NO, int NI>
+__device__ __forceinline__ void pc_put(float* st, const f32x16 (&dY)[NO], const f32x16 (&X)[NI], const uint32_t* smax,
+                                       int w, int lane) {
+#if ACN_DW_F16X3
+    const StageScale sc = pc_scale(smax);
+    stage_put<NO>(st, 0, dY, sc.kY, w, lane);
+    stage_put<NI>(st, X_ROW, X, sc.kX, w, lane);
+#else
+    (void)smax;
+    stage_put<NO>(st, 0, dY, w, lane);
+    stage_put<NI>(st, X_ROW, X, w, lane);
+#endif
+}
+
+// layer L (1 = colour head ... 6 = sigma trunk 0) uses maxima slot (L - 1) & 1
+__device__ __forceinline__ void pc_producer_round(const float* W, float* st, uint32_t* smax,
+                                                  const float* __restrict__ h0, const float* __restrict__ sh,
+                                                  const float* __restrict__ out, const float* __restrict__ gout,
+                                                  int64_t m, bool ok, int w, int lane, float* __restrict__ gh0) {
     const int h = lane >> 5;
+    uint32_t* s0 = smax;
+    uint32_t* s1 = smax + 8;
     f32x16 A1[2], A2[2], Hd[1], Cin[1], C1[2], C2[2], Rg[1];
     {
         f32x16 X0[1];
@@ -1210,23 +1260,26 @@ __device__ __forceinline__ void pc_producer_round(const float* W, float* st, con
         }
     }
     // colour head
-    stage_put<1>(st, 0, dRg, w, lane);
-    stage_put<2>(st, X_ROW, C2, w, lane);
+    if (kPcScaled) {
+        pc_publish<1, 2>(s0, dRg, C2, w, lane);
+        pc_sync();
+    }
+    pc_put<1, 2>(st, dRg, C2, s0, w, lane);
     pc_sync();
     f32x16 G2[2], G1[2], Gc[1];
     bwd_layer<2, 1, 3, 32>(W + L_WC2, S64, dRg, G2, lane);
     relu_mask<2>(G2, C2);
+    pc_publish<2, 2>(s1, G2, C1, w, lane);
     pc_sync();
     // colour layer 1
-    stage_put<2>(st, 0, G2, w, lane);
-    stage_put<2>(st, X_ROW, C1, w, lane);
+    pc_put<2, 2>(st, G2, C1, s1, w, lane);
     pc_sync();
     bwd_layer<2, 2, 64, 64>(W + L_WC1, S64, G2, G1, lane);
     relu_mask<2>(G1, C1);
+    pc_publish<2, 1>(s0, G1, Cin, w, lane);
     pc_sync();
     // colour layer 0
-    stage_put<2>(st, 0, G1, w, lane);
-    stage_put<1>(st, X_ROW, Cin, w, lane);
+    pc_put<2, 1>(st, G1, Cin, s0, w, lane);
     pc_sync();
     bwd_layer<1, 2, 64, 64>(W + L_WC0, S32, G1, Gc, lane);
 #pragma unroll
@@ -1234,27 +1287,27 @@ __device__ __forceinline__ void pc_producer_round(const float* W, float* st, con
         const int f = rho(r, h);
         dHd[0][r] = f < 15 ? Gc[0][r] : (f == 15 ? dsig : 0.0f);
     }
+    pc_publish<1, 2>(s1, dHd, A2, w, lane);
     pc_sync();
     // heads
-    stage_put<1>(st, 0, dHd, w, lane);
-    stage_put<2>(st, X_ROW, A2, w, lane);
+    pc_put<1, 2>(st, dHd, A2, s1, w, lane);
     pc_sync();
     f32x16 GA2[2], GA1[2], GH[1];
     bwd_layer<2, 1, 16, 32>(W + L_WH, S64, dHd, GA2, lane);
     relu_mask<2>(GA2, A2);
+    pc_publish<2, 2>(s0, GA2, A1, w, lane);
     pc_sync();
     // sigma trunk 1
-    stage_put<2>(st, 0, GA2, w, lane);
-    stage_put<2>(st, X_ROW, A1, w, lane);
+    pc_put<2, 2>(st, GA2, A1, s0, w, lane);
     pc_sync();
     bwd_layer<2, 2, 64, 64>(W + L_W1, S64, GA2, GA1, lane);
     relu_mask<2>(GA1, A1);
-    pc_sync();
-    // sigma trunk 0
     f32x16 X0[1];
     load_tiles<1>(h0, 32, 0, 32, m, ok, h, X0);
-    stage_put<2>(st, 0, GA1, w, lane);
-    stage_put<1>(st, X_ROW, X0, w, lane);
+    pc_publish<2, 1>(s1, GA1, X0, w, lane);
+    pc_sync();
+    // sigma trunk 0
+    pc_put<2, 1>(st, GA1, X0, s1, w, lane);
     pc_sync();
     if (gh0) {
         bwd_layer<1, 2, 64, 64>(W + L_W0, S32, GA1, GH, lane);
@@ -1263,25 +1316,27 @@ __device__ __forceinline__ void pc_producer_round(const float* W, float* st, con
     pc_sync();
 }
 
-__device__ __forceinline__ void pc_consumer_round(const float* st, int w, int lane, DwAcc& a) {
-    const StageScale sc{0, 0};
+__device__ __forceinline__ void pc_consumer_round(const float* st, const uint32_t* smax, int w, int lane, DwAcc& a) {
+    const uint32_t* s0 = smax;
+    const uint32_t* s1 = smax + 8;
+    if (kPcScaled) pc_sync();
     pc_sync();
-    dw_blocks<1>(st, 0, X_ROW + 16 * w, a.aWC2, a.bWC2, sc, lane);
-    pc_sync();
-    pc_sync();
-    dw_blocks<4>(st, 16 * w, X_ROW, a.aWC1, a.bWC1, sc, lane);
-    pc_sync();
-    pc_sync();
-    dw_blocks<2>(st, 16 * w, X_ROW, a.aWC0, a.bWC0, sc, lane);
+    dw_blocks<1>(st, 0, X_ROW + 16 * w, a.aWC2, a.bWC2, pc_scale(s0), lane);
     pc_sync();
     pc_sync();
-    dw_blocks<1>(st, 0, X_ROW + 16 * w, a.aHD, a.bHD, sc, lane);
+    dw_blocks<4>(st, 16 * w, X_ROW, a.aWC1, a.bWC1, pc_scale(s1), lane);
     pc_sync();
     pc_sync();
-    dw_blocks<4>(st, 16 * w, X_ROW, a.aW1, a.bW1, sc, lane);
+    dw_blocks<2>(st, 16 * w, X_ROW, a.aWC0, a.bWC0, pc_scale(s0), lane);
     pc_sync();
     pc_sync();
-    dw_blocks<2>(st, 16 * w, X_ROW, a.aW0, a.bW0, sc, lane);
+    dw_blocks<1>(st, 0, X_ROW + 16 * w, a.aHD, a.bHD, pc_scale(s1), lane);
+    pc_sync();
+    pc_sync();
+    dw_blocks<4>(st, 16 * w, X_ROW, a.aW1, a.bW1, pc_scale(s0), lane);
+    pc_sync();
+    pc_sync();
+    dw_blocks<2>(st, 16 * w, X_ROW, a.aW0, a.bW0, pc_scale(s1), lane);
     pc_sync();
 }
 
@@ -1291,28 +1346,29 @@ __global__ void __launch_bounds__(512) mlp_bwd_dw_pc_kernel(const float* __restr
                                                             float* __restrict__ gh0, float* __restrict__ partial) {
     __shared__ __attribute__((aligned(16))) float Wl[L_FLOATS];
     __shared__ __attribute__((aligned(16))) float st_base[ST_FLOATS];
+    __shared__ uint32_t pc_smax[16];   // two alternating slots of the 4 producers' max |dY|, |X| bits
     stage_weights(img, Wl);
     stage_init(st_base);   // the fp16 stage's ones row (bias sums); nothing for the fp32 stage
     __syncthreads();
     const int lane0 = threadIdx.x & 63, j = lane0 & 31;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), w = wv & 3;
     const int64_t ntiles = (M + 31) / 32;
-    // rounds are uniform over the workgroup (the same 12 barriers per round in both roles)
+    // rounds are uniform over the workgroup (the same 12 -- 13 with the scaled stage -- barriers per round in
+    // both roles)
     if (wv < 4) {
         for (int64_t base = (int64_t)blockIdx.x * 4; base < ntiles; base += (int64_t)gridDim.x * 4) {
             const int64_t m = (base + w) * 32 + j;
-            pc_producer_round(Wl + opaque_s(0), st_base + opaque_s(0), h0, sh, out, gout, m, m < M, w,
+            pc_producer_round(Wl + opaque_s(0), st_base + opaque_s(0), pc_smax, h0, sh, out, gout, m, m < M, w,
                               opaque_v(lane0), gh0);
         }
     } else {
         DwAcc a;
         dw_zero(a);
         for (int64_t base = (int64_t)blockIdx.x * 4; base < ntiles; base += (int64_t)gridDim.x * 4)
-            pc_consumer_round(st_base + opaque_s(0), w, opaque_v(lane0), a);
+            pc_consumer_round(st_base + opaque_s(0), pc_smax, w, opaque_v(lane0), a);
         dw_flush(a, partial + (int64_t)blockIdx.x * NDW, w, lane0);
     }
 }
-#endif
 
 // Pair-list variant (routed container): workgroup b takes the contiguous rounds [b R / G, (b+1) R / G)
 // (R = seg[K] / 128 from the device); when the expert of the next round differs, the running sums go
@@ -1510,7 +1566,7 @@ int bwd_dw_launch(const float* h0, const float* sh, const float* out, const floa
                   float* dw, float* gh0, float* partial, hipStream_t s) {
     const int64_t tiles = (M + 31) / 32, want = (tiles + 3) / 4;
     const int nblk = (int)(want < MAX_DW_BLOCKS ? want : MAX_DW_BLOCKS);
-#if ACN_DW_PC && (!ACN_DW_F16X3 || ACN_TRAIN_AMP)
+#if ACN_DW_PC
     hipLaunchKernelGGL(mlp_bwd_dw_pc_kernel, dim3(nblk), dim3(512), 0, s, img, h0, sh, out, gout, M, gh0, partial);
 #else
     hipLaunchKernelGGL(mlp_bwd_dw_kernel, dim3(nblk), dim3(256), 0, s, img, h0, sh, out, gout, M, gh0, partial);

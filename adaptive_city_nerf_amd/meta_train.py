@@ -524,6 +524,9 @@ class GraphedMetaStep:
                             "query": {"rays": torch.zeros(nq, 8, device=dev), "rgbs": torch.zeros(nq, 3, device=dev)},
                             "wq": torch.zeros((), device=dev)}
         self._load(cid, task)
+        sub = self.model.submodules[cid] if hasattr(self.model, "submodules") else None
+        if sub is not None and hasattr(sub, "_host_box"):
+            sub._host_box()   # host-side box cache filled outside the capture (a region first seen now)
         torch.cuda.synchronize(dev)
         g = torch.cuda.CUDAGraph()
         with graph_capture(g, pool=self.pool):

@@ -59,8 +59,9 @@ FUSED_BACKGROUND = os.environ.get("ACN_FUSED_BG", "1") != "0"
 # gradient for segments not touched this step
 ADAM_SEGMAP = os.environ.get("ACN_ADAM_SEGMAP", "1") != "0"
 # Split segment-mapped Adam: the early pass (segments touched before but not by this step) on a side stream
-# beside the step's forward / backward, the late pass after the clip coefficient
-ADAM_EARLY = os.environ.get("ACN_ADAM_EARLY", "1") != "0"
+# beside the step's forward / backward, the late pass after the clip coefficient (the two passes
+# contend for HBM with the step's own kernels: C5 1.75 -> 2.0 ms, so it stays off)
+ADAM_EARLY = os.environ.get("ACN_ADAM_EARLY", "0") != "0"   # measured slower: off
 
 
 def draw_jitter(n: int, S: int, device) -> torch.Tensor:
