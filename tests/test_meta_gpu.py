@@ -226,7 +226,8 @@ def test_drop_in_train_step_state_dict_current_without_sync(monkeypatch):
                 r = MT.train_step(P, step, m, o, td)
         results.append(r)
     g = ob._acn_meta_graph
-    assert isinstance(g, MT.GraphedMetaStep) and g.replays == 3
+    # call 0 eager, call 1 captures and replays, call 2 captures the new region's graph (_covers) and replays
+    assert isinstance(g, MT.GraphedMetaStep) and g.replays == 4 and g.eager_steps == 0
     sa, sb = oa.state_dict()["state"], ob.state_dict()["state"]
     assert sorted(sa) == sorted(sb)
     for i in sa:

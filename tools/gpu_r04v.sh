@@ -14,4 +14,10 @@ for v in base dwf16x3 base dwf16x3; do
   timeout -k 10 300 python -u bench.py --workload meta --no-cpu-baseline > $O/meta_$v.json 2>$O/meta_$v.err || exit 3
   python -c "import json; a=json.load(open('$O/meta_$v.json')); r=a['roofline']; print('meta $v', a['value'], a['ms_per_step'], r.get('kernel_ms'), r.get('frac'))"
 done
+
+for v in base band1 base band1; do
+  if [ $v = base ]; then unset ACNERF_LIB; else export ACNERF_LIB=$PWD/build_variants/libacnerf_$v.so; fi
+  timeout -k 10 200 python -u bench.py --workload c3 --no-cpu-baseline > $O/c3_$v.json 2>/dev/null || exit 4
+  python -c "import json; a=json.load(open('$O/c3_$v.json')); print('c3 $v', a['value'], a['roofline']['kernel_ms'])"
+done
 exit $rc
