@@ -453,6 +453,10 @@ def main():
                          "expert sort")
     ap.add_argument("--diag-expert-only-order", action="store_true",
                     help="diagnostic (c3): sort the batch by owning expert only (no direction-cell secondary key)")
+    ap.add_argument("--c5-order", choices=["none", "expert-mid"], default="none",
+                    help="diagnostic (c5): visit each batch's rays sorted by (owning expert, Morton code of the ray "
+                         "midpoint) -- the spatial pair order of VERDICT r03 item 7 (the loss is a mean: same update "
+                         "to fp32 order)")
     ap.add_argument("--mlp-precision", choices=["fp16x3", "fp32", "amp"], default="fp16x3",
                     help="c5 / meta: training-MLP arithmetic -- fp16x3 (default, fp32-accurate), fp32 (exact), or "
                          "amp (the reference's use_amp=True: autocast(float16) products + GradScaler)")
@@ -702,6 +706,23 @@ def main():
                                          n_rays_global=bsz if strong else world * bsz, grad_clip=1.0, group=pg,
                                          graph=a.ep_graph, warmup=2,
                                          capacity=None if a.ep_capacity == "full" else "adaptive")
+        if a.c5_order == "expert-mid":
+            def morton_mid(r):
+                near, far = r[:, 6], r[:, 7]
+                mid = r[:, :3] + r[:, 3:6] * torch.where(torch.isfinite(far), 0.5 * (near + far),
+                                                         torch.zeros_like(near)).unsqueeze(1)
+                lo, hi = mid.min(0).values, mid.max(0).values
+                q = ((mid - lo) / (hi - lo).clamp_min(1e-12) * 1023).clamp(0, 1023).long()
+                code = torch.zeros(r.shape[0], dtype=torch.int64, device=r.device)
+                for b in range(10):
+                    for ax in range(3):
+                        code |= ((q[:, ax] >> b) & 1) << (3 * b + ax)
+                return parallel.dominant_expert(r, model).to(torch.int64) * (1 << 30) + code
+            with torch.no_grad():
+                for i in range(nb):
+                    o = torch.argsort(morton_mid(pool[i]))
+                    pool[i] = pool[i][o]
+                    gtp[i] = gtp[i][o]
         loader = [(pool[i], gtp[i]) for i in range(nb)]   # a runtime_adapt data loader's batches (device)
         if world == 1 and a.driver == "step":  # the whole routed step (no host sync), one HIP graph (eager: --no-graph)
             from adaptive_city_nerf_amd.routed_train import RoutedAdaptStep
