@@ -2223,6 +2223,9 @@ __global__ void __launch_bounds__(256) sample_train_kernel(const float* __restri
 // go to the last cell.
 #define ACN_ORDER_MAX 8192
 #define ACN_ORDER_BINS 4096
+#ifndef ACN_ORDER_COUNTING
+#define ACN_ORDER_COUNTING 1  // stable counting sort with per-cell ranks (0: the two stable radix passes always)
+#endif
 __device__ __forceinline__ uint32_t spread6(uint32_t v) {
     v &= 63u;
     v = (v | (v << 4)) & 0x30Fu;
@@ -2399,7 +2402,60 @@ __global__ void __launch_bounds__(1024) ray_order_kernel(const float* __restrict
         }
         cell_of[i] = (uint16_t)c;
     }
-    __syncthreads();  // dir[] is free from here on: it holds the first pass's output
+    __syncthreads();  // dir[] is free from here on
+#if ACN_ORDER_COUNTING
+    // Counting sort by cell, made stable per cell afterwards: histogram (LDS atomics), scan, an unordered
+    // scatter of the indices into their cell's slice, then every element's rank inside its slice = the number
+    // of slice members with a smaller index (cells hold a few rays each: 4096 rays over 4096 cells).  A cell
+    // holding more than kOrderSlice rays (degenerate batches: many identical directions) takes the two
+    // stable radix passes instead, so the rank scan never goes quadratic.
+    {
+        constexpr int kOrderSlice = 64;
+        int* bins = reinterpret_cast<int*>(&dir[2][0]);     // ACN_ORDER_BINS ints: counts, then slice ends
+        int* start = reinterpret_cast<int*>(&dir[1][0]);    // ACN_ORDER_BINS ints: slice starts
+        uint16_t* lst = reinterpret_cast<uint16_t*>(&dir[0][0]);
+        __shared__ int maxc;
+        if (tid == 0) maxc = 0;
+        for (int b = tid; b < ACN_ORDER_BINS; b += 1024) bins[b] = 0;
+        __syncthreads();
+        int mloc = 0;
+        for (int i = tid; i < N; i += 1024) {
+            const int c = atomicAdd(&bins[cell_of[i]], 1) + 1;
+            mloc = c > mloc ? c : mloc;
+        }
+        if (mloc > kOrderSlice) atomicMax(&maxc, mloc);
+        __syncthreads();
+        if (maxc == 0) {
+            constexpr int BPT = ACN_ORDER_BINS / 1024;          // consecutive bins per thread
+            int c[BPT], tot = 0;
+#pragma unroll
+            for (int q = 0; q < BPT; ++q) tot += (c[q] = bins[tid * BPT + q]);
+            const int lane = tid & 63, w = tid >> 6;
+            const int incl = wave_incl_scan(tot);
+            if (lane == 63) wsum[w] = incl;
+            __syncthreads();
+            int base = incl - tot;
+            for (int k = 0; k < w; ++k) base += wsum[k];
+#pragma unroll
+            for (int q = 0; q < BPT; ++q) {
+                start[tid * BPT + q] = base;
+                bins[tid * BPT + q] = base;   // scatter cursor, ends at the slice end
+                base += c[q];
+            }
+            __syncthreads();
+            for (int i = tid; i < N; i += 1024) lst[atomicAdd(&bins[cell_of[i]], 1)] = (uint16_t)i;
+            __syncthreads();
+            for (int i = tid; i < N; i += 1024) {
+                const int cl = cell_of[i], s0 = start[cl], s1 = bins[cl];
+                int r = 0;
+                for (int j = s0; j < s1; ++j) r += (int)lst[j] < i ? 1 : 0;
+                order[s0 + r] = i;
+            }
+            return;
+        }
+        __syncthreads();
+    }
+#endif
     uint16_t* key1 = reinterpret_cast<uint16_t*>(&dir[0][0]);
     uint16_t* idx1 = reinterpret_cast<uint16_t*>(&dir[1][0]);
     radix_pass6<false>(cell_of, nullptr, 0, N, cnt, wsum, key1, idx1, nullptr);

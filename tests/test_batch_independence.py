@@ -90,17 +90,18 @@ def test_routed_render_bitwise_batch_independent(tag, prefix, scale, jitter, tau
                 assert _same(o, r[idx]), f"{tag} {prefix} 16-ray batch at {lo}: {what} differs"
 
 
-@pytest.mark.parametrize("n", [1, 63, 777, 4096, 8192])
-def test_ray_order_stable_and_reproducible(n):
+@pytest.mark.parametrize("n,dup", [(1, 4), (63, 4), (777, 4), (4096, 4), (8192, 4), (4096, 4096), (5000, 40)])
+def test_ray_order_stable_and_reproducible(n, dup):
     """ray_order_kernel (acn_ray_order) sorts a batch by direction cell with a stable sort: the result is
     a permutation, identical on every call, and rays with identical directions (one cell) keep their
-    index order."""
+    index order.  dup = rays per distinct direction on average: 4 (the counting sort's per-cell ranks),
+    4096 (every ray in one cell: the radix-pass fallback) and 40 (cells near the fallback threshold)."""
     from adaptive_city_nerf_amd import _lib, ops
     d = G.load("render_k1")
     base = d["render:rays"]
     rng = np.random.default_rng(n)
     # groups of duplicated rays: each distinct direction appears at several scattered indices
-    src = rng.integers(0, base.shape[0], max(1, n // 4))
+    src = rng.integers(0, base.shape[0], max(1, n // dup))
     rays = base[src[rng.integers(0, src.shape[0], n)]].copy()
     if n > 8:
         rays[5, 3:6] = np.nan      # invalid directions go to the last cell
