@@ -244,9 +244,30 @@ def graph_capture(graph, pool=None):
     gc.collect()
     was = gc.isenabled()
     gc.disable()
+    keep = []
+    _CAPTURE_KEEP.append(keep)
     try:
         with torch.cuda.graph(graph, pool=pool):
             yield
     finally:
+        _CAPTURE_KEEP.pop()
+        # buffers baked into this graph (per-capture workspaces: capture_keepalive) live as long as the graph
+        graph._acn_keepalive = getattr(graph, "_acn_keepalive", []) + keep
         if was:
             gc.enable()
+
+
+_CAPTURE_KEEP = []   # one list per active graph_capture
+
+
+def capture_keepalive(t):
+    """Tie ``t`` to the graph being captured (graph_capture): freed with the graph instead of living forever.
+    Outside graph_capture (a bare torch.cuda.graph) it falls back to a module list."""
+    if _CAPTURE_KEEP:
+        _CAPTURE_KEEP[-1].append(t)
+    else:
+        _UNTRACKED_CAPTURE.append(t)
+    return t
+
+
+_UNTRACKED_CAPTURE = []

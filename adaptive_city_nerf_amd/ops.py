@@ -332,7 +332,6 @@ def mse_linear_fwd(pred: torch.Tensor, gt: torch.Tensor) -> torch.Tensor:
 
 
 _MSE_WS = {}
-_MSE_WS_CAPTURED = []   # workspaces baked into captured graphs (kept alive with them)
 
 
 def _mse_ws(device) -> torch.Tensor:
@@ -342,8 +341,7 @@ def _mse_ws(device) -> torch.Tensor:
     otherwise share one ticket counter, and two of them replayed concurrently would race on it."""
     if torch.cuda.is_current_stream_capturing():
         ws = torch.zeros(int(_lib.lib().acn_mse_linear_workspace_bytes()), dtype=torch.uint8, device=device)
-        _MSE_WS_CAPTURED.append(ws)
-        return ws
+        return _lib.capture_keepalive(ws)   # lives as long as the graph it is baked into
     key = (device, int(torch.cuda.current_stream(device).cuda_stream))
     ws = _MSE_WS.get(key)
     if ws is None:
@@ -476,8 +474,8 @@ def background_bwd(dirs: torch.Tensor, background, g_out: torch.Tensor, grads: S
             raise AcnError("background_bwd: gradient buffers must be contiguous fp32 on the rays' device")
     L = _lib.lib()
     if torch.cuda.is_current_stream_capturing():   # one workspace per captured call (see _mse_ws)
-        ws = torch.empty(int(L.acn_background_bwd_workspace_bytes()), dtype=torch.uint8, device=d.device)
-        _MSE_WS_CAPTURED.append(ws)
+        ws = _lib.capture_keepalive(torch.empty(int(L.acn_background_bwd_workspace_bytes()), dtype=torch.uint8,
+                                                device=d.device))
     else:
         key = (d.device, int(torch.cuda.current_stream(d.device).cuda_stream))
         ws = _BG_WS.get(key)

@@ -132,6 +132,11 @@ def gather_rendered(local: Tensor, plan: ShardPlan, group=None) -> Tensor:
     buf[: local.shape[0]] = local
     if world == 1:
         full = buf
+    elif buf.is_cuda and dist.get_backend(group) == "gloo":
+        # gloo has no device all-gather: stage through the host (tests run two ranks on one GPU this way)
+        parts = [torch.empty(plan.chunk, C, dtype=local.dtype) for _ in range(world)]
+        dist.all_gather(parts, buf.cpu(), group=group)
+        full = torch.cat(parts).to(local.device)
     else:
         full = torch.empty(world * plan.chunk, C, device=local.device, dtype=local.dtype)
         dist.all_gather_into_tensor(full, buf, group=group)
@@ -145,6 +150,8 @@ def psnr_reduce(sse: float, count: float, device, group=None) -> float:
     world, _ = _world_rank(group)
     t = torch.tensor([sse, count], dtype=torch.float64, device=device)
     if world > 1:
+        if t.is_cuda and dist.get_backend(group) == "gloo":
+            t = t.cpu()
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
     mse = max(float(t[0]) / max(float(t[1]), 1.0), 1e-8)
     return -10.0 * math.log10(mse)

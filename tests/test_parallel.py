@@ -188,3 +188,49 @@ def test_sharded_render_image_equals_render_image_on_gpu():
     ref = _midpoint_owner(rays.cpu().numpy(), np.array(G.scene()["masks"][G.MASK["k4"]]["centroids"], np.float32))
     fin = np.isfinite(rays[:, 7].cpu().numpy())
     assert (own[fin] == ref[fin]).mean() > 0.999
+
+
+def _gpu_rank_main(rank, world, port, result_path):
+    """Two ranks on ONE GPU over gloo (host-staged collectives), each rendering its expert-sorted shard with
+    the HIP renderer -- the replicated layout's multi-rank path on the real kernels."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from test_module_api import build_model, reference_state_dict
+        from adaptive_city_nerf_amd import render_rays
+        from adaptive_city_nerf_amd.parallel import dominant_expert, expert_spatial_keys
+        d = G.load("render_k4")
+        m, gbox = build_model("k4")
+        m.load_state_dict(reference_state_dict(d, len(m.submodules), "w:"))
+        m = m.cuda().eval()
+        rays = torch.from_numpy(d["render:rays"]).cuda()
+        plan = expert_sorted_plan(expert_spatial_keys(rays, m).cpu(), world)
+
+        def fn(r):
+            rgb, depth, _, acc = render_rays(m, r, ray_samples=64, bg_color_default="white")
+            return rgb, depth, acc
+        with torch.no_grad():
+            rgb, depth, acc = render_rays_sharded(rays, fn, plan)
+            one = render_rays(m, rays, ray_samples=64, bg_color_default="white")
+        if rank == 0:
+            np.savez(result_path, rgb=rgb.cpu().numpy(), depth=depth.cpu().numpy(), acc=acc.cpu().numpy(),
+                     rgb1=one[0].cpu().numpy(), depth1=one[1].cpu().numpy(), acc1=one[3].cpu().numpy())
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_gloo_sharded_render_on_gpu_matches_reference(tmp_path):
+    """VERDICT r03 "what's weak" 6: the replicated layout's world-2 path on the HIP kernels (not the C
+    oracle): the gathered render equals the single-process render of the whole batch and the reference's
+    render_k4 fixture."""
+    out = tmp_path / "g.npz"
+    mp.spawn(_gpu_rank_main, args=(2, _free_port(), str(out)), nprocs=2, join=True)
+    r = np.load(out)
+    d = G.load("render_k4")
+    for k in ("rgb", "depth", "acc"):
+        np.testing.assert_array_equal(r[k], r[k + "1"])     # rays are independent: sharding changes nothing
+        np.testing.assert_allclose(r[k], d[f"render:{k}"], rtol=0, atol=1e-4 if k == "depth" else 1e-5)
