@@ -16,6 +16,7 @@ with torch.rand_like, ray_rendering.py:286) so a training step can be reproduced
 """
 from __future__ import annotations
 
+import os
 import threading
 import warnings
 from contextlib import contextmanager
@@ -81,6 +82,38 @@ def inner_loop_background_cache():
         yield
     finally:
         _GRAPH_MODE.bg_cache = prev
+
+
+# Training renders (the differentiable single-expert path: meta inner loops and queries, active_module
+# adaptation) visit their rays in direction-cell order (ray_order_kernel, the order render_kernel uses for
+# C2): the hash grid's gathers and scatter then see spatially coherent 32-sample tiles.  Every per-ray value is
+# computed exactly as before and the outputs are returned in the caller's order, so losses are unchanged; only
+# the MLP weight-gradient sums run in another order.  ACN_TRAIN_ORDER=0: the caller's order.
+TRAIN_RAY_ORDER = os.environ.get("ACN_TRAIN_ORDER", "1") != "0"
+_ORDER_MAX = 8192   # ray_order_kernel's single-workgroup limit (ACN_ORDER_MAX)
+
+
+def _train_order(rays: Tensor):
+    """(order, inverse) int64 permutations of ``rays`` by direction cell, through the inner-loop cache when open
+    (the support rays are rendered at every inner step)."""
+    cache = getattr(_GRAPH_MODE, "bg_cache", None)
+    key = ("order", id(rays))
+    if cache is not None:
+        hit = cache.get(key)
+        if hit is not None and hit[0] is rays and hit[1] == rays._version:
+            return hit[2], hit[3]
+    N = rays.shape[0]
+    o32 = torch.empty(N, dtype=torch.int32, device=rays.device)
+    from ._lib import check, lib, ptr
+    r = rays.contiguous()
+    check(lib().acn_ray_order(ptr(r), N, ptr(o32), int(torch.cuda.current_stream(rays.device).cuda_stream)),
+          "acn_ray_order")
+    order = o32.long()
+    inv = torch.empty_like(order)
+    inv[order] = torch.arange(N, device=rays.device)
+    if cache is not None:
+        cache[key] = (rays, rays._version, order, inv)
+    return order, inv
 
 
 def _frozen_background(model, rays, params, rgb_sigma, N, bg_color_default):
@@ -356,6 +389,13 @@ def render_rays_stratified(model, rays: Tensor, ray_samples: int, params=None, a
         if model.training and u is None:
             u = torch.rand_like(rays.new_empty(N, ray_samples))  # the reference's rand_like(low) draw
         mn, ext = sub._host_box()
+        rays_in = rays
+        order = None
+        if TRAIN_RAY_ORDER and 1 < N <= _ORDER_MAX:
+            order, inv = _train_order(rays)
+            rays = rays.index_select(0, order)
+            if u is not None:
+                u = u.to(rays.device).index_select(0, order)
         t_vals, x01, sh = ops.sample_stratified(rays, ray_samples, u if model.training else None, mn, ext,
                                                 ENC_EPS)
         if getattr(_GRAPH_MODE, "frozen_encoding", False):
@@ -365,13 +405,21 @@ def render_rays_stratified(model, rays: Tensor, ray_samples: int, params=None, a
             h0 = sub.xyz_encoder(x01)
         ws = [t.contiguous() for t in sub._mlp_tensors(params).values()]
         rgb_sigma = _FusedMLPFn.apply(h0.contiguous(), sh, *ws).view(N, ray_samples, 4)
+        # the background of the caller's rays (cached per rays tensor), then in the visiting order
         if getattr(_GRAPH_MODE, "frozen_encoding", False):
             with torch.no_grad():  # nor is the shared background head a fast weight: one fused HIP launch
-                bg_rgb = _frozen_background(model, rays, params, rgb_sigma, N, bg_color_default)
+                bg_rgb = _frozen_background(model, rays_in, params, rgb_sigma, N, bg_color_default)
         else:
-            bg_rgb = _get_bg_rgb(model, rays[:, 3:6], params, rgb_sigma, N=N, bg_color_default=bg_color_default)
-        return volume_render(rgb_sigma, t_vals, bg_rgb=bg_rgb, raw_rgb=False, raw_sigma=False,
-                             sigma_scale=sigma_scale)
+            bg_rgb = _get_bg_rgb(model, rays_in[:, 3:6], params, rgb_sigma, N=N, bg_color_default=bg_color_default)
+        last_sample = not getattr(model, "use_bg_nerf", False) and bg_color_default == "last_sample"
+        if order is not None and not last_sample and bg_rgb is not None and torch.is_tensor(bg_rgb) \
+                and bg_rgb.dim() == 2 and bg_rgb.shape[0] == N:
+            bg_rgb = bg_rgb.index_select(0, order)   # (last_sample reads the visiting-order samples already)
+        out = volume_render(rgb_sigma, t_vals, bg_rgb=bg_rgb, raw_rgb=False, raw_sigma=False,
+                            sigma_scale=sigma_scale)
+        if order is None:
+            return out
+        return tuple(None if x is None else x.index_select(0, inv) for x in out)   # the caller's order
     if _routed_train_ok(model, rays, active_module):
         return _render_routed(model, rays, ray_samples, params, kwargs.get("jitter_u"), bg_color_default,
                               sigma_scale)
