@@ -88,8 +88,10 @@ def inner_loop_background_cache():
 # adaptation) visit their rays in direction-cell order (ray_order_kernel, the order render_kernel uses for
 # C2): the hash grid's gathers and scatter then see spatially coherent 32-sample tiles.  Every per-ray value is
 # computed exactly as before and the outputs are returned in the caller's order, so losses are unchanged; only
-# the MLP weight-gradient sums run in another order.  ACN_TRAIN_ORDER=0: the caller's order.
-TRAIN_RAY_ORDER = os.environ.get("ACN_TRAIN_ORDER", "1") != "0"
+# the MLP weight-gradient sums run in another order.  Measured slower on the meta step (66.1 -> 69.2 ms: the
+# order launch and the permutations cost more than the gathers gain at 4000-ray tasks), so it
+# is off by default; ACN_TRAIN_ORDER=1 turns it on.
+TRAIN_RAY_ORDER = os.environ.get("ACN_TRAIN_ORDER", "0") != "0"
 _ORDER_MAX = 8192   # ray_order_kernel's single-workgroup limit (ACN_ORDER_MAX)
 
 
