@@ -1188,6 +1188,14 @@ __global__ void __launch_bounds__(256) mlp_bwd_dw_kernel(const float* __restrict
 // current layer), into one of two alternating LDS slots -- so the consumers, which read the current layer's
 // exponents after its put barrier, never race the producers' next publish; one extra barrier per round
 // publishes the first layer's maxima.
+#ifndef ACN_DIAG_NOPROD
+#define ACN_DIAG_NOPROD 0
+#endif
+#if ACN_DIAG_NOPROD
+#define PC_BWD(...) (void)0
+#else
+#define PC_BWD(...) __VA_ARGS__
+#endif
 __device__ __forceinline__ void pc_sync() { __syncthreads(); }
 constexpr bool kPcScaled = ACN_DW_F16X3 && !ACN_TRAIN_AMP;
 
@@ -1241,10 +1249,15 @@ __device__ __forceinline__ void pc_producer_round(const float* W, float* st, uin
     uint32_t* s0 = smax;
     uint32_t* s1 = smax + 8;
     f32x16 A1[2], A2[2], Hd[1], Cin[1], C1[2], C2[2], Rg[1];
+#if ACN_DIAG_NOPROD  // diagnostic build only: no forward recompute (zero activations): the consumers' time
+    A1[0] = A1[1] = A2[0] = A2[1] = Hd[0] = Cin[0] = C1[0] = C1[1] = C2[0] = C2[1] = Rg[0] = 0.0f;
+    (void)sh;
+#else
     {
         f32x16 X0[1];
         tile_forward(W, h0, sh, m, ok, lane, X0, A1, A2, Hd, Cin, C1, C2, Rg);
     }
+#endif
     f32x16 dRg[1], dHd[1];
     dRg[0] = 0.0f;
     float dsig = 0.0f;
@@ -1267,21 +1280,21 @@ __device__ __forceinline__ void pc_producer_round(const float* W, float* st, uin
     pc_put<1, 2>(st, dRg, C2, s0, w, lane);
     pc_sync();
     f32x16 G2[2], G1[2], Gc[1];
-    bwd_layer<2, 1, 3, 32>(W + L_WC2, S64, dRg, G2, lane);
+    PC_BWD(bwd_layer<2, 1, 3, 32>(W + L_WC2, S64, dRg, G2, lane));
     relu_mask<2>(G2, C2);
     pc_publish<2, 2>(s1, G2, C1, w, lane);
     pc_sync();
     // colour layer 1
     pc_put<2, 2>(st, G2, C1, s1, w, lane);
     pc_sync();
-    bwd_layer<2, 2, 64, 64>(W + L_WC1, S64, G2, G1, lane);
+    PC_BWD(bwd_layer<2, 2, 64, 64>(W + L_WC1, S64, G2, G1, lane));
     relu_mask<2>(G1, C1);
     pc_publish<2, 1>(s0, G1, Cin, w, lane);
     pc_sync();
     // colour layer 0
     pc_put<2, 1>(st, G1, Cin, s0, w, lane);
     pc_sync();
-    bwd_layer<1, 2, 64, 64>(W + L_WC0, S32, G1, Gc, lane);
+    PC_BWD(bwd_layer<1, 2, 64, 64>(W + L_WC0, S32, G1, Gc, lane));
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int f = rho(r, h);
@@ -1293,14 +1306,14 @@ __device__ __forceinline__ void pc_producer_round(const float* W, float* st, uin
     pc_put<1, 2>(st, dHd, A2, s1, w, lane);
     pc_sync();
     f32x16 GA2[2], GA1[2], GH[1];
-    bwd_layer<2, 1, 16, 32>(W + L_WH, S64, dHd, GA2, lane);
+    PC_BWD(bwd_layer<2, 1, 16, 32>(W + L_WH, S64, dHd, GA2, lane));
     relu_mask<2>(GA2, A2);
     pc_publish<2, 2>(s0, GA2, A1, w, lane);
     pc_sync();
     // sigma trunk 1
     pc_put<2, 2>(st, GA2, A1, s0, w, lane);
     pc_sync();
-    bwd_layer<2, 2, 64, 64>(W + L_W1, S64, GA2, GA1, lane);
+    PC_BWD(bwd_layer<2, 2, 64, 64>(W + L_W1, S64, GA2, GA1, lane));
     relu_mask<2>(GA1, A1);
     f32x16 X0[1];
     load_tiles<1>(h0, 32, 0, 32, m, ok, h, X0);
@@ -1310,7 +1323,7 @@ __device__ __forceinline__ void pc_producer_round(const float* W, float* st, uin
     pc_put<2, 1>(st, GA1, X0, s1, w, lane);
     pc_sync();
     if (gh0) {
-        bwd_layer<1, 2, 64, 64>(W + L_W0, S32, GA1, GH, lane);
+        PC_BWD(bwd_layer<1, 2, 64, 64>(W + L_W0, S32, GA1, GH, lane));
         store_tiles<1>(gh0, 32, 0, 32, m, ok, h, GH);
     }
     pc_sync();
