@@ -714,6 +714,12 @@ __device__ __forceinline__ void relu_mask(f32x16 (&G)[NT], const f32x16 (&Y)[NT]
 #error "the AMP build contracts [dW | db] on the fp16 stage"
 #endif
 constexpr int kStagePlanes = ACN_TRAIN_AMP ? 1 : 2;   // fp16 stage: hi (+ lo for the fp16x3 split)
+#ifndef ACN_DW_CSPLIT
+#define ACN_DW_CSPLIT 0   // fp32 stage, fp16x3 split by the consumer waves (producer / consumer kernel only)
+#endif
+#if ACN_DW_CSPLIT && (ACN_DW_F16X3 || !ACN_TRAIN_F16X3)
+#error "ACN_DW_CSPLIT is a variant of the default build's fp32-stage backward"
+#endif
 
 struct StageScale {
     int kY, kX;  // power-of-two exponents the staged dY / X carry (0: unscaled fp32 stage)
@@ -897,18 +903,96 @@ __device__ __forceinline__ void stage_put(float* st, int row0, const f32x16 (&T)
         for (int r = 0; r < 16; ++r) st[(row0 + 32 * t + rho(r, h)) * SW + 32 * w + j] = amp_r(T[t][r]);  // AMP: fp16 X
 }
 
+#if ACN_DW_CSPLIT
+// Consumer-side fp16x3 (ACN_DW_CSPLIT): the producers put fp32 values as before and publish the layer's
+// workgroup max |dY| / |X| (pc_publish); each consumer scales what it reads by those powers of two, splits
+// into hi / lo fp16 and contracts on v_mfma_f32_16x16x16_f16 (hi*hi + hi*lo + lo*hi): one MFMA per product
+// term covers the 16 samples the four fp32 16x16x4 MFMAs did.  The bias sums stay the exact fp32 VALU sums.
+typedef _Float16 f16x4d __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4 mfma16hd(const f16x4d& a, const f16x4d& b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0);
+}
+template <int NT>
+__device__ __forceinline__ uint32_t wave_absmax_bits(const f32x16 (&T)[NT]) {
+    uint32_t m = 0u;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const uint32_t b = __float_as_uint(T[t][r]) & 0x7fffffffu;
+            m = b > m ? b : m;
+        }
+    auto dmax = [](uint32_t v, uint32_t w) { return v > w ? v : w; };
+    m = dmax(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0xB1, 0xF, 0xF, false));
+    m = dmax(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x4E, 0xF, 0xF, false));
+    m = dmax(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x141, 0xF, 0xF, false));
+    m = dmax(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x140, 0xF, 0xF, false));
+    return dmax(dmax((uint32_t)__builtin_amdgcn_readlane((int)m, 0), (uint32_t)__builtin_amdgcn_readlane((int)m, 16)),
+                dmax((uint32_t)__builtin_amdgcn_readlane((int)m, 32), (uint32_t)__builtin_amdgcn_readlane((int)m, 48)));
+}
+__device__ __forceinline__ int exp_for_bits(uint32_t w) {  // as tile_scale_exp
+    if (w == 0u || w >= 0x7f800000u) return 0;
+    const int be = (int)(w >> 23);
+    const int k = 14 - ((be == 0 ? -126 : be - 127) + 1);
+    return k > 100 ? 100 : (k < -100 ? -100 : k);
+}
+__device__ __forceinline__ void split4(const f32x4& x, float sc, f16x4d& hi, f16x4d& lo) {
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const f32x2 v = (f32x2){x[2 * u], x[2 * u + 1]} * (f32x2){sc, sc};
+        const f16x2 h = __builtin_convertvector(v, f16x2);
+        const f16x2 l = __builtin_convertvector(v - __builtin_convertvector(h, f32x2), f16x2);
+        hi[2 * u] = h[0];
+        hi[2 * u + 1] = h[1];
+        lo[2 * u] = l[0];
+        lo[2 * u + 1] = l[1];
+    }
+}
+#endif
+
 // acc[n] += dY[16 rows from arow] . X[16 features from xrow + 16 n]^T over the 128 staged samples;
 // lane (i = l & 15, q = l >> 4) supplies k = sample 32 q + kk (4 k-steps per 16-B read).  bsum += this
 // lane's share of the bias row sum (the A operand is dY itself).
 template <int NCB>
 __device__ __forceinline__ void dw_blocks(const float* st, int arow, int xrow, f32x4 (&acc)[NCB], float& bsum,
-                                          StageScale, int lane) {
+                                          StageScale sc, int lane) {
 #if ACN_DIAG_NODW  // diagnostic build only: no weight-gradient contraction
     return;
 #endif
     const int i = lane & 15, q = lane >> 4;
     const float* pa = st + (arow + i) * SW + 32 * q;
     const float* pb = st + (xrow + i) * SW + 32 * q;
+#if ACN_DW_CSPLIT
+    const float sa = ldexpf(1.0f, sc.kY), sb = ldexpf(1.0f, sc.kX), uab = ldexpf(1.0f, -(sc.kY + sc.kX));
+    f32x4 tmp[NCB];
+#pragma unroll
+    for (int n = 0; n < NCB; ++n) tmp[n] = 0.0f;
+#pragma unroll
+    for (int k4 = 0; k4 < 8; ++k4) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(pa + 4 * k4);
+        bsum += (a[0] + a[1]) + (a[2] + a[3]);
+        f16x4d ah, al;
+        split4(a, sa, ah, al);
+#pragma unroll
+        for (int n = 0; n < NCB; ++n) {
+            const f32x4 b = *reinterpret_cast<const f32x4*>(pb + 16 * n * SW + 4 * k4);
+            f16x4d bh, bl;
+            split4(b, sb, bh, bl);
+            tmp[n] = mfma16hd(al, bh, tmp[n]);
+            tmp[n] = mfma16hd(ah, bl, tmp[n]);
+            tmp[n] = mfma16hd(ah, bh, tmp[n]);
+        }
+    }
+#pragma unroll
+    for (int n = 0; n < NCB; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[n][r] = __builtin_fmaf(tmp[n][r], uab, acc[n][r]);
+    return;
+#else
+    (void)sc;
+#endif
 #pragma unroll
     for (int k4 = 0; k4 < 8; ++k4) {
         const f32x4 a = *reinterpret_cast<const f32x4*>(pa + 4 * k4);
@@ -928,10 +1012,29 @@ __device__ __forceinline__ void dw_blocks(const float* st, int arow, int xrow, f
 template <int NO, int NI>
 __device__ __forceinline__ StageScale stage_layer(float* st, const f32x16 (&dY)[NO], const f32x16 (&X)[NI], int w,
                                                   int lane) {
+#if ACN_DW_CSPLIT   // the workgroup's max |dY| / |X| travel with the stage (the consumer-side split's scales)
+    __shared__ uint32_t smax_c[8];
+    const uint32_t my = wave_absmax_bits<NO>(dY), mx = wave_absmax_bits<NI>(X);
+    if (lane == 0) {
+        smax_c[w] = my;
+        smax_c[4 + w] = mx;
+    }
+#endif
     __syncthreads();
+#if ACN_DW_CSPLIT   // read between the barriers: no wave can overwrite them (next layer) before all have read
+    uint32_t ay = 0u, ax = 0u;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        ay = smax_c[v] > ay ? smax_c[v] : ay;
+        ax = smax_c[4 + v] > ax ? smax_c[4 + v] : ax;
+    }
+#endif
     stage_put<NO>(st, 0, dY, w, lane);
     stage_put<NI>(st, X_ROW, X, w, lane);
     __syncthreads();
+#if ACN_DW_CSPLIT
+    return StageScale{exp_for_bits(ay), exp_for_bits(ax)};
+#endif
     return StageScale{0, 0};
 }
 #endif
@@ -1197,12 +1300,12 @@ __global__ void __launch_bounds__(256) mlp_bwd_dw_kernel(const float* __restrict
 #define PC_BWD(...) __VA_ARGS__
 #endif
 __device__ __forceinline__ void pc_sync() { __syncthreads(); }
-constexpr bool kPcScaled = ACN_DW_F16X3 && !ACN_TRAIN_AMP;
+constexpr bool kPcScaled = (ACN_DW_F16X3 && !ACN_TRAIN_AMP) || ACN_DW_CSPLIT;
 
 template <int NO, int NI>
 __device__ __forceinline__ void pc_publish(uint32_t* smax, const f32x16 (&dY)[NO], const f32x16 (&X)[NI], int w,
                                            int lane) {
-#if ACN_DW_F16X3 && !ACN_TRAIN_AMP
+#if (ACN_DW_F16X3 && !ACN_TRAIN_AMP) || ACN_DW_CSPLIT
     const uint32_t my = wave_absmax_bits<NO>(dY), mx = wave_absmax_bits<NI>(X);
     if (lane == 0) {
         smax[w] = my;
@@ -1213,7 +1316,7 @@ __device__ __forceinline__ void pc_publish(uint32_t* smax, const f32x16 (&dY)[NO
 #endif
 }
 __device__ __forceinline__ StageScale pc_scale(const uint32_t* smax) {
-#if ACN_DW_F16X3 && !ACN_TRAIN_AMP
+#if (ACN_DW_F16X3 && !ACN_TRAIN_AMP) || ACN_DW_CSPLIT
     uint32_t ay = 0u, ax = 0u;
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
