@@ -358,7 +358,8 @@ def render_traffic_profile(workload: str, S: int, layout: str):
     'HBM', plus WRITE_SIZE), or None when no profile of this exact configuration is committed."""
     name = {("c2", 256, "replicated"): "r04_pmc_c2_render.json",
             ("c3", 256, "replicated"): "r04_pmc_c3_slots.json",
-            ("c4", 96, "replicated"): "r04_pmc_c4s96_slots.json"}.get((workload, S, layout))
+            ("c4", 96, "replicated"): "r04_pmc_c4s96_slots.json",
+            ("c4", 256, "replicated"): "r04_pmc_c4_slots.json"}.get((workload, S, layout))
     if name is None:
         return None
     p = REPO / "profiles" / name
