@@ -387,6 +387,9 @@ __device__ __forceinline__ void adam_chunk_zero(float* p, float* g, float* m, fl
 // s = vector / 4; the 4 vectors of a segment are 4 consecutive lanes of one wave-instruction (the map
 // loads precede the map stores for all of them); the first lane updates the maps.  chunk base is a
 // multiple of ACN_OPTIM_CHUNK floats (segment aligned).
+#ifndef ACN_ADAM_MAP_PIPE
+#define ACN_ADAM_MAP_PIPE 0  // adam_chunk_seg: next iteration's map bytes loaded ahead of this iteration's data
+#endif
 __device__ __forceinline__ bool seg_live(uint8_t nw, uint8_t ev, int phase) {
     return phase == 0 ? (nw | ev) != 0 : (phase == 1 ? (ev != 0 && nw == 0) : nw != 0);
 }
@@ -406,14 +409,46 @@ __device__ __forceinline__ void adam_chunk_seg(float* p, float* g, float* m, flo
     int64_t i = threadIdx.x;
     // kUnroll vectors per thread per iteration: every map byte first, then all their p / m / v / g loads in
     // flight together (the one-vector loop waited on the map load before each data load: 4.7 TB/s)
+#if ACN_ADAM_MAP_PIPE
+    // the map bytes of the NEXT iteration are loaded before this iteration's data loads: the compiler may not
+    // move them above this iteration's map stores itself (uint8_t stores alias anything), so without this
+    // every iteration waited for two dependent memory round trips (map, then data) instead of one.  The
+    // prefetched bytes belong to other segments than the ones this iteration clears, so values are unchanged.
+    uint8_t nx_nw[kUnroll], nx_ev[kUnroll];
+    if (i + (kUnroll - 1) * kThreads < n4) {
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const int64_t sgi = (i + u * kThreads) >> 2;
+            nx_nw[u] = now[sgi];
+            nx_ev[u] = ever[sgi];
+        }
+    }
+#endif
     for (; i + (kUnroll - 1) * kThreads < n4; i += kUnroll * kThreads) {
         uint8_t nw[kUnroll], ev[kUnroll];
+#if ACN_ADAM_MAP_PIPE
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            nw[u] = nx_nw[u];
+            ev[u] = nx_ev[u];
+        }
+        const int64_t inx = i + kUnroll * kThreads;
+        if (inx + (kUnroll - 1) * kThreads < n4) {
+#pragma unroll
+            for (int u = 0; u < kUnroll; ++u) {
+                const int64_t sgi = (inx + u * kThreads) >> 2;
+                nx_nw[u] = now[sgi];
+                nx_ev[u] = ever[sgi];
+            }
+        }
+#else
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
             const int64_t sgi = (i + u * kThreads) >> 2;
             nw[u] = now[sgi];
             ev[u] = ever[sgi];
         }
+#endif
         f4 pp[kUnroll], mm[kUnroll], vv[kUnroll], gg[kUnroll];
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
@@ -554,7 +589,12 @@ __device__ __forceinline__ void adam_chunk_seg_lds(float* p, float* g, float* m,
     }
 }
 
-__global__ void __launch_bounds__(kThreads) adam_slots_kernel(const acn_param_desc* __restrict__ descs,
+#ifdef ACN_ADAM_WPE   // occupancy experiment: waves per SIMD for adam_slots_kernel (compiler default 3 at 166 VGPRs)
+#define ACN_ADAM_SLOTS_ATTR __attribute__((amdgpu_waves_per_eu(ACN_ADAM_WPE, ACN_ADAM_WPE)))
+#else
+#define ACN_ADAM_SLOTS_ATTR
+#endif
+__global__ void __launch_bounds__(kThreads) ACN_ADAM_SLOTS_ATTR adam_slots_kernel(const acn_param_desc* __restrict__ descs,
                                                               const int32_t* __restrict__ chunk_tensor,
                                                               const int32_t* __restrict__ flags,
                                                               const GroupK* __restrict__ table, int ngroups,

@@ -403,6 +403,15 @@ class RoutedAdaptStep:
         ever = int(self.segmaps[:, 1].sum())
         return ever, int(self.segmaps[:, 1].numel())
 
+    def segment_line_stats(self):
+        """128-B lines (two adjacent 64-B segments) of the tables holding at least one ever-updated segment:
+        what the segment-mapped Adam's reads fetch if HBM lines are filled whole.  Host read."""
+        if self.segmaps is None:
+            return None
+        ev = self.segmaps[:, 1]
+        pairs = ev[:, : ev.shape[1] // 2 * 2].reshape(ev.shape[0], -1, 2)
+        return int((pairs.amax(dim=2) != 0).sum())
+
     def sync_state(self) -> None:
         """Host state['step'] of every parameter from the per-slot device counters (state_dict, or before
         an eager FusedAdam step on the same optimizer)."""

@@ -951,7 +951,9 @@ def main():
             nseg = ntab // 16
             now = hash_segments
             adam_bytes = 28 * (nparam - ntab) + 384 * ever + 128 * now + 2 * nseg
+            ever_lines = routed.segment_line_stats()
             segmap = {"table_segments_hit_experts": nseg, "ever_touched_segments": ever,
+                      "ever_touched_128B_lines": ever_lines,
                       "ever_touched_fraction": round(ever / max(total, 1), 4),
                       "segments_touched_this_step": now, "adam_bytes_dense": adam_bytes_dense,
                       "adam_bytes_segmap": adam_bytes,
@@ -1062,6 +1064,20 @@ def main():
             if segmap is not None:
                 roofline["bytes_per_param"] = "28 dense (MLP, head); table segments per segmap"
                 roofline["segmap"] = segmap
+                try:   # round-4 counters of the segment-mapped pass on this workload (tools/gpu_r04ai.sh)
+                    ad4 = json.loads((REPO / "profiles" / "r04_pmc_c5_adam.json").read_text())
+                except Exception:
+                    ad4 = None
+                if ad4 is not None and routed is not None and world == 1:
+                    roofline["traffic"] = ad4["traffic_bytes"]
+                    roofline["traffic_detail"] = {
+                        "source": "profiles/r04_pmc_c5_adam.json", "read_bytes": ad4["read_bytes"],
+                        "write_bytes": ad4["write_bytes"], "traffic_over_algorithmic_at_profile":
+                            ad4["traffic_over_algorithmic"], "correction": ad4["correction"]}
+                    pmc = dict(pmc)
+                    pmc["hashgrid_bwd_pairs"] = {"atomic_requests_per_launch":
+                                                 ad4["hashgrid_bwd_pairs"]["atomic_requests_per_launch"],
+                                                 "_src": "profiles/r04_pmc_c5_adam.json (TCC_EA0_ATOMIC_sum)"}
             hb = pmc.get("hashgrid_bwd_pairs", {})
             roofline["secondary"] = {
                 "kernel": "hashgrid_bwd_pairs (table-gradient scatter-add, returning float atomics that also telescope the tables share of the clip norm)",
@@ -1070,7 +1086,8 @@ def main():
                          "atomics'; 64 rows per instruction at 0.08 TB/s is the same request rate)",
                 "peak_requests_per_s": ATOMIC_REQ_PEAK,
                 "atomic_requests_per_launch": hb.get("atomic_requests_per_launch"),
-                "requests_source": "profiles/pmc_c5_r02.json (TCC_EA0_ATOMIC_sum, same workload)"}
+                "requests_source": pmc.get("hashgrid_bwd_pairs", {}).get("_src",
+                                           "profiles/pmc_c5_r02.json (TCC_EA0_ATOMIC_sum, same workload)")}
             if routed is not None:
                 sec = roofline["secondary"]
                 sec["kernel_ms"] = round(hash_bwd_ms, 4)
