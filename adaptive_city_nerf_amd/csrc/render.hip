@@ -941,6 +941,9 @@ __device__ __forceinline__ void render_ray(const RenderParams& p, const BgArgs& 
 #if ACN_DIAG_CLOCK  // diagnostic build only: depth[ray] <- in-kernel shader clock (MHz) over the ray
     const uint64_t diag_t0 = __builtin_amdgcn_s_memtime(), diag_r0 = __builtin_amdgcn_s_memrealtime();
 #endif
+#if ACN_DIAG_WAVETIME  // diagnostic build only: rgb[ray] <- bit patterns of (start, end) 100-MHz stamps, HW ids
+    const uint32_t diag_w0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#endif
     const float* rp = p.rays + ray * 8;
     const float ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
     const float near = rp[6], far = rp[7];
@@ -1020,6 +1023,12 @@ __device__ __forceinline__ void render_ray(const RenderParams& p, const BgArgs& 
         p.depth[ray] = (float)(__builtin_amdgcn_s_memtime() - diag_t0) * 100.0f /
                        (float)(__builtin_amdgcn_s_memrealtime() - diag_r0);
 #endif
+#if ACN_DIAG_WAVETIME
+        p.rgb[ray * 3 + 0] = __int_as_float((int)diag_w0);
+        p.rgb[ray * 3 + 1] = __int_as_float((int)(uint32_t)__builtin_amdgcn_s_memrealtime());
+        p.rgb[ray * 3 + 2] = __int_as_float((int)((__builtin_amdgcn_s_getreg((31 << 11) | 4) & 0xffffu) |
+                                                   (__builtin_amdgcn_s_getreg((31 << 11) | 20) << 16)));
+#endif
 #if ACN_DIAG_PHASE  // cycles per tile: depth <- hash phase, acc <- MLP phase, rgb.r <- compositing
         p.depth[ray] = (float)dg_hash / (float)dg_n;
         p.acc[ray] = (float)dg_mlp / (float)dg_n;
@@ -1067,6 +1076,156 @@ __global__ void __launch_bounds__(1024, 4) render_kernel(FieldCfg cfg, BgArgs bg
                        float& yb, float& ys) {
                        container_tile<INTERP, ROUTE, FOLD>(cfg, W, px, py, pz, shv, cb, &folded, lane, yr, yg, yb, ys);
                    });
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Single-expert render with the workgroup's field tiles shared (render_ws_kernel, the C2 path when there is no
+// early termination).  render_kernel gives every wave one ray, and all 4096 waves of a C2 batch are resident
+// at once, so a CU runs until its slowest ray ends: the per-wave timeline (tools/micro/wave_times.py) shows rays
+// of 190-295 us in a 297 us launch, 12 of 16 waves resident on average.  Here the 16 rays of a round are
+// split into their 32-sample tiles (the field's MFMA unit), and the waves take tiles from an LDS counter
+// (tile-major, so wave w starts on ray w's first tile, as before).  A tile's field values (rgb, sigma per
+// sample) go to LDS; the wave whose tile completes a ray composites that ray from LDS with render_ray's exact
+// sequence (t, dist, conditioning, composite_tile in tile order, background, reductions), so every output is
+// bit-identical to render_kernel.  Early ray termination needs the tiles in order: tau > 0 keeps render_kernel.
+#ifndef ACN_RENDER_WS
+#define ACN_RENDER_WS 1
+#endif
+constexpr int kWsMaxS = 256;   // LDS field buffer: 16 rays x kWsMaxS samples x 16 B = 64 KB
+
+template <int INTERP>
+__global__ void __launch_bounds__(1024, 4) render_ws_kernel(FieldCfg cfg, BgArgs bg, RenderParams p) {
+    constexpr bool FOLD = ACN_SHFOLD != 0;
+    __shared__ __attribute__((aligned(16))) float smem[PK_FLOATS];
+    __shared__ __attribute__((aligned(16))) float cbuf[FOLD ? 16 * 64 : 4];
+    __shared__ __attribute__((aligned(16))) f32x4 ybuf[16 * kWsMaxS];
+    __shared__ int qhead;
+    __shared__ int done[16];
+    stage_weights<1>(smem, p.packed);
+    const float* W = smem;
+    const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float* cb = FOLD ? cbuf + wave * 64 : nullptr;
+    const int S = p.S;
+    const int T = (S + 31) >> 5;
+    const float step = 1.0f / (float)(S - 1);
+    // the rays of a round: 16 consecutive positions, XCD bands as in render_kernel
+    int64_t base, hi, stride;
+    if ((gridDim.x & 7) == 0) {
+        const int64_t chunk = (p.N + 7) >> 3;
+        const int64_t lo = min(p.N, (int64_t)(blockIdx.x & 7) * chunk);
+        hi = min(p.N, lo + chunk);
+        base = lo + (int64_t)(blockIdx.x >> 3) * 16;
+        stride = (int64_t)(gridDim.x >> 3) * 16;
+    } else {
+        hi = p.N;
+        base = (int64_t)blockIdx.x * 16;
+        stride = (int64_t)gridDim.x * 16;
+    }
+    for (; base < hi; base += stride) {   // block-uniform
+        const int nr = (int)min((int64_t)16, hi - base);
+        if (threadIdx.x == 0) qhead = 0;
+        if (threadIdx.x < 16) done[threadIdx.x] = 0;
+        __syncthreads();
+        int64_t cur = -1;
+        uint32_t folded = 0u;
+        float shv[8];
+        float ox = 0.0f, oy = 0.0f, oz = 0.0f, dx = 0.0f, dy = 0.0f, dz = 0.0f, near = 0.0f, far = 0.0f;
+        const float* jit = nullptr;
+        for (;;) {
+            int item = 0;
+            if (lane == 0) item = __hip_atomic_fetch_add(&qhead, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            item = __builtin_amdgcn_readlane(item, 0);
+            if (item >= nr * T) break;
+            const int tile = item / nr, slot = item - tile * nr;
+            const int64_t ray = p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[base + slot]) : base + slot;
+            if (ray != cur) {
+                const float* rp = p.rays + ray * 8;
+                ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
+                near = rp[6], far = rp[7];
+                jit = p.jitter ? p.jitter + ray * S : nullptr;
+                float sh[16];
+                dir_sh(dx, dy, dz, sh);
+                sh_rows_for_half(sh, h, shv);
+                folded = 0u;
+                cur = ray;
+            }
+            const int s = tile * 32 + j;
+            const int sc = s < S ? s : S - 1;
+            float t;
+            if (!jit) {
+                const int i0 = sc < S - 1 ? sc : S - 2;
+                const float ta = tlin_sel(near, far, i0, S, step), tb = tlin_sel(near, far, i0 + 1, S, step);
+                t = sc < S - 1 ? ta : tb;
+            } else {
+                t = tval(near, far, sc, S, jit);
+            }
+            const float px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;
+            float yr, yg, yb, ys;
+            container_tile<INTERP, 0, FOLD>(cfg, W, px, py, pz, shv, cb, &folded, lane, yr, yg, yb, ys);
+            if (h == 0 && s < S) {
+                f32x4 v;
+                v[0] = yr, v[1] = yg, v[2] = yb, v[3] = ys;
+                ybuf[slot * kWsMaxS + s] = v;
+            }
+            // the wave's LDS writes are ordered before its count (workgroup-scope release / acquire)
+            int old = 0;
+            if (lane == 0) old = __hip_atomic_fetch_add(&done[slot], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+            old = __builtin_amdgcn_readlane(old, 0);
+            if (old != T - 1) continue;
+            // this tile completed the ray: composite it (render_ray's sequence, no early termination)
+            const float* rq = p.rays + ray * 8;
+            const float cox = rq[0], coy = rq[1], coz = rq[2], cdx = rq[3], cdy = rq[4], cdz = rq[5];
+            const float cnear = rq[6], cfar = rq[7];
+            (void)cox, (void)coy, (void)coz;
+            const float* cjit = p.jitter ? p.jitter + ray * S : nullptr;
+            RayAcc acc{1.0, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+            for (int s0 = 0; s0 < S; s0 += 32) {
+                const int cs = s0 + j;
+                const bool valid = cs < S;
+                const int csc = valid ? cs : S - 1;
+                float ct, dist;
+                if (!cjit) {
+                    const int i0 = csc < S - 1 ? csc : S - 2;
+                    const float ta = tlin_sel(cnear, cfar, i0, S, step), tb = tlin_sel(cnear, cfar, i0 + 1, S, step);
+                    ct = csc < S - 1 ? ta : tb;
+                    dist = tb - ta;
+                } else {
+                    ct = tval(cnear, cfar, csc, S, cjit);
+                    const float tn = (csc < S - 1) ? tval(cnear, cfar, csc + 1, S, cjit) : ct;
+                    const float tp = (csc == S - 1 && S > 1) ? tval(cnear, cfar, csc - 1, S, cjit) : ct;
+                    dist = (csc < S - 1) ? (tn - ct) : (ct - tp);
+                }
+                const f32x4 y = ybuf[slot * kWsMaxS + csc];
+                const float cr = clamp_nan(y[0], 0.0f, 1.0f);
+                const float cg = clamp_nan(y[1], 0.0f, 1.0f);
+                const float cbl = clamp_nan(y[2], 0.0f, 1.0f);
+                float sig = clamp_min_nan(y[3], 0.0f);
+                if (p.sigma_scale != 1.0f) sig = sig * p.sigma_scale;
+                float wv;
+                composite_tile(acc, valid, cr, cg, cbl, sig, ct, dist, j, &wv);
+                if (p.weights && valid && h == 0) p.weights[ray * S + cs] = wv;
+            }
+            float bgc[3];
+            background(bg, cdx, cdy, cdz, lane, bgc);
+            float r, g, b, dd, a;
+            finish_ray(acc, r, g, b, dd, a);
+            if (lane == 0) {
+                if (bg.mode != ACN_BG_NONE) {
+                    const float om = 1.0f - a;
+                    r = r + om * bgc[0];
+                    g = g + om * bgc[1];
+                    b = b + om * bgc[2];
+                }
+                p.rgb[ray * 3 + 0] = r;
+                p.rgb[ray * 3 + 1] = g;
+                p.rgb[ray * 3 + 2] = b;
+                p.depth[ray] = dd;
+                p.acc[ray] = a;
+            }
+        }
+        __syncthreads();   // ybuf / qhead / done reused by the next round
     }
 }
 
@@ -2609,6 +2768,13 @@ extern "C" int acn_render_stratified_fwd_ordered(const float* rays, int64_t N, i
         if (ACN_SLOTS && KL == 0 && R != 0) hipLaunchKernelGGL((render_slots_kernel<I, (R == 0 ? 1 : R)>), grid, dim3(ACN_SLOTS_THREADS), 0, s, cfg, b, p); \
         else hipLaunchKernelGGL((render_kernel<I, KL, R>), grid, block, 0, s, cfg, b, p);            \
     } while (0)
+    if (ACN_RENDER_WS && cfg.routing == 0 && S <= kWsMaxS && !(tau > 0.0f)) {
+        // one expert, no early termination: the workgroup shares its rays' field tiles (bit-identical outputs)
+        if (interp == 1) hipLaunchKernelGGL(render_ws_kernel<1>, grid, block, 0, s, cfg, b, p);
+        else if (interp == 0) hipLaunchKernelGGL(render_ws_kernel<0>, grid, block, 0, s, cfg, b, p);
+        else hipLaunchKernelGGL(render_ws_kernel<2>, grid, block, 0, s, cfg, b, p);
+        return acn_check_launch("acn_render_stratified_fwd");
+    }
     ACN_DISPATCH(ACN_RENDER_LAUNCH);
 #undef ACN_RENDER_LAUNCH
     return acn_check_launch("acn_render_stratified_fwd");

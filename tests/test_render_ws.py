@@ -1,0 +1,69 @@
+"""render_ws_kernel (one expert, no early termination: the workgroup's rays share their field tiles) against
+render_kernel on the same rays -- bit-identical outputs ('Work-shared tiles').
+
+Both kernels render each ray with the same arithmetic (reference nerfs/ray_rendering.py:290-345); the work-shared
+kernel only changes which wave evaluates a 32-sample tile and then composites the ray from LDS in tile order.
+A positive tau selects render_kernel (early termination needs the tiles in order).  tau = 1e-45 (the smallest
+float denormal) stops a ray only once its transmittance is below every float weight, so rgb, depth and acc are
+unchanged by it; weights of samples past such a stop are 0 there and at most a denormal here."""
+import numpy as np
+import pytest
+import torch
+
+import goldens as G
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+TAU_OLD = 1e-45       # > 0: render_kernel, never changes a float output
+
+
+def _t(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def _setup(tag, prefix="w:"):
+    from adaptive_city_nerf_amd import ops
+    d = G.load(f"render_{tag}")
+    sc = G.scene()["masks"][G.MASK[tag]]
+    K = len(sc["centroids"])
+    res = O.level_resolutions(16, 16, 4096)
+    specs = []
+    for k in range(K):
+        w = G.expert_weights(d, k, prefix)
+        tab = _t(G.table(int(d["table_seeds"][k]), float(d["table_scale"])))
+        mlp = {key: _t(v) for key, v in w.items() if key in ops.MLP_SHAPES}
+        specs.append(ops.ExpertSpec(tab, res.tolist(), 20, 1, sc["mins"][k],
+                                    d[f"w:submodules.{k}.aabb_extent"].tolist(), mlp))
+    routing = ops.make_routing(torch.tensor(sc["centroids"]), K, True, float(d["bm"]))
+    bgw = {k[len("bg_mlp."):]: _t(v) for k, v in G.bg_weights(d, prefix).items()}
+    bg, keep = ops.make_background("mlp", mlp=bgw)
+    return d, specs, routing, (bg, keep)
+
+
+def _same(a, b):
+    return np.array_equal(a.cpu().numpy(), b.cpu().numpy(), equal_nan=True)
+
+
+@pytest.mark.parametrize("tag,active", [("k1", None), ("k4", 2)])
+@pytest.mark.parametrize("S", [64, 200, 256, 300])
+@pytest.mark.parametrize("jitter", [False, True])
+@pytest.mark.parametrize("n", [1, 17, 4096])
+def test_work_shared_render_bitwise_equal_render_kernel(tag, active, S, jitter, n):
+    from adaptive_city_nerf_amd import ops
+    d, specs, routing, bg = _setup(tag)
+    base = _t(d["render:rays"])
+    g = torch.Generator(device=DEV).manual_seed(5 + n)
+    idx = torch.randint(0, base.shape[0], (n,), device=DEV, generator=g)
+    rays = base[idx].contiguous()
+    jit = torch.rand(n, S, device=DEV, generator=g) if jitter else None
+    with torch.no_grad():
+        new = ops.render_stratified(rays, S, specs, routing, active, bg[0], tau=0.0, jitter=jit)
+        old = ops.render_stratified(rays, S, specs, routing, active, bg[0], tau=TAU_OLD, jitter=jit)
+    for o, r, what in zip(new[::3] + new[1:2], old[::3] + old[1:2], ("rgb", "acc", "depth")):
+        assert _same(o, r), f"{tag} S={S} n={n} jitter={jitter}: {what} differs from render_kernel"
+    wn, wo = new[2].cpu().numpy(), old[2].cpu().numpy()
+    diff = wn != wo
+    assert not np.any(diff & ~((np.abs(wo) < 1e-38) & (np.abs(wn) < 1e-38))), \
+        f"{tag} S={S} n={n}: weights differ from render_kernel"
