@@ -1094,6 +1094,63 @@ __global__ void __launch_bounds__(1024, 4) render_kernel(FieldCfg cfg, BgArgs bg
 #endif
 constexpr int kWsMaxS = 256;   // LDS field buffer: 16 rays x kWsMaxS samples x 16 B = 64 KB
 
+// composite one ray from its samples' field values in LDS (ys[s] = rgb, sigma of sample s, as the field tile
+// returned them): render_ray's exact sequence without early termination -- t and dist, the volume_render
+// conditioning, composite_tile in tile order, weights, background, the double reductions, the outputs
+__device__ __forceinline__ void composite_ray_lds(const RenderParams& p, const BgArgs& bg, int64_t ray,
+                                                  const f32x4* __restrict__ ys, int lane, float step) {
+    const int j = lane & 31, h = lane >> 5;
+    const int S = p.S;
+    const float* rq = p.rays + ray * 8;
+    const float dx = rq[3], dy = rq[4], dz = rq[5];
+    const float near = rq[6], far = rq[7];
+    const float* jit = p.jitter ? p.jitter + ray * S : nullptr;
+    RayAcc acc{1.0, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    for (int s0 = 0; s0 < S; s0 += 32) {
+        const int s = s0 + j;
+        const bool valid = s < S;
+        const int sc = valid ? s : S - 1;
+        float t, dist;
+        if (!jit) {
+            const int i0 = sc < S - 1 ? sc : S - 2;
+            const float ta = tlin_sel(near, far, i0, S, step), tb = tlin_sel(near, far, i0 + 1, S, step);
+            t = sc < S - 1 ? ta : tb;
+            dist = tb - ta;
+        } else {
+            t = tval(near, far, sc, S, jit);
+            const float tn = (sc < S - 1) ? tval(near, far, sc + 1, S, jit) : t;
+            const float tp = (sc == S - 1 && S > 1) ? tval(near, far, sc - 1, S, jit) : t;
+            dist = (sc < S - 1) ? (tn - t) : (t - tp);
+        }
+        const f32x4 y = ys[sc];
+        const float cr = clamp_nan(y[0], 0.0f, 1.0f);
+        const float cg = clamp_nan(y[1], 0.0f, 1.0f);
+        const float cbl = clamp_nan(y[2], 0.0f, 1.0f);
+        float sig = clamp_min_nan(y[3], 0.0f);
+        if (p.sigma_scale != 1.0f) sig = sig * p.sigma_scale;
+        float wv;
+        composite_tile(acc, valid, cr, cg, cbl, sig, t, dist, j, &wv);
+        if (p.weights && valid && h == 0) p.weights[ray * S + s] = wv;
+    }
+    float bgc[3];
+    background(bg, dx, dy, dz, lane, bgc);
+    float r, g, b, dd, a;
+    finish_ray(acc, r, g, b, dd, a);
+    if (lane == 0) {
+        if (bg.mode != ACN_BG_NONE) {
+            const float om = 1.0f - a;
+            r = r + om * bgc[0];
+            g = g + om * bgc[1];
+            b = b + om * bgc[2];
+        }
+        p.rgb[ray * 3 + 0] = r;
+        p.rgb[ray * 3 + 1] = g;
+        p.rgb[ray * 3 + 2] = b;
+        p.depth[ray] = dd;
+        p.acc[ray] = a;
+    }
+}
+
 template <int INTERP>
 __global__ void __launch_bounds__(1024, 4) render_ws_kernel(FieldCfg cfg, BgArgs bg, RenderParams p) {
     constexpr bool FOLD = ACN_SHFOLD != 0;
@@ -1175,55 +1232,7 @@ __global__ void __launch_bounds__(1024, 4) render_ws_kernel(FieldCfg cfg, BgArgs
             old = __builtin_amdgcn_readlane(old, 0);
             if (old != T - 1) continue;
             // this tile completed the ray: composite it (render_ray's sequence, no early termination)
-            const float* rq = p.rays + ray * 8;
-            const float cox = rq[0], coy = rq[1], coz = rq[2], cdx = rq[3], cdy = rq[4], cdz = rq[5];
-            const float cnear = rq[6], cfar = rq[7];
-            (void)cox, (void)coy, (void)coz;
-            const float* cjit = p.jitter ? p.jitter + ray * S : nullptr;
-            RayAcc acc{1.0, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-            for (int s0 = 0; s0 < S; s0 += 32) {
-                const int cs = s0 + j;
-                const bool valid = cs < S;
-                const int csc = valid ? cs : S - 1;
-                float ct, dist;
-                if (!cjit) {
-                    const int i0 = csc < S - 1 ? csc : S - 2;
-                    const float ta = tlin_sel(cnear, cfar, i0, S, step), tb = tlin_sel(cnear, cfar, i0 + 1, S, step);
-                    ct = csc < S - 1 ? ta : tb;
-                    dist = tb - ta;
-                } else {
-                    ct = tval(cnear, cfar, csc, S, cjit);
-                    const float tn = (csc < S - 1) ? tval(cnear, cfar, csc + 1, S, cjit) : ct;
-                    const float tp = (csc == S - 1 && S > 1) ? tval(cnear, cfar, csc - 1, S, cjit) : ct;
-                    dist = (csc < S - 1) ? (tn - ct) : (ct - tp);
-                }
-                const f32x4 y = ybuf[slot * kWsMaxS + csc];
-                const float cr = clamp_nan(y[0], 0.0f, 1.0f);
-                const float cg = clamp_nan(y[1], 0.0f, 1.0f);
-                const float cbl = clamp_nan(y[2], 0.0f, 1.0f);
-                float sig = clamp_min_nan(y[3], 0.0f);
-                if (p.sigma_scale != 1.0f) sig = sig * p.sigma_scale;
-                float wv;
-                composite_tile(acc, valid, cr, cg, cbl, sig, ct, dist, j, &wv);
-                if (p.weights && valid && h == 0) p.weights[ray * S + cs] = wv;
-            }
-            float bgc[3];
-            background(bg, cdx, cdy, cdz, lane, bgc);
-            float r, g, b, dd, a;
-            finish_ray(acc, r, g, b, dd, a);
-            if (lane == 0) {
-                if (bg.mode != ACN_BG_NONE) {
-                    const float om = 1.0f - a;
-                    r = r + om * bgc[0];
-                    g = g + om * bgc[1];
-                    b = b + om * bgc[2];
-                }
-                p.rgb[ray * 3 + 0] = r;
-                p.rgb[ray * 3 + 1] = g;
-                p.rgb[ray * 3 + 2] = b;
-                p.depth[ray] = dd;
-                p.acc[ray] = a;
-            }
+            composite_ray_lds(p, bg, ray, ybuf + slot * kWsMaxS, lane, step);
         }
         __syncthreads();   // ybuf / qhead / done reused by the next round
     }
@@ -1286,9 +1295,86 @@ __device__ __forceinline__ uint32_t ray_expert_mask(const FieldCfg& cfg, int rou
 #ifndef ACN_SLOTS_BAND
 #define ACN_SLOTS_BAND 0
 #endif
+#ifndef ACN_SLOTS_WS
+#define ACN_SLOTS_WS 0  // 1: render_slots_kernel rounds share their field tiles (as render_ws_kernel); measured slower
+#endif
 #ifndef ACN_SLOTS_THREADS
 #define ACN_SLOTS_THREADS 512  // 2 waves/SIMD, 256 VGPRs: the 1024-thread build spills and was measured wrong
 #endif
+// the field of one 32-sample tile in render_slots_kernel: LDS slot experts, the rest from the packed images
+// in global memory (folded colour bias in cb[slot] / cbg); single = one expert with weight 1.0f on every sample
+template <int INTERP, int ROUTE, bool FOLD>
+__device__ __forceinline__ void slots_field(const FieldCfg& cfg, const RenderParams& p, const float* smem, float* cb,
+                                            float* cbg, int k0, int k1, bool single, int k_single, float px, float py,
+                                            float pz, const float (&shv)[8], uint32_t& folded, int lane, float& yr,
+                                            float& yg, float& yb, float& ys) {
+        if (single) {  // wave-uniform: one expert, weight 1.0f on every sample
+            const int k = k_single;
+            const int sl = (k == k0) ? 0 : ((k == k1) ? 1 : -1);
+            float sg;
+            if (sl >= 0) {
+                const float* Wk = smem + sl * PK_FLOATS;
+                float* cbk = FOLD ? cb + sl * 64 : nullptr;
+                if (FOLD && !((folded >> sl) & 1u)) {
+                    fold_sh_bias(Wk, shv, lane, cbk);
+                    folded |= 1u << sl;
+                }
+                field_tile<INTERP, FOLD>(Wk, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbk, lane, yr,
+                                         yg, yb, sg);
+            } else {
+                const float* Wg = p.packed + (size_t)k * PK_FLOATS;
+                if (FOLD) fold_sh_bias(Wg, shv, lane, cbg);
+                field_tile<INTERP, FOLD>(Wg, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbg, lane, yr,
+                                         yg, yb, sg);
+            }
+            ys = trunc_exp(sg);
+            return;
+        }
+    #if ACN_DIAG_SLOTS_NOMULTI  // diagnostic build only: the multi-expert blend path removed (register study)
+        yr = yg = yb = ys = 0.0f;
+        return;
+    #endif
+        const RouteState st = route_prep<ROUTE>(cfg, px, py, pz);
+        yr = yg = yb = ys = 0.0f;
+        for (int k = 0; k < cfg.K; ++k) {
+            const float wk = (ROUTE == 1) ? route_weight(cfg, st, k, px, py, pz) : 0.0f;
+            const bool need = (ROUTE == 1) ? (wk > 0.0f) : (st.hard == k);
+            if (__ballot(need) == 0ull) continue;
+            float r, g, b, sg;
+            const int sl = (k == k0) ? 0 : ((k == k1) ? 1 : -1);
+            if (sl >= 0) {
+                const float* Wk = smem + sl * PK_FLOATS;
+                float* cbk = FOLD ? cb + sl * 64 : nullptr;
+                if (FOLD && !((folded >> sl) & 1u)) {
+                    fold_sh_bias(Wk, shv, lane, cbk);
+                    folded |= 1u << sl;
+                }
+                field_tile<INTERP, FOLD>(Wk, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbk, lane, r, g,
+                                         b, sg);
+            } else {
+    #if ACN_SLOTS_NOFALLBACK  // diagnostic only: non-resident experts skipped
+                r = g = b = sg = 0.0f;
+    #else
+                const float* Wg = p.packed + (size_t)k * PK_FLOATS;
+                if (FOLD) fold_sh_bias(Wg, shv, lane, cbg);
+                field_tile<INTERP, FOLD>(Wg, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbg, lane, r, g,
+                                         b, sg);
+    #endif
+            }
+            sg = trunc_exp(sg);
+            if (need) {
+                if (ROUTE == 1) {
+                    yr = yr + r * wk;
+                    yg = yg + g * wk;
+                    yb = yb + b * wk;
+                    ys = ys + sg * wk;
+                } else {
+                    yr = r; yg = g; yb = b; ys = sg;
+                }
+            }
+        }
+}
+
 template <int INTERP, int ROUTE>
 __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) render_slots_kernel(FieldCfg cfg, BgArgs bg, RenderParams p) {
     constexpr bool FOLD = ACN_SHFOLD != 0;
@@ -1296,9 +1382,18 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
     // per wave: the folded SH bias of the two LDS slots and of the expert read from L2 (every expert's
     // colour layer 0 runs folded, wherever its weights are read from: a ray's arithmetic must not depend on
     // which experts its workgroup round keeps in LDS -- that choice depends on the other rays of the batch)
-    __shared__ __attribute__((aligned(16))) float cbuf[FOLD ? 16 * 3 * 64 : 4];
+    __shared__ __attribute__((aligned(16))) float cbuf[FOLD ? (ACN_SLOTS_THREADS / 64) * 3 * 64 : 4];
     __shared__ int cnt[kMaxK];
     __shared__ int slot_k[2], restage[2];
+#if ACN_SLOTS_WS
+    // work-shared tiles (as render_ws_kernel): the round's rays, their expert masks and field values
+    constexpr int kW = ACN_SLOTS_THREADS / 64;
+    __shared__ __attribute__((aligned(16))) f32x4 ybuf[kW * kWsMaxS];
+    __shared__ int64_t wray[kW];
+    __shared__ uint32_t wmask[kW];
+    __shared__ int qhead, done[kW];
+    const bool ws = !(p.tau > 0.0f) && p.S <= kWsMaxS;
+#endif
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     float* cb = FOLD ? cbuf + wave * 3 * 64 : nullptr;
@@ -1328,6 +1423,14 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
             for (int k = 0; k < cfg.K; ++k)
                 if ((m >> k) & 1u) atomicAdd(&cnt[k], 1);
         __syncthreads();
+#if ACN_SLOTS_WS
+        if (ws && lane == 0) {   // every wave has left the previous round: its LDS state can be replaced
+            wray[wave] = ray;
+            wmask[wave] = m;
+            done[wave] = 0;
+            if (wave == 0) qhead = 0;
+        }
+#endif
         if (threadIdx.x == 0) {
             int b0 = -1, b1 = -1;
             for (int k = 0; k < cfg.K; ++k) {
@@ -1359,77 +1462,71 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
 #else
         const int k0 = __builtin_amdgcn_readfirstlane(slot_k[0]), k1 = __builtin_amdgcn_readfirstlane(slot_k[1]);
 #endif
+#if ACN_SLOTS_WS
+        if (ws) {
+            const int nr = (int)min(waves_per_wg, lim - base);
+            const int S = p.S, T = (S + 31) >> 5;
+            const int j = lane & 31, h = lane >> 5;
+            int64_t cur = -1;
+            uint32_t folded = 0u, mm = 0u;
+            float shv[8];
+            float ox = 0.0f, oy = 0.0f, oz = 0.0f, dx = 0.0f, dy = 0.0f, dz = 0.0f, near = 0.0f, far = 0.0f;
+            const float* jit = nullptr;
+            for (;;) {
+                int item = 0;
+                if (lane == 0) item = __hip_atomic_fetch_add(&qhead, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                item = __builtin_amdgcn_readlane(item, 0);
+                if (item >= nr * T) break;
+                const int tile = item / nr, slot = item - tile * nr;
+                const int64_t tray = (int64_t)__builtin_amdgcn_readfirstlane((int)wray[slot]);
+                if (tray != cur) {
+                    const float* rp = p.rays + tray * 8;
+                    ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
+                    near = rp[6], far = rp[7];
+                    jit = p.jitter ? p.jitter + tray * S : nullptr;
+                    float sh[16];
+                    dir_sh(dx, dy, dz, sh);
+                    sh_rows_for_half(sh, h, shv);
+                    folded = 0u;
+                    mm = __builtin_amdgcn_readfirstlane(wmask[slot]);
+                    cur = tray;
+                }
+                const int s = tile * 32 + j;
+                const int sc = s < S ? s : S - 1;
+                float t;
+                if (!jit) {
+                    const int i0 = sc < S - 1 ? sc : S - 2;
+                    const float ta = tlin_sel(near, far, i0, S, step), tb = tlin_sel(near, far, i0 + 1, S, step);
+                    t = sc < S - 1 ? ta : tb;
+                } else {
+                    t = tval(near, far, sc, S, jit);
+                }
+                const float px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;
+                float yr, yg, yb, ys;
+                slots_field<INTERP, ROUTE, FOLD>(cfg, p, smem, cb, cbg, k0, k1, (mm & kSingleRay) != 0u,
+                                                 __builtin_ctz(mm | kSingleRay), px, py, pz, shv, folded, lane, yr,
+                                                 yg, yb, ys);
+                if (h == 0 && s < S) {
+                    f32x4 v;
+                    v[0] = yr, v[1] = yg, v[2] = yb, v[3] = ys;
+                    ybuf[slot * kWsMaxS + s] = v;
+                }
+                int old = 0;
+                if (lane == 0) old = __hip_atomic_fetch_add(&done[slot], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+                old = __builtin_amdgcn_readlane(old, 0);
+                if (old == T - 1) composite_ray_lds(p, bg, tray, ybuf + slot * kWsMaxS, lane, step);
+            }
+            continue;   // the next round's first barrier orders this round's LDS use before its resets
+        }
+#endif
         if (live) {
             const bool single = (m & kSingleRay) != 0u;
             const int k_single = __builtin_ctz(m | kSingleRay);
             render_ray(p, bg, ray, lane, step,
                        [&](int, float px, float py, float pz, const float (&shv)[8], uint32_t& folded, float& yr, float& yg,
                            float& yb, float& ys) {
-                           if (single) {  // wave-uniform: one expert, weight 1.0f on every sample
-                               const int k = k_single;
-                               const int sl = (k == k0) ? 0 : ((k == k1) ? 1 : -1);
-                               float sg;
-                               if (sl >= 0) {
-                                   const float* Wk = smem + sl * PK_FLOATS;
-                                   float* cbk = FOLD ? cb + sl * 64 : nullptr;
-                                   if (FOLD && !((folded >> sl) & 1u)) {
-                                       fold_sh_bias(Wk, shv, lane, cbk);
-                                       folded |= 1u << sl;
-                                   }
-                                   field_tile<INTERP, FOLD>(Wk, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbk, lane, yr,
-                                                            yg, yb, sg);
-                               } else {
-                                   const float* Wg = p.packed + (size_t)k * PK_FLOATS;
-                                   if (FOLD) fold_sh_bias(Wg, shv, lane, cbg);
-                                   field_tile<INTERP, FOLD>(Wg, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbg, lane, yr,
-                                                            yg, yb, sg);
-                               }
-                               ys = trunc_exp(sg);
-                               return;
-                           }
-#if ACN_DIAG_SLOTS_NOMULTI  // diagnostic build only: the multi-expert blend path removed (register study)
-                           yr = yg = yb = ys = 0.0f;
-                           return;
-#endif
-                           const RouteState st = route_prep<ROUTE>(cfg, px, py, pz);
-                           yr = yg = yb = ys = 0.0f;
-                           for (int k = 0; k < cfg.K; ++k) {
-                               const float wk = (ROUTE == 1) ? route_weight(cfg, st, k, px, py, pz) : 0.0f;
-                               const bool need = (ROUTE == 1) ? (wk > 0.0f) : (st.hard == k);
-                               if (__ballot(need) == 0ull) continue;
-                               float r, g, b, sg;
-                               const int sl = (k == k0) ? 0 : ((k == k1) ? 1 : -1);
-                               if (sl >= 0) {
-                                   const float* Wk = smem + sl * PK_FLOATS;
-                                   float* cbk = FOLD ? cb + sl * 64 : nullptr;
-                                   if (FOLD && !((folded >> sl) & 1u)) {
-                                       fold_sh_bias(Wk, shv, lane, cbk);
-                                       folded |= 1u << sl;
-                                   }
-                                   field_tile<INTERP, FOLD>(Wk, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbk, lane, r, g,
-                                                            b, sg);
-                               } else {
-#if ACN_SLOTS_NOFALLBACK  // diagnostic only: non-resident experts skipped
-                                   r = g = b = sg = 0.0f;
-#else
-                                   const float* Wg = p.packed + (size_t)k * PK_FLOATS;
-                                   if (FOLD) fold_sh_bias(Wg, shv, lane, cbg);
-                                   field_tile<INTERP, FOLD>(Wg, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbg, lane, r, g,
-                                                            b, sg);
-#endif
-                               }
-                               sg = trunc_exp(sg);
-                               if (need) {
-                                   if (ROUTE == 1) {
-                                       yr = yr + r * wk;
-                                       yg = yg + g * wk;
-                                       yb = yb + b * wk;
-                                       ys = ys + sg * wk;
-                                   } else {
-                                       yr = r; yg = g; yb = b; ys = sg;
-                                   }
-                               }
-                           }
+                           slots_field<INTERP, ROUTE, FOLD>(cfg, p, smem, cb, cbg, k0, k1, single, k_single, px, py,
+                                                            pz, shv, folded, lane, yr, yg, yb, ys);
                        });
         }
     }

@@ -359,7 +359,7 @@ def render_traffic_profile(workload: str, S: int, layout: str):
     """Round-4 counter summary of the render line's dominant kernel (tools/pmc_r04.sh + tools/pmc_fold_r04.py:
     separate rocprofv3 --pmc passes, FETCH_SIZE doubled per the gfx950 correction of MI355X_MICROARCH.md
     'HBM', plus WRITE_SIZE), or None when no profile of this exact configuration is committed."""
-    name = {("c2", 256, "replicated"): "r04_pmc_c2_render.json",
+    name = {("c2", 256, "replicated"): "r04_pmc_c2_ws.json",
             ("c3", 256, "replicated"): "r04_pmc_c3_slots.json",
             ("c4", 96, "replicated"): "r04_pmc_c4s96_slots.json",
             ("c4", 256, "replicated"): "r04_pmc_c4_slots.json"}.get((workload, S, layout))
@@ -982,9 +982,10 @@ def main():
     kname = {"c5": "adam_slots_kernel (Adam over every expert with routed samples + background head, clip coefficient "
                    "folded in, table gradients cleared in the same pass)",
              "c5a": "adam_kernel (fused clip + Adam over the adapted expert + background head)",
-             "c2": "ray_order_kernel + render_kernel<1,1,0> (one acn_render_stratified_fwd_ordered call: direction "
-                   "grouping of the batch, then the fused stratified render, 1 expert; kernel_ms = two HIP events "
-                   "bracketing the K timed calls on the launch stream / K)",
+             "c2": "ray_order_kernel + render_ws_kernel<1> (one acn_render_stratified_fwd_ordered call: direction "
+                   "grouping of the batch, then the fused stratified render, 1 expert, the workgroup's 16 rays "
+                   "sharing their 32-sample field tiles; kernel_ms = two HIP events bracketing the K timed calls on "
+                   "the launch stream / K)",
              "c3": "render_slots_kernel (fused stratified render, soft routing over 4 experts, two staged per round)",
              "c4": ("ep_field_kernel (the owned expert's fused MFMA field over the received per-sample records; "
                     "one-expert-per-GPU layout, kernel_ms per launch)"

@@ -1,9 +1,11 @@
-"""render_ws_kernel (one expert, no early termination: the workgroup's rays share their field tiles) against
-render_kernel on the same rays -- bit-identical outputs ('Work-shared tiles').
+"""Work-shared tiles (no early termination: a workgroup's rays share their 32-sample field tiles) against the
+per-wave-ray path on the same rays -- bit-identical outputs ('Work-shared tiles'): render_ws_kernel
+against render_kernel for one expert (K = 1, or active_module), render_slots_kernel's work-shared round
+against its per-wave round for the routed K = 4 / K = 8 containers.
 
 Both kernels render each ray with the same arithmetic (reference nerfs/ray_rendering.py:290-345); the work-shared
 kernel only changes which wave evaluates a 32-sample tile and then composites the ray from LDS in tile order.
-A positive tau selects render_kernel (early termination needs the tiles in order).  tau = 1e-45 (the smallest
+A positive tau selects the per-wave path (early termination needs the tiles in order).  tau = 1e-45 (the smallest
 float denormal) stops a ray only once its transmittance is below every float weight, so rgb, depth and acc are
 unchanged by it; weights of samples past such a stop are 0 there and at most a denormal here."""
 import numpy as np
@@ -46,7 +48,7 @@ def _same(a, b):
     return np.array_equal(a.cpu().numpy(), b.cpu().numpy(), equal_nan=True)
 
 
-@pytest.mark.parametrize("tag,active", [("k1", None), ("k4", 2)])
+@pytest.mark.parametrize("tag,active", [("k1", None), ("k4", 2), ("k4", None), ("k8", None)])
 @pytest.mark.parametrize("S", [64, 200, 256, 300])
 @pytest.mark.parametrize("jitter", [False, True])
 @pytest.mark.parametrize("n", [1, 17, 4096])
