@@ -1239,6 +1239,160 @@ __global__ void __launch_bounds__(1024, 4) render_ws_kernel(FieldCfg cfg, BgArgs
 }
 
 // ------------------------------------------------------------------------------------------
+// render_ws_kernel with the rays handed out at run time (render_dq_kernel, the ordered C2 path).  The static
+// rounds balance the tiles inside a CU, but each CU still owns 16 fixed rays, and CUs whose rays sit in
+// slow regions end last.  Here each XCD band of the visiting order is a queue (one device-scope counter per
+// band, zeroed by ray_order_kernel just before): a workgroup holds at most kDqLive of its band's rays at a
+// time in LDS slots, so the band keeps rays in reserve and the CUs that finish early take more of them.  A
+// wave works through its own slot's tiles; with nothing left there it takes the next ray of the band (while
+// the workgroup holds fewer than kDqLive), else any unclaimed tile of the workgroup's slots.  Only ray
+// indices cross CUs (the counter), never field values: tiles, LDS buffers and compositing stay in the
+// workgroup, with render_ws_kernel's arithmetic, so the outputs are bit-identical to render_kernel.
+#ifndef ACN_RENDER_DQ
+#define ACN_RENDER_DQ 0  // 1: band queues of rays (measured slower than render_ws_kernel)
+#endif
+constexpr int kDqSlots = 24;   // LDS ray slots (24 x 4 KB at S = 256; 158 KB of LDS in all)
+#ifndef ACN_DQ_LIVE
+#define ACN_DQ_LIVE 12         // rays a workgroup holds at once (the rest of its band stays in the queue)
+#endif
+
+template <int INTERP>
+__global__ void __launch_bounds__(1024, 4) render_dq_kernel(FieldCfg cfg, BgArgs bg, RenderParams p,
+                                                            int* __restrict__ bandq) {
+    constexpr bool FOLD = ACN_SHFOLD != 0;
+    __shared__ __attribute__((aligned(16))) float smem[PK_FLOATS];
+    __shared__ __attribute__((aligned(16))) float cbuf[FOLD ? 16 * 64 : 4];
+    __shared__ __attribute__((aligned(16))) f32x4 ybuf[kDqSlots * kWsMaxS];
+    __shared__ int sray[kDqSlots], snext[kDqSlots], sdone[kDqSlots];
+    __shared__ uint32_t slive;   // bit s: slot s holds a ray that is not composited yet
+    __shared__ int qempty;       // this workgroup saw its band's queue run out
+    const int S = p.S;
+    const int T = (S + 31) >> 5;
+    if (threadIdx.x < kDqSlots) {
+        snext[threadIdx.x] = T;   // nothing to claim in an empty slot
+        sdone[threadIdx.x] = 0;
+        sray[threadIdx.x] = 0;
+    }
+    if (threadIdx.x == 0) slive = 0u, qempty = 0;
+    stage_weights<1>(smem, p.packed);   // (ends with a workgroup barrier)
+    const float* W = smem;
+    const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float* cb = FOLD ? cbuf + wave * 64 : nullptr;
+    const float step = 1.0f / (float)(S - 1);
+    const bool banded = (gridDim.x & 7) == 0;
+    const int band = banded ? (int)(blockIdx.x & 7) : 0;
+    const int64_t chunk = banded ? (p.N + 7) >> 3 : p.N;
+    const int64_t lo = min(p.N, (int64_t)band * chunk), hi = min(p.N, lo + chunk);
+    auto claim = [&](int sl) -> int {
+        int t = 0;
+        if (lane == 0) t = __hip_atomic_fetch_add(&snext[sl], 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return __builtin_amdgcn_readlane(t, 0);
+    };
+    int my = -1;   // the slot this wave took from the queue (its tiles first)
+    int64_t cur = -1;
+    uint32_t folded = 0u;
+    float shv[8];
+    float ox = 0.0f, oy = 0.0f, oz = 0.0f, dx = 0.0f, dy = 0.0f, dz = 0.0f, near = 0.0f, far = 0.0f;
+    const float* jit = nullptr;
+    for (;;) {
+        int tile = -1, sl = -1;
+        if (my >= 0) {
+            const int t = claim(my);
+            if (t < T) tile = t, sl = my;
+            else my = -1;
+        }
+        // a new ray from the band, while the workgroup holds fewer than ACN_DQ_LIVE
+        if (tile < 0 && !__builtin_amdgcn_readfirstlane(qempty) &&
+            __builtin_popcount(__builtin_amdgcn_readfirstlane(slive)) < ACN_DQ_LIVE) {
+            int got = -1;
+            if (lane == 0) {
+                uint32_t freem = ~__hip_atomic_load(&slive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) &
+                                 ((1u << kDqSlots) - 1u);
+                while (freem) {
+                    const int s = __builtin_ctz(freem);
+                    const uint32_t old = __hip_atomic_fetch_or(&slive, 1u << s, __ATOMIC_ACQ_REL,
+                                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (!(old & (1u << s))) { got = s; break; }
+                    freem &= ~(1u << s);
+                }
+                if (got >= 0) {
+                    const int q = __hip_atomic_fetch_add(&bandq[band], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const int64_t pos = lo + q;
+                    if (pos < hi) {
+                        sray[got] = p.order ? p.order[pos] : (int)pos;
+                        sdone[got] = 0;
+                        // tile 0 is this wave's; the others become claimable with this store
+                        __hip_atomic_store(&snext[got], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    } else {
+                        qempty = 1;
+                        __hip_atomic_fetch_and(&slive, ~(1u << got), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        got = -1;
+                    }
+                }
+            }
+            got = __builtin_amdgcn_readlane(got, 0);
+            if (got >= 0) tile = 0, sl = got, my = got;
+        }
+        // help: any unclaimed tile of the workgroup's live rays
+        if (tile < 0) {
+            uint32_t m = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(&slive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+            while (m) {
+                const int s = __builtin_ctz(m);
+                m &= m - 1u;
+                const int t = claim(s);
+                if (t < T) { tile = t, sl = s; break; }
+            }
+        }
+        if (tile < 0) {
+            if (__builtin_amdgcn_readfirstlane(qempty)) break;   // the band is done; claimed tiles finish elsewhere
+            __builtin_amdgcn_s_sleep(2);                          // rays in flight will free slots
+            continue;
+        }
+        const int64_t ray = (int64_t)__builtin_amdgcn_readfirstlane(sray[sl]);
+        if (ray != cur) {
+            const float* rp = p.rays + ray * 8;
+            ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
+            near = rp[6], far = rp[7];
+            jit = p.jitter ? p.jitter + ray * S : nullptr;
+            float sh[16];
+            dir_sh(dx, dy, dz, sh);
+            sh_rows_for_half(sh, h, shv);
+            folded = 0u;
+            cur = ray;
+        }
+        const int s = tile * 32 + j;
+        const int sc = s < S ? s : S - 1;
+        float t;
+        if (!jit) {
+            const int i0 = sc < S - 1 ? sc : S - 2;
+            const float ta = tlin_sel(near, far, i0, S, step), tb = tlin_sel(near, far, i0 + 1, S, step);
+            t = sc < S - 1 ? ta : tb;
+        } else {
+            t = tval(near, far, sc, S, jit);
+        }
+        const float px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;
+        float yr, yg, yb, ys;
+        container_tile<INTERP, 0, FOLD>(cfg, W, px, py, pz, shv, cb, &folded, lane, yr, yg, yb, ys);
+        if (h == 0 && s < S) {
+            f32x4 v;
+            v[0] = yr, v[1] = yg, v[2] = yb, v[3] = ys;
+            ybuf[sl * kWsMaxS + s] = v;
+        }
+        int old = 0;
+        if (lane == 0) old = __hip_atomic_fetch_add(&sdone[sl], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+        old = __builtin_amdgcn_readlane(old, 0);
+        if (old != T - 1) continue;
+        composite_ray_lds(p, bg, ray, ybuf + sl * kWsMaxS, lane, step);
+        if (my == sl) my = -1;
+        // the slot's LDS reads are done before it can be handed out again
+        if (lane == 0)
+            __hip_atomic_fetch_and(&slive, ~(1u << sl), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // Routed render with more than two experts (C3 / C4).  LDS holds two expert SLOTS; per round of
 // 16 rays (one per wave) the workgroup routes every sample of its rays, counts how many waves
 // need each expert, and stages the two most needed ones into the slots (only when they change --
@@ -2581,7 +2735,10 @@ __device__ __forceinline__ void radix_pass6(const uint16_t* kin, const uint16_t*
     __syncthreads();
 }
 __global__ void __launch_bounds__(1024) ray_order_kernel(const float* __restrict__ rays, int N,
-                                                         int32_t* __restrict__ order) {
+                                                         int32_t* __restrict__ order, int* __restrict__ zero_ints,
+                                                         int nzero) {
+    // zero_ints: render_dq_kernel's band queue counters, cleared here (the launch right before it)
+    if ((int)threadIdx.x < nzero) zero_ints[threadIdx.x] = 0;
     constexpr int PER = ACN_ORDER_MAX / 1024;
     __shared__ int cnt[1024];
     __shared__ __attribute__((aligned(16))) float dir[3][ACN_ORDER_MAX];
@@ -2723,9 +2880,13 @@ extern "C" size_t acn_workspace_bytes(int K) { return (size_t)(K < 1 ? 1 : K) * 
 // scratch of the split routed render: code[N], list[N + 16 kMaxK], multi[N], hdr[kMaxK + 2]
 static size_t split_bytes(int64_t N) { return (size_t)(3 * N + 16 * kMaxK + kMaxK + 2) * sizeof(int32_t); }
 
+// order scratch of the ordered single-expert render: order[N], then (64-B aligned) the 8 band counters
+static size_t dq_band_offset(int64_t N) { return ((size_t)N * sizeof(int32_t) + 63) & ~(size_t)63; }
+static size_t dq_order_bytes(int64_t N) { return dq_band_offset(N) + 64; }
+
 extern "C" size_t acn_render_order_bytes(int64_t N) {
     if (N < 1) return 0;
-    const size_t ord = N <= ACN_ORDER_MAX ? (size_t)N * sizeof(int32_t) : 0;
+    const size_t ord = N <= ACN_ORDER_MAX ? (ACN_RENDER_DQ ? dq_order_bytes(N) : (size_t)N * sizeof(int32_t)) : 0;
     const size_t spl = ACN_SPLIT_ROUTED ? split_bytes(N) : 0;
     return ord > spl ? ord : spl;
 }
@@ -2734,7 +2895,8 @@ extern "C" int acn_ray_order(const float* rays, int64_t N, int32_t* order, void*
     ACN_REQUIRE(N >= 1 && N <= ACN_ORDER_MAX, "acn_ray_order: N must be in [1, %d], got %lld", ACN_ORDER_MAX,
                 (long long)N);
     ACN_REQUIRE(rays && order, "acn_ray_order: NULL pointer");
-    hipLaunchKernelGGL(ray_order_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, rays, (int)N, order);
+    hipLaunchKernelGGL(ray_order_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, rays, (int)N, order,
+                       (int*)nullptr, 0);
     return acn_check_launch("acn_ray_order");
 }
 
@@ -2802,9 +2964,20 @@ extern "C" int acn_render_stratified_fwd_ordered(const float* rays, int64_t N, i
     if ((num_cus() & 7) == 0) wgs = (wgs + 7) & ~(int64_t)7;  // whole XCD bands (render_kernel)
     const dim3 grid((unsigned)(wgs < num_cus() ? wgs : num_cus())), block(1024);
     const bool slots = ACN_SLOTS && cfg.routing != 0 && K != 2;  // render_slots_kernel keeps its own order
+    // render_dq_kernel: one expert, no early termination, the order scratch with room for the band counters
+    const bool dq = ACN_RENDER_DQ && cfg.routing == 0 && S <= kWsMaxS && !(tau > 0.0f) && order_scratch &&
+                    N <= ACN_ORDER_MAX && order_bytes >= dq_order_bytes(N);
+    int* bandq = dq ? (int*)((char*)order_scratch + dq_band_offset(N)) : nullptr;
     if (order_scratch && !slots && N <= ACN_ORDER_MAX && order_bytes >= (size_t)N * sizeof(int32_t)) {
-        hipLaunchKernelGGL(ray_order_kernel, dim3(1), dim3(1024), 0, s, rays, (int)N, (int32_t*)order_scratch);
+        hipLaunchKernelGGL(ray_order_kernel, dim3(1), dim3(1024), 0, s, rays, (int)N, (int32_t*)order_scratch, bandq,
+                           dq ? 8 : 0);
         p.order = (const int32_t*)order_scratch;
+    }
+    if (dq) {
+        if (interp == 1) hipLaunchKernelGGL(render_dq_kernel<1>, grid, block, 0, s, cfg, b, p, bandq);
+        else if (interp == 0) hipLaunchKernelGGL(render_dq_kernel<0>, grid, block, 0, s, cfg, b, p, bandq);
+        else hipLaunchKernelGGL(render_dq_kernel<2>, grid, block, 0, s, cfg, b, p, bandq);
+        return acn_check_launch("acn_render_stratified_fwd");
     }
     if (slots && ACN_ROUTED && S <= ACN_ROUTED_CHUNK) {
         // expert-major chunks (render_routed_kernel): R rays per chunk, two workgroups per CU
