@@ -3275,6 +3275,149 @@ __global__ void __launch_bounds__(1024, 4) occ_render_kernel(FieldCfg cfg, BgArg
     }
 }
 
+// The occupancy render with the workgroup's field tiles shared (one expert), as render_ws_kernel: rays carry
+// 0..hundreds of marched samples, so one wave per ray leaves a CU waiting on its longest ray.  A round's 16
+// rays are cut into 32-sample tiles (ray-major item list from an LDS prefix sum), waves take tiles from an LDS
+// counter, field values go to LDS, and the wave completing a ray composites it with render_ray_packed's exact
+// loop (bit-identical outputs).  A ray with more than kWsMaxS samples does not fit its LDS row: its own wave
+// renders it whole with render_ray_packed, and the round's other rays are shared.
+#ifndef ACN_OCC_WS
+#define ACN_OCC_WS 0  // 1: occ_ws_kernel (bit-identical, measured no faster: DESIGN 4i)
+#endif
+template <int INTERP>
+__global__ void __launch_bounds__(1024, 4) occ_ws_kernel(FieldCfg cfg, BgArgs bg, OccRenderParams p) {
+    constexpr bool FOLD = ACN_SHFOLD != 0;
+    __shared__ __attribute__((aligned(16))) float smem[PK_FLOATS];
+    __shared__ __attribute__((aligned(16))) float cbuf[FOLD ? 16 * 64 : 4];
+    __shared__ __attribute__((aligned(16))) f32x4 ybuf[16 * kWsMaxS];
+    __shared__ int cum[17];
+    __shared__ int qhead, done[16];
+    stage_weights<1>(smem, p.packed);
+    const float* W = smem;
+    const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float* cb = FOLD ? cbuf + wave * 64 : nullptr;
+    auto field = [&](float px, float py, float pz, const float (&shv)[8], uint32_t& folded, float& yr, float& yg,
+                     float& yb, float& ys) {
+        container_tile<INTERP, 0, FOLD>(cfg, W, px, py, pz, shv, cb, &folded, lane, yr, yg, yb, ys);
+    };
+    const int64_t stride = (int64_t)gridDim.x * 16;
+    for (int64_t base = (int64_t)blockIdx.x * 16; base < p.N; base += stride) {   // block-uniform
+        const int nr = (int)min((int64_t)16, p.N - base);
+        if (threadIdx.x == 0) {
+            int c = 0;
+            cum[0] = 0;
+            for (int r = 0; r < 16; ++r) {
+                const int64_t n = r < nr ? p.counts[base + r] : 0;
+                c += (n > 0 && n <= kWsMaxS) ? (int)((n + 31) >> 5) : 0;   // solo rays (n > kWsMaxS): no shared tiles
+                cum[r + 1] = c;
+            }
+            qhead = 0;
+        }
+        if (threadIdx.x < 16) done[threadIdx.x] = 0;
+        __syncthreads();
+        if (wave < nr) {   // a ray too long for its LDS row: this wave renders it alone
+            const int64_t n = p.counts[base + wave];
+            if (n > kWsMaxS) render_ray_packed(p, bg, base + wave, lane, field);
+            else if (n <= 0) render_ray_packed(p, bg, base + wave, lane, field);   // no samples: background only
+        }
+        const int items = cum[16];
+        int64_t cur = -1;
+        uint32_t folded = 0u;
+        float shv[8];
+        float ox = 0.0f, oy = 0.0f, oz = 0.0f, dx = 0.0f, dy = 0.0f, dz = 0.0f;
+        for (;;) {
+            int item = 0;
+            if (lane == 0) item = __hip_atomic_fetch_add(&qhead, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            item = __builtin_amdgcn_readlane(item, 0);
+            if (item >= items) break;
+            int slot = 0;
+            while (cum[slot + 1] <= item) ++slot;
+            const int tile = item - cum[slot];
+            const int T = cum[slot + 1] - cum[slot];
+            const int64_t ray = base + slot;
+            if (ray != cur) {
+                const float* rp = p.rays + ray * p.ld;
+                ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
+                float sh[16];
+                dir_sh(dx, dy, dz, sh);
+                sh_rows_for_half(sh, h, shv);
+                folded = 0u;
+                cur = ray;
+            }
+            const int64_t b = p.starts[ray], n = p.counts[ray];
+            const int64_t s = (int64_t)tile * 32 + j;
+            const bool valid = s < n;
+            const int64_t idx = b + (valid ? s : n - 1);
+            const float ta = p.t0[idx], tb = p.t1[idx];
+            const float tm = 0.5f * (ta + tb);
+            const float px = ox + dx * tm, py = oy + dy * tm, pz = oz + dz * tm;
+            float yr, yg, yb, ys;
+            field(px, py, pz, shv, folded, yr, yg, yb, ys);
+            if (h == 0 && valid) {
+                f32x4 v;
+                v[0] = yr, v[1] = yg, v[2] = yb, v[3] = ys;
+                ybuf[slot * kWsMaxS + (int)s] = v;
+            }
+            int old = 0;
+            if (lane == 0) old = __hip_atomic_fetch_add(&done[slot], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+            old = __builtin_amdgcn_readlane(old, 0);
+            if (old != T - 1) continue;
+            // composite from LDS: render_ray_packed's loop with the field values it would have computed
+            const f32x4* yrow = ybuf + slot * kWsMaxS;
+            double carry = 0.0;
+            float ar = 0.0f, ag = 0.0f, ab = 0.0f, ad = 0.0f, aa = 0.0f;
+            for (int64_t s0 = 0; s0 < n; s0 += 32) {
+                const bool cv = s0 + j < n;
+                const int64_t ci = cv ? s0 + j : n - 1;
+                const int64_t cidx = b + ci;
+                const float cta = p.t0[cidx], ctb = p.t1[cidx];
+                const float ctm = 0.5f * (cta + ctb);
+                const f32x4 y = yrow[ci];
+                const float sdt = cv ? y[3] * (ctb - cta) : 0.0f;
+                double incl = (double)sdt;
+#pragma unroll
+                for (int off = 1; off < 32; off <<= 1) {
+                    const double yv = __shfl_up(incl, off, 32);
+                    if (j >= off) incl += yv;
+                }
+                const float excl = (float)(carry + incl - (double)sdt);
+                const float alpha = 1.0f - expf(-sdt);
+                const float w = expf(-excl) * alpha;
+                if (cv && h == 0) {
+                    if (p.weights) p.weights[cidx] = w;
+                    ar += w * y[0];
+                    ag += w * y[1];
+                    ab += w * y[2];
+                    ad += w * ctm;
+                    aa += w;
+                }
+                carry += __shfl(incl, 31, 32);
+            }
+            float bgc[3];
+            background(bg, dx, dy, dz, lane, bgc);
+            const float r = (float)wave32_sum((double)ar), g = (float)wave32_sum((double)ag),
+                        bb = (float)wave32_sum((double)ab);
+            const float dd = (float)wave32_sum((double)ad), a = (float)wave32_sum((double)aa);
+            if (lane == 0) {
+                float orr = r, og = g, ob = bb;
+                if (bg.mode != ACN_BG_NONE) {
+                    const float om = 1.0f - a;
+                    orr = r + om * bgc[0];
+                    og = g + om * bgc[1];
+                    ob = bb + om * bgc[2];
+                }
+                p.rgb[ray * 3 + 0] = orr;
+                p.rgb[ray * 3 + 1] = og;
+                p.rgb[ray * 3 + 2] = ob;
+                p.depth[ray] = dd;
+                p.acc[ray] = a;
+            }
+        }
+        __syncthreads();   // cum / qhead / done / ybuf reused by the next round
+    }
+}
+
 }  // namespace
 
 extern "C" int acn_render_packed_fwd(const float* rays, int64_t ld, int64_t N, const int64_t* chunk_starts,
@@ -3300,6 +3443,12 @@ extern "C" int acn_render_packed_fwd(const float* rays, int64_t ld, int64_t N, c
                       rgb, depth, weights, acc};
     const int64_t wgs = (N + 15) / 16;
     const dim3 grid((unsigned)(wgs < num_cus() ? wgs : num_cus())), block(1024);
+    if (ACN_OCC_WS && cfg.routing == 0) {   // one expert: the workgroup's rays share their tiles (bit-identical)
+        if (interp == 1) hipLaunchKernelGGL(occ_ws_kernel<1>, grid, block, 0, s, cfg, b, p);
+        else if (interp == 0) hipLaunchKernelGGL(occ_ws_kernel<0>, grid, block, 0, s, cfg, b, p);
+        else hipLaunchKernelGGL(occ_ws_kernel<2>, grid, block, 0, s, cfg, b, p);
+        return acn_check_launch("acn_render_packed_fwd");
+    }
 #define ACN_OCC_LAUNCH(I, KL, R) hipLaunchKernelGGL((occ_render_kernel<I, KL, R>), grid, block, 0, s, cfg, b, p)
     ACN_DISPATCH(ACN_OCC_LAUNCH);
 #undef ACN_OCC_LAUNCH
