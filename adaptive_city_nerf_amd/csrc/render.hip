@@ -1450,6 +1450,9 @@ __device__ __forceinline__ uint32_t ray_expert_mask(const FieldCfg& cfg, int rou
 #define ACN_SLOTS_BAND 0
 #endif
 #ifndef ACN_SLOTS_WS
+#ifndef ACN_SLOTS_WS_RAYMAJOR
+#define ACN_SLOTS_WS_RAYMAJOR 0
+#endif
 #define ACN_SLOTS_WS 0  // 1: render_slots_kernel rounds share their field tiles (as render_ws_kernel); measured slower
 #endif
 #ifndef ACN_SLOTS_THREADS
@@ -1631,7 +1634,11 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
                 if (lane == 0) item = __hip_atomic_fetch_add(&qhead, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 item = __builtin_amdgcn_readlane(item, 0);
                 if (item >= nr * T) break;
+#if ACN_SLOTS_WS_RAYMAJOR  // each ray's tiles consecutive: a wave mostly stays on one ray (fewer re-folds)
+                const int slot = item / T, tile = item - slot * T;
+#else
                 const int tile = item / nr, slot = item - tile * nr;
+#endif
                 const int64_t tray = (int64_t)__builtin_amdgcn_readfirstlane((int)wray[slot]);
                 if (tray != cur) {
                     const float* rp = p.rays + tray * 8;

@@ -64,7 +64,12 @@ def test_work_shared_render_bitwise_equal_render_kernel(tag, active, S, jitter, 
         new = ops.render_stratified(rays, S, specs, routing, active, bg[0], tau=0.0, jitter=jit)
         old = ops.render_stratified(rays, S, specs, routing, active, bg[0], tau=TAU_OLD, jitter=jit)
     for o, r, what in zip(new[::3] + new[1:2], old[::3] + old[1:2], ("rgb", "acc", "depth")):
-        assert _same(o, r), f"{tag} S={S} n={n} jitter={jitter}: {what} differs from render_kernel"
+        if not _same(o, r):
+            a, b = o.cpu().numpy().reshape(n, -1), r.cpu().numpy().reshape(n, -1)
+            bad = np.nonzero(np.any(a != b, axis=1))[0]
+            raise AssertionError(f"{tag} S={S} n={n} jitter={jitter}: {what} differs from the per-wave path on "
+                                 f"{bad.size} rays (first {bad[:6].tolist()}), max |diff| "
+                                 f"{float(np.nanmax(np.abs(a - b)))}; e.g. {a[bad[0]].tolist()} vs {b[bad[0]].tolist()}")
     wn, wo = new[2].cpu().numpy(), old[2].cpu().numpy()
     diff = wn != wo
     assert not np.any(diff & ~((np.abs(wo) < 1e-38) & (np.abs(wn) < 1e-38))), \
