@@ -259,6 +259,26 @@ def broadcast_experts(model, group=None):
 # ============================================================================ one meta step
 # train_step's FOMAML steps through the cached GraphedMetaStep (ACN_FAST_META=0: the eager step every time)
 FAST_META_STEP = os.environ.get("ACN_FAST_META", "1") != "0"
+# Visit each task's support and query rays in ray_order_kernel's direction-cell order (one permutation of the
+# task's rays and colours per outer step, before its inner loop).  The reference draws a task's rays at random
+# (task_dataset.py), so the order of rays inside a task carries no meaning; the losses are means over rays
+# (equal up to fp summation order).  The hash-grid gathers of the 8 inner renders and the query render then
+# see neighbouring rays together.
+TASK_RAY_ORDER = os.environ.get("ACN_META_TASK_ORDER", "0") != "0"
+
+
+def _ordered_part(part: Mapping[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+    """{"rays", "rgbs"} of one task part in direction-cell order (TASK_RAY_ORDER), or unchanged."""
+    rays = part["rays"]
+    n = int(rays.shape[0])
+    if not TASK_RAY_ORDER or not rays.is_cuda or n < 2 or n > 8192:
+        return part
+    from .ray_rendering import _train_order
+    order, _ = _train_order(rays)
+    out = dict(part)
+    out["rays"] = rays.index_select(0, order)
+    out["rgbs"] = part["rgbs"].index_select(0, order)
+    return out
 
 
 def _graph_eligible(P, model, optimizer, scheduler, grad_scaler, group) -> bool:
@@ -368,8 +388,8 @@ def _train_step_eager(P, step, model, optimizer, task_data, scheduler=None, grad
                 sup_i, qry_i = task.support, task.query
             else:
                 sup_i, qry_i = task["support"], task["query"]
-            sup_i = to_device_tree(sup_i, device)
-            qry_i = to_device_tree(qry_i, device)
+            sup_i = _ordered_part(to_device_tree(sup_i, device))
+            qry_i = _ordered_part(to_device_tree(qry_i, device))
             time_data += time.perf_counter() - t1
             n_sup, n_q = int(sup_i["rays"].shape[0]), int(qry_i["rays"].shape[0])
             if n_sup == 0 or n_q == 0:
@@ -537,6 +557,8 @@ class GraphedMetaStep:
         sup, qry = (task.support, task.query) if hasattr(task, "support") else (task["support"], task["query"])
         st = self.static[cid]
         for part, src in (("support", sup), ("query", qry)):
+            if src["rays"].shape[0] == st[part]["rays"].shape[0]:
+                src = _ordered_part(src)
             if src["rays"].shape[0] != st[part]["rays"].shape[0]:
                 raise ValueError(f"GraphedMetaStep: region {cid} was captured for {st[part]['rays'].shape[0]} "
                                  f"{part} rays, got {src['rays'].shape[0]}")

@@ -449,6 +449,9 @@ def main():
     ap.add_argument("--driver", choices=["step", "runtime_adapt"], default="step",
                     help="c5: time RoutedAdaptStep calls (step), or the drop-in train.runtime_adapt(steps=K) over a "
                          "loader-like list of device batches (what a reference caller of runtime_adapt gets)")
+    ap.add_argument("--meta-task-order", type=int, choices=[0, 1], default=0,
+                    help="meta: visit each task's support / query rays in direction-cell order (one permutation per "
+                         "task and outer step; meta_train.TASK_RAY_ORDER)")
     ap.add_argument("--diag-shared-table", action="store_true",
                     help="diagnostic (c3/c4): every expert reads expert 0's hash table (one 128 MiB table instead of "
                          "K: isolates the Infinity-Cache capacity effect; outputs differ from the real render)")
@@ -600,6 +603,7 @@ def main():
         # the later ones replay the per-region task graphs + the outer graph (meta_train.GraphedMetaStep,
         # cached on the optimizer); --no-graph: ACN_FAST_META off, every step eager
         MT.FAST_META_STEP = not a.no_graph
+        MT.TASK_RAY_ORDER = a.meta_task_order
 
         def step():
             it[0] += 1
@@ -1202,7 +1206,8 @@ def main():
                                     "GPU: per-region task graphs + outer graph (meta_train.GraphedMetaStep)"
                                     + (" (disabled)" if a.no_graph else ""),
                         "experts": 4, "regions": 4, "tasks_per_region": 3,
-                        "inner_iter": a.inner_iter if a.workload == "meta" else None},
+                        "inner_iter": a.inner_iter if a.workload == "meta" else None,
+                        "task_ray_order": "direction cells" if a.meta_task_order else "as drawn"},
                "clusters": {"workload": "cluster creation (create_clusters.py, example dataset g22 configuration): "
                                         "one 1536x2048 frame per step -- ray generation + Voronoi routing of "
                                         "256 samples x 4 centroids per ray (YZ, margin 1.1) + per-expert AABB "
