@@ -12,7 +12,3 @@ for i in 1 2; do
     python -c "import json; a=json.load(open('$O/c5_bg${b}_$i.json')); r=a['roofline']; print('c5 bg_side=$b', a['value'], a['ms_per_step'], r['kernel_ms'], r['secondary'].get('kernel_ms'), a['val_psnr_db'])"
   done
 done
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --workload c5 --no-cpu-baseline > $O/c5_prof.json 2>/dev/null || exit 4
-f=$(find $O/prof -name '*kernel_stats.csv' | head -1); cp $f $O/c5_kernel_stats.csv
-find $O/prof -type f ! -name '*kernel_stats.csv' -delete
-grep -E "routed_scan|background_bwd|bg_bwd_reduce|adam_slots|hashgrid_bwd" $O/c5_kernel_stats.csv | cut -c1-120
