@@ -100,48 +100,36 @@ __global__ void __launch_bounds__(kBlk) routed_count_kernel(const float* __restr
 // segment can overflow): the expert-parallel send buffer, grouped by owner, with host-known split sizes
 __global__ void __launch_bounds__(1024) routed_scan_kernel(int32_t* __restrict__ blk_cnt, int64_t nblk, int K,
                                                            int align, Caps caps, int64_t* __restrict__ starts) {
-    // all K experts' scans at once: per-thread chunk sums, an inclusive wave scan (shuffles, no
-    // barriers), then the 16 wave totals through LDS (one barrier) -- integer sums, so the result equals
-    // the serial prefix sums exactly (a Hillis-Steele pass per expert cost 20 barriers each)
-    __shared__ int64_t wtot[16][kMaxK];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int64_t per = (nblk + 1023) / 1024;
-    const int64_t b0 = tid * per, b1 = b0 + per < nblk ? b0 + per : nblk;
-    int64_t sum[kMaxK], incl[kMaxK];
-#pragma unroll
-    for (int k = 0; k < kMaxK; ++k) sum[k] = 0;
-    for (int64_t b = b0; b < b1; ++b)
-#pragma unroll
-        for (int k = 0; k < kMaxK; ++k)
-            if (k < K) sum[k] += blk_cnt[b * K + k];
-#pragma unroll
-    for (int k = 0; k < kMaxK; ++k) {
-        int64_t v = sum[k];
+    // wave k scans expert k's block counts: each lane sums a contiguous run of blocks, one inclusive wave
+    // scan of the 64 run totals, then each lane writes its run's exclusive prefixes.  Integer sums, so the
+    // result equals the serial prefix sums exactly (the previous form had every wave scan all K experts)
+    static_assert(kMaxK <= 16, "one wave per expert in a 1024-thread block");
+    __shared__ int64_t etot[kMaxK];   // expert k's pair count
+    const int tid = threadIdx.x, lane = tid & 63, k = tid >> 6;
+    if (k < K) {
+        const int64_t per = (nblk + 63) / 64;
+        const int64_t b0 = lane * per, b1 = b0 + per < nblk ? b0 + per : nblk;
+        int64_t sum = 0;
+        for (int64_t b = b0; b < b1; ++b) sum += blk_cnt[b * K + k];
+        int64_t v = sum;
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
             const int64_t u = __shfl_up(v, off);
             if (lane >= off) v += u;
         }
-        incl[k] = v;
-        if (lane == 63 && k < K) wtot[w][k] = v;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kMaxK; ++k) {
-        if (k >= K) break;
-        int64_t run = incl[k] - sum[k];
-        for (int i = 0; i < w; ++i) run += wtot[i][k];
+        int64_t run = v - sum;
         for (int64_t b = b0; b < b1; ++b) {
             const int32_t c = blk_cnt[b * K + k];
             blk_cnt[b * K + k] = (int32_t)run;
             run += c;
         }
+        if (lane == 63) etot[k] = v;
     }
+    __syncthreads();
     if (tid == 0) {
         int64_t base = 0;
         for (int k = 0; k < K; ++k) {
-            int64_t total = 0;
-            for (int i = 0; i < 16; ++i) total += wtot[i][k];
+            const int64_t total = etot[k];
             starts[k] = caps.fixed ? caps.off[k] : base;
             starts[K + 1 + k] = total;                        // real pair count of expert k
             base += (total + align - 1) / align * align;      // segment padded to a multiple of align

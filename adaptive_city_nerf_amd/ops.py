@@ -319,12 +319,16 @@ def volume_render_bwd(rgb_sigma: torch.Tensor, t_vals: torch.Tensor, bg_rgb: Opt
     return g_rs, g_bg
 
 
-def mse_linear_fwd(pred: torch.Tensor, gt: torch.Tensor) -> torch.Tensor:
-    """compute_mse_loss's loss in color_space 'linear' (acn_mse_linear_fwd): a 0-d device tensor."""
+def mse_linear_fwd(pred: torch.Tensor, gt: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """compute_mse_loss's loss in color_space 'linear' (acn_mse_linear_fwd): a 0-d device tensor (written into
+    ``out``, a one-element fp32 tensor on the same device, when given)."""
     p, g = _f32(pred).reshape(-1), _f32(gt).reshape(-1)
     if p.numel() != g.numel() or p.numel() == 0:
         raise ValueError(f"mse_linear: pred / gt sizes {p.numel()} / {g.numel()}")
-    out = torch.empty((), device=p.device, dtype=torch.float32)
+    if out is None:
+        out = torch.empty((), device=p.device, dtype=torch.float32)
+    elif out.numel() != 1 or out.dtype != torch.float32 or out.device != p.device:
+        raise ValueError("mse_linear_fwd: out must be a one-element fp32 tensor on the inputs' device")
     ws = _mse_ws(p.device)
     check(_lib.lib().acn_mse_linear_fwd_ws(ptr(p), ptr(g), p.numel(), ptr(out), ptr(ws), ws.numel(), stream_of(p)),
           "acn_mse_linear_fwd_ws")

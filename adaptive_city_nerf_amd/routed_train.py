@@ -62,6 +62,9 @@ ADAM_SEGMAP = os.environ.get("ACN_ADAM_SEGMAP", "1") != "0"
 # beside the step's forward / backward, the late pass after the clip coefficient (the two passes
 # contend for HBM with the step's own kernels: C5 1.75 -> 2.0 ms, so it stays off)
 ADAM_EARLY = os.environ.get("ACN_ADAM_EARLY", "0") != "0"   # measured slower: off
+# The background head's backward (two small launches) on a side stream beside the experts' backward chain
+# (blend, MLP, table scatter), joined before the clip / Adam pass that reads its gradients
+BG_SIDE = os.environ.get("ACN_BG_SIDE", "0") != "0"   # measured within noise: off
 
 
 def draw_jitter(n: int, S: int, device) -> torch.Tensor:
@@ -209,7 +212,7 @@ class RoutedAdaptStep:
         # gradient is zero, so they need no clip coefficient; the late pass updates the touched segments and the
         # dense tensors.  Not with use_amp (a found_inf skip is decided after the backward).
         self.early = ADAM_EARLY and self.segmaps is not None and self.amp is None
-        self.side = torch.cuda.Stream(dev) if self.early else None
+        self.side = torch.cuda.Stream(dev) if (self.early or BG_SIDE) else None
         self.replays = 0          # graph replays
         self.steps_done = 0       # every update this object ran (eager and replayed): Adam table rows used
         self.graph = None
@@ -238,8 +241,11 @@ class RoutedAdaptStep:
             for g in self.gtables:
                 g.zero_()
         u, t = self.u[:N], self.t[:N]
-        if self.jitter_mode == "draw":
-            u.copy_(JITTER(N, S, dev))  # the reference's rand_like(low) draw
+        if self.jitter_mode == "draw":   # the reference's rand_like(low) draw
+            if JITTER is draw_jitter:
+                torch.rand(N, S, device=dev, out=u)   # straight into the step's buffer (no copy launch)
+            else:
+                u.copy_(JITTER(N, S, dev))
         check(L.acn_routed_count(ptr(self.rays), N, S, ptr(u), C.byref(self.routing), ALIGN, ptr(t),
                                  ptr(self.seg), ptr(self.rws), self.rws.numel(), s), "acn_routed_count")
         check(L.acn_routed_scatter(ptr(self.rays), N, S, K, ptr(t), ptr(self.seg), C.cast(self._mins, C.c_void_p),
@@ -249,7 +255,7 @@ class RoutedAdaptStep:
         enc = self.model.submodules[0].xyz_encoder
         capturing = torch.cuda.is_current_stream_capturing()   # no timing events inside a capture
         det = torch.are_deterministic_algorithms_enabled()
-        ev_early = None
+        ev_early = ev_bg = None
         if self.early and not det:
             # fork: the step's now[] marks from its pair list, then Adam's early pass, on the side stream
             main = torch.cuda.current_stream(dev)
@@ -284,10 +290,22 @@ class RoutedAdaptStep:
             rs_ = rs.detach()
             bg = ops.background_fwd(dirs, self.bg_spec)
             rgb = ops.volume_render(rs_, t, bg)[0]
-            loss = ops.mse_linear_fwd(rgb, rgbs)
+            loss = ops.mse_linear_fwd(rgb, rgbs, out=self.loss)
             g_rgb = ops.mse_linear_bwd(rgb, rgbs, self._one if self.amp is None else self.amp.scale)
             g_rs, g_bg = ops.volume_render_bwd(rs_, t, bg, 1.0, g_rgb, None, None, None)
-            ops.background_bwd(dirs, self.bg_spec, g_bg, self.gbg)
+            if BG_SIDE and self.side is not None:
+                # fork: the head's backward beside the experts' chain; joined before Adam (ev_bg)
+                main = torch.cuda.current_stream(dev)
+                e_fork = torch.cuda.Event()
+                e_fork.record(main)
+                self.side.wait_event(e_fork)
+                with torch.cuda.stream(self.side):
+                    ops.background_bwd(dirs, self.bg_spec, g_bg, self.gbg)
+                    ev_bg = torch.cuda.Event()
+                    ev_bg.record(self.side)
+                g_bg.record_stream(self.side)
+            else:
+                ops.background_bwd(dirs, self.bg_spec, g_bg, self.gbg)
         elif self.bg_spec is not None:
             dirs.copy_(rays[:, 3:6])
             bg = ops.background_fwd(dirs, self.bg_spec).requires_grad_(True)
@@ -305,7 +323,8 @@ class RoutedAdaptStep:
             g_rs = grads[0]
             for g, buf in zip(grads[1:], self.gbg):
                 buf.copy_(g)
-        self.loss.copy_(loss.detach())
+        if loss is not self.loss:
+            self.loss.copy_(loss.detach())
         gout = ops.routed_blend_bwd(g_rs.reshape(M, 4).contiguous(), self.pidx, self.pw, live=self.seg[K:K + 1])
         check(mfn("acn_mlp_train_bwd_dw_pairs")(ptr(self.h0), ptr(self.sh), ptr(self.out), ptr(gout), ptr(self.seg), K,
                                            ptr(self.mws), ptr(self.dw), ptr(self.gh0), s), "acn_mlp_train_bwd_dw_pairs")
@@ -336,6 +355,8 @@ class RoutedAdaptStep:
             bhook.append((b0, b1))
         if ev_early is not None:
             torch.cuda.current_stream(dev).wait_event(ev_early)   # join
+        if ev_bg is not None:
+            torch.cuda.current_stream(dev).wait_event(ev_bg)      # join: the head's gradients
         self.adam.step(self.seg, self.grad_clip, self.table_sumsq if self.tele else None,
                        hook=EVENT_HOOK if self.graph is None and not capturing else None, amp=self.amp,
                        phase=2 if self.early else 0)
