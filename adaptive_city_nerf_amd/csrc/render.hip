@@ -1221,6 +1221,15 @@ __global__ void __launch_bounds__(1024, 4) render_ws_kernel(FieldCfg cfg, BgArgs
             const float px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;
             float yr, yg, yb, ys;
             container_tile<INTERP, 0, FOLD>(cfg, W, px, py, pz, shv, cb, &folded, lane, yr, yg, yb, ys);
+#if ACN_WS_CHECK  // diagnostic build only: the tile evaluated twice; a differing lane poisons its sample (NaN rgb)
+            {
+                float cr, cg, cbb, cs;
+                container_tile<INTERP, 0, FOLD>(cfg, W, px, py, pz, shv, cb, &folded, lane, cr, cg, cbb, cs);
+                if (__float_as_uint(cr) != __float_as_uint(yr) || __float_as_uint(cg) != __float_as_uint(yg) ||
+                    __float_as_uint(cbb) != __float_as_uint(yb) || __float_as_uint(cs) != __float_as_uint(ys))
+                    yr = __int_as_float(0x7fc00000);
+            }
+#endif
             if (h == 0 && s < S) {
                 f32x4 v;
                 v[0] = yr, v[1] = yg, v[2] = yb, v[3] = ys;
