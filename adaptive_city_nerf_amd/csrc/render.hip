@@ -1093,6 +1093,9 @@ __global__ void __launch_bounds__(1024, 4) render_kernel(FieldCfg cfg, BgArgs bg
 #define ACN_RENDER_WS 1
 #endif
 constexpr int kWsMaxS = 256;   // LDS field buffer: 16 rays x kWsMaxS samples x 16 B = 64 KB
+#ifndef ACN_WS_PREFOLD
+#define ACN_WS_PREFOLD 1  // fold each round ray's SH colour bias once, at the round start (not per tile)
+#endif
 
 // composite one ray from its samples' field values in LDS (ys[s] = rgb, sigma of sample s, as the field tile
 // returned them): render_ray's exact sequence without early termination -- t and dist, the volume_render
@@ -1184,10 +1187,20 @@ __global__ void __launch_bounds__(1024, 4) render_ws_kernel(FieldCfg cfg, BgArgs
         const int nr = (int)min((int64_t)16, hi - base);
         if (threadIdx.x == 0) qhead = 0;
         if (threadIdx.x < 16) done[threadIdx.x] = 0;
+        constexpr bool PRE = FOLD && ACN_WS_PREFOLD;
+        if (PRE && wave < nr) {
+            // wave w folds round slot w's colour bias into cbuf[w] once; every tile of that ray reads it there
+            const int64_t r0 = p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[base + wave]) : base + wave;
+            const float* rp = p.rays + r0 * 8;
+            float sh[16], sv[8];
+            dir_sh(rp[3], rp[4], rp[5], sh);
+            sh_rows_for_half(sh, h, sv);
+            fold_sh_bias(W, sv, lane, cbuf + wave * 64);
+        }
         __syncthreads();
         int64_t cur = -1;
         uint32_t folded = 0u;
-        float shv[8];
+        float shv[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
         float ox = 0.0f, oy = 0.0f, oz = 0.0f, dx = 0.0f, dy = 0.0f, dz = 0.0f, near = 0.0f, far = 0.0f;
         const float* jit = nullptr;
         for (;;) {
@@ -1202,11 +1215,17 @@ __global__ void __launch_bounds__(1024, 4) render_ws_kernel(FieldCfg cfg, BgArgs
                 ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
                 near = rp[6], far = rp[7];
                 jit = p.jitter ? p.jitter + ray * S : nullptr;
-                float sh[16];
-                dir_sh(dx, dy, dz, sh);
-                sh_rows_for_half(sh, h, shv);
-                folded = 0u;
+                if (!PRE) {
+                    float sh[16];
+                    dir_sh(dx, dy, dz, sh);
+                    sh_rows_for_half(sh, h, shv);
+                    folded = 0u;
+                }
                 cur = ray;
+            }
+            if (PRE) {   // the slot's pre-folded bias (shv is not read by a folded field tile)
+                cb = cbuf + slot * 64;
+                folded = 1u;
             }
             const int s = tile * 32 + j;
             const int sc = s < S ? s : S - 1;
