@@ -2823,9 +2823,14 @@ __global__ void __launch_bounds__(1024) ray_order_kernel(const float* __restrict
         return fabsf(u) < 1.0e30f && fabsf(v) < 1.0e30f;
     };
     float umin = 3.0e38f, vmin = 3.0e38f, umax = -3.0e38f, vmax = -3.0e38f;
-    for (int i = tid; i < N; i += 1024) {
-        float u, v;
-        if (coords(i, u, v)) umin = fminf(umin, u), umax = fmaxf(umax, u), vmin = fminf(vmin, v), vmax = fmaxf(vmax, v);
+    // each thread's (u, v) kept in registers for the cell pass below (one coordinate pass over dir[], not two)
+    float cu[PER], cv[PER];
+    bool cok[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int i = tid + q * 1024;
+        cok[q] = i < N && coords(i, cu[q], cv[q]);
+        if (cok[q]) umin = fminf(umin, cu[q]), umax = fmaxf(umax, cu[q]), vmin = fminf(vmin, cv[q]), vmax = fmaxf(vmax, cv[q]);
     }
 #if ACN_ORDER_DIAG == 2  // diagnostic only: + mean direction and the coordinate pass, identity order
     for (int i = tid; i < N; i += 1024) order[i] = i + (int)(umin * 0.0f + umax * 0.0f);
@@ -2840,12 +2845,14 @@ __global__ void __launch_bounds__(1024) ray_order_kernel(const float* __restrict
 #endif
     const float su = umax > umin ? 63.999f / (umax - umin) : 0.0f;
     const float sv = vmax > vmin ? 63.999f / (vmax - vmin) : 0.0f;
-    for (int i = tid; i < N; i += 1024) {
-        float u, v;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int i = tid + q * 1024;
+        if (i >= N) break;
         int c = ACN_ORDER_BINS - 1;
-        if (coords(i, u, v)) {
-            const uint32_t qu = (uint32_t)fminf(fmaxf((u - umin) * su, 0.0f), 63.0f);
-            const uint32_t qv = (uint32_t)fminf(fmaxf((v - vmin) * sv, 0.0f), 63.0f);
+        if (cok[q]) {
+            const uint32_t qu = (uint32_t)fminf(fmaxf((cu[q] - umin) * su, 0.0f), 63.0f);
+            const uint32_t qv = (uint32_t)fminf(fmaxf((cv[q] - vmin) * sv, 0.0f), 63.0f);
             c = (int)(spread6(qu) | (spread6(qv) << 1));
         }
         cell_of[i] = (uint16_t)c;
