@@ -467,4 +467,49 @@ __device__ __forceinline__ float tval(float near, float far, int s, int S, const
     return lo + (hi - lo) * jit[s];
 }
 
+// ---- VALU -> MFMA operand fence.  The fp16 B fragments of every MLP layer are written by
+// v_cvt_pk_f16_f32 (VALU).  hipcc (ROCm 7.2) leaves the 2 wait states of its gfx950 VALU -> MFMA rule between
+// such a conversion and the MFMA reading it, and on MI355X that left rare, timing-dependent stale operands
+// (round 4: 16 columns of a tile off by ~1e-4; a 1-ulp render difference when the stale register held the
+// neighbouring ray's nearly equal value).  A pad placed by position is not enough: the compiler sinks the
+// last conversions past a scheduling barrier (tools/hazard_audit.py found 1031 such sites in render.hip).
+// So the fence takes the fragments as "+v" operands of ONE asm statement holding the pad: every conversion
+// must have retired into the fragments before it, every MFMA reads the asm's outputs after it, and the
+// audit checks that no VALU writes an MFMA A/B operand fewer than 16 wait states before it.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+#ifndef ACN_OPND_FENCE
+#define ACN_OPND_FENCE 1   // 0: diagnostic build only, the fence compiled out (the round-4 state without its pad)
+#endif
+#if ACN_OPND_FENCE
+#define ACN_OPND_PAD "s_nop 7\n\ts_nop 7"
+#else
+#define ACN_OPND_PAD ""
+#endif
+__device__ __forceinline__ void opnd_fence(f16x8& a) { asm volatile(ACN_OPND_PAD : "+v"(a)); }
+__device__ __forceinline__ void opnd_fence(f16x8& a, f16x8& b) { asm volatile(ACN_OPND_PAD : "+v"(a), "+v"(b)); }
+__device__ __forceinline__ void opnd_fence(f16x8& a, f16x8& b, f16x8& c, f16x8& d) {
+    asm volatile(ACN_OPND_PAD : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+}
+__device__ __forceinline__ void opnd_fence(f16x8& a, f16x8& b, f16x8& c, f16x8& d, f16x8& e, f16x8& f, f16x8& g,
+                                           f16x8& h) {
+    asm volatile(ACN_OPND_PAD : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e), "+v"(f), "+v"(g), "+v"(h));
+}
+// one plane of N fragments (N = 1, 2, 4, 8)
+template <int N>
+__device__ __forceinline__ void opnd_fence_n(f16x8 (&x)[N]) {
+    static_assert(N == 1 || N == 2 || N == 4 || N == 8, "opnd_fence_n: N in {1, 2, 4, 8}");
+    if constexpr (N == 1) opnd_fence(x[0]);
+    else if constexpr (N == 2) opnd_fence(x[0], x[1]);
+    else if constexpr (N == 4) opnd_fence(x[0], x[1], x[2], x[3]);
+    else opnd_fence(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7]);
+}
+// hi and lo planes of N fragments (N = 1, 2, 4)
+template <int N>
+__device__ __forceinline__ void opnd_fence_n(f16x8 (&x)[N], f16x8 (&y)[N]) {
+    static_assert(N == 1 || N == 2 || N == 4, "opnd_fence_n: N in {1, 2, 4}");
+    if constexpr (N == 1) opnd_fence(x[0], y[0]);
+    else if constexpr (N == 2) opnd_fence(x[0], x[1], y[0], y[1]);
+    else opnd_fence(x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]);
+}
+
 }  // namespace acn

@@ -296,6 +296,7 @@ __device__ __forceinline__ void fwd_layer(const float* W, int ld, const float* b
     (void)ROWS;
     f16x8 bh[2 * KT];
     cvt_tiles<KT>(X, bh);
+    acn::opnd_fence_n<2 * KT>(bh);   // VALU -> MFMA operand fence (acn_device.h)
     const _Float16* Wh = reinterpret_cast<const _Float16*>(W);
 #pragma unroll
     for (int to = 0; to < NT; ++to) {
@@ -315,6 +316,7 @@ __device__ __forceinline__ void fwd_layer(const float* W, int ld, const float* b
     const float usc = ldexpf(1.0f, -k);
     f16x8 bh[2 * KT], bl[2 * KT];
     split_tiles<KT>(X, k, bh, bl);
+    acn::opnd_fence_n<2 * KT>(bh, bl);
     const _Float16* Wh = reinterpret_cast<const _Float16*>(W);
     const _Float16* Wlo = Wh + ROWS * ld;
 #pragma unroll
@@ -361,11 +363,13 @@ __device__ __forceinline__ void bwd_layer(const float* W, int ld, const f32x16 (
 #if ACN_TRAIN_AMP
     f16x8 bh[2 * KT];
     cvt_tiles<KT>(dY, bh);
+    acn::opnd_fence_n<2 * KT>(bh);
 #else
     const int k = tile_scale_exp<KT>(dY);
     const float usc = ldexpf(1.0f, -k);
     f16x8 bh[2 * KT], bl[2 * KT];
     split_tiles<KT>(dY, k, bh, bl);
+    acn::opnd_fence_n<2 * KT>(bh, bl);
 #endif
     const _Float16* Wh = reinterpret_cast<const _Float16*>(W);
     const _Float16* Wlo = Wh + ROWS * ld;

@@ -24,7 +24,6 @@ using namespace acn;
 #ifndef ACN_MLP_F16X3
 #define ACN_MLP_F16X3 1  // MLP on v_mfma_f32_32x32x16_f16 with a 3-term fp16 split (hi*hi + hi*lo + lo*hi)
 #endif
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 #ifndef ACN_SLOTS
 #define ACN_SLOTS 1  // routed K > 2: stage the two most needed experts per workgroup (render_slots_kernel)
@@ -250,35 +249,20 @@ __device__ __forceinline__ void split_acc2(const f32x16& a0, const f32x16& a1, f
     }
 }
 
-// out[T] = bias + W . X over NK k-steps of 16, three fp16 products per k-step (small terms first)
-// Wait states between the operand split (VALU: v_cvt_pk_f16_f32 writes the B fragments) and the layer's first
-// MFMA.  hipcc (ROCm 7.2) separates them by the 2 wait states of its gfx950 VALU -> MFMA rule; in the routed
-// render's schedule that left rare, timing-dependent wrong B operands: 16 consecutive columns of a tile off by
-// ~1e-4 relative, different run to run (a self-check build that evaluated every tile twice in a row saw ~57
-// mismatching rays per 10 K=8 renders; with this pad, none).  0: compiler only, 1: s_nop 2,
-// 2: 16 wait states, 3: scheduling barrier only.
-#ifndef ACN_X3_NOP
-#define ACN_X3_NOP 2
-#endif
+// out[T] = bias + W . X over NK k-steps of 16, three fp16 products per k-step (small terms first).
+// The B fragments (bh, bl: v_cvt_pk_f16_f32 results) pass through the operand fence first (acn_device.h,
+// DESIGN.md §4j): the round-4 pad at this point (ACN_X3_NOP) was placed by position, and the compiler still
+// sank the last conversions past it into the k-step loop, 2 wait states before their MFMA.
 // REV: k-steps in reverse order (colour layer 0 with per-lane SH: the SH k-step first, the order the per-ray
 // fold accumulates in, so the result is bit-identical to fold_sh_bias + the folded layer)
 template <int NT, int NK, bool REV = false>
 __device__ __forceinline__ void layer_x3(const float* W, int seg, const float* bias_base, int bt, int lane, int h,
-                                         const f16x8 (&bh)[NK], const f16x8 (&bl)[NK], f32x16 (&out)[NT],
+                                         f16x8 (&bh)[NK], f16x8 (&bl)[NK], f32x16 (&out)[NT],
                                          int nk_used = NK) {
+    if (nk_used == 1) opnd_fence(bh[REV ? NK - 1 : 0], bl[REV ? NK - 1 : 0]);
+    else opnd_fence_n<NK>(bh, bl);
 #pragma unroll
     for (int T = 0; T < NT; ++T) out[T] = bias_frag_at(bias_base, bt + T, h);
-#if ACN_X3_NOP == 1
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_nop 2" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-#elif ACN_X3_NOP == 2
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-#elif ACN_X3_NOP == 3
-    __builtin_amdgcn_sched_barrier(0);
-#endif
 #pragma unroll
     for (int si = 0; si < NK; ++si) {
         if (si >= nk_used) break;
@@ -308,6 +292,7 @@ __device__ __forceinline__ void fold_sh_bias(const float* W, const float (&shv)[
     {   // k-step 1 of the colour-layer-0 image = head rows 16..31 = this half's SH values (shv)
         f16x8 sh_hi, sh_lo;
         split8(shv, sh_hi, sh_lo);
+        opnd_fence(sh_hi, sh_lo);   // the fold had no pad at all
         const float* f0 = W + PK_WC1 + (((0 * 2 + 1) * 2) * 64 + lane) * 4;
         const float* f1 = W + PK_WC1 + (((1 * 2 + 1) * 2) * 64 + lane) * 4;
         const f16x8 h0 = ldh8(f0), l0 = ldh8(f0 + 256), h1 = ldh8(f1), l1 = ldh8(f1 + 256);
@@ -447,7 +432,7 @@ __device__ __forceinline__ void hash_levels8(const ExpertMeta& em, int log2T, in
 // see fold_sh_bias): colour layer 0 then only runs the 8 k-steps of the [sigma_raw, geo] rows.
 // SHFIRST (with FOLD false): colour layer 0 runs unfolded on per-lane SH rows, the SH k-step before the
 // [sigma_raw, geo] one -- bit for bit the folded result of a ray whose lanes all carry its SH (the render of
-// compacted samples of several rays, render_routed_kernel)
+// compacted samples of several rays, ep_field_kernel)
 template <int INTERP, bool FOLD, bool SHFIRST = false>
 __device__ __forceinline__ void field_tile(const float* W, const ExpertMeta& em, int log2T, float px, float py,
                                            float pz, const float (&shv)[8], const float* cb, int lane, float& rr,
@@ -1093,6 +1078,9 @@ __global__ void __launch_bounds__(1024, 4) render_kernel(FieldCfg cfg, BgArgs bg
 #define ACN_RENDER_WS 1
 #endif
 constexpr int kWsMaxS = 256;   // LDS field buffer: 16 rays x kWsMaxS samples x 16 B = 64 KB
+#ifndef ACN_WS_CHECK
+#define ACN_WS_CHECK 0   // diagnostic self-check build (tools/dbg/selfcheck.py)
+#endif
 #ifndef ACN_WS_PREFOLD
 #define ACN_WS_PREFOLD 1  // fold each round ray's SH colour bias once, at the round start (not per tile)
 #endif
@@ -1215,11 +1203,11 @@ __global__ void __launch_bounds__(1024, 4) render_ws_kernel(FieldCfg cfg, BgArgs
                 ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
                 near = rp[6], far = rp[7];
                 jit = p.jitter ? p.jitter + ray * S : nullptr;
-                if (!PRE) {
+                if (!PRE || ACN_WS_CHECK) {
                     float sh[16];
                     dir_sh(dx, dy, dz, sh);
                     sh_rows_for_half(sh, h, shv);
-                    folded = 0u;
+                    if (!PRE) folded = 0u;
                 }
                 cur = ray;
             }
@@ -1240,10 +1228,12 @@ __global__ void __launch_bounds__(1024, 4) render_ws_kernel(FieldCfg cfg, BgArgs
             const float px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;
             float yr, yg, yb, ys;
             container_tile<INTERP, 0, FOLD>(cfg, W, px, py, pz, shv, cb, &folded, lane, yr, yg, yb, ys);
-#if ACN_WS_CHECK  // diagnostic build only: the tile evaluated twice; a differing lane poisons its sample (NaN rgb)
-            {
+#if ACN_WS_CHECK  // diagnostic build only: the tile evaluated twice; a differing lane poisons its sample (NaN rgb).
+            {   // The second evaluation runs colour layer 0 unfolded, SH k-step first: bit for bit the fold + folded
+                // layer (field_tile), so a stale operand in the per-ray fold is caught as well
                 float cr, cg, cbb, cs;
-                container_tile<INTERP, 0, FOLD>(cfg, W, px, py, pz, shv, cb, &folded, lane, cr, cg, cbb, cs);
+                field_tile<INTERP, false, true>(W, cfg.ex[0], cfg.log2T, px, py, pz, shv, nullptr, lane, cr, cg, cbb, cs);
+                cs = trunc_exp(cs);
                 if (__float_as_uint(cr) != __float_as_uint(yr) || __float_as_uint(cg) != __float_as_uint(yg) ||
                     __float_as_uint(cbb) != __float_as_uint(yb) || __float_as_uint(cs) != __float_as_uint(ys))
                     yr = __int_as_float(0x7fc00000);
@@ -1267,172 +1257,12 @@ __global__ void __launch_bounds__(1024, 4) render_ws_kernel(FieldCfg cfg, BgArgs
 }
 
 // ------------------------------------------------------------------------------------------
-// render_ws_kernel with the rays handed out at run time (render_dq_kernel, the ordered C2 path).  The static
-// rounds balance the tiles inside a CU, but each CU still owns 16 fixed rays, and CUs whose rays sit in
-// slow regions end last.  Here each XCD band of the visiting order is a queue (one device-scope counter per
-// band, zeroed by ray_order_kernel just before): a workgroup holds at most kDqLive of its band's rays at a
-// time in LDS slots, so the band keeps rays in reserve and the CUs that finish early take more of them.  A
-// wave works through its own slot's tiles; with nothing left there it takes the next ray of the band (while
-// the workgroup holds fewer than kDqLive), else any unclaimed tile of the workgroup's slots.  Only ray
-// indices cross CUs (the counter), never field values: tiles, LDS buffers and compositing stay in the
-// workgroup, with render_ws_kernel's arithmetic, so the outputs are bit-identical to render_kernel.
-#ifndef ACN_RENDER_DQ
-#define ACN_RENDER_DQ 0  // 1: band queues of rays (measured slower than render_ws_kernel)
-#endif
-constexpr int kDqSlots = 24;   // LDS ray slots (24 x 4 KB at S = 256; 158 KB of LDS in all)
-#ifndef ACN_DQ_LIVE
-#define ACN_DQ_LIVE 12         // rays a workgroup holds at once (the rest of its band stays in the queue)
-#endif
-
-template <int INTERP>
-__global__ void __launch_bounds__(1024, 4) render_dq_kernel(FieldCfg cfg, BgArgs bg, RenderParams p,
-                                                            int* __restrict__ bandq) {
-    constexpr bool FOLD = ACN_SHFOLD != 0;
-    __shared__ __attribute__((aligned(16))) float smem[PK_FLOATS];
-    __shared__ __attribute__((aligned(16))) float cbuf[FOLD ? 16 * 64 : 4];
-    __shared__ __attribute__((aligned(16))) f32x4 ybuf[kDqSlots * kWsMaxS];
-    __shared__ int sray[kDqSlots], snext[kDqSlots], sdone[kDqSlots];
-    __shared__ uint32_t slive;   // bit s: slot s holds a ray that is not composited yet
-    __shared__ int qempty;       // this workgroup saw its band's queue run out
-    const int S = p.S;
-    const int T = (S + 31) >> 5;
-    if (threadIdx.x < kDqSlots) {
-        snext[threadIdx.x] = T;   // nothing to claim in an empty slot
-        sdone[threadIdx.x] = 0;
-        sray[threadIdx.x] = 0;
-    }
-    if (threadIdx.x == 0) slive = 0u, qempty = 0;
-    stage_weights<1>(smem, p.packed);   // (ends with a workgroup barrier)
-    const float* W = smem;
-    const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    float* cb = FOLD ? cbuf + wave * 64 : nullptr;
-    const float step = 1.0f / (float)(S - 1);
-    const bool banded = (gridDim.x & 7) == 0;
-    const int band = banded ? (int)(blockIdx.x & 7) : 0;
-    const int64_t chunk = banded ? (p.N + 7) >> 3 : p.N;
-    const int64_t lo = min(p.N, (int64_t)band * chunk), hi = min(p.N, lo + chunk);
-    auto claim = [&](int sl) -> int {
-        int t = 0;
-        if (lane == 0) t = __hip_atomic_fetch_add(&snext[sl], 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        return __builtin_amdgcn_readlane(t, 0);
-    };
-    int my = -1;   // the slot this wave took from the queue (its tiles first)
-    int64_t cur = -1;
-    uint32_t folded = 0u;
-    float shv[8];
-    float ox = 0.0f, oy = 0.0f, oz = 0.0f, dx = 0.0f, dy = 0.0f, dz = 0.0f, near = 0.0f, far = 0.0f;
-    const float* jit = nullptr;
-    for (;;) {
-        int tile = -1, sl = -1;
-        if (my >= 0) {
-            const int t = claim(my);
-            if (t < T) tile = t, sl = my;
-            else my = -1;
-        }
-        // a new ray from the band, while the workgroup holds fewer than ACN_DQ_LIVE
-        if (tile < 0 && !__builtin_amdgcn_readfirstlane(qempty) &&
-            __builtin_popcount(__builtin_amdgcn_readfirstlane(slive)) < ACN_DQ_LIVE) {
-            int got = -1;
-            if (lane == 0) {
-                uint32_t freem = ~__hip_atomic_load(&slive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) &
-                                 ((1u << kDqSlots) - 1u);
-                while (freem) {
-                    const int s = __builtin_ctz(freem);
-                    const uint32_t old = __hip_atomic_fetch_or(&slive, 1u << s, __ATOMIC_ACQ_REL,
-                                                               __HIP_MEMORY_SCOPE_WORKGROUP);
-                    if (!(old & (1u << s))) { got = s; break; }
-                    freem &= ~(1u << s);
-                }
-                if (got >= 0) {
-                    const int q = __hip_atomic_fetch_add(&bandq[band], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const int64_t pos = lo + q;
-                    if (pos < hi) {
-                        sray[got] = p.order ? p.order[pos] : (int)pos;
-                        sdone[got] = 0;
-                        // tile 0 is this wave's; the others become claimable with this store
-                        __hip_atomic_store(&snext[got], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    } else {
-                        qempty = 1;
-                        __hip_atomic_fetch_and(&slive, ~(1u << got), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        got = -1;
-                    }
-                }
-            }
-            got = __builtin_amdgcn_readlane(got, 0);
-            if (got >= 0) tile = 0, sl = got, my = got;
-        }
-        // help: any unclaimed tile of the workgroup's live rays
-        if (tile < 0) {
-            uint32_t m = __builtin_amdgcn_readfirstlane(
-                __hip_atomic_load(&slive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-            while (m) {
-                const int s = __builtin_ctz(m);
-                m &= m - 1u;
-                const int t = claim(s);
-                if (t < T) { tile = t, sl = s; break; }
-            }
-        }
-        if (tile < 0) {
-            if (__builtin_amdgcn_readfirstlane(qempty)) break;   // the band is done; claimed tiles finish elsewhere
-            __builtin_amdgcn_s_sleep(2);                          // rays in flight will free slots
-            continue;
-        }
-        const int64_t ray = (int64_t)__builtin_amdgcn_readfirstlane(sray[sl]);
-        if (ray != cur) {
-            const float* rp = p.rays + ray * 8;
-            ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
-            near = rp[6], far = rp[7];
-            jit = p.jitter ? p.jitter + ray * S : nullptr;
-            float sh[16];
-            dir_sh(dx, dy, dz, sh);
-            sh_rows_for_half(sh, h, shv);
-            folded = 0u;
-            cur = ray;
-        }
-        const int s = tile * 32 + j;
-        const int sc = s < S ? s : S - 1;
-        float t;
-        if (!jit) {
-            const int i0 = sc < S - 1 ? sc : S - 2;
-            const float ta = tlin_sel(near, far, i0, S, step), tb = tlin_sel(near, far, i0 + 1, S, step);
-            t = sc < S - 1 ? ta : tb;
-        } else {
-            t = tval(near, far, sc, S, jit);
-        }
-        const float px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;
-        float yr, yg, yb, ys;
-        container_tile<INTERP, 0, FOLD>(cfg, W, px, py, pz, shv, cb, &folded, lane, yr, yg, yb, ys);
-        if (h == 0 && s < S) {
-            f32x4 v;
-            v[0] = yr, v[1] = yg, v[2] = yb, v[3] = ys;
-            ybuf[sl * kWsMaxS + s] = v;
-        }
-        int old = 0;
-        if (lane == 0) old = __hip_atomic_fetch_add(&sdone[sl], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-        old = __builtin_amdgcn_readlane(old, 0);
-        if (old != T - 1) continue;
-        composite_ray_lds(p, bg, ray, ybuf + sl * kWsMaxS, lane, step);
-        if (my == sl) my = -1;
-        // the slot's LDS reads are done before it can be handed out again
-        if (lane == 0)
-            __hip_atomic_fetch_and(&slive, ~(1u << sl), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-}
-
-// ------------------------------------------------------------------------------------------
 // Routed render with more than two experts (C3 / C4).  LDS holds two expert SLOTS; per round of
 // 16 rays (one per wave) the workgroup routes every sample of its rays, counts how many waves
 // need each expert, and stages the two most needed ones into the slots (only when they change --
 // with rays sorted by owning expert, parallel.expert_sorted_plan, a workgroup's rays mostly need
 // the same one or two experts, so staging is rare).  A sample whose expert is not resident is
 // evaluated from the packed image in global memory (L2), without the SH fold.
-#ifndef ACN_SPLIT_ROUTED
-// K > 2: single-expert rays through render_single_kernel, the rest through render_slots_kernel.  Off: measured
-// slower than the one slots launch on C3 and C4 (round 3, DESIGN.md 4: the single-expert kernel runs ~2x
-// render_kernel's per-ray time, the multi-expert remainder is latency-bound, plus two list passes)
-#define ACN_SPLIT_ROUTED 0
-#endif
 #ifndef ACN_SLOTS_SINGLE
 #define ACN_SLOTS_SINGLE 1  // single-expert rays (kSingleRay) skip the per-sample routing and blend
 #endif
@@ -1477,11 +1307,8 @@ __device__ __forceinline__ uint32_t ray_expert_mask(const FieldCfg& cfg, int rou
 #ifndef ACN_SLOTS_BAND
 #define ACN_SLOTS_BAND 0
 #endif
-#ifndef ACN_SLOTS_WS
-#ifndef ACN_SLOTS_WS_RAYMAJOR
-#define ACN_SLOTS_WS_RAYMAJOR 0
-#endif
-#define ACN_SLOTS_WS 0  // 1: render_slots_kernel rounds share their field tiles (as render_ws_kernel); measured slower
+#ifndef ACN_SLOTS_CHECK
+#define ACN_SLOTS_CHECK 0   // diagnostic self-check build (tools/dbg/selfcheck.py)
 #endif
 #ifndef ACN_SLOTS_THREADS
 #define ACN_SLOTS_THREADS 512  // 2 waves/SIMD, 256 VGPRs: the 1024-thread build spills and was measured wrong
@@ -1570,15 +1397,6 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
     __shared__ __attribute__((aligned(16))) float cbuf[FOLD ? (ACN_SLOTS_THREADS / 64) * 3 * 64 : 4];
     __shared__ int cnt[kMaxK];
     __shared__ int slot_k[2], restage[2];
-#if ACN_SLOTS_WS
-    // work-shared tiles (as render_ws_kernel): the round's rays, their expert masks and field values
-    constexpr int kW = ACN_SLOTS_THREADS / 64;
-    __shared__ __attribute__((aligned(16))) f32x4 ybuf[kW * kWsMaxS];
-    __shared__ int64_t wray[kW];
-    __shared__ uint32_t wmask[kW];
-    __shared__ int qhead, done[kW];
-    const bool ws = !(p.tau > 0.0f) && p.S <= kWsMaxS;
-#endif
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     float* cb = FOLD ? cbuf + wave * 3 * 64 : nullptr;
@@ -1608,14 +1426,6 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
             for (int k = 0; k < cfg.K; ++k)
                 if ((m >> k) & 1u) atomicAdd(&cnt[k], 1);
         __syncthreads();
-#if ACN_SLOTS_WS
-        if (ws && lane == 0) {   // every wave has left the previous round: its LDS state can be replaced
-            wray[wave] = ray;
-            wmask[wave] = m;
-            done[wave] = 0;
-            if (wave == 0) qhead = 0;
-        }
-#endif
         if (threadIdx.x == 0) {
             int b0 = -1, b1 = -1;
             for (int k = 0; k < cfg.K; ++k) {
@@ -1647,67 +1457,6 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
 #else
         const int k0 = __builtin_amdgcn_readfirstlane(slot_k[0]), k1 = __builtin_amdgcn_readfirstlane(slot_k[1]);
 #endif
-#if ACN_SLOTS_WS
-        if (ws) {
-            const int nr = (int)min(waves_per_wg, lim - base);
-            const int S = p.S, T = (S + 31) >> 5;
-            const int j = lane & 31, h = lane >> 5;
-            int64_t cur = -1;
-            uint32_t folded = 0u, mm = 0u;
-            float shv[8];
-            float ox = 0.0f, oy = 0.0f, oz = 0.0f, dx = 0.0f, dy = 0.0f, dz = 0.0f, near = 0.0f, far = 0.0f;
-            const float* jit = nullptr;
-            for (;;) {
-                int item = 0;
-                if (lane == 0) item = __hip_atomic_fetch_add(&qhead, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                item = __builtin_amdgcn_readlane(item, 0);
-                if (item >= nr * T) break;
-#if ACN_SLOTS_WS_RAYMAJOR  // each ray's tiles consecutive: a wave mostly stays on one ray (fewer re-folds)
-                const int slot = item / T, tile = item - slot * T;
-#else
-                const int tile = item / nr, slot = item - tile * nr;
-#endif
-                const int64_t tray = (int64_t)__builtin_amdgcn_readfirstlane((int)wray[slot]);
-                if (tray != cur) {
-                    const float* rp = p.rays + tray * 8;
-                    ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
-                    near = rp[6], far = rp[7];
-                    jit = p.jitter ? p.jitter + tray * S : nullptr;
-                    float sh[16];
-                    dir_sh(dx, dy, dz, sh);
-                    sh_rows_for_half(sh, h, shv);
-                    folded = 0u;
-                    mm = __builtin_amdgcn_readfirstlane(wmask[slot]);
-                    cur = tray;
-                }
-                const int s = tile * 32 + j;
-                const int sc = s < S ? s : S - 1;
-                float t;
-                if (!jit) {
-                    const int i0 = sc < S - 1 ? sc : S - 2;
-                    const float ta = tlin_sel(near, far, i0, S, step), tb = tlin_sel(near, far, i0 + 1, S, step);
-                    t = sc < S - 1 ? ta : tb;
-                } else {
-                    t = tval(near, far, sc, S, jit);
-                }
-                const float px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;
-                float yr, yg, yb, ys;
-                slots_field<INTERP, ROUTE, FOLD>(cfg, p, smem, cb, cbg, k0, k1, (mm & kSingleRay) != 0u,
-                                                 __builtin_ctz(mm | kSingleRay), px, py, pz, shv, folded, lane, yr,
-                                                 yg, yb, ys);
-                if (h == 0 && s < S) {
-                    f32x4 v;
-                    v[0] = yr, v[1] = yg, v[2] = yb, v[3] = ys;
-                    ybuf[slot * kWsMaxS + s] = v;
-                }
-                int old = 0;
-                if (lane == 0) old = __hip_atomic_fetch_add(&done[slot], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-                old = __builtin_amdgcn_readlane(old, 0);
-                if (old == T - 1) composite_ray_lds(p, bg, tray, ybuf + slot * kWsMaxS, lane, step);
-            }
-            continue;   // the next round's first barrier orders this round's LDS use before its resets
-        }
-#endif
         if (live) {
             const bool single = (m & kSingleRay) != 0u;
             const int k_single = __builtin_ctz(m | kSingleRay);
@@ -1716,6 +1465,16 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
                            float& yb, float& ys) {
                            slots_field<INTERP, ROUTE, FOLD>(cfg, p, smem, cb, cbg, k0, k1, single, k_single, px, py,
                                                             pz, shv, folded, lane, yr, yg, yb, ys);
+#if ACN_SLOTS_CHECK  // diagnostic build only: the tile evaluated again with every fold redone; a differing lane
+                     // poisons its sample (NaN rgb: tools/dbg/selfcheck.py)
+                           uint32_t f2 = 0u;
+                           float cr, cg, cbb, cs;
+                           slots_field<INTERP, ROUTE, FOLD>(cfg, p, smem, cb, cbg, k0, k1, single, k_single, px, py,
+                                                            pz, shv, f2, lane, cr, cg, cbb, cs);
+                           if (__float_as_uint(cr) != __float_as_uint(yr) || __float_as_uint(cg) != __float_as_uint(yg) ||
+                               __float_as_uint(cbb) != __float_as_uint(yb) || __float_as_uint(cs) != __float_as_uint(ys))
+                               yr = __int_as_float(0x7fc00000);
+#endif
                        });
         }
     }
@@ -1745,280 +1504,16 @@ __device__ __forceinline__ uint64_t same_digit_lanes(bool valid, int dig) {
 __device__ __forceinline__ int lanes_below(uint64_t m) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
-// ------------------------------------------------------------------------------------------
-// Routed render, expert-major chunks (C3 / C4: K > 2 experts, soft or hard routing; round 4).
-//
-// The reference evaluates the container expert by expert over the samples each one owns
-// (meta_container.py:300-337: index_select of the routed samples, MetaNGP.forward, index_add_ of y_k * w_k
-// in expert order) and then composites every ray (ray_rendering.py:114-165).  This kernel does the same
-// per CHUNK of rays, with every expert's MLP image read from LDS:
-//   A  route: every sample of the chunk's rays -> its expert mask (bit k: w_k > 0) in LDS;
-//   B  for each expert k the chunk needs, in ascending k: stage expert k's packed image (58 KB) into the
-//      workgroup's one LDS slot (skipped when it is already there), compact the
-//      chunk's samples that need k into a list, and evaluate them 32 per wave-tile (hash grid + MLP on
-//      per-lane SH: lanes may belong to different rays); each result y_k * w_k is added into the
-//      sample's accumulator in LDS -- 0 + y_a w_a + y_b w_b ... in ascending k, the reference's order;
-//   C  composite: one wave per ray reads its samples' accumulated (rgb, sigma) from LDS and runs the
-//      same compositing / background / output code as render_kernel.
-// Every sample is evaluated once per expert it needs (the per-ray kernels evaluate a whole 32-sample
-// tile for every expert any of its samples needs, and read non-resident experts' weights from L2).
-// Arithmetic per sample and expert is the one render_kernel / render_slots_kernel use (the SH k-step of
-// colour layer 0 first = the per-ray fold's order), so a ray's outputs do not depend on its batch.
-// 512 threads, two workgroups per CU (16 waves), <= 80 KB of LDS each.
-#ifndef ACN_ROUTED
-#define ACN_ROUTED 0  // 1: expert-major chunks for K > 2 (measured slower than render_slots_kernel)
-#endif
-#ifndef ACN_ROUTED_CHUNK
-#define ACN_ROUTED_CHUNK 1024  // samples per chunk (rays per chunk = ACN_ROUTED_CHUNK / S)
-#endif
-constexpr int kRtThreads = 512;
+constexpr int kRtThreads = 512;   // ep_field_kernel: two workgroups per CU (16 waves)
 constexpr int kRtWaves = kRtThreads / 64;
-static_assert(ACN_ROUTED_CHUNK == 2 * kRtThreads, "phase-B list build: two samples per thread");
-
-template <int INTERP, int ROUTE>
-__global__ void __launch_bounds__(kRtThreads, 4) render_routed_kernel(FieldCfg cfg, BgArgs bg, RenderParams p,
-                                                                       int R) {
-#if ACN_RT_ACCFIRST  // diagnostic: LDS layout with the accumulators first
-    __shared__ __attribute__((aligned(16))) f32x4 accs[ACN_ROUTED_CHUNK];  // per-sample container output
-    __shared__ __attribute__((aligned(16))) float Wsl[PK_FLOATS];     // the staged expert's packed image
-#else
-    __shared__ __attribute__((aligned(16))) float Wsl[PK_FLOATS];     // the staged expert's packed image
-    __shared__ __attribute__((aligned(16))) f32x4 accs[ACN_ROUTED_CHUNK];  // per-sample container output
-#endif
-#if ACN_RT_PAD  // diagnostic: > 80 KB of LDS, one workgroup per CU
-    __shared__ int pad_lds[1024];
-    if (threadIdx.x == 1023) pad_lds[0] = 0;
-#endif
-    __shared__ uint16_t emask[ACN_ROUTED_CHUNK];                         // per-sample expert mask
-    __shared__ uint16_t elist[ACN_ROUTED_CHUNK];                         // samples of the current expert
-    __shared__ int wsum[kRtWaves];
-    __shared__ uint32_t uni;
-    __shared__ int tctr;
-#if ACN_RT_DEBUG  // diagnostic build: per-sample count of expert evaluations
-    __shared__ uint8_t dvis[ACN_ROUTED_CHUNK];
-#endif
-#if ACN_RT_CHECK  // diagnostic build: per-sample self-check flags
-    __shared__ uint8_t dflag[ACN_ROUTED_CHUNK];
-#endif
-    const int tid = threadIdx.x, lane = tid & 63, j = lane & 31, h = lane >> 5;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int S = p.S;
-    const float step = 1.0f / (float)(S - 1);
-    const int64_t nchunks = (p.N + R - 1) / R;
-    // chunk range of this workgroup: with the grid a multiple of 8 (blocks dealt round-robin over the XCDs),
-    // XCD x owns the x-th contiguous eighth of the chunks, each of its workgroups a contiguous piece of it
-    int64_t c_lo, c_hi;
-    {
-        int64_t band_lo = 0, band_n = nchunks, q = blockIdx.x, Q = gridDim.x;
-        if ((gridDim.x & 7) == 0) {
-            const int x = blockIdx.x & 7;
-            band_lo = nchunks * x / 8;
-            band_n = nchunks * (x + 1) / 8 - band_lo;
-            q = blockIdx.x >> 3;
-            Q = gridDim.x >> 3;
-        }
-        c_lo = band_lo + band_n * q / Q;
-        c_hi = band_lo + band_n * (q + 1) / Q;
-    }
-    auto ray_at = [&](int64_t pos) -> int64_t {
-        return p.order ? (int64_t)p.order[pos] : pos;
-    };
-    int slot = -1;  // expert in the LDS slot (workgroup-uniform)
-    if (tid == 0) uni = 0u;
-    __syncthreads();
-    for (int64_t c = c_lo; c < c_hi; ++c) {
-        const int64_t r0 = c * R;
-        const int nr = (int)min((int64_t)R, p.N - r0);
-        const int ns = nr * S;
-        // ---- A: expert mask of every sample (meta_container.py:97-134)
-        for (int sl = tid; sl < ns; sl += kRtThreads) {
-            const int rl = sl / S, i = sl - rl * S;
-            const float* rp = p.rays + ray_at(r0 + rl) * 8;
-            const float near = rp[6], far = rp[7];
-            const float t = p.jitter ? tval(near, far, i, S, p.jitter + ray_at(r0 + rl) * S) : tlin_sel(near, far, i, S, step);
-            const float px = rp[0] + rp[3] * t, py = rp[1] + rp[4] * t, pz = rp[2] + rp[5] * t;
-            uint32_t m = 0u;
-            if (ROUTE == 1) {
-                const RouteState st = route_prep<1>(cfg, px, py, pz);
-                for (int k = 0; k < cfg.K; ++k)
-                    if (route_weight(cfg, st, k, px, py, pz) > 0.0f) m |= 1u << k;
-            } else {
-                m = 1u << route_prep<2>(cfg, px, py, pz).hard;
-            }
-            emask[sl] = (uint16_t)m;
-#if ACN_RT_CHECK
-            dflag[sl] = 0;
-#endif
-#if ACN_RT_DEBUG
-            dvis[sl] = 0;
-#endif
-            if (m == 0u) accs[sl] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};   // no expert: the container output is 0
-            uint32_t any = 0u;
-            for (int k = 0; k < cfg.K; ++k)
-                if (__ballot((m >> k) & 1u) != 0ull) any |= 1u << k;
-            if (lane == 0 && any) atomicOr(&uni, any);
-        }
-        __syncthreads();
-        const uint32_t U = (uint32_t)__builtin_amdgcn_readfirstlane((int)uni);
-        // ---- B: expert by expert, ascending
-        for (uint32_t rem = U; rem != 0u; rem &= rem - 1u) {
-            const int k = __builtin_ctz(rem);
-            if (k != slot) {
-                const f32x4* src = reinterpret_cast<const f32x4*>(p.packed + (size_t)k * PK_FLOATS);
-                f32x4* dst = reinterpret_cast<f32x4*>(Wsl);
-                for (int i = tid; i < PK_FLOATS / 4; i += kRtThreads) dst[i] = src[i];
-                slot = k;
-            }
-            // compact the chunk's samples that need k (two per thread, in sample order)
-            const int s0 = 2 * tid;
-            const bool f0 = s0 < ns && ((emask[s0] >> k) & 1u);
-            const bool f1 = s0 + 1 < ns && ((emask[s0 + 1] >> k) & 1u);
-            const int cnt2 = (int)f0 + (int)f1;
-            const int incl = wave_incl_scan(cnt2);
-            if (lane == 63) wsum[wave] = incl;
-            if (tid == 0) tctr = 0;
-            __syncthreads();
-            int base = incl - cnt2, total = 0;
-            for (int w = 0; w < kRtWaves; ++w) {
-                const int v = wsum[w];
-                base += w < wave ? v : 0;
-                total += v;
-            }
-            if (f0) elist[base] = (uint16_t)s0;
-            if (f1) elist[base + (int)f0] = (uint16_t)(s0 + 1);
-            __syncthreads();
-            // wave-tiles of 32 listed samples, pulled from a workgroup counter
-            const int ntiles = (total + 31) >> 5;
-#if ACN_RT_STATIC  // diagnostic: static tile assignment
-            for (int tile = wave; tile < ntiles; tile += kRtWaves) {
-#else
-            for (;;) {
-                int tile = 0;
-                if (lane == 0) tile = atomicAdd(&tctr, 1);
-                tile = __builtin_amdgcn_readfirstlane(tile);
-                if (tile >= ntiles) break;
-#endif
-#if ACN_RT_SYNC  // diagnostic: drain every counter at the start of a tile
-                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-                __builtin_amdgcn_sched_barrier(0);
-#endif
-                const int e = tile * 32 + j;
-                const bool valid = e < total;
-                const int sl = elist[valid ? e : total - 1];
-                const int rl = sl / S, i = sl - rl * S;
-                const int64_t ray = ray_at(r0 + rl);
-                const float* rp = p.rays + ray * 8;
-                const float ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
-                const float near = rp[6], far = rp[7];
-                const float t = p.jitter ? tval(near, far, i, S, p.jitter + ray * S) : tlin_sel(near, far, i, S, step);
-                const float px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;
-                float sh[16], shv[8];
-                dir_sh(dx, dy, dz, sh);
-                sh_rows_for_half(sh, h, shv);
-                float wk = 1.0f;
-                if (ROUTE == 1) wk = route_weight(cfg, route_prep<1>(cfg, px, py, pz), k, px, py, pz);
-                float r, g, b, sg;
-                // metadata straight from the kernel arguments (k is wave-uniform): the table pointer stays a
-                // global-address-space pointer (global_load gathers, not flat)
-#if ACN_RT_EXSEL  // diagnostic: the expert's metadata selected by compile-time indices
-                switch (k) {
-#define ACN_RT_CASE(Q) case Q: field_tile<INTERP, false, true>(Wsl, cfg.ex[Q], cfg.log2T, px, py, pz, shv, nullptr, lane, r, g, b, sg); break;
-                    ACN_RT_CASE(0) ACN_RT_CASE(1) ACN_RT_CASE(2) ACN_RT_CASE(3) ACN_RT_CASE(4) ACN_RT_CASE(5)
-                    ACN_RT_CASE(6) default: ACN_RT_CASE(7)
-#undef ACN_RT_CASE
-                }
-#else
-                field_tile<INTERP, false, true>(Wsl, cfg.ex[k], cfg.log2T, px, py, pz, shv, nullptr, lane, r, g, b, sg);
-#endif
-                sg = trunc_exp(sg);
-#if ACN_RT_CHECK
-                uint32_t fl = 0u;
-                {
-                    __builtin_amdgcn_sched_barrier(0);
-                    const float* rq = p.rays + ray * 8;
-                    if (rq[0] != ox || rq[1] != oy || rq[2] != oz || rq[3] != dx || rq[4] != dy || rq[5] != dz ||
-                        rq[6] != near || rq[7] != far) fl |= 1u;
-                    float r2, g2, b2, s2;
-                    field_tile<INTERP, false, true>(Wsl, cfg.ex[k], cfg.log2T, px, py, pz, shv, nullptr, lane, r2, g2, b2, s2);
-                    s2 = trunc_exp(s2);
-                    if (__float_as_uint(r2) != __float_as_uint(r) || __float_as_uint(s2) != __float_as_uint(sg)) fl |= 2u;
-                }
-#endif
-                if (valid && h == 0) {
-#if ACN_RT_CHECK
-                    dflag[sl] = (uint8_t)(dflag[sl] | fl);
-#endif
-                    f32x4 a;
-                    if (ROUTE == 1) {
-                        const bool first = (emask[sl] & ((1u << k) - 1u)) == 0u;
-                        a = first ? f32x4{0.0f, 0.0f, 0.0f, 0.0f} : accs[sl];
-                        a[0] = a[0] + r * wk;
-                        a[1] = a[1] + g * wk;
-                        a[2] = a[2] + b * wk;
-                        a[3] = a[3] + sg * wk;
-                    } else {
-                        a = f32x4{r, g, b, sg};
-                    }
-                    accs[sl] = a;
-#if ACN_RT_DEBUG
-                    dvis[sl] = dvis[sl] + 1;
-#endif
-                }
-            }
-            __syncthreads();
-        }
-        // ---- C: composite one ray per wave (ray_rendering.py:114-165, 23-45)
-        for (int rl = wave; rl < nr; rl += kRtWaves) {
-            const int rb = rl * S;
-            render_ray(p, bg, ray_at(r0 + rl), lane, step,
-                       [&](int sc, float, float, float, const float (&)[8], uint32_t&, float& yr, float& yg, float& yb,
-                           float& ys) {
-                           const f32x4 a = accs[rb + sc];
-                           yr = a[0];
-                           yg = a[1];
-                           yb = a[2];
-                           ys = a[3];
-                       });
-#if ACN_RT_DEBUG2  // diagnostic: weights <- the container's sigma per sample (the accumulated field output)
-            if (p.weights)
-                for (int i = lane; i < S; i += 64) p.weights[ray_at(r0 + rl) * S + i] = accs[rb + i][3];
-#endif
-#if ACN_RT_CHECK  // depth <- OR of the ray's samples' self-check flags
-            {
-                uint32_t f = 0u;
-                for (int i = lane; i < S; i += 64) f |= dflag[rb + i];
-                for (int off = 32; off >= 1; off >>= 1) f |= (uint32_t)__shfl_xor((int)f, off);
-                if (lane == 0) p.depth[ray_at(r0 + rl)] = (float)f;
-            }
-#endif
-#if ACN_RT_DEBUG  // depth <- samples of the ray whose evaluation count differs from their expert count
-            {
-                int bad = 0;
-                for (int i = lane; i < S; i += 64)
-                    bad += (__builtin_popcount((uint32_t)emask[rb + i]) != (int)dvis[rb + i]) ? 1 : 0;
-                for (int off = 32; off >= 1; off >>= 1) bad += __shfl_xor(bad, off);
-                int multi = 0;
-                for (int i = lane; i < S; i += 64) multi += __builtin_popcount((uint32_t)emask[rb + i]) > 1 ? 1 : 0;
-                for (int off = 32; off >= 1; off >>= 1) multi += __shfl_xor(multi, off);
-                if (lane == 0) {
-                    p.depth[ray_at(r0 + rl)] = (float)bad;
-                    p.acc[ray_at(r0 + rl)] = (float)multi;
-                }
-            }
-#endif
-        }
-        if (tid == 0) uni = 0u;
-        __syncthreads();
-    }
-}
 
 // ------------------------------------------------------------------------------------------
 // One expert per GPU, render (expert_parallel.ExpertParallelRenderer).  The routed render of
-// render_routed_kernel split at its expert boundary: the senders' (sample, expert) pairs travel to the
+// routed render split at its expert boundary: the senders' (sample, expert) pairs travel to the
 // experts' owners as 24-B [world point, direction] records in the fixed layout of acn_routed_count_fixed.
 //   ep_field_kernel     owner: each owned expert's field on the records received from every sender, in the
 //                       received layout [sender][local expert][cap] -> (rgb, sigma) per record, the same
-//                       per-(sample, expert) arithmetic as render_routed_kernel (LDS-staged image, SH-first
+//                       per-(sample, expert) arithmetic as the fused routed render (LDS-staged image, SH-first
 //                       colour layer 0 on per-lane SH), so a ray renders bit for bit as on one GPU;
 //   ep_composite_kernel sender: the blend sum_k y_k w_k in ascending k from zero (meta_container.py:320-337)
 //                       read from the returned pair slots, then render_kernel's compositing / background /
@@ -2106,185 +1601,6 @@ __global__ void __launch_bounds__(1024) ep_composite_kernel(BgArgs bg, RenderPar
                        yg = a[1];
                        yb = a[2];
                        ys = a[3];
-                   });
-    }
-}
-
-// ------------------------------------------------------------------------------------------
-// Split routed render (C3 / C4, K > 2).  The single-expert rays (every sample routed to ONE expert with
-// weight exactly 1.0f: kSingleRay) are most of a batch (C3 ~91%, C4 ~60%); they go through
-// render_single_kernel -- 16 waves per CU, <= 128 VGPRs, no per-ray routing or blend, one expert image in
-// LDS per workgroup, restaged only where the expert changes -- and only the multi-expert rays through
-// render_slots_kernel.  Every ray is still rendered by one wave and written at its own index with the
-// same arithmetic as the slots kernel's single path (0 + y_k * 1.0f == y_k), so the outputs are
-// bit-identical to the unsplit render.
-//   ray_class_kernel : one wave per ray, ray_expert_mask -> code[ray] = k (single expert k) or K (multi)
-//   ray_lists_kernel : one workgroup, stable counting sort of the codes: expert k's rays at
-//                      list[hdr[k] .. hdr[k] + n_k), its segment padded to 16 (one ray per wave of a
-//                      workgroup round) with -1; hdr[K] = single entries; the multi rays in input order in
-//                      multi[0 .. hdr[K + 1])
-template <int ROUTE>
-__global__ void __launch_bounds__(256) ray_class_kernel(FieldCfg cfg, RenderParams p, int32_t* __restrict__ code) {
-    const int lane = threadIdx.x & 63;
-    const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const float step = 1.0f / (float)(p.S - 1);
-    for (int64_t ray = wave; ray < p.N; ray += (int64_t)gridDim.x * 4) {
-        const uint32_t m = ray_expert_mask(cfg, ROUTE, p, ray, true, step, lane);
-        if (lane == 0) code[ray] = (m & kSingleRay) ? (int32_t)__builtin_ctz(m & ~kSingleRay) : cfg.K;
-    }
-}
-
-__global__ void __launch_bounds__(1024) ray_lists_kernel(const int32_t* __restrict__ code, int64_t N, int K,
-                                                         int32_t* __restrict__ list, int32_t* __restrict__ multi,
-                                                         int32_t* __restrict__ hdr) {
-    __shared__ int cnt[kMaxK + 1], base[kMaxK + 1], wtot[16][kMaxK + 1];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    if (tid <= K) cnt[tid] = 0;
-    __syncthreads();
-    int mine[kMaxK + 1];
-#pragma unroll
-    for (int c = 0; c <= kMaxK; ++c) mine[c] = 0;
-    for (int64_t i = tid; i < N; i += 1024) {
-        const int c = code[i];
-#pragma unroll
-        for (int q = 0; q <= kMaxK; ++q) mine[q] += (q == c) ? 1 : 0;
-    }
-#pragma unroll
-    for (int c = 0; c <= kMaxK; ++c)
-        if (c <= K && mine[c]) atomicAdd(&cnt[c], mine[c]);
-    __syncthreads();
-    if (tid == 0) {
-        int b = 0;
-        for (int k = 0; k < K; ++k) {
-            hdr[k] = b;
-            base[k] = b;
-            b += (cnt[k] + 15) & ~15;
-        }
-        hdr[K] = b;
-        base[K] = 0;   // the multi-expert rays: their own list
-        hdr[K + 1] = cnt[K];
-    }
-    __syncthreads();
-    for (int k = 0; k < K; ++k) {   // padding entries of every single-expert segment
-        const int p0 = base[k] + cnt[k], p1 = base[k] + ((cnt[k] + 15) & ~15);
-        for (int q = p0 + tid; q < p1; q += 1024) list[q] = -1;
-    }
-    const uint64_t below = (1ull << lane) - 1ull;
-    for (int64_t c0 = 0; c0 < N; c0 += 1024) {
-        const int64_t i = c0 + tid;
-        const int c = i < N ? code[i] : -1;
-        int pre = 0, mc = -1;
-        for (int q = 0; q <= K; ++q) {
-            const uint64_t b = __ballot(c == q);
-            if (lane == 0) wtot[w][q] = __popcll(b);
-            if (c == q) {
-                pre = __popcll(b & below);
-                mc = q;
-            }
-        }
-        __syncthreads();
-        if (mc >= 0) {
-            int off = base[mc] + pre;
-            for (int v = 0; v < w; ++v) off += wtot[v][mc];
-            (mc == K ? multi : list)[off] = (int32_t)i;
-        }
-        __syncthreads();
-        if (tid <= K) {
-            int t = 0;
-            for (int v = 0; v < 16; ++v) t += wtot[v][tid];
-            base[tid] += t;
-        }
-        __syncthreads();
-    }
-}
-
-#ifndef ACN_SINGLE_DBG
-#define ACN_SINGLE_DBG 0  // diagnostic builds: 1 no SH fold, 3 weights read from global memory (no LDS image)
-#endif
-#ifndef ACN_SINGLE_THREADS
-#define ACN_SINGLE_THREADS 1024  // rays per round = ACN_SINGLE_THREADS / 64 (divides the 16-ray segment padding)
-#endif
-// The block's expert metadata is selected from cfg.ex[] by compile-time indices.  Indexing the by-value
-// kernel argument with the runtime k inside the ray loop (ACN_SINGLE_EXSEL=0) gave run-to-run differences
-// in a few rays per launch (~1e-4 in RGB) on the MI355X -- only with the weights in LDS, never with the
-// same code reading them from global memory (tools/dbg/split_dbg5.py).
-#ifndef ACN_SINGLE_EXSEL
-#define ACN_SINGLE_EXSEL 1
-#endif
-template <int INTERP>
-__global__ void __launch_bounds__(ACN_SINGLE_THREADS, ACN_SINGLE_THREADS / 256) render_single_kernel(FieldCfg cfg, BgArgs bg, RenderParams p,
-                                                                const int32_t* __restrict__ list,
-                                                                const int32_t* __restrict__ hdr) {
-    constexpr bool FOLD = ACN_SHFOLD != 0 && ACN_SINGLE_DBG != 1 && ACN_SINGLE_DBG != 3;
-    __shared__ __attribute__((aligned(16))) float smem[ACN_SINGLE_DBG == 3 ? 4 : PK_FLOATS];
-    __shared__ __attribute__((aligned(16))) float cbuf[FOLD ? (ACN_SINGLE_THREADS / 64) * 64 : 4];
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    float* cb = FOLD ? cbuf + wave * 64 : nullptr;
-    const float step = 1.0f / (float)(p.S - 1);
-    const int K = cfg.K;
-    constexpr int WPR = ACN_SINGLE_THREADS / 64;   // rays (waves) per workgroup round
-    auto ld = [](const int32_t* a) -> int32_t { return *a; };
-    // Every workgroup renders rounds of ONE expert, whose image it stages into LDS once, before its loop
-    // (render_kernel's shape: no restaging inside the loop).
-    // Blocks are dealt to the experts in proportion to their rounds (at least one each), every block
-    // computing the same deal from hdr; virtual block ids keep consecutive ids on one XCD (block b runs on
-    // XCD b mod 8), so an XCD walks a contiguous stretch of the sorted list.
-    const int B = gridDim.x;
-    const int vb = (B & 7) == 0 ? (int)(blockIdx.x & 7) * (B >> 3) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
-    int nz = 0;
-    int64_t G = 0;
-    for (int e = 0; e < K; ++e) {
-        const int64_t r = (int64_t)(ld(hdr + e + 1) - ld(hdr + e)) / WPR;
-        G += r;
-        nz += r > 0 ? 1 : 0;
-    }
-    const int64_t avail = B > nz ? B - nz : 0;
-    int k = -1, first = 0, nb = 0;
-    for (int e = 0, acc = 0; e < K; ++e) {
-        const int64_t r = (int64_t)(ld(hdr + e + 1) - ld(hdr + e)) / WPR;
-        const int n = r > 0 ? 1 + (int)(avail * r / (G > 0 ? G : 1)) : 0;
-        if (k < 0 && vb < acc + n) {
-            k = e;
-            first = acc;
-            nb = n;
-        }
-        acc += n;
-    }
-    k = __builtin_amdgcn_readfirstlane(k);
-    if (k < 0) return;   // whole workgroup: more blocks than the deal uses
-    const int64_t base_k = ld(hdr + k) / WPR, rk = (ld(hdr + k + 1) - ld(hdr + k)) / WPR, j = vb - first;
-    // rounds j, j + nb, j + 2 nb, ... of the expert's segment: at any time its blocks work on a contiguous
-    // window of the (spatially ordered) list, as render_kernel's grid-stride loop does
-    const int64_t g0 = base_k + j, g1 = base_k + rk;
-#if ACN_SINGLE_EXSEL   // the expert's metadata selected by compile-time indices (no dynamic kernarg index)
-    ExpertMeta em = cfg.ex[0];
-#pragma unroll
-    for (int e = 1; e < kMaxK; ++e)
-        if (k == e) em = cfg.ex[e];
-#else
-    const ExpertMeta& em = cfg.ex[k];
-#endif
-    if (ACN_SINGLE_DBG != 3) {
-        const f32x4* src = reinterpret_cast<const f32x4*>(p.packed + (size_t)k * PK_FLOATS);
-        f32x4* dst = reinterpret_cast<f32x4*>(smem);
-        for (int i = threadIdx.x; i < PK_FLOATS / 4; i += blockDim.x) dst[i] = src[i];
-        __syncthreads();
-    }
-    for (int64_t g = g0; g < g1; g += nb) {
-        const int32_t ray = __builtin_amdgcn_readfirstlane(ld(list + WPR * g + wave));
-        if (ray < 0) continue;   // padding of expert k's segment
-        render_ray(p, bg, ray, lane, step,
-                   [&](int, float px, float py, float pz, const float (&shv)[8], uint32_t& folded, float& yr, float& yg,
-                       float& yb, float& ys) {
-                       const float* Wk = ACN_SINGLE_DBG == 3 ? p.packed + (size_t)k * PK_FLOATS : smem;
-                       if (FOLD && !(folded & 1u)) {
-                           fold_sh_bias(Wk, shv, lane, cb);
-                           folded |= 1u;
-                       }
-                       float sg;
-                       field_tile<INTERP, FOLD>(Wk, em, cfg.log2T, px, py, pz, shv, cb, lane, yr, yg, yb, sg);
-                       ys = trunc_exp(sg);
                    });
     }
 }
@@ -2770,10 +2086,7 @@ __device__ __forceinline__ void radix_pass6(const uint16_t* kin, const uint16_t*
     __syncthreads();
 }
 __global__ void __launch_bounds__(1024) ray_order_kernel(const float* __restrict__ rays, int N,
-                                                         int32_t* __restrict__ order, int* __restrict__ zero_ints,
-                                                         int nzero) {
-    // zero_ints: render_dq_kernel's band queue counters, cleared here (the launch right before it)
-    if ((int)threadIdx.x < nzero) zero_ints[threadIdx.x] = 0;
+                                                         int32_t* __restrict__ order) {
     constexpr int PER = ACN_ORDER_MAX / 1024;
     __shared__ int cnt[1024];
     __shared__ __attribute__((aligned(16))) float dir[3][ACN_ORDER_MAX];
@@ -2919,26 +2232,16 @@ __global__ void __launch_bounds__(1024) ray_order_kernel(const float* __restrict
 
 extern "C" size_t acn_workspace_bytes(int K) { return (size_t)(K < 1 ? 1 : K) * PK_BYTES; }
 
-// scratch of the split routed render: code[N], list[N + 16 kMaxK], multi[N], hdr[kMaxK + 2]
-static size_t split_bytes(int64_t N) { return (size_t)(3 * N + 16 * kMaxK + kMaxK + 2) * sizeof(int32_t); }
-
-// order scratch of the ordered single-expert render: order[N], then (64-B aligned) the 8 band counters
-static size_t dq_band_offset(int64_t N) { return ((size_t)N * sizeof(int32_t) + 63) & ~(size_t)63; }
-static size_t dq_order_bytes(int64_t N) { return dq_band_offset(N) + 64; }
-
 extern "C" size_t acn_render_order_bytes(int64_t N) {
     if (N < 1) return 0;
-    const size_t ord = N <= ACN_ORDER_MAX ? (ACN_RENDER_DQ ? dq_order_bytes(N) : (size_t)N * sizeof(int32_t)) : 0;
-    const size_t spl = ACN_SPLIT_ROUTED ? split_bytes(N) : 0;
-    return ord > spl ? ord : spl;
+    return N <= ACN_ORDER_MAX ? (size_t)N * sizeof(int32_t) : 0;
 }
 
 extern "C" int acn_ray_order(const float* rays, int64_t N, int32_t* order, void* stream) {
     ACN_REQUIRE(N >= 1 && N <= ACN_ORDER_MAX, "acn_ray_order: N must be in [1, %d], got %lld", ACN_ORDER_MAX,
                 (long long)N);
     ACN_REQUIRE(rays && order, "acn_ray_order: NULL pointer");
-    hipLaunchKernelGGL(ray_order_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, rays, (int)N, order,
-                       (int*)nullptr, 0);
+    hipLaunchKernelGGL(ray_order_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, rays, (int)N, order);
     return acn_check_launch("acn_ray_order");
 }
 
@@ -3006,74 +2309,9 @@ extern "C" int acn_render_stratified_fwd_ordered(const float* rays, int64_t N, i
     if ((num_cus() & 7) == 0) wgs = (wgs + 7) & ~(int64_t)7;  // whole XCD bands (render_kernel)
     const dim3 grid((unsigned)(wgs < num_cus() ? wgs : num_cus())), block(1024);
     const bool slots = ACN_SLOTS && cfg.routing != 0 && K != 2;  // render_slots_kernel keeps its own order
-    // render_dq_kernel: one expert, no early termination, the order scratch with room for the band counters
-    const bool dq = ACN_RENDER_DQ && cfg.routing == 0 && S <= kWsMaxS && !(tau > 0.0f) && order_scratch &&
-                    N <= ACN_ORDER_MAX && order_bytes >= dq_order_bytes(N);
-    int* bandq = dq ? (int*)((char*)order_scratch + dq_band_offset(N)) : nullptr;
     if (order_scratch && !slots && N <= ACN_ORDER_MAX && order_bytes >= (size_t)N * sizeof(int32_t)) {
-        hipLaunchKernelGGL(ray_order_kernel, dim3(1), dim3(1024), 0, s, rays, (int)N, (int32_t*)order_scratch, bandq,
-                           dq ? 8 : 0);
+        hipLaunchKernelGGL(ray_order_kernel, dim3(1), dim3(1024), 0, s, rays, (int)N, (int32_t*)order_scratch);
         p.order = (const int32_t*)order_scratch;
-    }
-    if (dq) {
-        if (interp == 1) hipLaunchKernelGGL(render_dq_kernel<1>, grid, block, 0, s, cfg, b, p, bandq);
-        else if (interp == 0) hipLaunchKernelGGL(render_dq_kernel<0>, grid, block, 0, s, cfg, b, p, bandq);
-        else hipLaunchKernelGGL(render_dq_kernel<2>, grid, block, 0, s, cfg, b, p, bandq);
-        return acn_check_launch("acn_render_stratified_fwd");
-    }
-    if (slots && ACN_ROUTED && S <= ACN_ROUTED_CHUNK) {
-        // expert-major chunks (render_routed_kernel): R rays per chunk, two workgroups per CU
-#if ACN_RT_R1  // diagnostic: one ray per chunk
-        const int R = 1;
-#else
-        const int R = ACN_ROUTED_CHUNK / S;
-#endif
-        const int64_t nch = (N + R - 1) / R;
-        int64_t g = 2 * (int64_t)num_cus();
-        if (nch < g) g = nch;
-        const dim3 rgrid((unsigned)g), rblock(kRtThreads);
-#define ACN_RT_LAUNCH(I, RT) hipLaunchKernelGGL((render_routed_kernel<I, RT>), rgrid, rblock, 0, s, cfg, b, p, R)
-        if (cfg.routing == 1) {
-            if (interp == 1) ACN_RT_LAUNCH(1, 1); else if (interp == 0) ACN_RT_LAUNCH(0, 1); else ACN_RT_LAUNCH(2, 1);
-        } else {
-            if (interp == 1) ACN_RT_LAUNCH(1, 2); else if (interp == 0) ACN_RT_LAUNCH(0, 2); else ACN_RT_LAUNCH(2, 2);
-        }
-#undef ACN_RT_LAUNCH
-        return acn_check_launch("acn_render_stratified_fwd");
-    }
-    if (slots && ACN_SPLIT_ROUTED && order_scratch && order_bytes >= split_bytes(N)) {
-        // split: single-expert rays through render_single_kernel, the rest through render_slots_kernel
-        int32_t* code = (int32_t*)order_scratch;
-        int32_t* list = code + N;
-        int32_t* multi = list + N + 16 * kMaxK;
-        int32_t* hdr = multi + N;
-        const int64_t cwg = (N + 3) / 4;
-        const dim3 cgrid((unsigned)(cwg < 4 * num_cus() ? cwg : 4 * num_cus()));
-        if (cfg.routing == 1) hipLaunchKernelGGL((ray_class_kernel<1>), cgrid, dim3(256), 0, s, cfg, p, code);
-        else hipLaunchKernelGGL((ray_class_kernel<2>), cgrid, dim3(256), 0, s, cfg, p, code);
-        hipLaunchKernelGGL(ray_lists_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)code, N, K, list, multi, hdr);
-
-        int64_t swgs = (N + ACN_SINGLE_THREADS / 64 - 1) / (ACN_SINGLE_THREADS / 64);
-        if ((num_cus() & 7) == 0) swgs = (swgs + 7) & ~(int64_t)7;
-        const int64_t scap = (int64_t)num_cus() * (1024 / ACN_SINGLE_THREADS);
-        int64_t sg_n = swgs < scap ? swgs : scap;
-        if (sg_n < K) sg_n = K;   // render_single_kernel deals at least one block to every expert
-        const dim3 sgrid((unsigned)sg_n);
-        const dim3 sblock(ACN_SINGLE_THREADS);
-        if (interp == 1) hipLaunchKernelGGL(render_single_kernel<1>, sgrid, sblock, 0, s, cfg, b, p, list, hdr);
-        else if (interp == 0) hipLaunchKernelGGL(render_single_kernel<0>, sgrid, sblock, 0, s, cfg, b, p, list, hdr);
-        else hipLaunchKernelGGL(render_single_kernel<2>, sgrid, sblock, 0, s, cfg, b, p, list, hdr);
-        RenderParams pm = p;
-        pm.order = multi;
-        pm.norder = hdr + K + 1;
-#define ACN_MULTI_LAUNCH(I, R) hipLaunchKernelGGL((render_slots_kernel<I, R>), grid, dim3(ACN_SLOTS_THREADS), 0, s, cfg, b, pm)
-        if (cfg.routing == 1) {
-            if (interp == 1) ACN_MULTI_LAUNCH(1, 1); else if (interp == 0) ACN_MULTI_LAUNCH(0, 1); else ACN_MULTI_LAUNCH(2, 1);
-        } else {
-            if (interp == 1) ACN_MULTI_LAUNCH(1, 2); else if (interp == 0) ACN_MULTI_LAUNCH(0, 2); else ACN_MULTI_LAUNCH(2, 2);
-        }
-#undef ACN_MULTI_LAUNCH
-        return acn_check_launch("acn_render_stratified_fwd");
     }
 #define ACN_RENDER_LAUNCH(I, KL, R)                                                                    \
     do {                                                                                              \
@@ -3317,149 +2555,6 @@ __global__ void __launch_bounds__(1024, 4) occ_render_kernel(FieldCfg cfg, BgArg
     }
 }
 
-// The occupancy render with the workgroup's field tiles shared (one expert), as render_ws_kernel: rays carry
-// 0..hundreds of marched samples, so one wave per ray leaves a CU waiting on its longest ray.  A round's 16
-// rays are cut into 32-sample tiles (ray-major item list from an LDS prefix sum), waves take tiles from an LDS
-// counter, field values go to LDS, and the wave completing a ray composites it with render_ray_packed's exact
-// loop (bit-identical outputs).  A ray with more than kWsMaxS samples does not fit its LDS row: its own wave
-// renders it whole with render_ray_packed, and the round's other rays are shared.
-#ifndef ACN_OCC_WS
-#define ACN_OCC_WS 0  // 1: occ_ws_kernel (bit-identical, measured no faster: DESIGN 4i)
-#endif
-template <int INTERP>
-__global__ void __launch_bounds__(1024, 4) occ_ws_kernel(FieldCfg cfg, BgArgs bg, OccRenderParams p) {
-    constexpr bool FOLD = ACN_SHFOLD != 0;
-    __shared__ __attribute__((aligned(16))) float smem[PK_FLOATS];
-    __shared__ __attribute__((aligned(16))) float cbuf[FOLD ? 16 * 64 : 4];
-    __shared__ __attribute__((aligned(16))) f32x4 ybuf[16 * kWsMaxS];
-    __shared__ int cum[17];
-    __shared__ int qhead, done[16];
-    stage_weights<1>(smem, p.packed);
-    const float* W = smem;
-    const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    float* cb = FOLD ? cbuf + wave * 64 : nullptr;
-    auto field = [&](float px, float py, float pz, const float (&shv)[8], uint32_t& folded, float& yr, float& yg,
-                     float& yb, float& ys) {
-        container_tile<INTERP, 0, FOLD>(cfg, W, px, py, pz, shv, cb, &folded, lane, yr, yg, yb, ys);
-    };
-    const int64_t stride = (int64_t)gridDim.x * 16;
-    for (int64_t base = (int64_t)blockIdx.x * 16; base < p.N; base += stride) {   // block-uniform
-        const int nr = (int)min((int64_t)16, p.N - base);
-        if (threadIdx.x == 0) {
-            int c = 0;
-            cum[0] = 0;
-            for (int r = 0; r < 16; ++r) {
-                const int64_t n = r < nr ? p.counts[base + r] : 0;
-                c += (n > 0 && n <= kWsMaxS) ? (int)((n + 31) >> 5) : 0;   // solo rays (n > kWsMaxS): no shared tiles
-                cum[r + 1] = c;
-            }
-            qhead = 0;
-        }
-        if (threadIdx.x < 16) done[threadIdx.x] = 0;
-        __syncthreads();
-        if (wave < nr) {   // a ray too long for its LDS row: this wave renders it alone
-            const int64_t n = p.counts[base + wave];
-            if (n > kWsMaxS) render_ray_packed(p, bg, base + wave, lane, field);
-            else if (n <= 0) render_ray_packed(p, bg, base + wave, lane, field);   // no samples: background only
-        }
-        const int items = cum[16];
-        int64_t cur = -1;
-        uint32_t folded = 0u;
-        float shv[8];
-        float ox = 0.0f, oy = 0.0f, oz = 0.0f, dx = 0.0f, dy = 0.0f, dz = 0.0f;
-        for (;;) {
-            int item = 0;
-            if (lane == 0) item = __hip_atomic_fetch_add(&qhead, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            item = __builtin_amdgcn_readlane(item, 0);
-            if (item >= items) break;
-            int slot = 0;
-            while (cum[slot + 1] <= item) ++slot;
-            const int tile = item - cum[slot];
-            const int T = cum[slot + 1] - cum[slot];
-            const int64_t ray = base + slot;
-            if (ray != cur) {
-                const float* rp = p.rays + ray * p.ld;
-                ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
-                float sh[16];
-                dir_sh(dx, dy, dz, sh);
-                sh_rows_for_half(sh, h, shv);
-                folded = 0u;
-                cur = ray;
-            }
-            const int64_t b = p.starts[ray], n = p.counts[ray];
-            const int64_t s = (int64_t)tile * 32 + j;
-            const bool valid = s < n;
-            const int64_t idx = b + (valid ? s : n - 1);
-            const float ta = p.t0[idx], tb = p.t1[idx];
-            const float tm = 0.5f * (ta + tb);
-            const float px = ox + dx * tm, py = oy + dy * tm, pz = oz + dz * tm;
-            float yr, yg, yb, ys;
-            field(px, py, pz, shv, folded, yr, yg, yb, ys);
-            if (h == 0 && valid) {
-                f32x4 v;
-                v[0] = yr, v[1] = yg, v[2] = yb, v[3] = ys;
-                ybuf[slot * kWsMaxS + (int)s] = v;
-            }
-            int old = 0;
-            if (lane == 0) old = __hip_atomic_fetch_add(&done[slot], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-            old = __builtin_amdgcn_readlane(old, 0);
-            if (old != T - 1) continue;
-            // composite from LDS: render_ray_packed's loop with the field values it would have computed
-            const f32x4* yrow = ybuf + slot * kWsMaxS;
-            double carry = 0.0;
-            float ar = 0.0f, ag = 0.0f, ab = 0.0f, ad = 0.0f, aa = 0.0f;
-            for (int64_t s0 = 0; s0 < n; s0 += 32) {
-                const bool cv = s0 + j < n;
-                const int64_t ci = cv ? s0 + j : n - 1;
-                const int64_t cidx = b + ci;
-                const float cta = p.t0[cidx], ctb = p.t1[cidx];
-                const float ctm = 0.5f * (cta + ctb);
-                const f32x4 y = yrow[ci];
-                const float sdt = cv ? y[3] * (ctb - cta) : 0.0f;
-                double incl = (double)sdt;
-#pragma unroll
-                for (int off = 1; off < 32; off <<= 1) {
-                    const double yv = __shfl_up(incl, off, 32);
-                    if (j >= off) incl += yv;
-                }
-                const float excl = (float)(carry + incl - (double)sdt);
-                const float alpha = 1.0f - expf(-sdt);
-                const float w = expf(-excl) * alpha;
-                if (cv && h == 0) {
-                    if (p.weights) p.weights[cidx] = w;
-                    ar += w * y[0];
-                    ag += w * y[1];
-                    ab += w * y[2];
-                    ad += w * ctm;
-                    aa += w;
-                }
-                carry += __shfl(incl, 31, 32);
-            }
-            float bgc[3];
-            background(bg, dx, dy, dz, lane, bgc);
-            const float r = (float)wave32_sum((double)ar), g = (float)wave32_sum((double)ag),
-                        bb = (float)wave32_sum((double)ab);
-            const float dd = (float)wave32_sum((double)ad), a = (float)wave32_sum((double)aa);
-            if (lane == 0) {
-                float orr = r, og = g, ob = bb;
-                if (bg.mode != ACN_BG_NONE) {
-                    const float om = 1.0f - a;
-                    orr = r + om * bgc[0];
-                    og = g + om * bgc[1];
-                    ob = bb + om * bgc[2];
-                }
-                p.rgb[ray * 3 + 0] = orr;
-                p.rgb[ray * 3 + 1] = og;
-                p.rgb[ray * 3 + 2] = ob;
-                p.depth[ray] = dd;
-                p.acc[ray] = a;
-            }
-        }
-        __syncthreads();   // cum / qhead / done / ybuf reused by the next round
-    }
-}
-
 }  // namespace
 
 extern "C" int acn_render_packed_fwd(const float* rays, int64_t ld, int64_t N, const int64_t* chunk_starts,
@@ -3485,12 +2580,6 @@ extern "C" int acn_render_packed_fwd(const float* rays, int64_t ld, int64_t N, c
                       rgb, depth, weights, acc};
     const int64_t wgs = (N + 15) / 16;
     const dim3 grid((unsigned)(wgs < num_cus() ? wgs : num_cus())), block(1024);
-    if (ACN_OCC_WS && cfg.routing == 0) {   // one expert: the workgroup's rays share their tiles (bit-identical)
-        if (interp == 1) hipLaunchKernelGGL(occ_ws_kernel<1>, grid, block, 0, s, cfg, b, p);
-        else if (interp == 0) hipLaunchKernelGGL(occ_ws_kernel<0>, grid, block, 0, s, cfg, b, p);
-        else hipLaunchKernelGGL(occ_ws_kernel<2>, grid, block, 0, s, cfg, b, p);
-        return acn_check_launch("acn_render_packed_fwd");
-    }
 #define ACN_OCC_LAUNCH(I, KL, R) hipLaunchKernelGGL((occ_render_kernel<I, KL, R>), grid, block, 0, s, cfg, b, p)
     ACN_DISPATCH(ACN_OCC_LAUNCH);
 #undef ACN_OCC_LAUNCH

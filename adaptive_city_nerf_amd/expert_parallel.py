@@ -243,7 +243,7 @@ class ExpertParallelRenderer:
       a2a #2  (rgb, sigma) back to the senders' pair slots
       sender  acn_ep_composite: blend in expert order + background + compositing in one launch -> rgb, depth,
               acc (+ weights): the (N, S, 4) field tensor is never materialised.
-    The per-sample arithmetic is render_routed_kernel's, so each ray renders bit for bit as in the fused
+    The per-sample arithmetic is the fused routed render's (SH-first colour layer 0), so each ray renders bit for bit as in the fused
     single-process routed render.  ``capacity`` C per (sender, expert) segment: n_rays * S (default, never
     overflows) or smaller to shrink the exchange; ``overflowed()`` reads the counts back (one host read, to be
     called lazily, e.g. once per frame) and a caller re-renders an overflowed batch at full capacity.

@@ -1,0 +1,72 @@
+"""Run-to-run determinism of the MFMA kernels: the same inputs give bitwise the same outputs on
+every call.  Round 4 recorded two one-off 1-ulp render differences whose cause was a VALU -> MFMA operand hazard
+(v_cvt_pk_f16_f32 writing an fp16 B fragment two wait states before the MFMA that reads it).  Every fp16
+fragment now passes the operand fence (acn_device.h); these tests repeat the cases where the differences were
+seen, and the training MLP kernels (same split -> MFMA idiom, tolerance-tested elsewhere), many times.
+
+Reference behaviour: rays are rendered independently and deterministically (nerfs/ray_rendering.py:290-345);
+the training MLP is MetaNGP's chain (models/inr/meta_ngp.py:171-241)."""
+import numpy as np
+import pytest
+import torch
+
+from test_render_ws import _setup, _t
+
+pytestmark = pytest.mark.gpu
+
+REPS = 20
+
+
+@pytest.mark.parametrize("tag,active", [("k4", None), ("k4", 2), ("k8", None)])
+@pytest.mark.parametrize("jitter", [False, True])
+def test_render_bitwise_stable_over_repeats(tag, active, jitter):
+    """The round-4 one-offs were K = 4, S = 200, 4096 rays (soft routing with jitter on render_slots_kernel's
+    per-wave path; active_module 2 on render_ws_kernel)."""
+    from adaptive_city_nerf_amd import ops
+    d, specs, routing, bg = _setup(tag)
+    S, n = 200, 4096
+    g = torch.Generator(device="cuda").manual_seed(11)
+    base = _t(d["render:rays"])
+    rays = base[torch.randint(0, base.shape[0], (n,), device="cuda", generator=g)].contiguous()
+    jit = torch.rand(n, S, device="cuda", generator=g) if jitter else None
+    with torch.no_grad():
+        ref = [x.clone() for x in ops.render_stratified(rays, S, specs, routing, active, bg[0], tau=0.0, jitter=jit)]
+        for it in range(REPS):
+            out = ops.render_stratified(rays, S, specs, routing, active, bg[0], tau=0.0, jitter=jit)
+            for name, a, b in zip(("rgb", "depth", "weights", "acc"), out, ref):
+                same = np.array_equal(a.cpu().numpy(), b.cpu().numpy(), equal_nan=True)
+                assert same, f"{tag} active={active} jitter={jitter}: {name} differs on repeat {it}"
+
+
+def _ws():
+    from test_mlp_train_gpu import _expert
+    sub = _expert()
+    return [t.detach().contiguous() for t in (
+        sub.sigma_trunk[0].linear.weight, sub.sigma_trunk[0].linear.bias, sub.sigma_trunk[1].linear.weight,
+        sub.sigma_trunk[1].linear.bias, sub.sigma_head.weight, sub.sigma_head.bias, sub.geo_head.weight,
+        sub.geo_head.bias, sub.color_mlp[0].linear.weight, sub.color_mlp[0].linear.bias,
+        sub.color_mlp[1].linear.weight, sub.color_mlp[1].linear.bias, sub.color_mlp[2].weight,
+        sub.color_mlp[2].bias)]
+
+
+@pytest.mark.parametrize("precision", ["fp16x3", "amp", "fp32"])
+@pytest.mark.parametrize("n", [4113, 362_666])
+def test_training_mlp_bitwise_stable_over_repeats(precision, n):
+    """mlp_train.hip forward and fused backward (the meta step's batch: 362,666 samples) repeated: outputs,
+    dL/dh0 and the 14 weight gradients bitwise equal to the first call."""
+    from adaptive_city_nerf_amd import ops
+    ws = _ws()
+    g = torch.Generator(device="cuda").manual_seed(n)
+    h0 = (torch.rand(n, 32, device="cuda", generator=g) - 0.5) * 2
+    sh = (torch.rand(n, 16, device="cuda", generator=g) - 0.5) * 2
+    gout = torch.randn(n, 4, device="cuda", generator=g) * (1024.0 if precision == "amp" else 1.0)
+    out0, _ = ops.mlp_train_fwd(h0, sh, ws, save=False, precision=precision)
+    dw0, gh0 = ops.mlp_train_bwd_dw(h0, sh, out0, gout, ws, want_h0=True, precision=precision)
+    dw0 = [t.clone() for t in dw0]
+    for it in range(REPS):
+        out, _ = ops.mlp_train_fwd(h0, sh, ws, save=False, precision=precision)
+        dw, gh = ops.mlp_train_bwd_dw(h0, sh, out0, gout, ws, want_h0=True, precision=precision)
+        assert torch.equal(out, out0), f"{precision} n={n}: forward differs on repeat {it}"
+        assert torch.equal(gh, gh0), f"{precision} n={n}: dL/dh0 differs on repeat {it}"
+        for k, (a, b) in enumerate(zip(dw, dw0)):
+            assert torch.equal(a, b), f"{precision} n={n}: gradient {k} differs on repeat {it}"
