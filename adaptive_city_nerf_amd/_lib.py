@@ -93,6 +93,8 @@ SIGNATURES = {
     "acn_routed_count_caps": ([vp, i64, i32, vp, vp, vp, vp, vp, vp, sz, vp], C.c_int),
     "acn_ep_gather_caps": ([vp, vp, i32, i32, vp, i32, vp, vp, f32, f32, vp, vp, vp, vp, vp, vp, vp, vp], C.c_int),
     "acn_ep_field_fwd": ([vp, vp, i32, i32, i64, vp, vp, sz, vp, vp], C.c_int),
+    "acn_ep_field_fwd_compact": ([vp, vp, i32, i32, i64, i64, vp, vp, sz, vp, vp], C.c_int),
+    "acn_routed_count_batches": ([vp, i64, i32, i64, vp, vp, vp, vp], C.c_int),
     "acn_ep_composite": ([vp, i64, i32, vp, vp, vp, vp, i32, i32, vp, f32, f32, vp, vp, vp, vp, vp], C.c_int),
     "acn_render_stratified_fwd_ordered": ([vp, i64, i32, vp, vp, vp, i32, vp, f32, f32, vp, sz, vp, vp, vp, vp,
                                            vp, sz, vp], C.c_int),
@@ -201,7 +203,10 @@ def lib():
                                f"`python -c 'import __graft_entry__ as g; g.build()'` (or make -C "
                                f"adaptive_city_nerf_amd/csrc)")
             L = C.CDLL(str(LIB_PATH))
+            variant = "ACNERF_LIB" in os.environ   # a developer build (tools/build_variants.sh) may predate an entry
             for name, (args, res) in SIGNATURES.items():
+                if variant and not hasattr(L, name):
+                    continue
                 fn = getattr(L, name)
                 fn.argtypes = args
                 fn.restype = res

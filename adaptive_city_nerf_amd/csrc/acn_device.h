@@ -485,14 +485,33 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 #else
 #define ACN_OPND_PAD ""
 #endif
-__device__ __forceinline__ void opnd_fence(f16x8& a) { asm volatile(ACN_OPND_PAD : "+v"(a)); }
-__device__ __forceinline__ void opnd_fence(f16x8& a, f16x8& b) { asm volatile(ACN_OPND_PAD : "+v"(a), "+v"(b)); }
+#ifndef ACN_OPND_MEM
+#define ACN_OPND_MEM 0
+#endif
+#ifndef ACN_OPND_SB
+#define ACN_OPND_SB 1   // scheduling barriers around the fence (0: measured run-to-run differences in field_kernel)
+#endif
+#if ACN_OPND_MEM
+#define ACN_OPND_CLOB : "memory"
+#else
+#define ACN_OPND_CLOB
+#endif
+#if ACN_OPND_SB
+#define ACN_OPND_SB0 __builtin_amdgcn_sched_barrier(0);
+#else
+#define ACN_OPND_SB0
+#endif
+__device__ __forceinline__ void opnd_fence(f16x8& a) { ACN_OPND_SB0 asm volatile(ACN_OPND_PAD : "+v"(a) : ACN_OPND_CLOB); ACN_OPND_SB0 }
+__device__ __forceinline__ void opnd_fence(f16x8& a, f16x8& b) {
+    ACN_OPND_SB0 asm volatile(ACN_OPND_PAD : "+v"(a), "+v"(b) : ACN_OPND_CLOB); ACN_OPND_SB0
+}
 __device__ __forceinline__ void opnd_fence(f16x8& a, f16x8& b, f16x8& c, f16x8& d) {
-    asm volatile(ACN_OPND_PAD : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+    ACN_OPND_SB0 asm volatile(ACN_OPND_PAD : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : ACN_OPND_CLOB); ACN_OPND_SB0
 }
 __device__ __forceinline__ void opnd_fence(f16x8& a, f16x8& b, f16x8& c, f16x8& d, f16x8& e, f16x8& f, f16x8& g,
                                            f16x8& h) {
-    asm volatile(ACN_OPND_PAD : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e), "+v"(f), "+v"(g), "+v"(h));
+    ACN_OPND_SB0 asm volatile(ACN_OPND_PAD : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e), "+v"(f), "+v"(g), "+v"(h)
+                              : ACN_OPND_CLOB); ACN_OPND_SB0
 }
 // one plane of N fragments (N = 1, 2, 4, 8)
 template <int N>

@@ -255,14 +255,24 @@ __device__ __forceinline__ void split_acc2(const f32x16& a0, const f32x16& a1, f
 // sank the last conversions past it into the k-step loop, 2 wait states before their MFMA.
 // REV: k-steps in reverse order (colour layer 0 with per-lane SH: the SH k-step first, the order the per-ray
 // fold accumulates in, so the result is bit-identical to fold_sh_bias + the folded layer)
+#ifndef ACN_X3_FENCE
+#define ACN_X3_FENCE 1
+#endif
 template <int NT, int NK, bool REV = false>
 __device__ __forceinline__ void layer_x3(const float* W, int seg, const float* bias_base, int bt, int lane, int h,
                                          f16x8 (&bh)[NK], f16x8 (&bl)[NK], f32x16 (&out)[NT],
                                          int nk_used = NK) {
+#if ACN_X3_FENCE
     if (nk_used == 1) opnd_fence(bh[REV ? NK - 1 : 0], bl[REV ? NK - 1 : 0]);
     else opnd_fence_n<NK>(bh, bl);
+#endif
 #pragma unroll
     for (int T = 0; T < NT; ++T) out[T] = bias_frag_at(bias_base, bt + T, h);
+#if !ACN_X3_FENCE   // the round-4 positional pad
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
     for (int si = 0; si < NK; ++si) {
         if (si >= nk_used) break;
@@ -1308,7 +1318,12 @@ __device__ __forceinline__ uint32_t ray_expert_mask(const FieldCfg& cfg, int rou
 #define ACN_SLOTS_BAND 0
 #endif
 #ifndef ACN_SLOTS_CHECK
-#define ACN_SLOTS_CHECK 0   // diagnostic self-check build (tools/dbg/selfcheck.py)
+#define ACN_SLOTS_CHECK 0   // diagnostic self-check build (tools/dbg/selfcheck.py; 2: mismatches recorded)
+#endif
+#if ACN_SLOTS_CHECK > 1
+constexpr unsigned kChkMax = 4096;
+__device__ float g_chk[16 * kChkMax];
+__device__ unsigned g_chk_n;
 #endif
 #ifndef ACN_SLOTS_THREADS
 #define ACN_SLOTS_THREADS 512  // 2 waves/SIMD, 256 VGPRs: the 1024-thread build spills and was measured wrong
@@ -1461,8 +1476,9 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
             const bool single = (m & kSingleRay) != 0u;
             const int k_single = __builtin_ctz(m | kSingleRay);
             render_ray(p, bg, ray, lane, step,
-                       [&](int, float px, float py, float pz, const float (&shv)[8], uint32_t& folded, float& yr, float& yg,
+                       [&](int sc_, float px, float py, float pz, const float (&shv)[8], uint32_t& folded, float& yr, float& yg,
                            float& yb, float& ys) {
+                           (void)sc_;
                            slots_field<INTERP, ROUTE, FOLD>(cfg, p, smem, cb, cbg, k0, k1, single, k_single, px, py,
                                                             pz, shv, folded, lane, yr, yg, yb, ys);
 #if ACN_SLOTS_CHECK  // diagnostic build only: the tile evaluated again with every fold redone; a differing lane
@@ -1472,8 +1488,19 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
                            slots_field<INTERP, ROUTE, FOLD>(cfg, p, smem, cb, cbg, k0, k1, single, k_single, px, py,
                                                             pz, shv, f2, lane, cr, cg, cbb, cs);
                            if (__float_as_uint(cr) != __float_as_uint(yr) || __float_as_uint(cg) != __float_as_uint(yg) ||
-                               __float_as_uint(cbb) != __float_as_uint(yb) || __float_as_uint(cs) != __float_as_uint(ys))
+                               __float_as_uint(cbb) != __float_as_uint(yb) || __float_as_uint(cs) != __float_as_uint(ys)) {
+#if ACN_SLOTS_CHECK > 1   // record the mismatch (tools/dbg/selfcheck.py --detail)
+                               const unsigned q = atomicAdd(&g_chk_n, 1u);
+                               if (q < kChkMax) {
+                                   float* o = g_chk + 16 * q;
+                                   o[0] = (float)ray; o[1] = (float)sc_; o[2] = single ? 1.0f : 0.0f; o[3] = (float)k_single;
+                                   o[4] = (float)k0; o[5] = (float)k1; o[6] = yr; o[7] = cr; o[8] = yg; o[9] = cg;
+                                   o[10] = yb; o[11] = cbb; o[12] = ys; o[13] = cs; o[14] = (float)lane;
+                                   o[15] = (float)folded;
+                               }
+#endif
                                yr = __int_as_float(0x7fc00000);
+                           }
 #endif
                        });
         }
@@ -1506,6 +1533,7 @@ __device__ __forceinline__ int lanes_below(uint64_t m) {
 }
 constexpr int kRtThreads = 512;   // ep_field_kernel: two workgroups per CU (16 waves)
 constexpr int kRtWaves = kRtThreads / 64;
+constexpr int kEpMaxSeg = 1024;   // W * E segments of the compact received layout (ep_field_kernel)
 
 // ------------------------------------------------------------------------------------------
 // One expert per GPU, render (expert_parallel.ExpertParallelRenderer).  The routed render of
@@ -1524,14 +1552,25 @@ __global__ void __launch_bounds__(kRtThreads, 4) ep_field_kernel(FieldCfg cfg, c
                                                                   int64_t cap, const float* __restrict__ packed,
                                                                   float* __restrict__ ret) {
     __shared__ __attribute__((aligned(16))) float Wsl[PK_FLOATS];
+    __shared__ int64_t pre[kEpMaxSeg];   // cap == 0 (compact layout): start of segment (w, e), row-major
     const int tid = threadIdx.x, lane = tid & 63, j = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int64_t G = (int64_t)gridDim.x * kRtWaves;
+    const bool compact = cap == 0;
+    if (compact && tid == 0) {
+        int64_t o = 0;
+        for (int q = 0; q < W * E; ++q) {
+            pre[q] = o;
+            o += cnt[q];
+        }
+    }
+    __syncthreads();
+    const int64_t cap_eff = compact ? INT64_MAX : cap;
     int slot = -1;
     for (int e = 0; e < E; ++e) {
         int64_t T = 0;   // wave-tiles of local expert e over all senders (records past cap were not sent)
         for (int w = 0; w < W; ++w) {
-            const int64_t c = min(cnt[(int64_t)w * E + e], cap);
+            const int64_t c = min(cnt[(int64_t)w * E + e], cap_eff);
             T += (c + 31) >> 5;
         }
         if ((int64_t)blockIdx.x * kRtWaves >= T) continue;   // no tile of this expert for this workgroup
@@ -1547,14 +1586,15 @@ __global__ void __launch_bounds__(kRtThreads, 4) ep_field_kernel(FieldCfg cfg, c
             int64_t tl = g, c = 0;
             int w = 0;
             for (; w < W; ++w) {   // sender of wave-tile g
-                c = min(cnt[(int64_t)w * E + e], cap);
+                c = min(cnt[(int64_t)w * E + e], cap_eff);
                 const int64_t nt = (c + 31) >> 5;
                 if (tl < nt) break;
                 tl -= nt;
             }
             const int64_t i = tl * 32 + j;
             const bool valid = i < c;
-            const int64_t rec = ((int64_t)w * E + e) * cap + (valid ? i : c - 1);
+            const int64_t seg0 = compact ? pre[w * E + e] : ((int64_t)w * E + e) * cap;
+            const int64_t rec = seg0 + (valid ? i : c - 1);
             const float* r = xd + rec * 6;
             const float px = r[0], py = r[1], pz = r[2];
             float sh[16], shv[8];
@@ -1564,7 +1604,7 @@ __global__ void __launch_bounds__(kRtThreads, 4) ep_field_kernel(FieldCfg cfg, c
             field_tile<INTERP, false, true>(Wsl, cfg.ex[e], cfg.log2T, px, py, pz, shv, nullptr, lane, rr, rg, rb, sg);
             sg = trunc_exp(sg);
             if (valid && h == 0)
-                *reinterpret_cast<f32x4*>(ret + 4 * (((int64_t)w * E + e) * cap + i)) = f32x4{rr, rg, rb, sg};
+                *reinterpret_cast<f32x4*>(ret + 4 * (seg0 + i)) = f32x4{rr, rg, rb, sg};
         }
     }
 }
@@ -2603,7 +2643,14 @@ extern "C" int acn_sample_stratified(const float* rays, int64_t N, int S, const 
 extern "C" int acn_ep_field_fwd(const float* recv_xd, const int64_t* recv_cnt, int W, int E, int64_t cap,
                                 const acn_expert* experts, const void* packed, size_t packed_bytes, float* ret,
                                 void* stream) {
-    ACN_REQUIRE(W >= 1 && E >= 1 && E <= kMaxK && cap >= 1, "acn_ep_field_fwd: bad arguments");
+    return acn_ep_field_fwd_compact(recv_xd, recv_cnt, W, E, cap, cap, experts, packed, packed_bytes, ret, stream);
+}
+
+extern "C" int acn_ep_field_fwd_compact(const float* recv_xd, const int64_t* recv_cnt, int W, int E, int64_t cap,
+                                        int64_t max_cnt, const acn_expert* experts, const void* packed,
+                                        size_t packed_bytes, float* ret, void* stream) {
+    ACN_REQUIRE(W >= 1 && E >= 1 && E <= kMaxK && cap >= 0 && (int64_t)W * E <= kEpMaxSeg && (cap > 0 || max_cnt >= 0),
+                "acn_ep_field_fwd: bad arguments");
     ACN_REQUIRE(recv_xd && recv_cnt && experts && packed && ret, "acn_ep_field_fwd: NULL pointer");
     acn_routing rt{};
     rt.K = E;
@@ -2613,7 +2660,8 @@ extern "C" int acn_ep_field_fwd(const float* recv_xd, const int64_t* recv_cnt, i
     int st = prepare(experts, &rt, -1, (void*)packed, packed_bytes, (hipStream_t)stream, cfg, interp, K, false);
     if (st) return st;
     int64_t g = 2 * (int64_t)num_cus();
-    const int64_t tiles = (int64_t)W * E * ((cap + 31) / 32);
+    // wave-tiles to cover: W E segments of at most cap records (compact: at most max_cnt records each)
+    const int64_t tiles = (int64_t)W * E * (((cap > 0 ? cap : max_cnt) + 31) / 32);
     const int64_t need = (tiles + kRtWaves - 1) / kRtWaves;
     if (need < g) g = need < 1 ? 1 : need;
     const dim3 grid((unsigned)g), block(kRtThreads);
@@ -2647,3 +2695,16 @@ extern "C" int acn_ep_composite(const float* rays, int64_t N, int S, const float
     else hipLaunchKernelGGL(ep_composite_kernel<1>, grid, block, 0, s, b, p, yr, pw, pmap, K);
     return acn_check_launch("acn_ep_composite");
 }
+
+#if ACN_SLOTS_CHECK > 1
+// diagnostic build only: copy out (and clear) the recorded self-check mismatches; returns their count
+extern "C" int acn_debug_check_fetch(float* host, int max_records) {
+    unsigned n = 0;
+    if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_chk_n), sizeof(n)) != hipSuccess) return -1;
+    const unsigned m = n < (unsigned)max_records ? n : (unsigned)max_records;
+    if (m && hipMemcpyFromSymbol(host, HIP_SYMBOL(g_chk), (size_t)m * 16 * sizeof(float)) != hipSuccess) return -1;
+    const unsigned z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_chk_n), &z, sizeof(z)) != hipSuccess) return -1;
+    return (int)n;
+}
+#endif

@@ -389,6 +389,44 @@ __global__ void __launch_bounds__(256) ep_gather_grad_kernel(const float4* __res
 
 constexpr unsigned kEpBlocks = 1024;  // fixed grids (graph-replayable): they stride to the device slot count
 
+// The exchange plan of a planned expert-parallel frame (expert_parallel.render_rays_ep_batched): per batch b of
+// `batch` consecutive rays and expert k, the number of samples routed to k (w_k > 0) -- the counts acn_routed_count*
+// gives that batch's pairs (the same t values and routing arithmetic, route_row), so a batch whose segment
+// capacities are these counts moves exactly its live records.  One lane per sample; a wave's lanes of one batch
+// add their ballot count with one atomic per expert (integer sums: the result does not depend on the order).
+__global__ void __launch_bounds__(kBlk) routed_count_batches_kernel(const float* __restrict__ rays, int64_t N, int S,
+                                                                    int64_t batch, const float* __restrict__ jit,
+                                                                    RouteCfg cfg, unsigned long long* __restrict__ cnt) {
+    const int64_t M = N * (int64_t)S;
+    const int lane = threadIdx.x & 63;
+    for (int64_t m0 = (int64_t)blockIdx.x * kBlk + (threadIdx.x & ~63); m0 < M; m0 += (int64_t)gridDim.x * kBlk) {
+        const int64_t m = m0 + lane;
+        const bool live = m < M;
+        float w[kMaxK];
+#pragma unroll
+        for (int k = 0; k < kMaxK; ++k) w[k] = 0.0f;
+        int64_t b = 0;
+        if (live) {
+            const int64_t ray = m / S;
+            const int s = (int)(m - ray * S);
+            b = ray / batch;
+            const float* rp = rays + ray * 8;
+            const float t = tval(rp[6], rp[7], s, S, jit ? jit + ray * S : nullptr);
+            route_row(cfg, rp[0] + rp[3] * t, rp[1] + rp[4] * t, rp[2] + rp[5] * t, w);
+        }
+        const int64_t last = (m0 + 63 < M ? m0 + 63 : M - 1) / S / batch;
+        const int64_t b0 = m0 / S / batch;
+        for (int k = 0; k < cfg.K; ++k) {
+            if (b0 == last) {   // wave-uniform: the whole wave in one batch
+                const uint64_t bal = __ballot(w[k] > 0.0f);
+                if (lane == 0 && bal) atomicAdd(&cnt[b0 * cfg.K + k], (unsigned long long)__popcll(bal));
+            } else if (live && w[k] > 0.0f) {
+                atomicAdd(&cnt[b * cfg.K + k], 1ull);
+            }
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" size_t acn_routed_workspace_bytes(int64_t M, int K) {
@@ -447,7 +485,7 @@ extern "C" int acn_routed_count_caps(const float* rays, int64_t N, int S, const 
     Caps caps{};
     caps.fixed = 1;
     for (int k = 0; k < K; ++k) {
-        ACN_REQUIRE(caps_host[k] >= 1, "acn_routed_count_caps: capacity of expert %d must be >= 1", k);
+        ACN_REQUIRE(caps_host[k] >= 0, "acn_routed_count_caps: capacity of expert %d must be >= 0", k);
         caps.cap[k] = caps_host[k];
         caps.off[k + 1] = caps.off[k] + caps_host[k];
     }
@@ -610,4 +648,31 @@ extern "C" int acn_ep_gather_grad(const float* gy, const int64_t* back, const in
     hipLaunchKernelGGL(ep_gather_grad_kernel, dim3(kEpBlocks), dim3(256), 0, (hipStream_t)stream, (const float4*)gy,
                        back, seg, E, (float4*)gout);
     return acn_check_launch("acn_ep_gather_grad");
+}
+
+extern "C" int acn_routed_count_batches(const float* rays, int64_t N, int S, int64_t batch, const float* jitter,
+                                        const acn_routing* routing, int64_t* counts, void* stream) {
+    ACN_REQUIRE(N >= 0 && S >= 1 && batch >= 1 && routing && counts, "acn_routed_count_batches: bad arguments");
+    const int K = routing->K;
+    ACN_REQUIRE(K >= 1 && K <= kMaxK, "acn_routed_count_batches: K = %d outside [1, %d]", K, kMaxK);
+    const int64_t nb = (N + batch - 1) / batch;
+    hipStream_t s = (hipStream_t)stream;
+    if (nb > 0) {
+        const hipError_t e = hipMemsetAsync(counts, 0, (size_t)(nb * K) * sizeof(int64_t), s);
+        if (e != hipSuccess) return acn_set_error((int)e, "acn_routed_count_batches: memset failed");
+    }
+    const int64_t M = N * (int64_t)S;
+    if (M == 0) return ACN_OK;
+    ACN_REQUIRE(rays, "acn_routed_count_batches: NULL rays");
+    RouteCfg cfg{};
+    cfg.K = K;
+    cfg.cluster_2d = routing->cluster_2d;
+    cfg.bm = routing->boundary_margin;
+    cfg.routing = routing->boundary_margin > 1.0f ? 1 : 2;
+    for (int k = 0; k < K; ++k)
+        for (int a = 0; a < 3; ++a) cfg.cent[k][a] = routing->centroids[k][a];
+    const unsigned blocks = blocks_for(M, kBlk) < 8192u ? blocks_for(M, kBlk) : 8192u;
+    hipLaunchKernelGGL(routed_count_batches_kernel, dim3(blocks), dim3(kBlk), 0, s, rays, N, S, batch, jitter, cfg,
+                       (unsigned long long*)counts);
+    return acn_check_launch("acn_routed_count_batches");
 }

@@ -243,11 +243,15 @@ class ExpertParallelRenderer:
       a2a #2  (rgb, sigma) back to the senders' pair slots
       sender  acn_ep_composite: blend in expert order + background + compositing in one launch -> rgb, depth,
               acc (+ weights): the (N, S, 4) field tensor is never materialised.
-    The per-sample arithmetic is the fused routed render's (SH-first colour layer 0), so each ray renders bit for bit as in the fused
-    single-process routed render.  ``capacity`` C per (sender, expert) segment: n_rays * S (default, never
-    overflows) or smaller to shrink the exchange; ``overflowed()`` reads the counts back (one host read, to be
-    called lazily, e.g. once per frame) and a caller re-renders an overflowed batch at full capacity.
-    Reference: models/inr/meta_container.py:300-337, nerfs/ray_rendering.py:577-627."""
+    The per-sample arithmetic is the fused routed render's (SH-first colour layer 0), so each ray renders bit
+    for bit as in the fused single-process routed render.  ``capacity`` C per (sender, expert) segment:
+    n_rays * S (default, never overflows) or smaller to shrink the exchange; ``overflowed()`` reads the counts
+    back (one host read, to be called lazily, e.g. once per frame) and a caller re-renders an overflowed batch at
+    full capacity.  ``render_planned(rays, counts)``: the exchange sized to the live records -- ``counts`` (W, K)
+    are every rank's pair counts of this batch (acn_routed_count_batches, all-gathered once per frame by
+    render_rays_ep_batched), the (sender, expert) segments hold exactly those pairs, so the all-to-alls move
+    40 B per live pair and nothing else (the reference sends each expert only its routed samples:
+    meta_container.py:307-321).  Reference: models/inr/meta_container.py:300-337, nerfs/ray_rendering.py:577-627."""
 
     def __init__(self, model, n_rays: int, ray_samples: int, group=None, capacity: Optional[int] = None,
                  graph: bool = False, bg_color_default: str = "white", want_weights: bool = False):
@@ -316,6 +320,8 @@ class ExpertParallelRenderer:
         self.graph = None
         self._graph_wanted = bool(graph)
         self.replays = 0
+        self.owner = owner
+        self.last_exchange = None    # bytes this rank sent in the last call: {"sent": .., "live": ..}
 
     def _run(self, n: int) -> None:
         import ctypes as C
@@ -348,6 +354,68 @@ class ExpertParallelRenderer:
                                  C.byref(self.bg_spec), 1.0, 0.0, ptr(self.rgb), ptr(self.depth), ptr(self.weights),
                                  ptr(self.acc), s), "acn_ep_composite")
 
+    def _run_planned(self, n: int, counts, recv_cnt: Tensor) -> None:
+        """One batch with the exchange sized by ``counts`` (host (W, K) ints: every rank's pair counts of this
+        batch, the capacities of its segments): compact layouts on both sides, no padding slot crosses a link.
+        ``recv_cnt``: the (W, E) counts of the owned experts on the device (int64; read by the field kernel)."""
+        import ctypes as C
+        from . import _lib
+        from ._lib import check, ptr
+        L = _lib.lib()
+        s = int(torch.cuda.current_stream(self.device).cuda_stream)
+        K, E, W, S, comm, rank, own, owner = self.K, self.E, self.W, self.S, self.comm, self.comm.rank, self.own, self.owner
+        mine = [int(c) for c in counts[rank]]
+        caps = (C.c_int64 * K)(*mine)
+        check(L.acn_routed_count_caps(ptr(self.rays), n, S, None, C.byref(self.routing), caps, ptr(self.t),
+                                      ptr(self.seg), ptr(self.rws), self.rws.numel(), s), "acn_routed_count_caps")
+        check(L.acn_routed_scatter_xd(ptr(self.rays), n, S, K, ptr(self.t), ptr(self.seg), ptr(self.rws),
+                                      ptr(self.pidx), ptr(self.pw), ptr(self.xd), ptr(self.pmap), ptr(self.pk), s),
+              "acn_routed_scatter_xd")
+        send = [sum(mine[k] for k in range(K) if owner[k] == o) for o in range(W)]
+        rc = [int(counts[w][k]) for w in range(W) for k in own]
+        recv = [sum(rc[w * E:(w + 1) * E]) for w in range(W)]
+        ps, pr = sum(send), sum(recv)
+        comm.all_to_all(self.recv_xd[:pr], self.xd[:ps], recv, send)
+        check(L.acn_pack_experts(self._own_arr, C.byref(self.own_routing), -1, ptr(self.packed),
+                                 self.packed.numel() * 4, s), "acn_pack_experts")
+        if pr > 0:
+            from . import ops
+            hook = ops.EVENT_HOOK   # bench.py timing (eager only: this path is never captured)
+            if hook is not None:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+            check(L.acn_ep_field_fwd_compact(ptr(self.recv_xd), ptr(recv_cnt), W, E, 0, max(rc), self._own_arr,
+                                             ptr(self.packed), self.packed.numel() * 4, ptr(self.ret), s),
+                  "acn_ep_field_fwd_compact")
+            if hook is not None:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record()
+                hook.append((e0, e1))
+        comm.all_to_all(self.yr[:ps], self.ret[:pr], send, recv)
+        check(L.acn_ep_composite(ptr(self.rays), n, S, None, ptr(self.yr), ptr(self.pw), ptr(self.pmap), K, self.hard,
+                                 C.byref(self.bg_spec), 1.0, 0.0, ptr(self.rgb), ptr(self.depth), ptr(self.weights),
+                                 ptr(self.acc), s), "acn_ep_composite")
+        # sent: the records out (24 B) and the results of the received records back (16 B); the live pairs of this
+        # rank are ps (its records) and pr (the records it evaluates for the others)
+        self.last_exchange = {"sent": 24 * ps + 16 * pr, "live": 24 * ps + 16 * pr, "pairs_sent": ps,
+                              "pairs_evaluated": pr}
+
+    def render_planned(self, rays: Tensor, counts, recv_cnt: Optional[Tensor] = None):
+        """As __call__, with the exchange sized by ``counts`` (host (W, K): every rank's pair counts of this batch,
+        acn_routed_count_batches).  Eager (the split sizes change per batch); collective over the group.
+        ``recv_cnt``: counts[w][own[e]] as a device int64 (W * E) tensor, if the caller already holds one."""
+        from ._lib import AcnError
+        n = int(rays.shape[0])
+        if rays.dim() != 2 or rays.shape[1] != 8 or not 0 < n <= self.N:
+            raise AcnError(f"ExpertParallelRenderer was built for up to {self.N} rays per rank; got {tuple(rays.shape)}")
+        self.rays[:n].copy_(rays, non_blocking=True)
+        if recv_cnt is None:   # a fresh device tensor per call: a reused pinned buffer could be rewritten before
+            recv_cnt = torch.tensor([int(counts[w][k]) for w in range(self.W) for k in self.own],   # its copy ran
+                                    dtype=torch.int64).to(self.device)
+        self._run_planned(n, counts, recv_cnt)
+        w = self.weights[:n] if self.weights is not None else None
+        return self.rgb[:n], self.depth[:n], w, self.acc[:n]
+
     def __call__(self, rays: Tensor):
         """(rgb (n,3), depth (n,), weights (n,S) or None, acc (n,)) of this rank's ``rays`` (n <= n_rays): views
         of persistent buffers, valid until the next call.  Collective over the group."""
@@ -356,6 +424,7 @@ class ExpertParallelRenderer:
         if rays.dim() != 2 or rays.shape[1] != 8 or not 0 < n <= self.N:
             raise AcnError(f"ExpertParallelRenderer was built for up to {self.N} rays per rank; got {tuple(rays.shape)}")
         self.rays[:n].copy_(rays, non_blocking=True)
+        self.last_exchange = {"sent": 8 * self.K + (24 + 16) * sum(self.split_send), "live": None}
         if n == self.N and self.graph is not None:
             self.graph.replay()
             self.replays += 1
@@ -388,13 +457,21 @@ def _renderer_for(model, n: int, S: int, group, cap: Optional[int]) -> ExpertPar
 
 @torch.no_grad()
 def render_rays_ep_batched(model, rays: Tensor, ray_samples: int, group=None, batch: int = 32768,
-                           capacity_frac: float = 1.0):
+                           capacity_frac: Optional[float] = None, stats: Optional[dict] = None):
     """(rgb, depth, acc) of this rank's ``rays`` through ExpertParallelRenderer in batches of ``batch`` rays.
     Every rank must make the same number of calls: the batch count is agreed on with one all-reduce (MAX) of
-    the rank's batch count.  ``capacity_frac`` < 1 sizes each (sender, expert) exchange segment to that share
-    of a batch's samples; the counts of all batches are read back once at the end and any overflowed batch is
-    re-rendered at full capacity (collectively)."""
-    world, _ = world_rank(group)
+    the rank's batch count.
+
+    Default (``capacity_frac`` None): the planned exchange.  One routing pass over the rank's rays counts the
+    pairs of every (batch, expert) (acn_routed_count_batches), one all-gather gives every rank all counts and
+    ONE host read per frame sizes every batch's all-to-alls to exactly its live pairs (40 B each: the 24-B
+    record out, the 16-B (rgb, sigma) back); the counts each batch actually routed are checked against the
+    plan at the end (the same routing arithmetic: a mismatch raises).
+    ``capacity_frac`` in (0, 1]: the fixed layout of ExpertParallelRenderer -- every (sender, expert) segment
+    holds that share of a batch's samples; the counts of all batches are read back once at the end and any
+    overflowed batch is re-rendered at full capacity (collectively).
+    ``stats``: filled with the bytes this rank sent ("sent") and the live pair bytes ("live") over the frame."""
+    world, rank = world_rank(group)
     n, S = int(rays.shape[0]), int(ray_samples)
     dev = rays.device
     nb = (n + batch - 1) // batch
@@ -402,6 +479,8 @@ def render_rays_ep_batched(model, rays: Tensor, ray_samples: int, group=None, ba
         t = torch.tensor([nb], dtype=torch.int64, device=dev)
         _Comm(group).all_reduce_max(t)
         nb = int(t)
+    if capacity_frac is None:
+        return _render_planned(model, rays, S, group, batch, nb, stats)
     M = batch * S
     cap = None if capacity_frac >= 1.0 else max(1, int(M * capacity_frac))
     r = _renderer_for(model, batch, S, group, cap)
@@ -433,12 +512,63 @@ def render_rays_ep_batched(model, rays: Tensor, ray_samples: int, group=None, ba
     return rgb, depth, acc
 
 
+def _render_planned(model, rays: Tensor, S: int, group, batch: int, nb: int, stats: Optional[dict]):
+    """render_rays_ep_batched's planned exchange (see there)."""
+    import ctypes as C
+    from . import _lib
+    from ._lib import AcnError, check, ptr
+    world, rank = world_rank(group)
+    n = int(rays.shape[0])
+    dev = rays.device
+    r = _renderer_for(model, batch, S, group, None)
+    K = r.K
+    L = _lib.lib()
+    plan = torch.zeros(nb, K, device=dev, dtype=torch.int64)
+    s = int(torch.cuda.current_stream(dev).cuda_stream)
+    if n:
+        check(L.acn_routed_count_batches(ptr(rays.contiguous()), n, S, batch, None, C.byref(r.routing), ptr(plan), s),
+              "acn_routed_count_batches")
+    if world > 1:
+        allp = torch.empty(world * nb, K, device=dev, dtype=torch.int64)
+        if r.comm.staged:
+            parts = [torch.empty(nb, K, dtype=torch.int64) for _ in range(world)]
+            dist.all_gather(parts, plan.cpu(), group=group)
+            allp = torch.cat(parts)
+        else:
+            dist.all_gather_into_tensor(allp, plan, group=group)
+        host = allp.view(world, nb, K).cpu().tolist()      # the one host read of the frame's plan
+    else:
+        host = [plan.cpu().tolist()]
+    rgb = torch.empty(n, 3, device=dev)
+    depth = torch.empty(n, device=dev)
+    acc = torch.empty(n, device=dev)
+    seen = torch.zeros(nb, K, device=dev, dtype=torch.int64)
+    dummy = rays[:1] if n else torch.zeros(1, 8, device=dev)
+    # every batch's received counts of the owned experts, on the device in one copy
+    rc_all = torch.tensor([[host[w][b][k] for w in range(world) for k in r.own] for b in range(nb)],
+                          dtype=torch.int64).to(dev)
+    sent = 0
+    for b in range(nb):
+        lo, hi = b * batch, min(n, (b + 1) * batch)
+        counts = [host[w][b] for w in range(world)]
+        o = r.render_planned(rays[lo:hi] if hi > lo else dummy, counts, rc_all[b])
+        if hi > lo:
+            rgb[lo:hi], depth[lo:hi], acc[lo:hi] = o[0], o[1], o[3]
+            seen[b] = r.seg[K + 1: 2 * K + 1]
+        sent += r.last_exchange["sent"]
+    if n and not torch.equal(seen[: (n + batch - 1) // batch], plan[: (n + batch - 1) // batch]):
+        raise AcnError("render_rays_ep_batched: a batch routed other pair counts than its plan")
+    if stats is not None:
+        stats.update(sent=sent, live=sent, batches=nb)
+    return rgb, depth, acc
+
+
 @torch.no_grad()
 def render_image_expert_parallel(model, *, H: int, W: int, fx: float, fy: float, cx: float, cy: float, c2w: Tensor,
                                  scene_box, ray_samples: int = 64, center_pixels: bool = True,
                                  gt_srgb: Optional[Tensor] = None, metrics_space: str = "linear", group=None,
                                  backend=None, rays: Optional[Tensor] = None, batch: int = 32768,
-                                 capacity_frac: float = 1.0):
+                                 capacity_frac: Optional[float] = None, stats: Optional[dict] = None):
     """render_image (ray_rendering.py:577-627) with the experts distributed: rank r renders a contiguous
     band of the frame's pixels through render_rays_expert_parallel (its samples' records go to the
     experts' owners), then the rendered rows are all-gathered and the PSNR all-reduced (parallel.py).
@@ -457,7 +587,7 @@ def render_image_expert_parallel(model, *, H: int, W: int, fx: float, fy: float,
                                                          len(model.submodules), group)
     else:
         rgb, depth, acc = render_rays_ep_batched(model, rays[idx].contiguous(), ray_samples, group=group,
-                                                 batch=batch, capacity_frac=capacity_frac)
+                                                 batch=batch, capacity_frac=capacity_frac, stats=stats)
     local = torch.cat([rgb.float().view(-1, 3), depth.float().view(-1, 1), acc.float().view(-1, 1)], dim=1)
     full = gather_rendered(local, plan, group)
     rgb_img = full[:, :3].reshape(H, W, 3).clamp_(0, 1)

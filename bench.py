@@ -794,6 +794,7 @@ def main():
     else:
         H, W, intr, c2w = frame_camera(scene, a.frame, a.frame)
         samples_per_step = H * W * S
+        ep_stats = {}   # --layout expert: the planned exchange's bytes of the last frame
         gt = torch.rand(H, W, 3, device=device, generator=torch.Generator(device).manual_seed(7))
 
         def step():
@@ -802,7 +803,8 @@ def main():
                     from adaptive_city_nerf_amd.expert_parallel import render_image_expert_parallel
                     return render_image_expert_parallel(model, H=H, W=W, fx=intr[0], fy=intr[1], cx=intr[2],
                                                         cy=intr[3], c2w=c2w, scene_box=gbox, ray_samples=S,
-                                                        gt_srgb=gt, group=dist.group.WORLD if world > 1 else None)
+                                                        gt_srgb=gt, group=dist.group.WORLD if world > 1 else None,
+                                                        stats=ep_stats)
                 return parallel.render_image_sharded(model, H=H, W=W, fx=intr[0], fy=intr[1], cx=intr[2], cy=intr[3],
                                                      c2w=c2w, scene_box=gbox, ray_samples=S, gt_srgb=gt)
         frays, fvalid = ops.get_rays_image(H, W, *intr, c2w, gbox.aabb, device, near_far_override=(None, None))
@@ -1263,6 +1265,13 @@ def main():
                                             "slot at the step's capacities; live = the same for the routed pairs"}
         if a.workload == "c4":
             line["psnr_vs_synthetic_gt_db"] = round(float(out[3]), 4)
+            if a.layout == "expert" and ep_stats:
+                line["exchange"] = {"bytes_sent_per_frame_per_rank": int(ep_stats["sent"]),
+                                    "live_pair_bytes_per_frame_per_rank": int(ep_stats["live"]),
+                                    "batches": int(ep_stats["batches"]),
+                                    "note": "planned exchange (acn_routed_count_batches + one all-gather and one "
+                                            "host read per frame): 24 B record out + 16 B result back per routed "
+                                            "pair, no padding slot; rank 0's figures"}
         if a.workload in ("c5", "meta"):
             line["mlp_precision"] = a.mlp_precision
             if a.mlp_precision == "amp":

@@ -549,7 +549,8 @@ int acn_routed_pad_pairs(const int64_t* seg, int K, int64_t max_pad, int32_t* pi
 /* Per-expert capacities (HOST arrays): acn_routed_count_caps lays expert k's pairs at [sum_{j<k} caps[j], + caps[k]);
  * acn_ep_gather_caps reads sender s's records of local expert j at s * sum(caps) + sum_{i<j} caps[i].  The
  * uniform-capacity forms above are these with every capacity equal (an exchange sized per expert to the
- * live records: expert_parallel.ExpertParallelAdaptStep(capacity="adaptive")).                             */
+ * live records: expert_parallel.ExpertParallelAdaptStep(capacity="adaptive")).  A capacity may be 0 (the
+ * planned exchange: capacities = the counts of acn_routed_count_batches, so the layout is compact).          */
 int acn_routed_count_caps(const float* rays, int64_t N, int S, const float* jitter, const acn_routing* routing,
                           const int64_t* caps, float* t_vals, int64_t* seg, void* workspace, size_t workspace_bytes,
                           void* stream);
@@ -577,6 +578,20 @@ int acn_ep_gather_grad(const float* gy, const int64_t* back, const int64_t* seg,
  *                       acn_render_stratified_fwd (weights may be NULL).                                   */
 int acn_ep_field_fwd(const float* recv_xd, const int64_t* recv_cnt, int W, int E, int64_t cap,
                      const acn_expert* experts, const void* packed, size_t packed_bytes, float* ret, void* stream);
+/* acn_ep_field_fwd_compact -> as acn_ep_field_fwd; cap = 0 selects the COMPACT received layout of a planned
+ *                       exchange: segment (src w, local expert e) holds exactly recv_cnt[w][e] records, segments in
+ *                       row-major (w, e) order with no gaps (W * E <= 1024); max_cnt = the largest recv_cnt (host,
+ *                       sizes the grid).  cap > 0: the fixed layout of acn_ep_field_fwd (max_cnt ignored). */
+int acn_ep_field_fwd_compact(const float* recv_xd, const int64_t* recv_cnt, int W, int E, int64_t cap, int64_t max_cnt,
+                             const acn_expert* experts, const void* packed, size_t packed_bytes, float* ret,
+                             void* stream);
+/* acn_routed_count_batches -> the plan of a planned expert-parallel frame: counts (ceil(N / batch), K) int64
+ *                       (device) = per batch of `batch` consecutive rays, the samples routed to each expert
+ *                       (w_k > 0; the counts acn_routed_count / _caps give that batch, same t and routing
+ *                       arithmetic).  Replaces nothing in the reference: it sizes the all-to-all that stands in
+ *                       for MetaContainer.forward's per-expert index_select (meta_container.py:307-321). */
+int acn_routed_count_batches(const float* rays, int64_t N, int S, int64_t batch, const float* jitter,
+                             const acn_routing* routing, int64_t* counts, void* stream);
 int acn_ep_composite(const float* rays, int64_t N, int S, const float* jitter, const float* yr, const float* pw,
                      const int32_t* pmap, int K, int hard, const acn_background* bg, float sigma_scale, float tau,
                      float* rgb, float* depth, float* weights, float* acc, void* stream);

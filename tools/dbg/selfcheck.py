@@ -22,6 +22,14 @@ from adaptive_city_nerf_amd import ops
 
 lib = os.environ.get("ACNERF_LIB", "default")
 total = 0
+import ctypes
+from adaptive_city_nerf_amd import _lib
+L = _lib.lib()
+fetch = getattr(L, "acn_debug_check_fetch", None)   # ACN_SLOTS_CHECK=2 builds: the recorded mismatches
+recs = []
+if fetch is not None:
+    fetch.argtypes, fetch.restype = [ctypes.c_void_p, ctypes.c_int], ctypes.c_int
+    buf = np.zeros((4096, 16), np.float32)
 for tag, active in (("k4", 2), ("k4", None), ("k8", None)):
     d, specs, routing, bg = _setup(tag)
     base = _t(d["render:rays"])
@@ -41,7 +49,20 @@ for tag, active in (("k4", 2), ("k4", None), ("k8", None)):
                         first = rgb.clone()
                     bad += int(torch.isnan(rgb).any(dim=-1).sum())
                     bad += int((~((rgb == first) | torch.isnan(rgb) | torch.isnan(first))).any(dim=-1).sum())
+                    if fetch is not None:
+                        torch.cuda.synchronize()
+                        nrec = fetch(buf.ctypes.data, 4096)
+                        for r in buf[:min(nrec, 4096)]:
+                            recs.append((tag, S, jitter) + tuple(float(v) for v in r))
             total += bad
             print(f"{os.path.basename(lib)} {tag} active={active} S={S} jitter={jitter}: {bad} rays flagged "
                   f"over {reps} renders", flush=True)
 print(f"{os.path.basename(lib)} TOTAL flagged: {total}", flush=True)
+if recs:
+    print("recorded mismatches: tag S jitter | ray sample single k_single k0 k1 | r1 r2 g1 g2 b1 b2 s1 s2 | lane folded")
+    for r in recs[:200]:
+        t = r[:3]
+        v = r[3:]
+        d = [abs(v[6] - v[7]), abs(v[8] - v[9]), abs(v[10] - v[11]), abs(v[12] - v[13]) / max(abs(v[13]), 1e-30)]
+        print(t, [int(x) for x in v[:6]], "diff r/g/b/rel-sigma %.3g %.3g %.3g %.3g" % tuple(d), "lane", int(v[14]),
+              "folded", int(v[15]))
