@@ -1507,6 +1507,208 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Routed render with the workgroup's field tiles shared (render_rws_kernel, C3 / C4: K > 2 experts, no early
+// termination).  render_ws_kernel's work sharing for the routed container: the 16 rays of a round are cut into
+// 32-sample tiles, waves take tiles from an LDS counter in tile-major order, a tile's (rgb, sigma) per sample goes
+// to LDS and the wave that completes a ray composites it with render_ray's exact sequence.  Each TILE is routed
+// on its own (render_slots_kernel routes whole rays): a tile whose 32 samples all go to ONE expert k with weight
+// exactly 1.0f takes that expert's field alone (0 + y_k * 1.0f == y_k), the others blend every needed expert in
+// ascending k from zero (meta_container.py:320-337).  One LDS slot holds the expert most of the round's rays need
+// (the rays arrive sorted by owning expert, parallel.expert_sorted_plan), folded per ray once at the round start;
+// any other expert is read from its packed image in global memory (L2) and folded per tile, as the slots kernel
+// does.  Every (sample, expert) evaluation, blend and composite is the slots kernel's arithmetic, so the outputs
+// are bit-identical to render_slots_kernel (tests/test_render_ws.py, test_k8.py, test_batch_independence.py).
+// 1024 threads, 128 VGPRs (16 waves per CU, as render_ws_kernel; the slots kernel runs 8).
+#ifndef ACN_ROUTED_WS
+#define ACN_ROUTED_WS 0   // experimental
+#endif
+
+#ifndef ACN_DIAG_RWS_NOGLOBAL
+#define ACN_DIAG_RWS_NOGLOBAL 0   // diagnostic build only: every expert from the LDS slot (wrong values; timing)
+#endif
+constexpr int kRwsMaxT = kWsMaxS / 32;   // tiles per ray
+constexpr uint32_t kTileSingle = 1u << 31;
+
+// the field of one tile through an expert read from L2 (fold + folded field tile, the slots kernel's L2 path),
+// out of line: its global-address arithmetic would otherwise raise the register pressure of the LDS path
+template <int INTERP>
+__device__ __attribute__((noinline)) void field_tile_l2(const float* Wg, const ExpertMeta& em, int log2T, float px,
+                                                        float py, float pz, const float (&shv)[8], float* cbg, int lane,
+                                                        float& r, float& g, float& b, float& sg) {
+    fold_sh_bias(Wg, shv, lane, cbg);
+    field_tile<INTERP, true>(Wg, em, log2T, px, py, pz, shv, cbg, lane, r, g, b, sg);
+}
+
+template <int INTERP, int ROUTE>
+__global__ void __launch_bounds__(1024, 4) render_rws_kernel(FieldCfg cfg, BgArgs bg, RenderParams p) {
+    static_assert(ACN_SHFOLD != 0, "render_rws_kernel folds the SH colour bias");
+    __shared__ __attribute__((aligned(16))) float smem[PK_FLOATS];        // the slot expert's packed image
+    __shared__ __attribute__((aligned(16))) float cbuf[16 * 64];          // round ray r: slot expert's folded bias
+    __shared__ __attribute__((aligned(16))) float cbgb[16 * 64];          // wave w: an L2 expert's folded bias
+    __shared__ __attribute__((aligned(16))) f32x4 ybuf[16 * kWsMaxS];
+    __shared__ uint32_t tmask[16][kRwsMaxT];   // per round ray and tile: expert bits | kTileSingle
+    __shared__ uint32_t rmask[16];             // per round ray: union of its tiles' experts
+    __shared__ int qhead, done[16], slot_k;
+    const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float* cbg = cbgb + wave * 64;
+    const int S = p.S;
+    const int T = (S + 31) >> 5;
+    const float step = 1.0f / (float)(S - 1);
+    if (threadIdx.x == 0) slot_k = -1;
+    int64_t base, hi, stride;
+    if ((gridDim.x & 7) == 0) {   // XCD bands (render_kernel)
+        const int64_t chunk = (p.N + 7) >> 3;
+        const int64_t lo = min(p.N, (int64_t)(blockIdx.x & 7) * chunk);
+        hi = min(p.N, lo + chunk);
+        base = lo + (int64_t)(blockIdx.x >> 3) * 16;
+        stride = (int64_t)(gridDim.x >> 3) * 16;
+    } else {
+        hi = p.N;
+        base = (int64_t)blockIdx.x * 16;
+        stride = (int64_t)gridDim.x * 16;
+    }
+    for (; base < hi; base += stride) {   // block-uniform
+        const int nr = (int)min((int64_t)16, hi - base);
+        // ---- A: wave w routes round ray w, tile by tile (sample sc = min(s, S - 1), as the field evaluates it)
+        if (wave < nr) {
+            const int64_t r0 = p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[base + wave]) : base + wave;
+            const float* rp = p.rays + r0 * 8;
+            const float ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
+            const float near = rp[6], far = rp[7];
+            const float* jit = p.jitter ? p.jitter + r0 * S : nullptr;
+            uint32_t un = 0u;
+            for (int t = 0; t < T; ++t) {
+                const int s = t * 32 + j;
+                const int sc = s < S ? s : S - 1;
+                const float tv = jit ? tval(near, far, sc, S, jit) : tlin_sel(near, far, sc, S, step);
+                const float px = ox + dx * tv, py = oy + dy * tv, pz = oz + dz * tv;
+                uint32_t m = 0u;
+                bool exact = true;
+                if (ROUTE == 1) {
+                    const RouteState st = route_prep<1>(cfg, px, py, pz);
+                    for (int k = 0; k < cfg.K; ++k) {
+                        const float w = route_weight(cfg, st, k, px, py, pz);
+                        if (w > 0.0f) m |= 1u << k;
+                        exact = exact && (w == 0.0f || w == 1.0f);
+                    }
+                } else {
+                    m = 1u << route_prep<2>(cfg, px, py, pz).hard;
+                }
+                uint32_t tm = 0u;
+                for (int k = 0; k < cfg.K; ++k)
+                    if (__ballot((m >> k) & 1u) != 0ull) tm |= 1u << k;
+                if (__popc(tm) == 1 && __ballot(!exact) == 0ull) tm |= kTileSingle;
+                un |= tm & ~kTileSingle;
+                if (lane == 0) tmask[wave][t] = tm;
+            }
+            if (lane == 0) rmask[wave] = un;
+        }
+        if (threadIdx.x == 0) qhead = 0;
+        if (threadIdx.x < 16) done[threadIdx.x] = 0;
+        __syncthreads();
+        // ---- B: the slot expert = the one most of the round's rays need (kept when tied with the resident one)
+        int want = -1;
+        {
+            int best = 0;
+            for (int k = 0; k < cfg.K; ++k) {
+                int c = 0;
+                for (int r = 0; r < nr; ++r) c += (rmask[r] >> k) & 1u;
+                if (c > best || (c == best && c > 0 && k == slot_k)) { best = c; want = k; }
+            }
+        }
+        want = __builtin_amdgcn_readfirstlane(want);
+        if (want >= 0 && want != __builtin_amdgcn_readfirstlane(slot_k)) {
+            __syncthreads();   // every wave has read slot_k
+            const f32x4* src = reinterpret_cast<const f32x4*>(p.packed + (size_t)want * PK_FLOATS);
+            f32x4* dst = reinterpret_cast<f32x4*>(smem);
+            for (int i = threadIdx.x; i < PK_FLOATS / 4; i += blockDim.x) dst[i] = src[i];
+            if (threadIdx.x == 0) slot_k = want;
+            __syncthreads();
+        }
+        const int ks = __builtin_amdgcn_readfirstlane(slot_k);
+        // ---- B2: wave w folds the slot expert's SH colour bias for its ray (used by every tile of the ray)
+        if (wave < nr && ks >= 0 && ((rmask[wave] >> ks) & 1u)) {
+            const int64_t r0 = p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[base + wave]) : base + wave;
+            const float* rp = p.rays + r0 * 8;
+            float sh[16], sv[8];
+            dir_sh(rp[3], rp[4], rp[5], sh);
+            sh_rows_for_half(sh, h, sv);
+            fold_sh_bias(smem, sv, lane, cbuf + wave * 64);
+        }
+        __syncthreads();
+        // ---- C: tiles, tile-major
+        int64_t cur = -1;
+        float shv[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+        float ox = 0.0f, oy = 0.0f, oz = 0.0f, dx = 0.0f, dy = 0.0f, dz = 0.0f, near = 0.0f, far = 0.0f;
+        const float* jit = nullptr;
+        for (;;) {
+            int item = 0;
+            if (lane == 0) item = __hip_atomic_fetch_add(&qhead, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            item = __builtin_amdgcn_readlane(item, 0);
+            if (item >= nr * T) break;
+            const int tile = item / nr, slot = item - tile * nr;
+            const int64_t ray = p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[base + slot]) : base + slot;
+            if (ray != cur) {
+                const float* rp = p.rays + ray * 8;
+                ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
+                near = rp[6], far = rp[7];
+                jit = p.jitter ? p.jitter + ray * S : nullptr;
+                float sh[16];
+                dir_sh(dx, dy, dz, sh);
+                sh_rows_for_half(sh, h, shv);
+                cur = ray;
+            }
+            const int s = tile * 32 + j;
+            const int sc = s < S ? s : S - 1;
+            const float t = jit ? tval(near, far, sc, S, jit) : tlin_sel(near, far, sc, S, step);
+            const float px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;
+            const uint32_t tm = __builtin_amdgcn_readfirstlane(tmask[slot][tile]);
+            // the container over the tile's experts in ascending k from zero (meta_container.py:320-337); a single-
+            // expert tile has weight exactly 1.0f on every sample, so 0 + y_k * 1.0f == y_k needs no routing
+            const bool single = (tm & kTileSingle) != 0u;
+            RouteState st{0.0f, 1.0f, 0};
+            if (!single) st = route_prep<ROUTE>(cfg, px, py, pz);
+            float yr = 0.0f, yg = 0.0f, yb = 0.0f, ys = 0.0f;
+            for (uint32_t rest = tm & ~kTileSingle; rest; rest &= rest - 1u) {
+                const int k = __builtin_ctz(rest);
+                float r, g, b, sg;
+                if (ACN_DIAG_RWS_NOGLOBAL || k == ks)   // the slot expert: LDS image, the ray's folded bias
+                    field_tile<INTERP, true>(smem, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbuf + slot * 64, lane, r, g,
+                                             b, sg);
+                else           // another expert: its packed image in L2, folded per tile (out of line)
+                    field_tile_l2<INTERP>(p.packed + (size_t)k * PK_FLOATS, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbg,
+                                          lane, r, g, b, sg);
+                sg = trunc_exp(sg);
+                const float wk = single ? 1.0f : ((ROUTE == 1) ? route_weight(cfg, st, k, px, py, pz) : 0.0f);
+                const bool need = single || ((ROUTE == 1) ? (wk > 0.0f) : (st.hard == k));
+                if (need) {
+                    if (ROUTE == 1 || single) {
+                        yr = yr + r * wk;
+                        yg = yg + g * wk;
+                        yb = yb + b * wk;
+                        ys = ys + sg * wk;
+                    } else {
+                        yr = r; yg = g; yb = b; ys = sg;
+                    }
+                }
+            }
+            if (h == 0 && s < S) {
+                f32x4 v;
+                v[0] = yr, v[1] = yg, v[2] = yb, v[3] = ys;
+                ybuf[slot * kWsMaxS + s] = v;
+            }
+            int old = 0;
+            if (lane == 0) old = __hip_atomic_fetch_add(&done[slot], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+            old = __builtin_amdgcn_readlane(old, 0);
+            if (old != T - 1) continue;
+            composite_ray_lds(p, bg, ray, ybuf + slot * kWsMaxS, lane, step);
+        }
+        __syncthreads();   // ybuf / tmask / rmask / cbuf / qhead / done reused by the next round
+    }
+}
+
 // inclusive scan over the 64 lanes of a wave on DPP: row_shr 1/2/4/8 inside each 16-lane row, then
 // row_bcast:15 / :31 carry the row totals upward (gfx9-family DPP)
 __device__ __forceinline__ int wave_incl_scan(int v) {
@@ -2358,6 +2560,18 @@ extern "C" int acn_render_stratified_fwd_ordered(const float* rays, int64_t N, i
         if (ACN_SLOTS && KL == 0 && R != 0) hipLaunchKernelGGL((render_slots_kernel<I, (R == 0 ? 1 : R)>), grid, dim3(ACN_SLOTS_THREADS), 0, s, cfg, b, p); \
         else hipLaunchKernelGGL((render_kernel<I, KL, R>), grid, block, 0, s, cfg, b, p);            \
     } while (0)
+    if (ACN_ROUTED_WS && slots && S <= kWsMaxS && !(tau > 0.0f)) {
+        // routed container, no early termination: tiles routed one by one and shared by the workgroup
+        // (bit-identical to render_slots_kernel)
+#define ACN_RWS_LAUNCH(I, R) hipLaunchKernelGGL((render_rws_kernel<I, R>), grid, block, 0, s, cfg, b, p)
+        if (cfg.routing == 1) {
+            if (interp == 1) ACN_RWS_LAUNCH(1, 1); else if (interp == 0) ACN_RWS_LAUNCH(0, 1); else ACN_RWS_LAUNCH(2, 1);
+        } else {
+            if (interp == 1) ACN_RWS_LAUNCH(1, 2); else if (interp == 0) ACN_RWS_LAUNCH(0, 2); else ACN_RWS_LAUNCH(2, 2);
+        }
+#undef ACN_RWS_LAUNCH
+        return acn_check_launch("acn_render_stratified_fwd");
+    }
     if (ACN_RENDER_WS && cfg.routing == 0 && S <= kWsMaxS && !(tau > 0.0f)) {
         // one expert, no early termination: the workgroup shares its rays' field tiles (bit-identical outputs)
         if (interp == 1) hipLaunchKernelGGL(render_ws_kernel<1>, grid, block, 0, s, cfg, b, p);

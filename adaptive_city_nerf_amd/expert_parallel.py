@@ -134,7 +134,11 @@ def adapt_step_expert_parallel(P, backend, rays: Tensor, rgbs: Tensor, optimizer
     experts get the complete gradients of the samples routed to them from every rank; the ``shared``
     background head is all-reduced; the clip norm is global (shared parameters counted once).  Returns the
     global MSE (device)."""
+    from . import ops
     from .optim import FusedAdam
+    if ops.TRAIN_MLP_PRECISION == "amp":
+        raise ValueError("adapt_step_expert_parallel: the use_amp MLP precision needs a loss scale; select 'fp16x3' "
+                         "or 'fp32' for expert-parallel steps")
     world, _ = world_rank(group)
     optimizer.zero_grad()
     rgb = render_rays_expert_parallel(backend, rays, S=int(P.ray_samples), K=K, group=group, u=u)[0]
@@ -528,7 +532,7 @@ def _render_planned(model, rays: Tensor, S: int, group, batch: int, nb: int, sta
     if n:
         check(L.acn_routed_count_batches(ptr(rays.contiguous()), n, S, batch, None, C.byref(r.routing), ptr(plan), s),
               "acn_routed_count_batches")
-    if world > 1:
+    if r.comm.direct:
         allp = torch.empty(world * nb, K, device=dev, dtype=torch.int64)
         if r.comm.staged:
             parts = [torch.empty(nb, K, dtype=torch.int64) for _ in range(world)]
@@ -599,6 +603,9 @@ def render_image_expert_parallel(model, *, H: int, W: int, fx: float, fy: float,
 
 
 # ============================================================================ sync-free expert-parallel step
+FORCE_COLLECTIVES = False   # tests: the exchanges through the process group even at world size 1 (RCCL on one GPU)
+
+
 class _Comm:
     """The step's collectives on device buffers of host-known constant sizes (no count exchange on the
     host): RCCL directly (``nccl`` backend), ``gloo`` through staged host copies (the multi-process tests of
@@ -607,10 +614,13 @@ class _Comm:
     def __init__(self, group=None):
         self.world, self.rank = world_rank(group)
         self.group = group
-        self.staged = self.world > 1 and dist.get_backend(group) == "gloo"
+        # FORCE_COLLECTIVES: run the collectives even at world size 1 (tests: RCCL on one GPU)
+        self.force = FORCE_COLLECTIVES and dist.is_available() and dist.is_initialized()
+        self.direct = self.world > 1 or self.force
+        self.staged = self.direct and dist.get_backend(group) == "gloo"
 
     def all_to_all(self, out: Tensor, inp: Tensor, out_splits: Sequence[int], in_splits: Sequence[int]) -> None:
-        if self.world == 1:
+        if not self.direct:
             out.copy_(inp)
         elif self.staged:
             oc = torch.empty(out.shape, dtype=out.dtype)
@@ -620,7 +630,7 @@ class _Comm:
             dist.all_to_all_single(out, inp, list(out_splits), list(in_splits), group=self.group)
 
     def all_reduce(self, t: Tensor) -> None:
-        if self.world == 1:
+        if not self.direct:
             return
         if self.staged:
             c = t.cpu()
@@ -630,7 +640,7 @@ class _Comm:
             dist.all_reduce(t, group=self.group)
 
     def all_reduce_max(self, t: Tensor) -> None:
-        if self.world == 1:
+        if not self.direct:
             return
         if self.staged:
             c = t.cpu()
@@ -691,6 +701,11 @@ class ExpertParallelAdaptStep:
         W, rank = comm.world, comm.rank
         self.P, self.model, self.opt, self.grad_clip = P, model, optimizer, grad_clip
         self.mlp_precision = ops.TRAIN_MLP_PRECISION   # training MLP kernels (ops.set_train_mlp_precision)
+        if self.mlp_precision == "amp":
+            # the fp16 (use_amp) kernels need a loss scale, and this step carries none: gradients of
+            # magnitude < 2^-24 would flush to zero (test_amp_underflow_without_loss_scale)
+            raise AcnError("ExpertParallelAdaptStep: the use_amp MLP precision needs a loss scale this step does not "
+                           "carry; select 'fp16x3' or 'fp32' (ops.set_train_mlp_precision)")
         self.jitter_mode = jitter
         self.clear_in_adam = bool(clear_in_adam)
         self.tele = TELESCOPED_TABLE_NORM and grad_clip is not None
@@ -941,7 +956,7 @@ class ExpertParallelAdaptStep:
         self.adam.step(self.eseg, self.grad_clip, self.table_sumsq if self.tele else None,
                        hook=RT.EVENT_HOOK if self.graph is None and not torch.cuda.is_current_stream_capturing()
                        else None,
-                       allreduce=comm.all_reduce if self.W > 1 else None)
+                       allreduce=comm.all_reduce if self.W > 1 else None)   # the norm's split form: W > 1 only
         self.loss_global.copy_(self.loss.view(1))
         comm.all_reduce(self.loss_global)
         if saved is not None:
@@ -1035,5 +1050,13 @@ class ExpertParallelAdaptStep:
         return self.adam.scale
 
     def sync_state(self) -> None:
+        """flush() + the host Adam state.  Call it at the end of an adaptation loop and before reading the
+        parameters: a capacity-bounded step that overflowed is re-run only here or at the next call."""
         self.flush()
         self.adam.sync_state()
+
+    def __del__(self):
+        if getattr(self, "_check", None) is not None:
+            import warnings
+            warnings.warn("ExpertParallelAdaptStep dropped with an unsettled capacity-bounded step: call flush() "
+                          "(or sync_state()) after the last step, or an overflowed last update is lost")

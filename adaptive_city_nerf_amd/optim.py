@@ -327,7 +327,14 @@ class AmpScaler:
     def state_dict(self) -> dict:
         """GradScaler.state_dict()'s keys."""
         return {"scale": self.get_scale(), "growth_factor": self.growth_factor, "backoff_factor": self.backoff_factor,
-                "growth_interval": self.growth_interval, "_growth_tracker": int(self.tracker[0])}
+                "growth_interval": self.growth_interval,
+                "_growth_tracker": int(self.tracker.reshape(-1)[0])}   # a wrapped GradScaler's tracker is 0-dim
+
+    def reset(self, init_scale: float = 2.0 ** 16) -> None:
+        """A fresh GradScaler's state (the reference builds one per runtime_adapt call, runtime_adapt.py:237)."""
+        self.scale_t.fill_(float(init_scale))
+        self.tracker.zero_()
+        self.found.zero_()
 
     def load_state_dict(self, d: dict) -> None:
         self.growth_factor, self.backoff_factor = float(d["growth_factor"]), float(d["backoff_factor"])

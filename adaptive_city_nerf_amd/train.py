@@ -4,8 +4,9 @@ nerfs/losses.py:10-32 ``compute_mse_loss``) on the HIP path.
 One step = ``render_rays`` in training mode (stratified jitter) through the differentiable
 per-expert forward -> sRGB/linear colour transform -> MSE -> backward (the hash-grid gather
 backward is a HIP scatter-add kernel) -> ``clip_grad_norm_`` + Adam as one fused multi-tensor HIP
-step (optim.FusedAdam).  The reference wraps the forward in fp16 autocast with a GradScaler; this
-build computes in fp32 (SURVEY §8(b) "Autocast / dtype"), so the scaler is the identity.
+step (optim.FusedAdam).  The reference wraps the forward in fp16 autocast with a GradScaler; the default
+fp16x3 MLP keeps fp32 accuracy, so no scale is needed; the use_amp precision (the reference's fp16
+arithmetic, ops.set_train_mlp_precision("amp")) runs under a GradScaler like the reference's.
 
 Expert-parallel use: ``adapt_step(..., group=)`` on the routed container
 (active_module None, the online stage's call, runtime_adapt.py:88-90) distributes the experts over the
@@ -66,12 +67,15 @@ def compute_mse_loss(P, model, data, params=None, active_module=None, reduction:
 
 
 def adapt_step(P, base, rays, rgbs, optimizer, active_module=None, grad_clip: Optional[float] = 1.0,
-               group=None, shared: Optional[list] = None, **render_kwargs) -> torch.Tensor:
+               group=None, shared: Optional[list] = None, grad_scaler=None, **render_kwargs) -> torch.Tensor:
     """One optimizer update of runtime_adapt (runtime_adapt.py:288-313).  Returns the loss (device).
 
     ``group`` (expert parallel): ``rays`` / ``rgbs`` are this rank's shard of the global batch, the
     container's experts are distributed over the group (expert_parallel.adapt_step_expert_parallel);
-    ``shared`` are the replicated parameters (default: the background head)."""
+    ``shared`` are the replicated parameters (default: the background head).
+    With the use_amp MLP precision (ops.set_train_mlp_precision("amp")) the step runs under a GradScaler as
+    the reference's does (runtime_adapt.py:237-268): ``grad_scaler`` (a torch.amp.GradScaler; a fresh one when
+    None) scales the loss, unscales, skips a non-finite step and updates its scale."""
     if group is not None and torch.distributed.is_initialized() and torch.distributed.get_world_size(group) > 1:
         from .expert_parallel import HipBackend, adapt_step_expert_parallel
         if active_module is not None:
@@ -85,6 +89,18 @@ def adapt_step(P, base, rays, rgbs, optimizer, active_module=None, grad_clip: Op
     optimizer.zero_grad()
     loss = compute_mse_loss(P, model=base, data={"rays": rays, "rgbs": rgbs}, params=None,
                             active_module=active_module, reduction="mean", **render_kwargs)
+    if ops.TRAIN_MLP_PRECISION == "amp":
+        scaler = grad_scaler if grad_scaler is not None else torch.amp.GradScaler("cuda")
+        scaler.scale(loss).backward()
+        scaler.unscale_(optimizer)
+        if isinstance(optimizer, FusedAdam):
+            scaler.step(optimizer, max_norm=grad_clip)
+        else:
+            if grad_clip is not None:
+                torch.nn.utils.clip_grad_norm_(base.parameters(), grad_clip)
+            scaler.step(optimizer)
+        scaler.update()
+        return loss.detach()
     loss.backward()
     if isinstance(optimizer, FusedAdam):
         optimizer.step(max_norm=grad_clip)  # clip_grad_norm_ folded into the fused step
@@ -206,6 +222,10 @@ def runtime_adapt(*, P, model, data_loader: Iterable, optimizer, steps: Optional
     base = model.submodules[active_module] if active_module is not None else model
     last_loss, step_count = None, 0
     fast = [None, active_module is None]   # [RoutedAdaptStep, still worth trying]
+    # use_amp: a fresh GradScaler per call (runtime_adapt.py:237); the cached RoutedAdaptStep's scaler restarts too
+    amp = ops.TRAIN_MLP_PRECISION == "amp"
+    scaler = torch.amp.GradScaler("cuda") if amp else None
+    reset = set()
 
     def run(rays, rgbs):
         nonlocal last_loss, step_count
@@ -214,9 +234,13 @@ def runtime_adapt(*, P, model, data_loader: Iterable, optimizer, steps: Optional
             fast[0] = _routed_step_for(P, base, optimizer, int(rays.shape[0]), grad_clip)
             fast[1] = fast[0] is not None
         if fast[0] is not None:
+            if amp and getattr(fast[0], "amp", None) is not None and id(fast[0]) not in reset:
+                fast[0].amp.reset()
+                reset.add(id(fast[0]))
             last_loss = fast[0](rays, rgbs)
         else:
-            last_loss = adapt_step(P, base, rays, rgbs, optimizer, active_module=active_module, grad_clip=grad_clip)
+            last_loss = adapt_step(P, base, rays, rgbs, optimizer, active_module=active_module, grad_clip=grad_clip,
+                                   grad_scaler=scaler)
         step_count += 1
 
     if steps is None:

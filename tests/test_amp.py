@@ -291,3 +291,81 @@ def test_amp_graphed_meta_step_matches_eager_gradscaler(monkeypatch):
         _compare_meta_runs(ma, oa, mb, ob, ra, rb, lambda n: 4)
     finally:
         ops.set_train_mlp_precision(was)
+
+
+def test_expert_parallel_step_rejects_amp_without_loss_scale():
+    """the expert-parallel step carries no loss scale, so it refuses the use_amp kernels."""
+    from types import SimpleNamespace
+    import goldens as G
+    from test_module_api import build_model, reference_state_dict
+    from adaptive_city_nerf_amd import ops
+    from adaptive_city_nerf_amd._lib import AcnError
+    from adaptive_city_nerf_amd.expert_parallel import ExpertParallelAdaptStep
+    from adaptive_city_nerf_amd.optim import build_optimizer
+    d = G.load("train_k8")
+    P = SimpleNamespace(ray_samples=96, chunk_points=4_000_000, color_space="linear", optimizer="adam", lr=1e-4,
+                        encoding_lr=0.01, sigma_lr=0.002, color_lr=0.002, bg_lr=0.001, weight_decay=0.0)
+    m, _ = build_model("k8")
+    m.load_state_dict(reference_state_dict(d, 8, "w:"))
+    m = m.cuda().train()
+    opt = build_optimizer(P, m)
+    was = ops.TRAIN_MLP_PRECISION
+    ops.set_train_mlp_precision("amp")
+    try:
+        with pytest.raises(AcnError, match="loss scale"):
+            ExpertParallelAdaptStep(P, m, 1000, opt)
+    finally:
+        ops.set_train_mlp_precision(was)
+
+
+def test_eager_adapt_step_under_amp_uses_a_grad_scaler():
+    """the eager adapt_step (ragged batches, active_module updates) with the use_amp kernels runs
+    under a GradScaler as the reference's runtime_adapt does (runtime_adapt.py:237-268): the loss scale reaches
+    the fp16 backward (no underflow to all-zero tables) and the step equals the fp16x3 step within use_amp's
+    tolerance; the scaler's scale is used and kept."""
+    from types import SimpleNamespace
+    import goldens as G
+    from test_module_api import build_model, reference_state_dict
+    from adaptive_city_nerf_amd import ops
+    from adaptive_city_nerf_amd.optim import build_optimizer
+    from adaptive_city_nerf_amd.train import adapt_step
+    d = G.load("train_k8")
+    P = SimpleNamespace(ray_samples=96, chunk_points=4_000_000, color_space="linear", optimizer="adam", lr=1e-4,
+                        encoding_lr=0.01, sigma_lr=0.002, color_lr=0.002, bg_lr=0.001, weight_decay=0.0)
+    rays = torch.from_numpy(d["train0:rays"]).cuda()
+    rgbs = torch.from_numpy(d["train0:rgbs"]).cuda()
+    u = torch.from_numpy(d["train0:u"]).cuda()
+    res = {}
+    was = ops.TRAIN_MLP_PRECISION
+    for prec in ("fp16x3", "amp"):
+        ops.set_train_mlp_precision(prec)
+        try:
+            m, _ = build_model("k8")
+            m.load_state_dict(reference_state_dict(d, 8, "w:"))
+            m = m.cuda().train()
+            opt = build_optimizer(P, m)
+            gs = torch.amp.GradScaler("cuda")
+            loss = adapt_step(P, m, rays, rgbs, opt, active_module=2, grad_clip=1.0, grad_scaler=gs, jitter_u=u)
+            g = m.submodules[2].xyz_encoder.hash_table.grad
+            res[prec] = (float(loss), None if g is None else g.detach().clone(), gs.get_scale())
+        finally:
+            ops.set_train_mlp_precision(was)
+    (l0, g0, _), (l1, g1, s1) = res["fp16x3"], res["amp"]
+    assert abs(l1 - l0) <= 2e-3 * l0
+    assert s1 == 2.0 ** 16                     # a finite first step keeps the initial scale
+    assert g1 is not None and int((g1 != 0).sum()) > 0.9 * int((g0 != 0).sum())
+
+
+def test_amp_scaler_wrap_state_dict_and_reset():
+    """state_dict() of an AmpScaler wrapping a torch GradScaler (0-dim tracker); reset() restores a
+    fresh scaler's state (one GradScaler per runtime_adapt call in the reference)."""
+    from adaptive_city_nerf_amd.optim import AmpScaler
+    gs = torch.amp.GradScaler("cuda", init_scale=1024.0)
+    a = AmpScaler.wrap(gs, torch.device("cuda"))
+    sd = a.state_dict()
+    assert sd["scale"] == 1024.0 and sd["_growth_tracker"] == 0
+    a.scale_t.fill_(8.0)
+    a.tracker.fill_(3)
+    assert a.state_dict()["_growth_tracker"] == 3 and gs.get_scale() == 8.0
+    a.reset()
+    assert a.get_scale() == 2.0 ** 16 and a.state_dict()["_growth_tracker"] == 0
