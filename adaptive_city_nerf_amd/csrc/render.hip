@@ -1509,50 +1509,38 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
 
 // ------------------------------------------------------------------------------------------
 // Routed render with the workgroup's field tiles shared (render_rws_kernel, C3 / C4: K > 2 experts, no early
-// termination).  render_ws_kernel's work sharing for the routed container: the 16 rays of a round are cut into
-// 32-sample tiles, waves take tiles from an LDS counter in tile-major order, a tile's (rgb, sigma) per sample goes
-// to LDS and the wave that completes a ray composites it with render_ray's exact sequence.  Each TILE is routed
-// on its own (render_slots_kernel routes whole rays): a tile whose 32 samples all go to ONE expert k with weight
-// exactly 1.0f takes that expert's field alone (0 + y_k * 1.0f == y_k), the others blend every needed expert in
-// ascending k from zero (meta_container.py:320-337).  One LDS slot holds the expert most of the round's rays need
-// (the rays arrive sorted by owning expert, parallel.expert_sorted_plan), folded per ray once at the round start;
-// any other expert is read from its packed image in global memory (L2) and folded per tile, as the slots kernel
-// does.  Every (sample, expert) evaluation, blend and composite is the slots kernel's arithmetic, so the outputs
-// are bit-identical to render_slots_kernel (tests/test_render_ws.py, test_k8.py, test_batch_independence.py).
-// 1024 threads, 128 VGPRs (16 waves per CU, as render_ws_kernel; the slots kernel runs 8).
+// termination).  render_ws_kernel's work sharing for the routed container, expert by expert:
+//   A  wave w routes round ray w tile by tile (32 samples, the MFMA unit): per tile the experts its samples need,
+//      and whether every sample goes to ONE expert with weight exactly 1.0f (then 0 + y_k * 1.0f == y_k and the
+//      tile needs no per-sample routing later);
+//   B  for each expert k the round needs, in ascending k (the container's blend order, meta_container.py:320-337):
+//      stage k's packed image into the workgroup's LDS slot (only when it changes: rays arrive sorted by owning
+//      expert, parallel.expert_sorted_plan), fold its SH colour bias per ray, then the waves take the round's tiles
+//      that need k from an LDS counter (tile-major) and add y_k * w_k per sample into the LDS accumulator of the
+//      sample (hard routing: the argmin expert's y_k);
+//   C  the wave that completes a ray's last (tile, expert) evaluation composites it from LDS with render_ray's
+//      exact sequence (composite_ray_lds).
+// Per (sample, expert) the arithmetic is render_slots_kernel's (fold + folded field tile, trunc_exp, blend in
+// ascending k from zero), so the outputs are bit-identical to it (tests/test_render_ws.py, test_k8.py,
+// test_batch_independence.py).  No expert is ever read from L2 inside a field tile: one field_tile
+// instantiation, 1024 threads at <= 128 VGPRs (16 waves per CU; the slots kernel runs 8 at 256 VGPRs).
 #ifndef ACN_ROUTED_WS
-#define ACN_ROUTED_WS 0   // experimental
-#endif
-
-#ifndef ACN_DIAG_RWS_NOGLOBAL
-#define ACN_DIAG_RWS_NOGLOBAL 0   // diagnostic build only: every expert from the LDS slot (wrong values; timing)
+#define ACN_ROUTED_WS 0   // measured slower than render_slots_kernel; bit-identical
 #endif
 constexpr int kRwsMaxT = kWsMaxS / 32;   // tiles per ray
 constexpr uint32_t kTileSingle = 1u << 31;
 
-// the field of one tile through an expert read from L2 (fold + folded field tile, the slots kernel's L2 path),
-// out of line: its global-address arithmetic would otherwise raise the register pressure of the LDS path
-template <int INTERP>
-__device__ __attribute__((noinline)) void field_tile_l2(const float* Wg, const ExpertMeta& em, int log2T, float px,
-                                                        float py, float pz, const float (&shv)[8], float* cbg, int lane,
-                                                        float& r, float& g, float& b, float& sg) {
-    fold_sh_bias(Wg, shv, lane, cbg);
-    field_tile<INTERP, true>(Wg, em, log2T, px, py, pz, shv, cbg, lane, r, g, b, sg);
-}
-
 template <int INTERP, int ROUTE>
 __global__ void __launch_bounds__(1024, 4) render_rws_kernel(FieldCfg cfg, BgArgs bg, RenderParams p) {
     static_assert(ACN_SHFOLD != 0, "render_rws_kernel folds the SH colour bias");
-    __shared__ __attribute__((aligned(16))) float smem[PK_FLOATS];        // the slot expert's packed image
-    __shared__ __attribute__((aligned(16))) float cbuf[16 * 64];          // round ray r: slot expert's folded bias
-    __shared__ __attribute__((aligned(16))) float cbgb[16 * 64];          // wave w: an L2 expert's folded bias
-    __shared__ __attribute__((aligned(16))) f32x4 ybuf[16 * kWsMaxS];
+    __shared__ __attribute__((aligned(16))) float smem[PK_FLOATS];        // the staged expert's packed image
+    __shared__ __attribute__((aligned(16))) float cbuf[16 * 64];          // round ray r: its folded bias
+    __shared__ __attribute__((aligned(16))) f32x4 ybuf[16 * kWsMaxS];     // per sample: sum_k y_k w_k so far
     __shared__ uint32_t tmask[16][kRwsMaxT];   // per round ray and tile: expert bits | kTileSingle
     __shared__ uint32_t rmask[16];             // per round ray: union of its tiles' experts
-    __shared__ int qhead, done[16], slot_k;
+    __shared__ int qhead, left[16], slot_k;
     const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    float* cbg = cbgb + wave * 64;
     const int S = p.S;
     const int T = (S + 31) >> 5;
     const float step = 1.0f / (float)(S - 1);
@@ -1571,7 +1559,8 @@ __global__ void __launch_bounds__(1024, 4) render_rws_kernel(FieldCfg cfg, BgArg
     }
     for (; base < hi; base += stride) {   // block-uniform
         const int nr = (int)min((int64_t)16, hi - base);
-        // ---- A: wave w routes round ray w, tile by tile (sample sc = min(s, S - 1), as the field evaluates it)
+        // ---- A: wave w routes round ray w (sample sc = min(s, S - 1), as the field tile evaluates it) and zeroes
+        //      its accumulators
         if (wave < nr) {
             const int64_t r0 = p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[base + wave]) : base + wave;
             const float* rp = p.rays + r0 * 8;
@@ -1579,6 +1568,7 @@ __global__ void __launch_bounds__(1024, 4) render_rws_kernel(FieldCfg cfg, BgArg
             const float near = rp[6], far = rp[7];
             const float* jit = p.jitter ? p.jitter + r0 * S : nullptr;
             uint32_t un = 0u;
+            int evals = 0;
             for (int t = 0; t < T; ++t) {
                 const int s = t * 32 + j;
                 const int sc = s < S ? s : S - 1;
@@ -1599,113 +1589,99 @@ __global__ void __launch_bounds__(1024, 4) render_rws_kernel(FieldCfg cfg, BgArg
                 uint32_t tm = 0u;
                 for (int k = 0; k < cfg.K; ++k)
                     if (__ballot((m >> k) & 1u) != 0ull) tm |= 1u << k;
+                un |= tm;
+                evals += __popc(tm);
                 if (__popc(tm) == 1 && __ballot(!exact) == 0ull) tm |= kTileSingle;
-                un |= tm & ~kTileSingle;
                 if (lane == 0) tmask[wave][t] = tm;
             }
-            if (lane == 0) rmask[wave] = un;
-        }
-        if (threadIdx.x == 0) qhead = 0;
-        if (threadIdx.x < 16) done[threadIdx.x] = 0;
-        __syncthreads();
-        // ---- B: the slot expert = the one most of the round's rays need (kept when tied with the resident one)
-        int want = -1;
-        {
-            int best = 0;
-            for (int k = 0; k < cfg.K; ++k) {
-                int c = 0;
-                for (int r = 0; r < nr; ++r) c += (rmask[r] >> k) & 1u;
-                if (c > best || (c == best && c > 0 && k == slot_k)) { best = c; want = k; }
+            if (lane == 0) {
+                rmask[wave] = un;
+                left[wave] = evals;
             }
+            for (int s = lane; s < S; s += 64) ybuf[wave * kWsMaxS + s] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
         }
-        want = __builtin_amdgcn_readfirstlane(want);
-        if (want >= 0 && want != __builtin_amdgcn_readfirstlane(slot_k)) {
-            __syncthreads();   // every wave has read slot_k
-            const f32x4* src = reinterpret_cast<const f32x4*>(p.packed + (size_t)want * PK_FLOATS);
-            f32x4* dst = reinterpret_cast<f32x4*>(smem);
-            for (int i = threadIdx.x; i < PK_FLOATS / 4; i += blockDim.x) dst[i] = src[i];
-            if (threadIdx.x == 0) slot_k = want;
+        __syncthreads();
+        uint32_t need_k = 0u;
+        for (int r = 0; r < nr; ++r) need_k |= rmask[r];
+        need_k = __builtin_amdgcn_readfirstlane(need_k);
+        // ---- B: expert by expert, ascending k
+        for (uint32_t rest = need_k; rest; rest &= rest - 1u) {   // block-uniform
+            const int k = __builtin_ctz(rest);
+            if (k != __builtin_amdgcn_readfirstlane(slot_k)) {
+                __syncthreads();   // every wave is done with the previous image
+                const f32x4* src = reinterpret_cast<const f32x4*>(p.packed + (size_t)k * PK_FLOATS);
+                f32x4* dst = reinterpret_cast<f32x4*>(smem);
+                for (int i = threadIdx.x; i < PK_FLOATS / 4; i += blockDim.x) dst[i] = src[i];
+                __syncthreads();
+                if (threadIdx.x == 0) slot_k = k;
+            }
+            if (wave < nr && ((rmask[wave] >> k) & 1u)) {   // wave w folds expert k's SH colour bias for ray w
+                const int64_t r0 = p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[base + wave]) : base + wave;
+                const float* rp = p.rays + r0 * 8;
+                float sh[16], sv[8];
+                dir_sh(rp[3], rp[4], rp[5], sh);
+                sh_rows_for_half(sh, h, sv);
+                fold_sh_bias(smem, sv, lane, cbuf + wave * 64);
+            }
+            if (threadIdx.x == 0) qhead = 0;
             __syncthreads();
-        }
-        const int ks = __builtin_amdgcn_readfirstlane(slot_k);
-        // ---- B2: wave w folds the slot expert's SH colour bias for its ray (used by every tile of the ray)
-        if (wave < nr && ks >= 0 && ((rmask[wave] >> ks) & 1u)) {
-            const int64_t r0 = p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[base + wave]) : base + wave;
-            const float* rp = p.rays + r0 * 8;
-            float sh[16], sv[8];
-            dir_sh(rp[3], rp[4], rp[5], sh);
-            sh_rows_for_half(sh, h, sv);
-            fold_sh_bias(smem, sv, lane, cbuf + wave * 64);
-        }
-        __syncthreads();
-        // ---- C: tiles, tile-major
-        int64_t cur = -1;
-        float shv[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-        float ox = 0.0f, oy = 0.0f, oz = 0.0f, dx = 0.0f, dy = 0.0f, dz = 0.0f, near = 0.0f, far = 0.0f;
-        const float* jit = nullptr;
-        for (;;) {
-            int item = 0;
-            if (lane == 0) item = __hip_atomic_fetch_add(&qhead, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            item = __builtin_amdgcn_readlane(item, 0);
-            if (item >= nr * T) break;
-            const int tile = item / nr, slot = item - tile * nr;
-            const int64_t ray = p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[base + slot]) : base + slot;
-            if (ray != cur) {
-                const float* rp = p.rays + ray * 8;
-                ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
-                near = rp[6], far = rp[7];
-                jit = p.jitter ? p.jitter + ray * S : nullptr;
-                float sh[16];
-                dir_sh(dx, dy, dz, sh);
-                sh_rows_for_half(sh, h, shv);
-                cur = ray;
-            }
-            const int s = tile * 32 + j;
-            const int sc = s < S ? s : S - 1;
-            const float t = jit ? tval(near, far, sc, S, jit) : tlin_sel(near, far, sc, S, step);
-            const float px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;
-            const uint32_t tm = __builtin_amdgcn_readfirstlane(tmask[slot][tile]);
-            // the container over the tile's experts in ascending k from zero (meta_container.py:320-337); a single-
-            // expert tile has weight exactly 1.0f on every sample, so 0 + y_k * 1.0f == y_k needs no routing
-            const bool single = (tm & kTileSingle) != 0u;
-            RouteState st{0.0f, 1.0f, 0};
-            if (!single) st = route_prep<ROUTE>(cfg, px, py, pz);
-            float yr = 0.0f, yg = 0.0f, yb = 0.0f, ys = 0.0f;
-            for (uint32_t rest = tm & ~kTileSingle; rest; rest &= rest - 1u) {
-                const int k = __builtin_ctz(rest);
-                float r, g, b, sg;
-                if (ACN_DIAG_RWS_NOGLOBAL || k == ks)   // the slot expert: LDS image, the ray's folded bias
-                    field_tile<INTERP, true>(smem, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbuf + slot * 64, lane, r, g,
-                                             b, sg);
-                else           // another expert: its packed image in L2, folded per tile (out of line)
-                    field_tile_l2<INTERP>(p.packed + (size_t)k * PK_FLOATS, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbg,
-                                          lane, r, g, b, sg);
-                sg = trunc_exp(sg);
-                const float wk = single ? 1.0f : ((ROUTE == 1) ? route_weight(cfg, st, k, px, py, pz) : 0.0f);
-                const bool need = single || ((ROUTE == 1) ? (wk > 0.0f) : (st.hard == k));
-                if (need) {
-                    if (ROUTE == 1 || single) {
-                        yr = yr + r * wk;
-                        yg = yg + g * wk;
-                        yb = yb + b * wk;
-                        ys = ys + sg * wk;
-                    } else {
-                        yr = r; yg = g; yb = b; ys = sg;
-                    }
+            int64_t cur = -1;
+            float shv[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};   // not read by a folded tile
+            float ox = 0.0f, oy = 0.0f, oz = 0.0f, dx = 0.0f, dy = 0.0f, dz = 0.0f, near = 0.0f, far = 0.0f;
+            const float* jit = nullptr;
+            for (;;) {
+                int item = 0;
+                if (lane == 0) item = __hip_atomic_fetch_add(&qhead, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                item = __builtin_amdgcn_readlane(item, 0);
+                if (item >= nr * T) break;
+                const int tile = item / nr, slot = item - tile * nr;
+                const uint32_t tm = __builtin_amdgcn_readfirstlane(tmask[slot][tile]);
+                if (!((tm >> k) & 1u)) continue;   // no sample of this tile needs expert k
+                const int64_t ray = p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[base + slot]) : base + slot;
+                if (ray != cur) {
+                    const float* rp = p.rays + ray * 8;
+                    ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
+                    near = rp[6], far = rp[7];
+                    jit = p.jitter ? p.jitter + ray * S : nullptr;
+                    cur = ray;
                 }
+                const int s = tile * 32 + j;
+                const int sc = s < S ? s : S - 1;
+                const float t = jit ? tval(near, far, sc, S, jit) : tlin_sel(near, far, sc, S, step);
+                const float px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;
+                float r, g, b, sg;
+                field_tile<INTERP, true>(smem, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbuf + slot * 64, lane, r, g, b,
+                                         sg);
+                sg = trunc_exp(sg);
+                // the sample's weight for expert k: exactly 1.0f on a single-expert tile, else the routing
+                float wk = 1.0f;
+                bool need = true;
+                if (!(tm & kTileSingle)) {
+                    const RouteState st = route_prep<ROUTE>(cfg, px, py, pz);
+                    wk = (ROUTE == 1) ? route_weight(cfg, st, k, px, py, pz) : 1.0f;
+                    need = (ROUTE == 1) ? (wk > 0.0f) : (st.hard == k);
+                }
+                if (need && h == 0 && s < S) {
+                    f32x4* a = ybuf + slot * kWsMaxS + s;
+                    f32x4 v = *a;
+                    if (ROUTE == 1 || (tm & kTileSingle)) {   // y = 0 + sum_k y_k w_k, ascending k
+                        v[0] = v[0] + r * wk;
+                        v[1] = v[1] + g * wk;
+                        v[2] = v[2] + b * wk;
+                        v[3] = v[3] + sg * wk;
+                    } else {                                  // hard: index_copy_ of the argmin expert's y
+                        v[0] = r; v[1] = g; v[2] = b; v[3] = sg;
+                    }
+                    *a = v;
+                }
+                // the wave's LDS writes are ordered before its count (workgroup-scope release / acquire)
+                int old = 0;
+                if (lane == 0) old = __hip_atomic_fetch_add(&left[slot], -1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+                old = __builtin_amdgcn_readlane(old, 0);
+                if (old == 1) composite_ray_lds(p, bg, ray, ybuf + slot * kWsMaxS, lane, step);
             }
-            if (h == 0 && s < S) {
-                f32x4 v;
-                v[0] = yr, v[1] = yg, v[2] = yb, v[3] = ys;
-                ybuf[slot * kWsMaxS + s] = v;
-            }
-            int old = 0;
-            if (lane == 0) old = __hip_atomic_fetch_add(&done[slot], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-            old = __builtin_amdgcn_readlane(old, 0);
-            if (old != T - 1) continue;
-            composite_ray_lds(p, bg, ray, ybuf + slot * kWsMaxS, lane, step);
+            __syncthreads();   // qhead / cbuf / smem reused by the next expert
         }
-        __syncthreads();   // ybuf / tmask / rmask / cbuf / qhead / done reused by the next round
     }
 }
 
