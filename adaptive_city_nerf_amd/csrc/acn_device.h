@@ -485,17 +485,10 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 #else
 #define ACN_OPND_PAD ""
 #endif
-#ifndef ACN_OPND_MEM
-#define ACN_OPND_MEM 0
-#endif
 #ifndef ACN_OPND_SB
 #define ACN_OPND_SB 1   // scheduling barriers around the fence (0: measured run-to-run differences in field_kernel)
 #endif
-#if ACN_OPND_MEM
-#define ACN_OPND_CLOB : "memory"
-#else
 #define ACN_OPND_CLOB
-#endif
 #if ACN_OPND_SB
 #define ACN_OPND_SB0 __builtin_amdgcn_sched_barrier(0);
 #else

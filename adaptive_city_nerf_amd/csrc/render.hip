@@ -255,24 +255,14 @@ __device__ __forceinline__ void split_acc2(const f32x16& a0, const f32x16& a1, f
 // sank the last conversions past it into the k-step loop, 2 wait states before their MFMA.
 // REV: k-steps in reverse order (colour layer 0 with per-lane SH: the SH k-step first, the order the per-ray
 // fold accumulates in, so the result is bit-identical to fold_sh_bias + the folded layer)
-#ifndef ACN_X3_FENCE
-#define ACN_X3_FENCE 1
-#endif
 template <int NT, int NK, bool REV = false>
 __device__ __forceinline__ void layer_x3(const float* W, int seg, const float* bias_base, int bt, int lane, int h,
                                          f16x8 (&bh)[NK], f16x8 (&bl)[NK], f32x16 (&out)[NT],
                                          int nk_used = NK) {
-#if ACN_X3_FENCE
     if (nk_used == 1) opnd_fence(bh[REV ? NK - 1 : 0], bl[REV ? NK - 1 : 0]);
     else opnd_fence_n<NK>(bh, bl);
-#endif
 #pragma unroll
     for (int T = 0; T < NT; ++T) out[T] = bias_frag_at(bias_base, bt + T, h);
-#if !ACN_X3_FENCE   // the round-4 positional pad
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-#endif
 #pragma unroll
     for (int si = 0; si < NK; ++si) {
         if (si >= nk_used) break;
@@ -1507,184 +1497,6 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
     }
 }
 
-// ------------------------------------------------------------------------------------------
-// Routed render with the workgroup's field tiles shared (render_rws_kernel, C3 / C4: K > 2 experts, no early
-// termination).  render_ws_kernel's work sharing for the routed container, expert by expert:
-//   A  wave w routes round ray w tile by tile (32 samples, the MFMA unit): per tile the experts its samples need,
-//      and whether every sample goes to ONE expert with weight exactly 1.0f (then 0 + y_k * 1.0f == y_k and the
-//      tile needs no per-sample routing later);
-//   B  for each expert k the round needs, in ascending k (the container's blend order, meta_container.py:320-337):
-//      stage k's packed image into the workgroup's LDS slot (only when it changes: rays arrive sorted by owning
-//      expert, parallel.expert_sorted_plan), fold its SH colour bias per ray, then the waves take the round's tiles
-//      that need k from an LDS counter (tile-major) and add y_k * w_k per sample into the LDS accumulator of the
-//      sample (hard routing: the argmin expert's y_k);
-//   C  the wave that completes a ray's last (tile, expert) evaluation composites it from LDS with render_ray's
-//      exact sequence (composite_ray_lds).
-// Per (sample, expert) the arithmetic is render_slots_kernel's (fold + folded field tile, trunc_exp, blend in
-// ascending k from zero), so the outputs are bit-identical to it (tests/test_render_ws.py, test_k8.py,
-// test_batch_independence.py).  No expert is ever read from L2 inside a field tile: one field_tile
-// instantiation, 1024 threads at <= 128 VGPRs (16 waves per CU; the slots kernel runs 8 at 256 VGPRs).
-#ifndef ACN_ROUTED_WS
-#define ACN_ROUTED_WS 0   // measured slower than render_slots_kernel; bit-identical
-#endif
-constexpr int kRwsMaxT = kWsMaxS / 32;   // tiles per ray
-constexpr uint32_t kTileSingle = 1u << 31;
-
-template <int INTERP, int ROUTE>
-__global__ void __launch_bounds__(1024, 4) render_rws_kernel(FieldCfg cfg, BgArgs bg, RenderParams p) {
-    static_assert(ACN_SHFOLD != 0, "render_rws_kernel folds the SH colour bias");
-    __shared__ __attribute__((aligned(16))) float smem[PK_FLOATS];        // the staged expert's packed image
-    __shared__ __attribute__((aligned(16))) float cbuf[16 * 64];          // round ray r: its folded bias
-    __shared__ __attribute__((aligned(16))) f32x4 ybuf[16 * kWsMaxS];     // per sample: sum_k y_k w_k so far
-    __shared__ uint32_t tmask[16][kRwsMaxT];   // per round ray and tile: expert bits | kTileSingle
-    __shared__ uint32_t rmask[16];             // per round ray: union of its tiles' experts
-    __shared__ int qhead, left[16], slot_k;
-    const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int S = p.S;
-    const int T = (S + 31) >> 5;
-    const float step = 1.0f / (float)(S - 1);
-    if (threadIdx.x == 0) slot_k = -1;
-    int64_t base, hi, stride;
-    if ((gridDim.x & 7) == 0) {   // XCD bands (render_kernel)
-        const int64_t chunk = (p.N + 7) >> 3;
-        const int64_t lo = min(p.N, (int64_t)(blockIdx.x & 7) * chunk);
-        hi = min(p.N, lo + chunk);
-        base = lo + (int64_t)(blockIdx.x >> 3) * 16;
-        stride = (int64_t)(gridDim.x >> 3) * 16;
-    } else {
-        hi = p.N;
-        base = (int64_t)blockIdx.x * 16;
-        stride = (int64_t)gridDim.x * 16;
-    }
-    for (; base < hi; base += stride) {   // block-uniform
-        const int nr = (int)min((int64_t)16, hi - base);
-        // ---- A: wave w routes round ray w (sample sc = min(s, S - 1), as the field tile evaluates it) and zeroes
-        //      its accumulators
-        if (wave < nr) {
-            const int64_t r0 = p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[base + wave]) : base + wave;
-            const float* rp = p.rays + r0 * 8;
-            const float ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
-            const float near = rp[6], far = rp[7];
-            const float* jit = p.jitter ? p.jitter + r0 * S : nullptr;
-            uint32_t un = 0u;
-            int evals = 0;
-            for (int t = 0; t < T; ++t) {
-                const int s = t * 32 + j;
-                const int sc = s < S ? s : S - 1;
-                const float tv = jit ? tval(near, far, sc, S, jit) : tlin_sel(near, far, sc, S, step);
-                const float px = ox + dx * tv, py = oy + dy * tv, pz = oz + dz * tv;
-                uint32_t m = 0u;
-                bool exact = true;
-                if (ROUTE == 1) {
-                    const RouteState st = route_prep<1>(cfg, px, py, pz);
-                    for (int k = 0; k < cfg.K; ++k) {
-                        const float w = route_weight(cfg, st, k, px, py, pz);
-                        if (w > 0.0f) m |= 1u << k;
-                        exact = exact && (w == 0.0f || w == 1.0f);
-                    }
-                } else {
-                    m = 1u << route_prep<2>(cfg, px, py, pz).hard;
-                }
-                uint32_t tm = 0u;
-                for (int k = 0; k < cfg.K; ++k)
-                    if (__ballot((m >> k) & 1u) != 0ull) tm |= 1u << k;
-                un |= tm;
-                evals += __popc(tm);
-                if (__popc(tm) == 1 && __ballot(!exact) == 0ull) tm |= kTileSingle;
-                if (lane == 0) tmask[wave][t] = tm;
-            }
-            if (lane == 0) {
-                rmask[wave] = un;
-                left[wave] = evals;
-            }
-            for (int s = lane; s < S; s += 64) ybuf[wave * kWsMaxS + s] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        }
-        __syncthreads();
-        uint32_t need_k = 0u;
-        for (int r = 0; r < nr; ++r) need_k |= rmask[r];
-        need_k = __builtin_amdgcn_readfirstlane(need_k);
-        // ---- B: expert by expert, ascending k
-        for (uint32_t rest = need_k; rest; rest &= rest - 1u) {   // block-uniform
-            const int k = __builtin_ctz(rest);
-            if (k != __builtin_amdgcn_readfirstlane(slot_k)) {
-                __syncthreads();   // every wave is done with the previous image
-                const f32x4* src = reinterpret_cast<const f32x4*>(p.packed + (size_t)k * PK_FLOATS);
-                f32x4* dst = reinterpret_cast<f32x4*>(smem);
-                for (int i = threadIdx.x; i < PK_FLOATS / 4; i += blockDim.x) dst[i] = src[i];
-                __syncthreads();
-                if (threadIdx.x == 0) slot_k = k;
-            }
-            if (wave < nr && ((rmask[wave] >> k) & 1u)) {   // wave w folds expert k's SH colour bias for ray w
-                const int64_t r0 = p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[base + wave]) : base + wave;
-                const float* rp = p.rays + r0 * 8;
-                float sh[16], sv[8];
-                dir_sh(rp[3], rp[4], rp[5], sh);
-                sh_rows_for_half(sh, h, sv);
-                fold_sh_bias(smem, sv, lane, cbuf + wave * 64);
-            }
-            if (threadIdx.x == 0) qhead = 0;
-            __syncthreads();
-            int64_t cur = -1;
-            float shv[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};   // not read by a folded tile
-            float ox = 0.0f, oy = 0.0f, oz = 0.0f, dx = 0.0f, dy = 0.0f, dz = 0.0f, near = 0.0f, far = 0.0f;
-            const float* jit = nullptr;
-            for (;;) {
-                int item = 0;
-                if (lane == 0) item = __hip_atomic_fetch_add(&qhead, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                item = __builtin_amdgcn_readlane(item, 0);
-                if (item >= nr * T) break;
-                const int tile = item / nr, slot = item - tile * nr;
-                const uint32_t tm = __builtin_amdgcn_readfirstlane(tmask[slot][tile]);
-                if (!((tm >> k) & 1u)) continue;   // no sample of this tile needs expert k
-                const int64_t ray = p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[base + slot]) : base + slot;
-                if (ray != cur) {
-                    const float* rp = p.rays + ray * 8;
-                    ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
-                    near = rp[6], far = rp[7];
-                    jit = p.jitter ? p.jitter + ray * S : nullptr;
-                    cur = ray;
-                }
-                const int s = tile * 32 + j;
-                const int sc = s < S ? s : S - 1;
-                const float t = jit ? tval(near, far, sc, S, jit) : tlin_sel(near, far, sc, S, step);
-                const float px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;
-                float r, g, b, sg;
-                field_tile<INTERP, true>(smem, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbuf + slot * 64, lane, r, g, b,
-                                         sg);
-                sg = trunc_exp(sg);
-                // the sample's weight for expert k: exactly 1.0f on a single-expert tile, else the routing
-                float wk = 1.0f;
-                bool need = true;
-                if (!(tm & kTileSingle)) {
-                    const RouteState st = route_prep<ROUTE>(cfg, px, py, pz);
-                    wk = (ROUTE == 1) ? route_weight(cfg, st, k, px, py, pz) : 1.0f;
-                    need = (ROUTE == 1) ? (wk > 0.0f) : (st.hard == k);
-                }
-                if (need && h == 0 && s < S) {
-                    f32x4* a = ybuf + slot * kWsMaxS + s;
-                    f32x4 v = *a;
-                    if (ROUTE == 1 || (tm & kTileSingle)) {   // y = 0 + sum_k y_k w_k, ascending k
-                        v[0] = v[0] + r * wk;
-                        v[1] = v[1] + g * wk;
-                        v[2] = v[2] + b * wk;
-                        v[3] = v[3] + sg * wk;
-                    } else {                                  // hard: index_copy_ of the argmin expert's y
-                        v[0] = r; v[1] = g; v[2] = b; v[3] = sg;
-                    }
-                    *a = v;
-                }
-                // the wave's LDS writes are ordered before its count (workgroup-scope release / acquire)
-                int old = 0;
-                if (lane == 0) old = __hip_atomic_fetch_add(&left[slot], -1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-                old = __builtin_amdgcn_readlane(old, 0);
-                if (old == 1) composite_ray_lds(p, bg, ray, ybuf + slot * kWsMaxS, lane, step);
-            }
-            __syncthreads();   // qhead / cbuf / smem reused by the next expert
-        }
-    }
-}
-
 // inclusive scan over the 64 lanes of a wave on DPP: row_shr 1/2/4/8 inside each 16-lane row, then
 // row_bcast:15 / :31 carry the row totals upward (gfx9-family DPP)
 __device__ __forceinline__ int wave_incl_scan(int v) {
@@ -2536,18 +2348,6 @@ extern "C" int acn_render_stratified_fwd_ordered(const float* rays, int64_t N, i
         if (ACN_SLOTS && KL == 0 && R != 0) hipLaunchKernelGGL((render_slots_kernel<I, (R == 0 ? 1 : R)>), grid, dim3(ACN_SLOTS_THREADS), 0, s, cfg, b, p); \
         else hipLaunchKernelGGL((render_kernel<I, KL, R>), grid, block, 0, s, cfg, b, p);            \
     } while (0)
-    if (ACN_ROUTED_WS && slots && S <= kWsMaxS && !(tau > 0.0f)) {
-        // routed container, no early termination: tiles routed one by one and shared by the workgroup
-        // (bit-identical to render_slots_kernel)
-#define ACN_RWS_LAUNCH(I, R) hipLaunchKernelGGL((render_rws_kernel<I, R>), grid, block, 0, s, cfg, b, p)
-        if (cfg.routing == 1) {
-            if (interp == 1) ACN_RWS_LAUNCH(1, 1); else if (interp == 0) ACN_RWS_LAUNCH(0, 1); else ACN_RWS_LAUNCH(2, 1);
-        } else {
-            if (interp == 1) ACN_RWS_LAUNCH(1, 2); else if (interp == 0) ACN_RWS_LAUNCH(0, 2); else ACN_RWS_LAUNCH(2, 2);
-        }
-#undef ACN_RWS_LAUNCH
-        return acn_check_launch("acn_render_stratified_fwd");
-    }
     if (ACN_RENDER_WS && cfg.routing == 0 && S <= kWsMaxS && !(tau > 0.0f)) {
         // one expert, no early termination: the workgroup shares its rays' field tiles (bit-identical outputs)
         if (interp == 1) hipLaunchKernelGGL(render_ws_kernel<1>, grid, block, 0, s, cfg, b, p);

@@ -30,14 +30,10 @@ def test_library_loads_and_exports_every_declared_symbol():
     assert L.acn_version() == 1
     assert set(_lib.exported_symbols()) == set(declared_symbols())
     assert L.acn_workspace_bytes(1) > 50_000 and L.acn_workspace_bytes(4) == 4 * L.acn_workspace_bytes(1)
-    # the scratch of acn_render_stratified_fwd_ordered: the ray order (n <= 8192 rays, 4 B each), and, when the
-    # split routed render is compiled in (ACN_SPLIT_ROUTED, off by default), its ray lists (code[n],
-    # list[n + 16 kMaxK], multi[n], hdr[kMaxK + 2] int32)
+    # the scratch of acn_render_stratified_fwd_ordered: the ray order (n <= 8192 rays, 4 B each)
     order = lambda n: 4 * n if n <= 8192 else 0  # noqa: E731
-    split = lambda n: max(order(n), 4 * (3 * n + 16 * 16 + 16 + 2))  # noqa: E731
-    want = split if L.acn_render_order_bytes(512) >= 3 * 512 * 4 else order
-    assert [L.acn_render_order_bytes(n) for n in (0, 1, 4096, 8192, 8193)] == [0] + [want(n) for n in (1, 4096, 8192,
-                                                                                                       8193)]
+    assert [L.acn_render_order_bytes(n) for n in (0, 1, 4096, 8192, 8193)] == [0] + [order(n) for n in (1, 4096, 8192,
+                                                                                                         8193)]
 
 
 def test_argument_errors_are_reported_without_a_gpu():

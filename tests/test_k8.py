@@ -210,35 +210,3 @@ def test_c4_full_frame_vs_oracle(S):
                                                  bg_mlp=G.bg_weights(d, "hiw:"), want_weights=False)
     assert np.abs(img[idx] - np.clip(orgb, 0, 1)).max() <= 1e-4
     assert np.abs(acc[idx] - oacc).max() <= 1e-4
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("variant", ["render", "render_hi", "render_default"])
-@pytest.mark.parametrize("jitter", [False, True])
-def test_split_routed_render_bit_identical(variant, jitter):
-    """The split routed render (single-expert rays through render_single_kernel, the rest through
-    render_slots_kernel with a device-side ray list) equals the unsplit render_slots_kernel bit for bit:
-    every ray is still rendered by one wave with the same field tile and compositing code.  Also with a
-    shuffled batch (rays of several experts interleaved), a ragged batch and training jitter."""
-    from adaptive_city_nerf_amd import _lib, ops, render_rays
-    if int(_lib.lib().acn_render_order_bytes(512)) < 3 * 512 * 4:
-        pytest.skip("split routed render compiled out (ACN_SPLIT_ROUTED=0, the default: DESIGN.md 4)")
-    d = G.load("render_k8")
-    m, _ = _model(d, "hiw:" if variant == "render_hi" else "w:", _scale(variant))
-    if jitter:
-        m.train()   # eval ignores jitter_u; under no_grad the fused render takes it as the training jitter
-    rays = torch.from_numpy(d["render:rays"]).cuda()
-    g = torch.Generator(device="cuda").manual_seed(5)
-    perm = torch.randperm(rays.shape[0], device="cuda", generator=g)
-    for r in (rays, rays[perm].contiguous(), rays[perm[:777]].contiguous()):
-        u = torch.rand(r.shape[0], 64, device="cuda", generator=g) if jitter else None
-        outs = []
-        for split in (True, False):
-            ops.REORDER = split      # the split needs the scratch; without it the slots kernel renders all rays
-            try:
-                with torch.no_grad():
-                    outs.append(render_rays(m, r, ray_samples=64, bg_color_default="white", jitter_u=u))
-            finally:
-                ops.REORDER = True
-        for x, y in zip(*outs):
-            assert torch.equal(x, y)
