@@ -108,6 +108,9 @@ SIGNATURES = {
     "acn_background_fwd": ([vp, i64, vp, vp, vp], C.c_int),
     "acn_background_bwd_workspace_bytes": ([], C.c_size_t),
     "acn_background_bwd": ([vp, i64, vp, vp, vp, vp, vp, vp, vp, C.c_size_t, vp], C.c_int),
+    "acn_composite_mse_train_workspace_bytes": ([], C.c_size_t),
+    "acn_routed_composite_mse_train": ([vp, i64, i32, vp, vp, vp, vp, i32, vp, i64, vp, vp, vp, vp, vp, vp, vp, vp,
+                                        vp, vp, C.c_size_t, vp], C.c_int),
     "acn_volume_render_bwd": ([vp, vp, vp, i64, i32, f32, vp, vp, vp, vp, vp, vp, vp], C.c_int),
     "acn_grad_sumsq": ([vp, vp, i64, vp, vp, vp], C.c_int),
     "acn_mse_linear_fwd": ([vp, vp, i64, vp, vp], C.c_int),
@@ -174,6 +177,7 @@ SIGNATURES = {
     "acn_mlp_train_bwd_dw_pairs": ([vp, vp, vp, vp, vp, i32, vp, vp, vp, vp], C.c_int),
     "acn_grad_sumsq_slots": ([vp, vp, i64, vp, vp, i32, vp, vp, vp], C.c_int),
     "acn_grad_sumsq_slots_ex": ([vp, vp, i64, vp, vp, i32, vp, vp, vp, vp], C.c_int),
+    "acn_grad_clip_slots": ([vp, vp, i64, vp, vp, i32, vp, vp, vp, C.c_float, vp, vp, vp], C.c_int),
     "acn_adam_step_slots": ([vp, vp, i64, vp, vp, i32, i32, vp, i32, vp, i32, vp, vp], C.c_int),
     "acn_adam_step_slots_segmap": ([vp, vp, i64, vp, vp, i32, i32, vp, i32, vp, i32, vp, vp, vp], C.c_int),
     "acn_adam_step_slots_segmap_phase": ([vp, vp, i64, vp, vp, i32, i32, vp, i32, vp, i32, vp, vp, i32, vp], C.c_int),

@@ -35,6 +35,23 @@ __device__ __forceinline__ float clamp_nan(float v, float lo, float hi) {
     return v > hi ? hi : v;
 }
 
+// lane l's double (l wave-uniform: two scalar readlanes)
+__device__ __forceinline__ double lane_f64(double v, int l) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
+// compute_mse_loss in color_space "linear" (nerfs/losses.py:10-32, color_space.py:13-19, 22-66): pred.clamp(0,1)
+// against gt.clamp(0,1) -> srgb_to_linear -> clamp(0,1); float scalars and powf as the torch ops (loss.hip and
+// the fused training compositing in render.hip)
+__device__ __forceinline__ float clamp01(float x) { return x < 0.0f ? 0.0f : (x > 1.0f ? 1.0f : x); }
+__device__ __forceinline__ float srgb_to_linear(float x) {
+    return x <= 0.04045f ? x / 12.92f : powf((x + 0.055f) / 1.055f, 2.4f);
+}
+__device__ __forceinline__ float gt_linear(float g) { return clamp01(srgb_to_linear(clamp01(g))); }
+
 // get_ray_directions (nerfs/ray_sampling.py:122-136) for pixel (i, j)
 __device__ __forceinline__ void pixel_dir(int i, int j, float fx, float fy, float cx, float cy, int center,
                                           float& dx, float& dy, float& dz) {

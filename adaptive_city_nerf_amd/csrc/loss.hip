@@ -7,20 +7,15 @@
 // sums, one fixed reduction order: deterministic) and one elementwise launch backward.
 // Float semantics follow the torch ops: scalars as float (12.92f, 0.055f, 1.055f, 0.04045f), powf with
 // the float exponent, clamps that pass NaN through, and mse_loss_backward's double `2 / numel` factor.
+#include "acn_device.h"
 #include "acn_internal.h"
 
 namespace {
 
+using acn::clamp01;
+using acn::gt_linear;   // gt (sRGB in [0,1] after the clamp) -> linear, clamped again
+
 constexpr int kThreads = 1024;
-
-__device__ __forceinline__ float clamp01(float x) { return x < 0.0f ? 0.0f : (x > 1.0f ? 1.0f : x); }
-
-__device__ __forceinline__ float srgb_to_linear(float x) {
-    return x <= 0.04045f ? x / 12.92f : powf((x + 0.055f) / 1.055f, 2.4f);
-}
-
-// gt (sRGB in [0,1] after the clamp) -> linear, clamped again
-__device__ __forceinline__ float gt_linear(float g) { return clamp01(srgb_to_linear(clamp01(g))); }
 
 __global__ void __launch_bounds__(kThreads) mse_linear_fwd_kernel(const float* __restrict__ pred,
                                                                   const float* __restrict__ gt, int64_t n,
@@ -47,7 +42,7 @@ __global__ void __launch_bounds__(kThreads) mse_linear_fwd_kernel(const float* _
 // Multi-workgroup form (acn_mse_linear_fwd_ws): G workgroups of 256 threads (G sized for ~2 elements per
 // thread, at most 256), thread i of workgroup b sums elements b*256 + i, + G*256, ... in double; the
 // workgroup sums in a fixed order into partials[b]; the last workgroup to finish (ticket counter) adds
-// partials[0..G) in order, writes the loss and resets the counter.  Deterministic (fixed assignment and
+// partials[0..G) in a fixed tree, writes the loss and resets the counter.  Deterministic (fixed assignment and
 // order for a given n).  The time of this launch is memory latency, not arithmetic: a thread's loads are
 // issued 4 at a time ahead of the sums (same per-thread order), and the grid is wide enough that a thread
 // has one or two such rounds (8 dependent rounds per thread measured 11 us at n = 12000,
@@ -92,22 +87,20 @@ __global__ void __launch_bounds__(kWsThreads) mse_linear_fwd_ws_kernel(const flo
         last = atomicAdd(counter, 1u) == gridDim.x - 1;
     }
     __syncthreads();
-    // last workgroup: wave 0's lanes load the G <= 256 partials at once (lane l: partials[l + 64 j]), then
-    // every lane adds them in index order through the cross-lane shuffle -- the same summation order as a
-    // serial loop over partials[0..G)
-    if (last && threadIdx.x < 64) {
+    // last workgroup: thread i loads partial i (G <= 256), then a fixed xor tree per wave and the waves in order
+    // (deterministic for a given n; a serial in-order sum through one wave measured ~10 us of this launch)
+    if (last) {
         __threadfence();
         const unsigned int G = gridDim.x;
-        double v[kWsMaxBlocks / 64];
+        double v = threadIdx.x < G ? __hip_atomic_load(&partials[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                   : 0.0;
 #pragma unroll
-        for (int j = 0; j < kWsMaxBlocks / 64; ++j) {
-            const unsigned int b = threadIdx.x + 64u * j;
-            v[j] = b < G ? __hip_atomic_load(&partials[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
-        }
+        for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+        __syncthreads();   // red[] is reused (thread 0 read it above)
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+        __syncthreads();
         double t = 0.0;
-#pragma unroll
-        for (int j = 0; j < kWsMaxBlocks / 64; ++j)
-            for (unsigned int b = 0; b < 64u && 64u * j + b < G; ++b) t += __shfl(v[j], (int)b);
+        for (int i = 0; i < kWsThreads / 64; ++i) t += red[i];
         if (threadIdx.x == 0) {
             loss[0] = (float)(t / (double)n);
             counter[0] = 0u;

@@ -286,11 +286,19 @@ __global__ void bump_slots_kernel(int32_t* __restrict__ step_dev, const int64_t*
     if (s < nslots && slot_active(seg, K, s)) step_dev[s] += 1;
 }
 
+// CLIP: the last workgroup to finish (ticket counter, reset for the next call) also runs reduce_kernel's sum
+// over the partials (same threads, same order: the same double) and clip_coef_kernel -- one launch instead of
+// three, bitwise the same total and coefficient
+template <bool CLIP>
 __global__ void __launch_bounds__(kThreads) sumsq_slots_kernel(const acn_param_desc* __restrict__ descs,
                                                                const int32_t* __restrict__ chunk_tensor,
                                                                const int32_t* __restrict__ flags,
                                                                const int64_t* __restrict__ seg, int K,
-                                                               double* __restrict__ partials) {
+                                                               double* __restrict__ partials,
+                                                               double* __restrict__ total = nullptr,
+                                                               double* __restrict__ extra = nullptr,
+                                                               float max_norm = 0.0f, float* __restrict__ out = nullptr,
+                                                               unsigned int* __restrict__ counter = nullptr) {
     const int t = chunk_tensor[blockIdx.x];
     const acn_param_desc d = descs[t];
     double acc = 0.0;
@@ -322,6 +330,34 @@ __global__ void __launch_bounds__(kThreads) sumsq_slots_kernel(const acn_param_d
     }
     const double tot = block_sum(acc);
     if (threadIdx.x == 0) partials[blockIdx.x] = tot;
+    if constexpr (CLIP) {
+        __shared__ bool last;
+        if (threadIdx.x == 0) {
+            __threadfence();
+            last = atomicAdd(counter, 1u) == gridDim.x - 1;
+        }
+        __syncthreads();
+        if (!last) return;
+        __threadfence();
+        double a2 = 0.0;
+        for (int64_t i = threadIdx.x; i < (int64_t)gridDim.x; i += kThreads)
+            a2 += __hip_atomic_load(&partials[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const double t = block_sum(a2);
+        if (threadIdx.x == 0) {
+            double tt = t;
+            if (extra) {
+                tt = t + extra[0];
+                extra[0] = 0.0;
+            }
+            total[0] = tt;
+            const float norm = (float)sqrt(tt);
+            float coef = max_norm / (norm + 1e-6f);
+            coef = coef > 1.0f ? 1.0f : coef;  // NaN passes through, like torch.clamp
+            out[0] = norm;
+            out[1] = coef;
+            counter[0] = 0u;
+        }
+    }
 }
 
 // adam_chunk + clearing the gradient vectors that were non-zero (most table rows get no gradient; A/B
@@ -803,10 +839,21 @@ extern "C" int acn_grad_sumsq_slots_ex(const acn_param_desc* descs, const int32_
     ACN_REQUIRE(nchunks >= 1 && nchunks <= 0x7fffffff && descs && chunk_tensor && flags && partials && total,
                 "acn_grad_sumsq_slots: bad arguments");
     hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(sumsq_slots_kernel, dim3((unsigned)nchunks), dim3(kThreads), 0, s, descs, chunk_tensor, flags, seg,
-                       K, partials);
+    hipLaunchKernelGGL(sumsq_slots_kernel<false>, dim3((unsigned)nchunks), dim3(kThreads), 0, s, descs, chunk_tensor,
+                       flags, seg, K, partials, nullptr, nullptr, 0.0f, nullptr, nullptr);
     hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(kThreads), 0, s, partials, nchunks, total, extra);
     return acn_check_launch("acn_grad_sumsq_slots");
+}
+
+extern "C" int acn_grad_clip_slots(const acn_param_desc* descs, const int32_t* chunk_tensor, int64_t nchunks,
+                                   const int32_t* flags, const int64_t* seg, int K, double* partials, double* total,
+                                   double* extra, float max_norm, float* out, unsigned int* counter, void* stream) {
+    ACN_REQUIRE(nchunks >= 1 && nchunks <= 0x7fffffff && descs && chunk_tensor && flags && partials && total && out &&
+                    counter,
+                "acn_grad_clip_slots: bad arguments");
+    hipLaunchKernelGGL(sumsq_slots_kernel<true>, dim3((unsigned)nchunks), dim3(kThreads), 0, (hipStream_t)stream, descs,
+                       chunk_tensor, flags, seg, K, partials, total, extra, max_norm, out, counter);
+    return acn_check_launch("acn_grad_clip_slots");
 }
 
 extern "C" int acn_adam_step_slots(const acn_param_desc* descs, const int32_t* chunk_tensor, int64_t nchunks,

@@ -762,12 +762,6 @@ __device__ __forceinline__ double dpp_f64(double v) {
     const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0x3ff00000, (int)(uint32_t)(b >> 32), CTRL, ROWMASK, 0xF, false);
     return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
-__device__ __forceinline__ double lane_f64(double v, int l) {
-    const uint64_t b = __builtin_bit_cast(uint64_t, v);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
-    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
-}
 
 // sum over the 32 lanes of half 0 (both halves hold the same per-sample partials): DPP inside each
 // 16-lane row, then rows 0 and 1 through readlanes (a wave-uniform result)
@@ -1635,7 +1629,33 @@ __global__ void __launch_bounds__(1024) ep_composite_kernel(BgArgs bg, RenderPar
     }
 }
 
-// standalone volume_render: one wave per ray, 32-sample tiles
+// volume_render of one ray (one wave, 32-sample tiles; both lane halves hold the same samples) over
+// fetch(sc) = the (N,S,4) rgb_sigma row of sample sc: rgb, depth, acc wave-uniform, weights row written
+__device__ __forceinline__ float4 ld_rs(const float* v) { return make_float4(v[0], v[1], v[2], v[3]); }
+template <class Fetch>
+__device__ __forceinline__ void vr_fwd_ray(Fetch fetch, const float* __restrict__ t, int S, int raw_rgb, int raw_sigma,
+                                           float sigma_scale, int j, int h, float* wrow, float& r, float& g, float& b,
+                                           float& dd, float& a) {
+    RayAcc acc{1.0, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    for (int s0 = 0; s0 < S; s0 += 32) {
+        const int s = s0 + j;
+        const bool valid = s < S;
+        const int sc = valid ? s : S - 1;
+        const float4 v = fetch(sc);
+        float cr = v.x, cg = v.y, cb = v.z, sg = v.w;
+        if (raw_rgb) { cr = sigmoidf_(cr); cg = sigmoidf_(cg); cb = sigmoidf_(cb); }
+        else { cr = clamp_nan(cr, 0.0f, 1.0f); cg = clamp_nan(cg, 0.0f, 1.0f); cb = clamp_nan(cb, 0.0f, 1.0f); }
+        sg = raw_sigma ? trunc_exp(sg) : clamp_min_nan(sg, 0.0f);
+        if (sigma_scale != 1.0f) sg = sg * sigma_scale;
+        const float dist = (sc < S - 1) ? (t[sc + 1] - t[sc]) : (t[sc] - t[sc - 1]);
+        float wv;
+        composite_tile(acc, valid, cr, cg, cb, sg, t[sc], dist, j, &wv);
+        if (wrow && valid && h == 0) wrow[s] = wv;
+    }
+    finish_ray(acc, r, g, b, dd, a);
+}
+
+// standalone volume_render: one wave per ray
 __global__ void __launch_bounds__(256) volume_render_kernel(const float* __restrict__ rs, const float* __restrict__ tv,
                                                             const float* __restrict__ bgp, int64_t N, int S,
                                                             int raw_rgb, int raw_sigma, float sigma_scale,
@@ -1643,25 +1663,9 @@ __global__ void __launch_bounds__(256) volume_render_kernel(const float* __restr
     const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
     const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
     for (int64_t ray = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); ray < N; ray += nw) {
-        RayAcc acc{1.0, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-        const float* t = tv + ray * S;
-        for (int s0 = 0; s0 < S; s0 += 32) {
-            const int s = s0 + j;
-            const bool valid = s < S;
-            const int sc = valid ? s : S - 1;
-            const float* v = rs + (ray * S + sc) * 4;
-            float cr = v[0], cg = v[1], cb = v[2], sg = v[3];
-            if (raw_rgb) { cr = sigmoidf_(cr); cg = sigmoidf_(cg); cb = sigmoidf_(cb); }
-            else { cr = clamp_nan(cr, 0.0f, 1.0f); cg = clamp_nan(cg, 0.0f, 1.0f); cb = clamp_nan(cb, 0.0f, 1.0f); }
-            sg = raw_sigma ? trunc_exp(sg) : clamp_min_nan(sg, 0.0f);
-            if (sigma_scale != 1.0f) sg = sg * sigma_scale;
-            const float dist = (sc < S - 1) ? (t[sc + 1] - t[sc]) : (t[sc] - t[sc - 1]);
-            float wv;
-            composite_tile(acc, valid, cr, cg, cb, sg, t[sc], dist, j, &wv);
-            if (weights && valid && h == 0) weights[ray * S + s] = wv;
-        }
         float r, g, b, dd, a;
-        finish_ray(acc, r, g, b, dd, a);
+        vr_fwd_ray([&](int sc) { return ld_rs(rs + (ray * S + sc) * 4); }, tv + ray * S, S, raw_rgb, raw_sigma,
+                   sigma_scale, j, h, weights ? weights + ray * S : nullptr, r, g, b, dd, a);
         if (lane == 0) {
             if (bgp) {
                 const float om = 1.0f - a;
@@ -1685,6 +1689,77 @@ __global__ void __launch_bounds__(256) volume_render_kernel(const float* __restr
 // is G - P_i.  Then alpha's clamp mask, d(1 - exp(-sigma delta))/dsigma = delta exp(-sigma delta),
 // sigma_scale and clamp_min(0)'s mask; rgb gets w_i G_rgb under clamp(0,1)'s mask; bg gets
 // (1 - acc) G_rgb.  t_vals get no gradient (stratified_t_vals runs under no_grad).
+// fetch(sc) as vr_fwd_ray; store(s, grad) receives sample s's dL/d(rgb_sigma) on the h == 0 lanes; returns
+// acc = sum w (double, wave-uniform) for the background gradient.
+template <class Fetch, class Store>
+__device__ __forceinline__ double vr_bwd_ray(Fetch fetch, Store store, const float* __restrict__ t, int S,
+                                             float sigma_scale, float gr, float gg, float gb, float gd, float ga,
+                                             float br, float bgg, float bb, const float* __restrict__ gwrow, int j,
+                                             int h) {
+    double G = 0.0, acc = 0.0;
+    for (int pass = 0; pass < 2; ++pass) {
+        double T = 1.0, P = 0.0;
+        for (int s0 = 0; s0 < S; s0 += 32) {
+            const int s = s0 + j;
+            const bool valid = s < S;
+            const int sc = valid ? s : S - 1;
+            const float4 v = fetch(sc);
+            const float cr = clamp_nan(v.x, 0.0f, 1.0f), cg = clamp_nan(v.y, 0.0f, 1.0f),
+                        cb = clamp_nan(v.z, 0.0f, 1.0f);
+            float sg = clamp_min_nan(v.w, 0.0f);
+            if (sigma_scale != 1.0f) sg = sg * sigma_scale;
+            float dist = (sc < S - 1) ? (t[sc + 1] - t[sc]) : (t[sc] - t[sc - 1]);
+            dist = clamp_min_nan(dist, 1e-4f);
+            const float e = expf(-sg * dist);
+            const float a = 1.0f - e;
+            const float alpha = clamp_nan(a, 0.0f, (float)(1.0 - 1e-7));
+            float x = (1.0f - alpha) + 1e-10f;
+            if (!valid) x = 1.0f;
+            double incl = (double)x;
+#pragma unroll
+            for (int off = 1; off < 32; off <<= 1) {
+                const double y = __shfl_up(incl, off, 32);
+                if (j >= off) incl *= y;
+            }
+            double excl = __shfl_up(incl, 1, 32);
+            if (j == 0) excl = 1.0;
+            const float Ts = (float)(T * excl);
+            const float w = valid ? alpha * Ts : 0.0f;
+            float g = gr * (cr - br) + gg * (cg - bgg) + gb * (cb - bb) + gd * t[sc] + ga;
+            if (gwrow && valid) g += gwrow[s];
+            const double gw = valid ? (double)g * (double)w : 0.0;
+            if (pass == 0) {
+                G += gw;
+                acc += (double)w;
+            } else {
+                double pre = gw;  // inclusive prefix of g_k w_k over the tile
+#pragma unroll
+                for (int off = 1; off < 32; off <<= 1) {
+                    const double y = __shfl_up(pre, off, 32);
+                    if (j >= off) pre += y;
+                }
+                const double suffix = G - (P + pre);
+                const float dalpha = (float)((double)g * (double)Ts - suffix / (double)x);
+                const bool amask = (a >= 0.0f) && (a <= (float)(1.0 - 1e-7));
+                float dsig = amask ? dalpha * dist * e : 0.0f;
+                if (sigma_scale != 1.0f) dsig = dsig * sigma_scale;
+                const float gsr = (v.w >= 0.0f) ? dsig : 0.0f;
+                if (valid && h == 0)
+                    store(s, make_float4((v.x >= 0.0f && v.x <= 1.0f) ? w * gr : 0.0f,
+                                         (v.y >= 0.0f && v.y <= 1.0f) ? w * gg : 0.0f,
+                                         (v.z >= 0.0f && v.z <= 1.0f) ? w * gb : 0.0f, gsr));
+                P += __shfl(pre, 31, 32);
+            }
+            T = T * __shfl(incl, 31, 32);
+        }
+        if (pass == 0) {
+            G = wave32_sum(G);
+            acc = wave32_sum(acc);
+        }
+    }
+    return acc;
+}
+
 __global__ void __launch_bounds__(256) volume_render_bwd_kernel(
     const float* __restrict__ rs, const float* __restrict__ tv, const float* __restrict__ bgp, int64_t N, int S,
     float sigma_scale, const float* __restrict__ g_rgb, const float* __restrict__ g_depth,
@@ -1693,82 +1768,205 @@ __global__ void __launch_bounds__(256) volume_render_bwd_kernel(
     const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
     const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
     for (int64_t ray = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); ray < N; ray += nw) {
-        const float* t = tv + ray * S;
         const float gr = g_rgb ? g_rgb[3 * ray] : 0.0f, gg = g_rgb ? g_rgb[3 * ray + 1] : 0.0f,
                     gb = g_rgb ? g_rgb[3 * ray + 2] : 0.0f;
         const float gd = g_depth ? g_depth[ray] : 0.0f, ga = g_acc ? g_acc[ray] : 0.0f;
         const float br = bgp ? bgp[3 * ray] : 0.0f, bgg = bgp ? bgp[3 * ray + 1] : 0.0f,
                     bb = bgp ? bgp[3 * ray + 2] : 0.0f;
-        double G = 0.0, acc = 0.0;
-        for (int pass = 0; pass < 2; ++pass) {
-            double T = 1.0, P = 0.0;
-            for (int s0 = 0; s0 < S; s0 += 32) {
-                const int s = s0 + j;
-                const bool valid = s < S;
-                const int sc = valid ? s : S - 1;
-                const float* v = rs + (ray * S + sc) * 4;
-                const float cr = clamp_nan(v[0], 0.0f, 1.0f), cg = clamp_nan(v[1], 0.0f, 1.0f),
-                            cb = clamp_nan(v[2], 0.0f, 1.0f);
-                float sg = clamp_min_nan(v[3], 0.0f);
-                if (sigma_scale != 1.0f) sg = sg * sigma_scale;
-                float dist = (sc < S - 1) ? (t[sc + 1] - t[sc]) : (t[sc] - t[sc - 1]);
-                dist = clamp_min_nan(dist, 1e-4f);
-                const float e = expf(-sg * dist);
-                const float a = 1.0f - e;
-                const float alpha = clamp_nan(a, 0.0f, (float)(1.0 - 1e-7));
-                float x = (1.0f - alpha) + 1e-10f;
-                if (!valid) x = 1.0f;
-                double incl = (double)x;
-#pragma unroll
-                for (int off = 1; off < 32; off <<= 1) {
-                    const double y = __shfl_up(incl, off, 32);
-                    if (j >= off) incl *= y;
-                }
-                double excl = __shfl_up(incl, 1, 32);
-                if (j == 0) excl = 1.0;
-                const float Ts = (float)(T * excl);
-                const float w = valid ? alpha * Ts : 0.0f;
-                float g = gr * (cr - br) + gg * (cg - bgg) + gb * (cb - bb) + gd * t[sc] + ga;
-                if (g_w && valid) g += g_w[ray * S + s];
-                const double gw = valid ? (double)g * (double)w : 0.0;
-                if (pass == 0) {
-                    G += gw;
-                    acc += (double)w;
-                } else {
-                    double pre = gw;  // inclusive prefix of g_k w_k over the tile
-#pragma unroll
-                    for (int off = 1; off < 32; off <<= 1) {
-                        const double y = __shfl_up(pre, off, 32);
-                        if (j >= off) pre += y;
-                    }
-                    const double suffix = G - (P + pre);
-                    const float dalpha = (float)((double)g * (double)Ts - suffix / (double)x);
-                    const bool amask = (a >= 0.0f) && (a <= (float)(1.0 - 1e-7));
-                    float dsig = amask ? dalpha * dist * e : 0.0f;
-                    if (sigma_scale != 1.0f) dsig = dsig * sigma_scale;
-                    const float gsr = (v[3] >= 0.0f) ? dsig : 0.0f;
-                    if (valid && h == 0) {
-                        float* o = g_rs + (ray * S + s) * 4;
-                        o[0] = (v[0] >= 0.0f && v[0] <= 1.0f) ? w * gr : 0.0f;
-                        o[1] = (v[1] >= 0.0f && v[1] <= 1.0f) ? w * gg : 0.0f;
-                        o[2] = (v[2] >= 0.0f && v[2] <= 1.0f) ? w * gb : 0.0f;
-                        o[3] = gsr;
-                    }
-                    P += __shfl(pre, 31, 32);
-                }
-                T = T * __shfl(incl, 31, 32);
-            }
-            if (pass == 0) {
-                G = wave32_sum(G);
-                acc = wave32_sum(acc);
-            }
-        }
+        const double acc = vr_bwd_ray(
+            [&](int sc) { return ld_rs(rs + (ray * S + sc) * 4); },
+            [&](int s, float4 o) { *reinterpret_cast<float4*>(g_rs + (ray * S + s) * 4) = o; }, tv + ray * S, S,
+            sigma_scale, gr, gg, gb, gd, ga, br, bgg, bb, g_w ? g_w + ray * S : nullptr, j, h);
         if (g_bg && lane == 0) {
             const float om = 1.0f - (float)acc;
             g_bg[3 * ray] = om * gr;
             g_bg[3 * ray + 1] = om * gg;
             g_bg[3 * ray + 2] = om * gb;
         }
+    }
+}
+
+// Fused training compositing of the routed adaptation step (routed_train.RoutedAdaptStep: linear colour space,
+// background from the SH-4 MLP head), one wave per ray:
+//   rs  = the routed blend of the pair outputs (blend_fwd_kernel; meta_container.py:322-337)
+//   bg  = background_color(dirs) (background_kernel), dirs = rays[:, 3:6] written out for the head's backward
+//   rgb = volume_render(rs, t, bg) (ray_rendering.py:137-165), the linear-space MSE's gradient
+//         (mse_linear_bwd_kernel; losses.py:10-32), volume_render's backward (vr_bwd_ray) and the blend's
+//         backward into the pair slots (blend_bwd_kernel; padding slots below the live count get zeros)
+// -- the arithmetic of those kernels, in one launch instead of eight.  The reported loss: a double sum per
+// workgroup in ray order, the last workgroup to finish adds the G partials in index order (deterministic).
+constexpr int kCmThreads = 256;
+constexpr int kCmMaxBlocks = 4096;
+#ifndef ACN_CM_PROF
+#define ACN_CM_PROF 0   // diagnostic build: per-ray section timestamps (acn_debug_cmprof_fetch)
+#endif
+#if ACN_CM_PROF
+__device__ unsigned long long g_cmprof[4096 * 8];
+__device__ unsigned long long g_cmblk[4096 * 4];
+#define CM_MARK(i) if (lane == 0 && ray < 4096) g_cmprof[ray * 8 + (i)] = wall_clock64();
+#define CM_BLK(i) if (threadIdx.x == 0 && blockIdx.x < 4096) g_cmblk[blockIdx.x * 4 + (i)] = wall_clock64();
+#else
+#define CM_MARK(i)
+#define CM_BLK(i)
+#endif
+constexpr int kCmMaxS = 1024;   // the per-wave LDS rows of S float4 + S float (4 waves: 80 KB at S = 1024)
+// a wave's LDS writes visible to its own later reads (in-order LDS; keeps the compiler from reordering)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__global__ void __launch_bounds__(kCmThreads) composite_mse_train_kernel(
+    BgArgs bg, const float* __restrict__ rays, const float4* __restrict__ y, const float* __restrict__ pw,
+    const int32_t* __restrict__ pmap, int K, const float* __restrict__ tv, const float* __restrict__ gt, int64_t N,
+    int S, const float* __restrict__ g_loss, float* __restrict__ rgb_out, float* __restrict__ dirs_out,
+    float* __restrict__ g_bg, float4* __restrict__ gy, const int32_t* __restrict__ pidx,
+    const int64_t* __restrict__ live, int64_t P, double* __restrict__ partials, unsigned int* __restrict__ counter,
+    float* __restrict__ loss) {
+    extern __shared__ float4 cm_rows[];   // [4 waves][S] float4: blended rgb_sigma, then dL/d(rgb_sigma); then
+                                          // [4 waves][S] float: the ray's t_vals
+    __shared__ double red[kCmThreads / 64];
+    __shared__ bool last;
+    const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5, wv = threadIdx.x >> 6;
+    CM_BLK(0)
+    float4* row = cm_rows + wv * S;
+    float* trow = reinterpret_cast<float*>(cm_rows + (kCmThreads / 64) * S) + wv * S;
+    const int64_t nw = (int64_t)gridDim.x * (kCmThreads >> 6);
+    const int64_t n = 3 * N;
+    const float gl = g_loss[0];
+    double lsum = 0.0;
+    // a sample's pair slots and weights: all its loads issued together (kept in registers for S <= 128, the
+    // blend backward reuses them)
+    int32_t pp[2][ACN_MAX_EXPERTS];
+    float w[2][ACN_MAX_EXPERTS];
+    auto load_pairs = [&](int64_t m, int u) {
+        const int32_t* pm = pmap + m * K;
+#pragma unroll
+        for (int k = 0; k < ACN_MAX_EXPERTS; ++k) pp[u][k] = k < K ? pm[k] : -1;
+#pragma unroll
+        for (int k = 0; k < ACN_MAX_EXPERTS; ++k) w[u][k] = pp[u][k] >= 0 ? pw[pp[u][k]] : 0.0f;
+    };
+    for (int64_t ray = (int64_t)blockIdx.x * (kCmThreads >> 6) + wv; ray < N; ray += nw) {
+        CM_MARK(0)
+        const float dx = rays[8 * ray + 3], dy = rays[8 * ray + 4], dz = rays[8 * ray + 5];
+        const int64_t m0 = ray * S;
+        const float* tg = tv + m0;
+        // blend (blend_fwd_kernel's order: acc + y_k w_k over k), every lane its own samples, 128 per round
+        for (int s0 = 0; s0 < S; s0 += 128) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int s = s0 + 64 * u + lane;
+                if (s < S) {
+                    load_pairs(m0 + s, u);
+                    trow[s] = tg[s];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int s = s0 + 64 * u + lane;
+                if (s >= S) continue;
+                float4 v[ACN_MAX_EXPERTS];
+#pragma unroll
+                for (int k = 0; k < ACN_MAX_EXPERTS; ++k)
+                    if (pp[u][k] >= 0) v[k] = y[pp[u][k]];
+                float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+                for (int k = 0; k < ACN_MAX_EXPERTS; ++k) {
+                    if (pp[u][k] < 0) continue;
+                    acc.x = acc.x + v[k].x * w[u][k];
+                    acc.y = acc.y + v[k].y * w[u][k];
+                    acc.z = acc.z + v[k].z * w[u][k];
+                    acc.w = acc.w + v[k].w * w[u][k];
+                }
+                row[s] = acc;
+            }
+        }
+        CM_MARK(1)
+        const float gt3[3] = {gt[3 * ray], gt[3 * ray + 1], gt[3 * ray + 2]};
+        float c[3];
+        background(bg, dx, dy, dz, lane, c);
+        if (lane < 3) dirs_out[3 * ray + lane] = lane == 0 ? dx : (lane == 1 ? dy : dz);
+        wave_lds_sync();
+        CM_MARK(2)
+        auto fetch = [&](int sc) { return row[sc]; };
+        float r, g, b, dd, a;
+        vr_fwd_ray(fetch, trow, S, 0, 0, 1.0f, j, h, nullptr, r, g, b, dd, a);
+        const float om = 1.0f - a;
+        const float pr[3] = {r + om * c[0], g + om * c[1], b + om * c[2]};
+        float gq[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const float d = clamp01(pr[q]) - gt_linear(gt3[q]);
+            lsum += (double)(d * d);
+            const float gv = (float)((2.0 / (double)n) * (double)d * (double)gl);
+            gq[q] = (pr[q] >= 0.0f && pr[q] <= 1.0f) ? gv : 0.0f;
+        }
+        if (lane == 0) {
+            rgb_out[3 * ray] = pr[0];
+            rgb_out[3 * ray + 1] = pr[1];
+            rgb_out[3 * ray + 2] = pr[2];
+        }
+        CM_MARK(3)
+        // the backward's second sweep reads sample s, then writes its gradient over it (same lane, same tile)
+        const double acc = vr_bwd_ray(fetch, [&](int s, float4 o) { row[s] = o; }, trow, S, 1.0f, gq[0], gq[1],
+                                      gq[2], 0.0f, 0.0f, c[0], c[1], c[2], nullptr, j, h);
+        if (g_bg && lane == 0) {
+            const float omb = 1.0f - (float)acc;
+            g_bg[3 * ray] = omb * gq[0];
+            g_bg[3 * ray + 1] = omb * gq[1];
+            g_bg[3 * ray + 2] = omb * gq[2];
+        }
+        wave_lds_sync();
+        CM_MARK(4)
+        // blend backward (blend_bwd_kernel): every pair slot of sample s gets dL/d(rgb_sigma)_s * w
+        for (int s0 = 0; s0 < S; s0 += 128) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int s = s0 + 64 * u + lane;
+                if (s >= S) continue;
+                if (S > 128) load_pairs(m0 + s, u);   // else: still in registers from the blend
+                const float4 o = row[s];
+#pragma unroll
+                for (int k = 0; k < ACN_MAX_EXPERTS; ++k)
+                    if (pp[u][k] >= 0)
+                        gy[pp[u][k]] = make_float4(o.x * w[u][k], o.y * w[u][k], o.z * w[u][k], o.w * w[u][k]);
+            }
+        }
+        wave_lds_sync();
+        CM_MARK(5)
+    }
+    CM_BLK(1)
+    // padding slots of the pair segments (pidx < 0 below the live count): zero gradients, as blend_bwd_kernel
+    const int64_t nl = live ? (live[0] < P ? live[0] : P) : P;
+    for (int64_t p = (int64_t)blockIdx.x * kCmThreads + threadIdx.x; p < nl; p += (int64_t)gridDim.x * kCmThreads)
+        if (pidx[p] < 0) gy[p] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    CM_BLK(2)
+    if (lane == 0) red[wv] = lsum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int i = 0; i < kCmThreads / 64; ++i) t += red[i];
+        partials[blockIdx.x] = t;
+        __threadfence();
+        last = atomicAdd(counter, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last) {   // the G partials in a fixed tree (thread i: partials i, i + 256, ...; xor tree; waves in order)
+        __threadfence();
+        double v = 0.0;
+        for (unsigned int i = threadIdx.x; i < gridDim.x; i += kCmThreads)
+            v += __hip_atomic_load(&partials[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+        if (lane == 0) red[wv] = v;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double t = 0.0;
+            for (int i = 0; i < kCmThreads / 64; ++i) t += red[i];
+            loss[0] = (float)(t / (double)n);
+            counter[0] = 0u;
+        }
+        CM_BLK(3)
     }
 }
 
@@ -2388,6 +2586,40 @@ extern "C" int acn_volume_render_bwd(const float* rgb_sigma, const float* t_vals
     return acn_check_launch("acn_volume_render_bwd");
 }
 
+extern "C" size_t acn_composite_mse_train_workspace_bytes(void) { return kCmMaxBlocks * sizeof(double) + 16; }
+
+extern "C" int acn_routed_composite_mse_train(const float* rays, int64_t N, int S, const float* t_vals,
+                                              const float* pair_out, const float* pair_w, const int32_t* pmap, int K,
+                                              const int32_t* pidx, int64_t P, const int64_t* live,
+                                              const acn_background* bg, const float* rgbs, const float* g_loss,
+                                              float* rgb, float* dirs, float* g_bg, float* g_pair_out, float* loss,
+                                              void* workspace, size_t workspace_bytes, void* stream) {
+    ACN_REQUIRE(N >= 1 && S >= 2 && S <= kCmMaxS && K >= 1 && K <= ACN_MAX_EXPERTS && P >= 0 && bg,
+                "acn_routed_composite_mse_train: bad sizes (N=%lld S=%d K=%d P=%lld)", (long long)N, S, K,
+                (long long)P);
+    ACN_REQUIRE(rays && t_vals && pmap && rgbs && g_loss && rgb && dirs && loss && workspace &&
+                    (P == 0 || (pair_out && pair_w && pidx && g_pair_out)),
+                "acn_routed_composite_mse_train: NULL pointer");
+    ACN_REQUIRE(workspace_bytes >= acn_composite_mse_train_workspace_bytes(),
+                "acn_routed_composite_mse_train: workspace too small");
+    ACN_REQUIRE(((uintptr_t)pair_out & 15) == 0 && ((uintptr_t)g_pair_out & 15) == 0,
+                "acn_routed_composite_mse_train: pair buffers must be 16-byte aligned");
+    if (bg->mode == ACN_BG_MLP) {
+        ACN_REQUIRE(bg->w1 && bg->b1 && bg->w2 && bg->b2, "background MLP pointers are NULL");
+        ACN_REQUIRE(bg->hidden >= 1 && bg->hidden <= 64, "bg_hidden must be in [1, 64], got %d", bg->hidden);
+    }
+    BgArgs b{bg->mode, bg->hidden, {bg->color[0], bg->color[1], bg->color[2]}, bg->w1, bg->b1, bg->w2, bg->b2};
+    int64_t wgs = (N + 3) / 4;
+    wgs = wgs < kCmMaxBlocks ? wgs : kCmMaxBlocks;
+    double* partials = (double*)workspace;
+    unsigned int* counter = (unsigned int*)((char*)workspace + kCmMaxBlocks * sizeof(double));
+    const size_t lds = (size_t)(kCmThreads / 64) * S * (sizeof(float4) + sizeof(float));
+    hipLaunchKernelGGL(composite_mse_train_kernel, dim3((unsigned)wgs), dim3(kCmThreads), lds, (hipStream_t)stream, b,
+                       rays, (const float4*)pair_out, pair_w, pmap, K, t_vals, rgbs, N, S, g_loss, rgb, dirs, g_bg,
+                       (float4*)g_pair_out, pidx, live, P, partials, counter, loss);
+    return acn_check_launch("acn_routed_composite_mse_train");
+}
+
 extern "C" int acn_routing_fwd(const float* pts, int64_t M, int64_t ld, const acn_routing* routing, float* weights,
                                int32_t* hard, void* stream) {
     ACN_REQUIRE(routing && routing->K >= 1 && routing->K <= ACN_MAX_EXPERTS, "acn_routing_fwd: bad routing");
@@ -2686,6 +2918,18 @@ extern "C" int acn_ep_composite(const float* rays, int64_t N, int S, const float
     return acn_check_launch("acn_ep_composite");
 }
 
+#if ACN_CM_PROF
+extern "C" int acn_debug_cmprof_fetch(unsigned long long* host, int max_rays) {
+    const int m = max_rays < 4096 ? max_rays : 4096;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_cmprof), (size_t)m * 8 * sizeof(unsigned long long)) == hipSuccess
+               ? m : -1;
+}
+extern "C" int acn_debug_cmblk_fetch(unsigned long long* host, int max_blocks) {
+    const int m = max_blocks < 4096 ? max_blocks : 4096;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_cmblk), (size_t)m * 4 * sizeof(unsigned long long)) == hipSuccess
+               ? m : -1;
+}
+#endif
 #if ACN_SLOTS_CHECK > 1
 // diagnostic build only: copy out (and clear) the recorded self-check mismatches; returns their count
 extern "C" int acn_debug_check_fetch(float* host, int max_records) {

@@ -12,6 +12,7 @@ There is no CPU path: parameters must live on a HIP device.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Iterable, Optional
 
 import torch
@@ -68,6 +69,9 @@ class _Plan:
 # Optional timing hook (bench.py): when set to a list, FusedAdam.step appends a pair of recorded
 # HIP events bracketing exactly the Adam launch on the current stream.
 EVENT_HOOK = None
+# SlottedAdam: the clip norm's partial sums, their reduction and the clip coefficient in one launch
+# (acn_grad_clip_slots) instead of three; bitwise the same (tests/test_routed_glue.py)
+FUSED_CLIP = os.environ.get("ACN_FUSED_CLIP", "1") != "0"
 
 
 def bump_versions(params) -> None:
@@ -410,6 +414,7 @@ class SlottedAdam:
         self.partials = torch.empty(first, device=dev, dtype=torch.float64)
         self.total = torch.empty(1, device=dev, dtype=torch.float64)
         self.scale = torch.ones(2, device=dev, dtype=torch.float32)
+        self.ticket = torch.zeros(1, device=dev, dtype=torch.int32)   # acn_grad_clip_slots' counter
         self.step_dev = torch.tensor([slots_seen.get(s, 0) for s in range(self.nslots)], device=dev,
                                      dtype=torch.int32)
         self.ngroups = len(optimizer.param_groups)
@@ -537,18 +542,20 @@ class SlottedAdam:
                 check(L.acn_grad_sumsq_slots_ex(ptr(self.descs_sh), ptr(self.chunk_sh), self.nchunks_sh,
                                                 ptr(self.flags_sh), ptr(seg), self.K, ptr(self.partials_sh),
                                                 ptr(self.total), ptr(self.total_own), s), "acn_grad_sumsq_slots_ex")
-            elif self.norm_plan is not None:
-                descs, chunks, nch, flags, partials = self.norm_plan
-                check(L.acn_grad_sumsq_slots_ex(ptr(descs), ptr(chunks), nch, ptr(flags), ptr(seg), self.K,
-                                                ptr(partials), ptr(self.total), ptr(table_sumsq), s),
-                      "acn_grad_sumsq_slots_ex")
             else:
-                check(L.acn_grad_sumsq_slots_ex(ptr(self.descs), ptr(self.chunk_tensor), self.nchunks,
-                                                ptr(self.flags), ptr(seg), self.K, ptr(self.partials), ptr(self.total),
-                                                ptr(table_sumsq), s), "acn_grad_sumsq_slots_ex")
+                descs, chunks, nch, flags, partials = self.norm_plan if self.norm_plan is not None else (
+                    self.descs, self.chunk_tensor, self.nchunks, self.flags, self.partials)
+                if amp is None and FUSED_CLIP:   # norm + clip coefficient in one launch
+                    check(L.acn_grad_clip_slots(ptr(descs), ptr(chunks), nch, ptr(flags), ptr(seg), self.K,
+                                                ptr(partials), ptr(self.total), ptr(table_sumsq), float(max_norm),
+                                                ptr(self.scale), ptr(self.ticket), s), "acn_grad_clip_slots")
+                else:
+                    check(L.acn_grad_sumsq_slots_ex(ptr(descs), ptr(chunks), nch, ptr(flags), ptr(seg), self.K,
+                                                    ptr(partials), ptr(self.total), ptr(table_sumsq), s),
+                          "acn_grad_sumsq_slots_ex")
             if amp is not None:
                 amp.unscale_coef(self.total, max_norm, self.scale, seg, self.K)
-            else:
+            elif allreduce is not None or not FUSED_CLIP:
                 check(L.acn_clip_coef(ptr(self.total), float(max_norm), ptr(self.scale), s), "acn_clip_coef")
             scale = self.scale
         if hook is not None:

@@ -65,6 +65,10 @@ ADAM_EARLY = os.environ.get("ACN_ADAM_EARLY", "0") != "0"   # measured slower (D
 # The background head's backward (two small launches) on a side stream beside the experts' backward chain
 # (blend, MLP, table scatter), joined before the clip / Adam pass that reads its gradients
 BG_SIDE = os.environ.get("ACN_BG_SIDE", "0") != "0"   # measured within noise: off
+# The compositing glue of the step in one launch (acn_routed_composite_mse_train: blend, background forward,
+# compositing, the linear MSE and the backward of all three down to the pair outputs) instead of eight launches
+# and a copy; same arithmetic (tests/test_routed_glue.py compares the two bitwise)
+FUSED_COMPOSITE = os.environ.get("ACN_FUSED_COMPOSITE", "1") != "0"
 
 
 def draw_jitter(n: int, S: int, device) -> torch.Tensor:
@@ -153,6 +157,10 @@ class RoutedAdaptStep:
         self.bg_params = list(model.bg_mlp.parameters())
         self.gbg = [torch.zeros_like(p) for p in self.bg_params]
         self.dirs = torch.zeros(N, 3, **f32)
+        self.rgb = torch.zeros(N, 3, **f32)
+        self.g_bg = torch.zeros(N, 3, **f32)
+        self.gout = torch.zeros(cap, 4, **f32)
+        self.cws = torch.zeros(int(L.acn_composite_mse_train_workspace_bytes()), device=dev, dtype=torch.uint8)
         try:   # (acn_background, the tensors it points into)
             self.bg_spec, self._bg_keep = model.background_spec() if FUSED_BACKGROUND else (None, None)
         except AcnError:
@@ -277,13 +285,24 @@ class RoutedAdaptStep:
         check(mfn("acn_mlp_pack_pairs")(self._mlp_ptrs, K, ptr(self.mws), s), "acn_mlp_pack_pairs")
         check(mfn("acn_mlp_train_fwd_pairs")(ptr(self.h0), ptr(self.sh), ptr(self.seg), K, ptr(self.mws), ptr(self.out), s),
               "acn_mlp_train_fwd_pairs")
-        rs = ops.routed_blend_fwd(self.out, self.pw, self.pmap[:M]).view(N, S, 4).requires_grad_(True)
         rays, rgbs, dirs = self.rays[:N], self.rgbs[:N], self.dirs[:N]
+        linear = str(self.P.color_space).lower() == "linear"
+        if FUSED_COMPOSITE and self.bg_spec is not None and linear and S <= 1024:   # S: the kernel's LDS rows
+            check(L.acn_routed_composite_mse_train(
+                ptr(rays), N, S, ptr(t), ptr(self.out), ptr(self.pw), ptr(self.pmap), K, ptr(self.pidx), self.cap,
+                ptr(self.seg[K:K + 1]), C.byref(self.bg_spec), ptr(rgbs), ptr(self._one if self.amp is None
+                                                                            else self.amp.scale),
+                ptr(self.rgb), ptr(dirs), ptr(self.g_bg), ptr(self.gout), ptr(self.loss), ptr(self.cws),
+                self.cws.numel(), s), "acn_routed_composite_mse_train")
+            ev_bg = self._head_bwd(dirs, self.g_bg[:N])
+            self._experts_bwd(self.gout, enc, det, capturing, ev_early, ev_bg)
+            return
+        rs = ops.routed_blend_fwd(self.out, self.pw, self.pmap[:M]).view(N, S, 4).requires_grad_(True)
         # the shared part: compositing, colour transform and MSE under torch autograd (HIP kernels); the
         # background head as its fused HIP forward and backward (writing the persistent .grad buffers), or
         # under autograd when the head is not the HIP-supported SH-4 MLP
         from .ray_rendering import volume_render
-        if self.bg_spec is not None and str(self.P.color_space).lower() == "linear":
+        if self.bg_spec is not None and linear:
             # the kernels autograd would run (compositing, the linear-space MSE and their backwards), called
             # directly: no ones-fill for the loss gradient, no autograd bookkeeping launches
             dirs.copy_(rays[:, 3:6])
@@ -293,19 +312,7 @@ class RoutedAdaptStep:
             loss = ops.mse_linear_fwd(rgb, rgbs, out=self.loss)
             g_rgb = ops.mse_linear_bwd(rgb, rgbs, self._one if self.amp is None else self.amp.scale)
             g_rs, g_bg = ops.volume_render_bwd(rs_, t, bg, 1.0, g_rgb, None, None, None)
-            if BG_SIDE and self.side is not None:
-                # fork: the head's backward beside the experts' chain; joined before Adam (ev_bg)
-                main = torch.cuda.current_stream(dev)
-                e_fork = torch.cuda.Event()
-                e_fork.record(main)
-                self.side.wait_event(e_fork)
-                with torch.cuda.stream(self.side):
-                    ops.background_bwd(dirs, self.bg_spec, g_bg, self.gbg)
-                    ev_bg = torch.cuda.Event()
-                    ev_bg.record(self.side)
-                g_bg.record_stream(self.side)
-            else:
-                ops.background_bwd(dirs, self.bg_spec, g_bg, self.gbg)
+            ev_bg = self._head_bwd(dirs, g_bg)
         elif self.bg_spec is not None:
             dirs.copy_(rays[:, 3:6])
             bg = ops.background_fwd(dirs, self.bg_spec).requires_grad_(True)
@@ -326,6 +333,32 @@ class RoutedAdaptStep:
         if loss is not self.loss:
             self.loss.copy_(loss.detach())
         gout = ops.routed_blend_bwd(g_rs.reshape(M, 4).contiguous(), self.pidx, self.pw, live=self.seg[K:K + 1])
+        self._experts_bwd(gout, enc, det, capturing, ev_early, ev_bg)
+
+    def _head_bwd(self, dirs: torch.Tensor, g_bg: torch.Tensor):
+        """The background head's backward into its persistent .grad buffers; on the side stream (BG_SIDE)
+        it returns the event the Adam pass joins."""
+        if BG_SIDE and self.side is not None:
+            # fork: the head's backward beside the experts' chain; joined before Adam (ev_bg)
+            main = torch.cuda.current_stream(self.device)
+            e_fork = torch.cuda.Event()
+            e_fork.record(main)
+            self.side.wait_event(e_fork)
+            with torch.cuda.stream(self.side):
+                ops.background_bwd(dirs, self.bg_spec, g_bg, self.gbg)
+                ev_bg = torch.cuda.Event()
+                ev_bg.record(self.side)
+            g_bg.record_stream(self.side)
+            return ev_bg
+        ops.background_bwd(dirs, self.bg_spec, g_bg, self.gbg)
+        return None
+
+    def _experts_bwd(self, gout: torch.Tensor, enc, det: bool, capturing: bool, ev_early, ev_bg) -> None:
+        """From dL/d(pair outputs): the experts' MLP [dW | db] and table gradients, then clip + Adam."""
+        L = _lib.lib()
+        dev, K = self.device, self.K
+        s = _stream(dev)
+        mfn = lambda name: ops.mlp_fn(name, self.mlp_precision)  # noqa: E731
         check(mfn("acn_mlp_train_bwd_dw_pairs")(ptr(self.h0), ptr(self.sh), ptr(self.out), ptr(gout), ptr(self.seg), K,
                                            ptr(self.mws), ptr(self.dw), ptr(self.gh0), s), "acn_mlp_train_bwd_dw_pairs")
         bhook = BWD_HOOK if self.graph is None and not capturing else None

@@ -220,6 +220,26 @@ size_t acn_background_bwd_workspace_bytes(void);
 int acn_background_bwd(const float* dirs, int64_t N, const acn_background* bg, const float* g_out, float* g_w1,
                        float* g_b1, float* g_w2, float* g_b2, void* workspace, size_t workspace_bytes, void* stream);
 
+/* The routed adaptation step's compositing, loss and their backward in one launch (replaces, in
+ * routed_train.RoutedAdaptStep, acn_routed_blend_fwd + acn_background_fwd + the dirs copy +
+ * acn_volume_render_fwd + acn_mse_linear_fwd_ws + acn_mse_linear_bwd + acn_volume_render_bwd +
+ * acn_routed_blend_bwd with the same arithmetic).  Reference: the train-mode render_rays +
+ * compute_mse_loss + loss.backward() down to the experts' outputs, runtime_adapt.py:286-304,
+ * meta_container.py:322-337 (blend), ray_rendering.py:137-165 (compositing), losses.py:10-32 (linear MSE).
+ *   rays (N,8), t_vals (N,S); pair_out (P,4) / pair_w (P) / pidx (P) / pmap (N*S,K) the routed pairs of
+ *   acn_routed_scatter, live (device int64, may be NULL = P) the live pair count; rgbs (N,3) targets;
+ *   g_loss (device float) dL/dloss (1, or the AMP loss scale).
+ * Writes rgb (N,3), dirs (N,3) = rays[:,3:6] (for acn_background_bwd), g_bg (N,3) dL/d(background rgb)
+ * (may be NULL), g_pair_out (P,4) dL/d(pair outputs) (padding slots below live: 0), loss (device float,
+ * deterministic double sum).  pair_out / g_pair_out 16-byte aligned; workspace of
+ * acn_composite_mse_train_workspace_bytes(), zeroed once (its counter returns to 0 after each call). */
+size_t acn_composite_mse_train_workspace_bytes(void);
+int acn_routed_composite_mse_train(const float* rays, int64_t N, int S, const float* t_vals, const float* pair_out,
+                                   const float* pair_w, const int32_t* pmap, int K, const int32_t* pidx, int64_t P,
+                                   const int64_t* live, const acn_background* bg, const float* rgbs,
+                                   const float* g_loss, float* rgb, float* dirs, float* g_bg, float* g_pair_out,
+                                   float* loss, void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---------------------------------------------------------------------------------------- */
 /* Optimizer step of the online adaptation loop (pipelines/online_stage/runtime_adapt.py:305-309):
  * torch.nn.utils.clip_grad_norm_(params, max_norm) followed by torch.optim.Adam(param_groups)
@@ -290,6 +310,12 @@ int acn_grad_sumsq_slots(const acn_param_desc* descs, const int32_t* chunk_tenso
 int acn_grad_sumsq_slots_ex(const acn_param_desc* descs, const int32_t* chunk_tensor, int64_t nchunks,
                             const int32_t* flags, const int64_t* seg, int K, double* partials, double* total,
                             double* extra, void* stream);
+/* acn_grad_sumsq_slots_ex followed by acn_clip_coef(total, max_norm, out) in ONE launch (the last workgroup to
+ * finish reduces the partials and writes total, out[0] = norm, out[1] = clip coefficient): bitwise the same
+ * results.  counter: a device uint zeroed once (returns to 0 after each call). */
+int acn_grad_clip_slots(const acn_param_desc* descs, const int32_t* chunk_tensor, int64_t nchunks,
+                        const int32_t* flags, const int64_t* seg, int K, double* partials, double* total,
+                        double* extra, float max_norm, float* out, unsigned int* counter, void* stream);
 int acn_adam_step_slots(const acn_param_desc* descs, const int32_t* chunk_tensor, int64_t nchunks,
                         const int32_t* flags, const void* table, int ngroups, int table_steps, int32_t* step_dev,
                         int nslots, const int64_t* seg, int K, const float* grad_scale, void* stream);
