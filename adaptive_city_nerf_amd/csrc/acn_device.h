@@ -511,16 +511,23 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 #else
 #define ACN_OPND_SB0
 #endif
-__device__ __forceinline__ void opnd_fence(f16x8& a) { ACN_OPND_SB0 asm volatile(ACN_OPND_PAD : "+v"(a) : ACN_OPND_CLOB); ACN_OPND_SB0 }
+#ifdef ACN_OPND_OFF   // diagnostic A/B builds only: no fence statement at all
+#undef ACN_OPND_SB0
+#define ACN_OPND_SB0
+#define ACN_OPND_ASM(...)
+#else
+#define ACN_OPND_ASM(...) asm volatile(__VA_ARGS__)
+#endif
+__device__ __forceinline__ void opnd_fence(f16x8& a) { ACN_OPND_SB0 ACN_OPND_ASM(ACN_OPND_PAD : "+v"(a) : ACN_OPND_CLOB); ACN_OPND_SB0 }
 __device__ __forceinline__ void opnd_fence(f16x8& a, f16x8& b) {
-    ACN_OPND_SB0 asm volatile(ACN_OPND_PAD : "+v"(a), "+v"(b) : ACN_OPND_CLOB); ACN_OPND_SB0
+    ACN_OPND_SB0 ACN_OPND_ASM(ACN_OPND_PAD : "+v"(a), "+v"(b) : ACN_OPND_CLOB); ACN_OPND_SB0
 }
 __device__ __forceinline__ void opnd_fence(f16x8& a, f16x8& b, f16x8& c, f16x8& d) {
-    ACN_OPND_SB0 asm volatile(ACN_OPND_PAD : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : ACN_OPND_CLOB); ACN_OPND_SB0
+    ACN_OPND_SB0 ACN_OPND_ASM(ACN_OPND_PAD : "+v"(a), "+v"(b), "+v"(c), "+v"(d) : ACN_OPND_CLOB); ACN_OPND_SB0
 }
 __device__ __forceinline__ void opnd_fence(f16x8& a, f16x8& b, f16x8& c, f16x8& d, f16x8& e, f16x8& f, f16x8& g,
                                            f16x8& h) {
-    ACN_OPND_SB0 asm volatile(ACN_OPND_PAD : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e), "+v"(f), "+v"(g), "+v"(h)
+    ACN_OPND_SB0 ACN_OPND_ASM(ACN_OPND_PAD : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e), "+v"(f), "+v"(g), "+v"(h)
                               : ACN_OPND_CLOB); ACN_OPND_SB0
 }
 // one plane of N fragments (N = 1, 2, 4, 8)

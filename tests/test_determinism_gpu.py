@@ -6,6 +6,7 @@ seen, and the training MLP kernels (same split -> MFMA idiom, tolerance-tested e
 
 Reference behaviour: rays are rendered independently and deterministically (nerfs/ray_rendering.py:290-345);
 the training MLP is MetaNGP's chain (models/inr/meta_ngp.py:171-241)."""
+import os
 import numpy as np
 import pytest
 import torch
@@ -14,7 +15,7 @@ from test_render_ws import _setup, _t
 
 pytestmark = pytest.mark.gpu
 
-REPS = 20
+REPS = int(os.environ.get("ACN_DET_REPS", "20"))   # repeats per case (A/B stress runs raise it)
 
 
 @pytest.mark.parametrize("tag,active", [("k4", None), ("k4", 2), ("k8", None)])
