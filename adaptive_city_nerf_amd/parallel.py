@@ -105,6 +105,16 @@ def expert_spatial_keys(rays: Tensor, model, bits: int = 6) -> Tensor:
     return dominant_expert(rays, model).to(torch.int64) * (1 << (2 * bits)) + direction_cell(rays, bits)
 
 
+def multi_expert_rays(rays: Tensor, model, ray_samples: int) -> Tensor:
+    """(N,) bool: rays whose eval-mode samples (stratified, no jitter) reach more than one expert under the
+    container's soft routing -- the rays render_slots_kernel evaluates with two or more experts per tile."""
+    from . import ops
+    S = int(ray_samples)
+    _, _, _, _, _, pmap, _ = ops.routed_pairs_xd(rays, S, None, model.routing_spec())
+    hit = (pmap.view(rays.shape[0], S, -1) >= 0).any(dim=1)     # (N, K): expert k reached by some sample
+    return hit.sum(dim=1) > 1
+
+
 def dominant_expert(rays: Tensor, model) -> Tensor:
     """Expert owning each ray's midpoint o + d (near + far)/2: argmin centroid distance, the hard
     routing rule of meta_container.py:119-121 (HIP kernel acn_routing_fwd)."""

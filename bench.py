@@ -462,6 +462,9 @@ def main():
     ap.add_argument("--diag-pixel-order", action="store_true",
                     help="diagnostic (c3): the batch in scanline pixel order instead of random order before the "
                          "expert sort")
+    ap.add_argument("--diag-multi-last", action="store_true",
+                    help="diagnostic (c3): the plan visits the rays whose samples reach more than one expert after "
+                         "the single-expert rays (same outputs; measured slower, DESIGN.md 4k)")
     ap.add_argument("--diag-expert-only-order", action="store_true",
                     help="diagnostic (c3): sort the batch by owning expert only (no direction-cell secondary key)")
     ap.add_argument("--c5-order", choices=["none", "expert-mid"], default="none",
@@ -557,6 +560,10 @@ def main():
         grays = make_rays(scene, gbox, device, world * a.rays, 1234, pixel_order=a.diag_pixel_order)
         keys = (parallel.dominant_expert(grays, model) if a.diag_expert_only_order
                 else parallel.expert_spatial_keys(grays, model))
+        if a.diag_multi_last:
+            multi = parallel.multi_expert_rays(grays, model, S)
+            keys = keys + multi.to(torch.int64) * (1 << 40)
+            multi_frac = float(multi.float().mean())
         plan = parallel.expert_sorted_plan(keys, world)
         samples_per_step = grays.shape[0] * S
 
@@ -1222,8 +1229,11 @@ def main():
                                     f"routed, keep-filtered, stably binned per cell and copied to the host per step; "
                                     f"metric counts routed rays", "rays_per_gpu": a.data_rays}}[a.workload]
         cfg.update({"samples_per_ray": S, "parallelism": f"ray-sharded x{world}"})
+        if a.workload == "c3" and a.diag_multi_last:
+            cfg["plan"] = {"multi_expert_rays_last": True, "multi_expert_fraction": round(multi_frac, 4)}
         diag = {k: v for k, v in (("shared_table", a.diag_shared_table), ("pixel_order", a.diag_pixel_order),
                                   ("expert_only_order", a.diag_expert_only_order),
+                                  ("multi_expert_rays_last", a.diag_multi_last),
                                   ("expert_box", a.diag_expert_box != "own" and a.diag_expert_box)) if v}
         if diag:        # a diagnostic run: not the workload's real render, never a headline line
             cfg["diagnostic"] = diag
