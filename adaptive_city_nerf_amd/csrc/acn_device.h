@@ -397,8 +397,9 @@ __device__ __forceinline__ void hash_level_f2(const float2* __restrict__ tl, flo
 // Routing (meta_container.py:97-134), cdist mm-path restated exactly as in the oracle.
 // Computed without per-expert arrays (runtime-indexed arrays would live in scratch): a first
 // pass gives min distance / denominator (soft) or argmin (hard), then w_k is recomputed per k.
+// squared centroid distance of the cdist mm-path, clamped at 0 (NaN -> 0); route_dist = its square root
 template <typename Cfg>
-__device__ __forceinline__ float route_dist(const Cfg& cfg, int k, float px, float py, float pz) {
+__device__ __forceinline__ float route_dist2(const Cfg& cfg, int k, float px, float py, float pz) {
     float s = 0.0f, xn, cn;
     if (cfg.cluster_2d) {
         const float cy = cfg.cent[k][1], cz = cfg.cent[k][2];
@@ -416,7 +417,11 @@ __device__ __forceinline__ float route_dist(const Cfg& cfg, int k, float px, flo
     }
     s = s + xn;
     s = s + cn;
-    return sqrtf(s > 0.0f ? s : 0.0f);
+    return s > 0.0f ? s : 0.0f;
+}
+template <typename Cfg>
+__device__ __forceinline__ float route_dist(const Cfg& cfg, int k, float px, float py, float pz) {
+    return sqrtf(route_dist2(cfg, k, px, py, pz));
 }
 
 struct RouteState {
@@ -428,12 +433,11 @@ template <int ROUTE, typename Cfg>
 __device__ __forceinline__ RouteState route_prep(const Cfg& cfg, float px, float py, float pz) {
     RouteState st{0.0f, 0.0f, 0};
     if (ROUTE == 1) {
-        float mind = INFINITY;
-        for (int k = 0; k < cfg.K; ++k) {
-            float d = route_dist(cfg, k, px, py, pz);
-            d = d < 1e-6f ? 1e-6f : d;
-            mind = fminf(mind, d);
-        }
+        // min_k max(sqrt(s_k), 1e-6) = max(sqrt(min_k s_k), 1e-6) (monotonic): one square root, not K
+        float mins = INFINITY;
+        for (int k = 0; k < cfg.K; ++k) mins = fminf(mins, route_dist2(cfg, k, px, py, pz));
+        float mind = sqrtf(mins);
+        mind = mind < 1e-6f ? 1e-6f : mind;
         st.thr = cfg.bm * mind;
         float den = 0.0f;
         for (int k = 0; k < cfg.K; ++k) {

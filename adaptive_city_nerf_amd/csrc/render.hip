@@ -905,6 +905,16 @@ __device__ __forceinline__ float tlin_sel(float near, float far, int i, int S, f
     return near * (1.0f - u) + far * u;
 }
 
+#ifndef ACN_SLOTS_PROF
+#define ACN_SLOTS_PROF 0   // diagnostic build: per-ray section stamps of render_slots_kernel (acn_debug_slprof_fetch)
+#endif
+#if ACN_SLOTS_PROF
+constexpr int kSlProfRays = 1 << 20;
+__device__ unsigned long long g_slprof[kSlProfRays * 6];
+#define SL_MARK(ray, i) if (lane == 0 && (ray) < kSlProfRays) g_slprof[(ray) * 6 + (i)] = wall_clock64();
+#else
+#define SL_MARK(ray, i)
+#endif
 // One ray, front to back in 32-sample tiles: t-values -> field(px, py, pz, shv, folded, y...) ->
 // volume_render conditioning -> compositing -> background -> outputs.  `field` evaluates the
 // (routed) container for this lane's sample; it is a template callable so the single-expert, the
@@ -980,6 +990,7 @@ __device__ __forceinline__ void render_ray(const RenderParams& p, const BgArgs& 
         const int stop = __builtin_amdgcn_readfirstlane((int)(acc.T < (double)p.tau));
         if (stop) { s0 += 32; break; }
     }
+    SL_MARK(ray, 4)
     if (p.weights && h == 0)  // samples skipped by early termination carry zero weight
         for (int s = s0 + j; s < S; s += 32) p.weights[ray * S + s] = 0.0f;
     float bgc[3];
@@ -1264,6 +1275,38 @@ __global__ void __launch_bounds__(1024, 4) render_ws_kernel(FieldCfg cfg, BgArgs
 // exactly 1.0f (soft: (1/d)/den with den = 1/d; hard: always), so the container's blend
 // 0 + y_k * 1.0f is y_k bit for bit and the ray can skip the per-sample routing and blend.
 constexpr uint32_t kSingleRay = 1u << 31;
+// The expert bits and the exactness test of route_prep<1> + route_weight for one sample, without the
+// quotients: w_k = ((d_k <= thr) ? 1/d_k : 0) / den is > 0 exactly when d_k <= thr and d_k is finite
+// (den >= 1e-6 and finite), and is exactly 0 or 1 on every expert when at most one finite d_k is inside
+// the margin and, if one is, (1/d_k) / max(1/d_k, 1e-6) == 1 (den is then 0 + 1/d_k: the other terms
+// add +0).  With two or more inside, the ray has two bits and is never a single-expert ray, so its
+// exactness does not matter.  K + 1 square roots per sample instead of 3K plus 3K divisions.
+__device__ __forceinline__ void soft_route_bits(const FieldCfg& cfg, float px, float py, float pz, uint32_t& m,
+                                                bool& exact) {
+    // min_k max(sqrt(max(s_k, 0)), 1e-6) = max(sqrt(min_k max(s_k, 0)), 1e-6): sqrt and the clamps are
+    // monotonic, so the minimum is taken on the squared distances (one square root instead of K)
+    float mins = INFINITY;
+    for (int k = 0; k < cfg.K; ++k) mins = fminf(mins, route_dist2(cfg, k, px, py, pz));
+    float mind = sqrtf(mins);
+    mind = mind < 1e-6f ? 1e-6f : mind;
+    const float thr = cfg.bm * mind;
+    int cnt = 0;
+    float dsel = 1.0f;
+    for (int k = 0; k < cfg.K; ++k) {
+        float d = route_dist(cfg, k, px, py, pz);
+        d = d < 1e-6f ? 1e-6f : d;
+        if (d <= thr && d < INFINITY) {
+            m |= 1u << k;
+            ++cnt;
+            dsel = d;
+        }
+    }
+    if (cnt == 1) {
+        const float inv = 1.0f / dsel;
+        const float den = inv < 1e-6f ? 1e-6f : inv;
+        exact = exact && (inv / den == 1.0f);
+    }
+}
 __device__ __forceinline__ uint32_t ray_expert_mask(const FieldCfg& cfg, int route, const RenderParams& p, int64_t ray,
                                                     bool live, float step, int lane) {
     uint32_t m = 0u;
@@ -1277,12 +1320,7 @@ __device__ __forceinline__ uint32_t ray_expert_mask(const FieldCfg& cfg, int rou
             const float t = jit ? tval(near, far, s, p.S, jit) : tlin_sel(near, far, s, p.S, step);
             const float px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;
             if (route == 1) {
-                const RouteState st = route_prep<1>(cfg, px, py, pz);
-                for (int k = 0; k < cfg.K; ++k) {
-                    const float w = route_weight(cfg, st, k, px, py, pz);
-                    if (w > 0.0f) m |= 1u << k;
-                    exact = exact && (w == 0.0f || w == 1.0f);
-                }
+                soft_route_bits(cfg, px, py, pz, m, exact);
             } else {
                 m |= 1u << route_prep<2>(cfg, px, py, pz).hard;
             }
@@ -1420,7 +1458,9 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
         const bool live = base + wave < lim;
         const int64_t ray = !live ? 0 : (p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[base + wave])
                                                  : base + wave);
+        if (live) { SL_MARK(ray, 0) }
         const uint32_t m = ray_expert_mask(cfg, ROUTE, p, ray, live, step, lane);
+        if (live) { SL_MARK(ray, 1) }
         if (lane == 0)
             for (int k = 0; k < cfg.K; ++k)
                 if ((m >> k) & 1u) atomicAdd(&cnt[k], 1);
@@ -1456,6 +1496,7 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
 #else
         const int k0 = __builtin_amdgcn_readfirstlane(slot_k[0]), k1 = __builtin_amdgcn_readfirstlane(slot_k[1]);
 #endif
+        if (live) { SL_MARK(ray, 2) }
         if (live) {
             const bool single = (m & kSingleRay) != 0u;
             const int k_single = __builtin_ctz(m | kSingleRay);
@@ -1487,6 +1528,7 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
                            }
 #endif
                        });
+            SL_MARK(ray, 5)
         }
     }
 }
@@ -2918,6 +2960,13 @@ extern "C" int acn_ep_composite(const float* rays, int64_t N, int S, const float
     return acn_check_launch("acn_ep_composite");
 }
 
+#if ACN_SLOTS_PROF
+extern "C" int acn_debug_slprof_fetch(unsigned long long* host, int max_rays) {
+    const int m = max_rays < kSlProfRays ? max_rays : kSlProfRays;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_slprof), (size_t)m * 6 * sizeof(unsigned long long)) == hipSuccess
+               ? m : -1;
+}
+#endif
 #if ACN_CM_PROF
 extern "C" int acn_debug_cmprof_fetch(unsigned long long* host, int max_rays) {
     const int m = max_rays < 4096 ? max_rays : 4096;
