@@ -1350,6 +1350,14 @@ __device__ unsigned g_chk_n;
 #ifndef ACN_SLOTS_THREADS
 #define ACN_SLOTS_THREADS 512  // 2 waves/SIMD, 256 VGPRs: the 1024-thread build spills and was measured wrong
 #endif
+// `folded` (per ray, wave-uniform): bits 0-1 = LDS slot 0 / 1 folded; bit 3 = cbg holds the fold of expert
+// (folded >> 4) & 31, the expert read from global memory last (its fold is reused while it stays the same)
+__device__ __forceinline__ bool cbg_holds(uint32_t folded, int k) {
+    return (folded & 8u) && (int)((folded >> 4) & 31u) == k;
+}
+__device__ __forceinline__ uint32_t cbg_set(uint32_t folded, int k) {
+    return (folded & 7u) | 8u | ((uint32_t)k << 4);
+}
 // the field of one 32-sample tile in render_slots_kernel: LDS slot experts, the rest from the packed images
 // in global memory (folded colour bias in cb[slot] / cbg); single = one expert with weight 1.0f on every sample
 template <int INTERP, int ROUTE, bool FOLD>
@@ -1372,7 +1380,10 @@ __device__ __forceinline__ void slots_field(const FieldCfg& cfg, const RenderPar
                                          yg, yb, sg);
             } else {
                 const float* Wg = p.packed + (size_t)k * PK_FLOATS;
-                if (FOLD) fold_sh_bias(Wg, shv, lane, cbg);
+                if (FOLD && !cbg_holds(folded, k)) {
+                    fold_sh_bias(Wg, shv, lane, cbg);
+                    folded = cbg_set(folded, k);
+                }
                 field_tile<INTERP, FOLD>(Wg, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbg, lane, yr,
                                          yg, yb, sg);
             }
@@ -1405,7 +1416,10 @@ __device__ __forceinline__ void slots_field(const FieldCfg& cfg, const RenderPar
                 r = g = b = sg = 0.0f;
     #else
                 const float* Wg = p.packed + (size_t)k * PK_FLOATS;
-                if (FOLD) fold_sh_bias(Wg, shv, lane, cbg);
+                if (FOLD && !cbg_holds(folded, k)) {
+                    fold_sh_bias(Wg, shv, lane, cbg);
+                    folded = cbg_set(folded, k);
+                }
                 field_tile<INTERP, FOLD>(Wg, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbg, lane, r, g,
                                          b, sg);
     #endif
@@ -1432,16 +1446,19 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
     // colour layer 0 runs folded, wherever its weights are read from: a ray's arithmetic must not depend on
     // which experts its workgroup round keeps in LDS -- that choice depends on the other rays of the batch)
     __shared__ __attribute__((aligned(16))) float cbuf[FOLD ? (ACN_SLOTS_THREADS / 64) * 3 * 64 : 4];
-    __shared__ int cnt[kMaxK];
-    __shared__ int slot_k[2], restage[2];
+    // per-round expert counts, three buffers by round index: round q counts into cnt[q % 3], every wave reads
+    // that buffer after the round's barrier, and thread 0 clears cnt[(q + 2) % 3] (read in round q - 1, before
+    // this barrier; written again in round q + 2, after the next one) -- one barrier per round, not three
+    __shared__ int cnt[3][kMaxK];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     float* cb = FOLD ? cbuf + wave * 3 * 64 : nullptr;
     float* cbg = FOLD ? cb + 2 * 64 : nullptr;
     const float step = 1.0f / (float)(p.S - 1);
-    if (threadIdx.x < kMaxK) cnt[threadIdx.x] = 0;
-    if (threadIdx.x < 2) slot_k[threadIdx.x] = -1;
+    if (threadIdx.x < 3 * kMaxK) (&cnt[0][0])[threadIdx.x] = 0;
     __syncthreads();
+    // the two LDS slots' experts: wave-uniform registers, updated identically by every wave from the counts
+    int sk0 = -1, sk1 = -1, rbuf = 0;
     const int64_t waves_per_wg = blockDim.x >> 6;
     // XCD bands (as render_kernel): with the grid a multiple of 8, XCD x walks the x-th contiguous
     // eighth of the rays, so a frame's neighbouring rays share one L2 (ACN_SLOTS_BAND=0: interleaved)
@@ -1461,40 +1478,44 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
         if (live) { SL_MARK(ray, 0) }
         const uint32_t m = ray_expert_mask(cfg, ROUTE, p, ray, live, step, lane);
         if (live) { SL_MARK(ray, 1) }
+        int* cq = cnt[rbuf];
         if (lane == 0)
             for (int k = 0; k < cfg.K; ++k)
-                if ((m >> k) & 1u) atomicAdd(&cnt[k], 1);
-        __syncthreads();
-        if (threadIdx.x == 0) {
+                if ((m >> k) & 1u) atomicAdd(&cq[k], 1);
+        __syncthreads();   // this round's counts complete; every wave is done with the previous round's slots
+        {
+            // the two most needed experts (the same choice in every wave: same counts, same slot state)
             int b0 = -1, b1 = -1;
             for (int k = 0; k < cfg.K; ++k) {
-                const int c = cnt[k];
+                const int c = cq[k];
                 if (c == 0) continue;
-                if (b0 < 0 || c > cnt[b0]) { b1 = b0; b0 = k; }
-                else if (b1 < 0 || c > cnt[b1]) b1 = k;
+                if (b0 < 0 || c > cq[b0]) { b1 = b0; b0 = k; }
+                else if (b1 < 0 || c > cq[b1]) b1 = k;
             }
-            for (int k = 0; k < cfg.K; ++k) cnt[k] = 0;
+            b0 = __builtin_amdgcn_readfirstlane(b0);
+            b1 = __builtin_amdgcn_readfirstlane(b1);
+            const int rclear = rbuf == 0 ? 2 : rbuf - 1;   // (q + 2) % 3
+            if (threadIdx.x < kMaxK) cnt[rclear][threadIdx.x] = 0;
+            rbuf = rbuf == 2 ? 0 : rbuf + 1;
             // keep an expert in the slot it already occupies
-            int want[2] = {b0, b1};
-            if (want[0] == slot_k[1] || want[1] == slot_k[0]) { const int t = want[0]; want[0] = want[1]; want[1] = t; }
-            for (int sl = 0; sl < 2; ++sl) {
-                restage[sl] = (want[sl] >= 0 && want[sl] != slot_k[sl]) ? 1 : 0;
-                if (want[sl] >= 0) slot_k[sl] = want[sl];
+            if (b0 == sk1 || b1 == sk0) { const int t = b0; b0 = b1; b1 = t; }
+            const bool rs0 = b0 >= 0 && b0 != sk0, rs1 = b1 >= 0 && b1 != sk1;
+            if (b0 >= 0) sk0 = b0;
+            if (b1 >= 0) sk1 = b1;
+            if (rs0 || rs1) {   // block-uniform
+                for (int sl = 0; sl < 2; ++sl) {
+                    if (sl == 0 ? !rs0 : !rs1) continue;
+                    const f32x4* src = reinterpret_cast<const f32x4*>(p.packed + (size_t)(sl == 0 ? sk0 : sk1) * PK_FLOATS);
+                    f32x4* dst = reinterpret_cast<f32x4*>(smem + sl * PK_FLOATS);
+                    for (int i = threadIdx.x; i < PK_FLOATS / 4; i += blockDim.x) dst[i] = src[i];
+                }
+                __syncthreads();
             }
         }
-        __syncthreads();
-        for (int sl = 0; sl < 2; ++sl) {
-            if (restage[sl]) {
-                const f32x4* src = reinterpret_cast<const f32x4*>(p.packed + (size_t)slot_k[sl] * PK_FLOATS);
-                f32x4* dst = reinterpret_cast<f32x4*>(smem + sl * PK_FLOATS);
-                for (int i = threadIdx.x; i < PK_FLOATS / 4; i += blockDim.x) dst[i] = src[i];
-            }
-        }
-        __syncthreads();
 #if ACN_DIAG_NOSLOTS  // diagnostic build only: every expert from global memory
         const int k0 = -1, k1 = -1;
 #else
-        const int k0 = __builtin_amdgcn_readfirstlane(slot_k[0]), k1 = __builtin_amdgcn_readfirstlane(slot_k[1]);
+        const int k0 = sk0, k1 = sk1;
 #endif
         if (live) { SL_MARK(ray, 2) }
         if (live) {

@@ -3,7 +3,7 @@
 # divisions): render parity suites, C3 / C4 lines, section profile
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r05ab; mkdir -p $O
+O=gpurun_out/r05ad; mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests/test_render_ws.py tests/test_k8.py tests/test_batch_independence.py tests/test_determinism_gpu.py tests/test_gpu_kernels.py tests/test_parallel.py tests/test_expert_parallel.py tests/test_train.py tests/test_routed_glue.py -q -m gpu -x --timeout 300 --timeout-method thread > $O/parity.log 2>&1 || { tail -30 $O/parity.log; exit 1; }
 tail -1 $O/parity.log
 run() { tag=$1; shift; timeout -k 10 300 python -u bench.py "$@" > $O/$tag.json 2>$O/$tag.err || { echo "bench $tag failed"; tail -5 $O/$tag.err; exit 2; }
