@@ -968,6 +968,7 @@ __device__ __forceinline__ void render_ray(const RenderParams& p, const BgArgs& 
         const uint64_t dA = __builtin_amdgcn_s_memtime();
 #endif
         field(sc, px, py, pz, shv, folded, yr, yg, yb, ys);
+        if (s0 == 0) { SL_MARK(ray, 3) }
 #if ACN_DIAG_PHASE
         const uint64_t dB = __builtin_amdgcn_s_memtime();
         const uint32_t dS = __builtin_amdgcn_readfirstlane((uint32_t)g_diag_stamp[wave]);

@@ -1,7 +1,8 @@
 """Per-ray section timings of render_slots_kernel (C4 frame at S = 96 and 256, C3 batch) from its
 ACN_SLOTS_PROF=1 build (tools/build_variants.sh slprof:render.hip:"-DACN_SLOTS_PROF=1"; run with
 ACNERF_LIB=build_variants/libacnerf_slprof.so).  Lane 0 of each ray's wave stamps wall_clock64() (100 MHz) at:
-0 round start, 1 after ray_expert_mask, 2 after the round's slot choice / restage barriers, 4 after the tile loop,
+0 round start, 1 after ray_expert_mask, 2 after the round's slot choice / restage barriers, 3 after the first
+tile's field evaluation, 4 after the tile loop,
 5 after the ray's background / outputs.  Prints per-section medians and totals summed over rays."""
 import ctypes
 import os
@@ -28,7 +29,8 @@ def report(tag, n, ms):
     ok = (t[:, 0] > 0) & (t[:, 5] >= t[:, 0])
     t = t[ok]
     sec = {"mask": (t[:, 1] - t[:, 0]), "round barriers + restage": (t[:, 2] - t[:, 1]),
-           "tiles": (t[:, 4] - t[:, 2]), "background + outputs": (t[:, 5] - t[:, 4])}
+           "first tile (field only, folds included)": (t[:, 3] - t[:, 2]),
+           "later tiles + compositing": (t[:, 4] - t[:, 3]), "background + outputs": (t[:, 5] - t[:, 4])}
     tot = t[:, 5] - t[:, 0]
     line = ", ".join(f"{k} {np.median(v) / 100:.2f} us ({v.sum() / tot.sum():.1%})" for k, v in sec.items())
     print(f"{tag}: {t.shape[0]} rays, kernel {ms:.2f} ms | per ray median {np.median(tot) / 100:.2f} us | {line}",
