@@ -551,7 +551,7 @@ def _render_planned(model, rays: Tensor, S: int, group, batch: int, nb: int, sta
     # every batch's received counts of the owned experts, on the device in one copy
     rc_all = torch.tensor([[host[w][b][k] for w in range(world) for k in r.own] for b in range(nb)],
                           dtype=torch.int64).to(dev)
-    sent = 0
+    sent = evaluated = 0
     for b in range(nb):
         lo, hi = b * batch, min(n, (b + 1) * batch)
         counts = [host[w][b] for w in range(world)]
@@ -560,10 +560,14 @@ def _render_planned(model, rays: Tensor, S: int, group, batch: int, nb: int, sta
             rgb[lo:hi], depth[lo:hi], acc[lo:hi] = o[0], o[1], o[3]
             seen[b] = r.seg[K + 1: 2 * K + 1]
         sent += r.last_exchange["sent"]
+        evaluated += r.last_exchange["pairs_evaluated"]
     if n and not torch.equal(seen[: (n + batch - 1) // batch], plan[: (n + batch - 1) // batch]):
         raise AcnError("render_rays_ep_batched: a batch routed other pair counts than its plan")
     if stats is not None:
-        stats.update(sent=sent, live=sent, batches=nb)
+        # live: 24 B per pair this rank's rays actually routed (the device counts of every batch, independent of
+        # the split sizes the exchange used) + 16 B per pair it evaluated for the senders (their own plans, which
+        # each sender checks against its routed counts the same way)
+        stats.update(sent=sent, live=24 * int(seen.sum()) + 16 * evaluated, batches=nb)
     return rgb, depth, acc
 
 
