@@ -18,7 +18,7 @@ from test_train import P
 pytestmark = pytest.mark.gpu
 
 
-def _run(monkeypatch, composite, clip, precision="fp16x3", steps=4):
+def _run(monkeypatch, composite, clip, precision="fp16x3", steps=4, S=96):
     from test_module_api import build_model, reference_state_dict
     from adaptive_city_nerf_amd import ops
     from adaptive_city_nerf_amd import optim as O
@@ -26,9 +26,11 @@ def _run(monkeypatch, composite, clip, precision="fp16x3", steps=4):
     monkeypatch.setattr(RT, "FUSED_COMPOSITE", composite)
     monkeypatch.setattr(O, "FUSED_CLIP", clip)
     d = G.load("train_k8")
-    Pk = SimpleNamespace(**{**vars(P), "ray_samples": 96, "chunk_points": 4_000_000})
+    Pk = SimpleNamespace(**{**vars(P), "ray_samples": S, "chunk_points": 4_000_000})
+    g = torch.Generator().manual_seed(5)
     batches = [(torch.from_numpy(d[f"train{s}:rays"]).cuda(), torch.from_numpy(d[f"train{s}:rgbs"]).cuda(),
-                torch.from_numpy(d[f"train{s}:u"]).cuda()) for s in range(3)]
+                torch.from_numpy(d[f"train{s}:u"]).cuda() if S == 96 else torch.rand(1000, S, generator=g).cuda())
+               for s in range(3)]
     was = ops.TRAIN_MLP_PRECISION
     ops.set_train_mlp_precision(precision)
     torch.use_deterministic_algorithms(True)
@@ -72,4 +74,15 @@ def test_fused_composite_and_clip_bitwise_equal_separate_launches(monkeypatch, p
     assert mixed[0] == ref2[0]
     for n in mixed[2]:
         for a, b in zip(mixed[2][n], ref2[2][n]):
+            assert torch.equal(a, b), n
+
+
+def test_fused_composite_bitwise_equal_separate_launches_long_rays(monkeypatch):
+    """S = 200 (> 128): the fused kernel's blend backward reloads each sample's pair slots instead of keeping them
+    in registers; two steps and a ragged one, bitwise equal to the separate launches."""
+    fused = _run(monkeypatch, True, True, steps=3, S=200)
+    plain = _run(monkeypatch, False, False, steps=3, S=200)
+    assert fused[0] == plain[0], (fused[0], plain[0])
+    for n in fused[2]:
+        for a, b in zip(fused[2][n], plain[2][n]):
             assert torch.equal(a, b), n
