@@ -18,7 +18,7 @@ from test_train import P
 pytestmark = pytest.mark.gpu
 
 
-def _run(monkeypatch, composite, clip, precision="fp16x3", steps=4, S=96):
+def _run(monkeypatch, composite, clip, precision="fp16x3", steps=4, S=96, n_rays=1000):
     from test_module_api import build_model, reference_state_dict
     from adaptive_city_nerf_amd import ops
     from adaptive_city_nerf_amd import optim as O
@@ -28,9 +28,9 @@ def _run(monkeypatch, composite, clip, precision="fp16x3", steps=4, S=96):
     d = G.load("train_k8")
     Pk = SimpleNamespace(**{**vars(P), "ray_samples": S, "chunk_points": 4_000_000})
     g = torch.Generator().manual_seed(5)
-    batches = [(torch.from_numpy(d[f"train{s}:rays"]).cuda(), torch.from_numpy(d[f"train{s}:rgbs"]).cuda(),
-                torch.from_numpy(d[f"train{s}:u"]).cuda() if S == 96 else torch.rand(1000, S, generator=g).cuda())
-               for s in range(3)]
+    batches = [(torch.from_numpy(d[f"train{s}:rays"][:n_rays]).cuda(), torch.from_numpy(d[f"train{s}:rgbs"][:n_rays]).cuda(),
+                torch.from_numpy(d[f"train{s}:u"][:n_rays]).cuda() if S == 96 else
+                torch.rand(n_rays, S, generator=g).cuda()) for s in range(3)]
     was = ops.TRAIN_MLP_PRECISION
     ops.set_train_mlp_precision(precision)
     torch.use_deterministic_algorithms(True)
@@ -39,12 +39,13 @@ def _run(monkeypatch, composite, clip, precision="fp16x3", steps=4, S=96):
         m.load_state_dict(reference_state_dict(d, 8, "w:"))
         m = m.cuda().train()
         opt = O.build_optimizer(Pk, m)
-        st = RT.RoutedAdaptStep(Pk, m, 1000, opt, grad_clip=1.0, graph=False, jitter="given")
+        st = RT.RoutedAdaptStep(Pk, m, n_rays, opt, grad_clip=1.0, graph=False, jitter="given")
         losses, norms = [], []
         for i in range(steps):
             r, c, u = batches[i % 3]
             if i == steps - 1:          # a ragged batch through the same buffers
-                r, c, u = r[:613], c[:613], u[:613]
+                k = max(1, (613 * n_rays) // 1000)
+                r, c, u = r[:k], c[:k], u[:k]
             losses.append(float(st(r, c, jitter_u=u)))
             norms.append(st.last_norm.detach().cpu().clone())
         torch.cuda.synchronize()
@@ -82,6 +83,18 @@ def test_fused_composite_bitwise_equal_separate_launches_long_rays(monkeypatch):
     in registers; two steps and a ragged one, bitwise equal to the separate launches."""
     fused = _run(monkeypatch, True, True, steps=3, S=200)
     plain = _run(monkeypatch, False, False, steps=3, S=200)
+    assert fused[0] == plain[0], (fused[0], plain[0])
+    for n in fused[2]:
+        for a, b in zip(fused[2][n], plain[2][n]):
+            assert torch.equal(a, b), n
+
+
+@pytest.mark.parametrize("n_rays,S", [(5, 2), (7, 33), (3, 129)])
+def test_fused_composite_bitwise_equal_separate_launches_small_sizes(monkeypatch, n_rays, S):
+    """Edge sizes of the fused launch: a ray count that is not a multiple of the workgroup's 4 waves, the minimum
+    S = 2, a partial last 32-sample tile, and S just past 128 (the reload path); two steps, bitwise."""
+    fused = _run(monkeypatch, True, True, steps=2, S=S, n_rays=n_rays)
+    plain = _run(monkeypatch, False, False, steps=2, S=S, n_rays=n_rays)
     assert fused[0] == plain[0], (fused[0], plain[0])
     for n in fused[2]:
         for a, b in zip(fused[2][n], plain[2][n]):
