@@ -427,11 +427,15 @@ __device__ __forceinline__ float route_dist(const Cfg& cfg, int k, float px, flo
 struct RouteState {
     float thr, den;  // soft: bm * min dist, sum of masked inverse distances
     int hard;        // hard: argmin
+    float thr2;      // soft: thr^2 (1 + 1e-3); a squared distance above it is outside the margin for sure
 };
+// A squared distance s > thr^2 (1 + 1e-3) (the products rounded ~1e-7 relative) has fl(sqrt(s)) > thr -- sqrt is
+// correctly rounded and monotonic -- so its expert is outside the margin (w = 0 exactly) without the square root.
+__device__ __forceinline__ float route_thr2(float thr) { return (thr * thr) * 1.001f; }
 
 template <int ROUTE, typename Cfg>
 __device__ __forceinline__ RouteState route_prep(const Cfg& cfg, float px, float py, float pz) {
-    RouteState st{0.0f, 0.0f, 0};
+    RouteState st{0.0f, 0.0f, 0, 0.0f};
     if (ROUTE == 1) {
         // min_k max(sqrt(s_k), 1e-6) = max(sqrt(min_k s_k), 1e-6) (monotonic): one square root, not K
         float mins = INFINITY;
@@ -439,9 +443,12 @@ __device__ __forceinline__ RouteState route_prep(const Cfg& cfg, float px, float
         float mind = sqrtf(mins);
         mind = mind < 1e-6f ? 1e-6f : mind;
         st.thr = cfg.bm * mind;
+        st.thr2 = route_thr2(st.thr);
         float den = 0.0f;
         for (int k = 0; k < cfg.K; ++k) {
-            float d = route_dist(cfg, k, px, py, pz);
+            const float s2 = route_dist2(cfg, k, px, py, pz);
+            if (s2 > st.thr2) continue;   // outside the margin: adds 0
+            float d = sqrtf(s2);
             d = d < 1e-6f ? 1e-6f : d;
             den = den + ((d <= st.thr) ? 1.0f / d : 0.0f);
         }
@@ -459,7 +466,9 @@ __device__ __forceinline__ RouteState route_prep(const Cfg& cfg, float px, float
 template <typename Cfg>
 __device__ __forceinline__ float route_weight(const Cfg& cfg, const RouteState& st, int k, float px, float py,
                                               float pz) {
-    float d = route_dist(cfg, k, px, py, pz);
+    const float s2 = route_dist2(cfg, k, px, py, pz);
+    if (s2 > st.thr2) return 0.0f;   // = 0 / den
+    float d = sqrtf(s2);
     d = d < 1e-6f ? 1e-6f : d;
     return ((d <= st.thr) ? 1.0f / d : 0.0f) / st.den;
 }

@@ -1281,7 +1281,8 @@ constexpr uint32_t kSingleRay = 1u << 31;
 // (den >= 1e-6 and finite), and is exactly 0 or 1 on every expert when at most one finite d_k is inside
 // the margin and, if one is, (1/d_k) / max(1/d_k, 1e-6) == 1 (den is then 0 + 1/d_k: the other terms
 // add +0).  With two or more inside, the ray has two bits and is never a single-expert ray, so its
-// exactness does not matter.  K + 1 square roots per sample instead of 3K plus 3K divisions.
+// exactness does not matter.  One square root per sample for the minimum, and one per expert near the margin
+// only (route_thr2), instead of 3K square roots and 3K divisions.
 __device__ __forceinline__ void soft_route_bits(const FieldCfg& cfg, float px, float py, float pz, uint32_t& m,
                                                 bool& exact) {
     // min_k max(sqrt(max(s_k, 0)), 1e-6) = max(sqrt(min_k max(s_k, 0)), 1e-6): sqrt and the clamps are
@@ -1290,11 +1291,13 @@ __device__ __forceinline__ void soft_route_bits(const FieldCfg& cfg, float px, f
     for (int k = 0; k < cfg.K; ++k) mins = fminf(mins, route_dist2(cfg, k, px, py, pz));
     float mind = sqrtf(mins);
     mind = mind < 1e-6f ? 1e-6f : mind;
-    const float thr = cfg.bm * mind;
+    const float thr = cfg.bm * mind, thr2 = route_thr2(thr);
     int cnt = 0;
     float dsel = 1.0f;
     for (int k = 0; k < cfg.K; ++k) {
-        float d = route_dist(cfg, k, px, py, pz);
+        const float s2 = route_dist2(cfg, k, px, py, pz);
+        if (s2 > thr2) continue;   // outside the margin (route_thr2)
+        float d = sqrtf(s2);
         d = d < 1e-6f ? 1e-6f : d;
         if (d <= thr && d < INFINITY) {
             m |= 1u << k;
