@@ -2,7 +2,7 @@
 # round 5 closing run on the final build: full GPU suite, smoke, and the render / C5 bench lines
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r05fin; mkdir -p $O
+O=gpurun_out/r05fin2; mkdir -p $O
 timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $O/suite.log 2>&1; rc=$?
 tail -1 $O/suite.log
 [ $rc -eq 0 ] || exit 1
