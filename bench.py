@@ -358,12 +358,12 @@ def load_traffic(name: str = "render", rnd: str = "r01"):
 def render_traffic_profile(workload: str, S: int, layout: str):
     """Counter summary of the render line's dominant kernel (tools/pmc_r04.sh + tools/pmc_fold_r04.py: separate
     rocprofv3 --pmc passes, FETCH_SIZE doubled per the gfx950 correction of MI355X_MICROARCH.md 'HBM', plus
-    WRITE_SIZE) -- round 5 for C2 / C3 (the final render build), round 4 for C4 (the same slots kernel) -- or None
+    WRITE_SIZE) -- round 5, the final render build -- or None
     when no profile of this exact configuration is committed."""
     name = {("c2", 256, "replicated"): "r05_pmc_c2_ws.json",
             ("c3", 256, "replicated"): "r05_pmc_c3_slots.json",
-            ("c4", 96, "replicated"): "r04_pmc_c4s96_slots.json",
-            ("c4", 256, "replicated"): "r04_pmc_c4_slots.json"}.get((workload, S, layout))
+            ("c4", 96, "replicated"): "r05_pmc_c4s96_slots.json",
+            ("c4", 256, "replicated"): "r05_pmc_c4_slots.json"}.get((workload, S, layout))
     if name is None:
         return None
     p = REPO / "profiles" / name
