@@ -2,7 +2,7 @@
 # round 5: G rounds of render_slots_kernel per slot choice (one barrier per group): parity, then C3 / C4 A/B
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r05al; mkdir -p $O
+O=gpurun_out/r05am; mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests/test_render_ws.py tests/test_k8.py tests/test_batch_independence.py tests/test_determinism_gpu.py tests/test_gpu_kernels.py tests/test_parallel.py -q -m gpu -x --timeout 300 --timeout-method thread > $O/parity.log 2>&1 || { tail -30 $O/parity.log; exit 1; }
 tail -1 $O/parity.log
 for v in g4 g1 g2 g4b g1b; do
