@@ -367,6 +367,15 @@ __device__ __forceinline__ void layer64x64(const float* W, int seg, int btile, i
 #define ACN_HASH_DEPTH 2  // levels whose gathers are in flight together (1 = issue + wait per level)
 #endif
 
+#ifndef ACN_FIELD_CHECK
+#define ACN_FIELD_CHECK 0
+#endif
+#if ACN_FIELD_CHECK
+__device__ uint32_t g_fchk[3];   // diagnostic: tiles whose hash features differed between two evaluations, lane mask
+constexpr unsigned kFchkMax = 4096;
+__device__ float g_fchk_rec[40 * kFchkMax];
+__device__ unsigned g_fchk_n;
+#endif
 #if ACN_DIAG_PHASE  // diagnostic build only: per-wave timestamp taken right after the hash phase
 __shared__ uint64_t g_diag_stamp[16];
 #endif
@@ -433,7 +442,7 @@ __device__ __forceinline__ void hash_levels8(const ExpertMeta& em, int log2T, in
 // SHFIRST (with FOLD false): colour layer 0 runs unfolded on per-lane SH rows, the SH k-step before the
 // [sigma_raw, geo] one -- bit for bit the folded result of a ray whose lanes all carry its SH (the render of
 // compacted samples of several rays, ep_field_kernel)
-template <int INTERP, bool FOLD, bool SHFIRST = false>
+template <int INTERP, bool FOLD, bool SHFIRST = false, bool FCHK = false>
 __device__ __forceinline__ void field_tile(const float* W, const ExpertMeta& em, int log2T, float px, float py,
                                            float pz, const float (&shv)[8], const float* cb, int lane, float& rr,
                                            float& rg, float& rb, float& sraw) {
@@ -456,6 +465,33 @@ __device__ __forceinline__ void field_tile(const float* W, const ExpertMeta& em,
     for (int i = 0; i < 16; ++i) feat[i] = x0 * (float)(i + 1) - x1 + x2 * (float)i;
 #else
     hash_levels8<INTERP>(em, log2T, h, x0, x1, x2, feat);
+#endif
+#if ACN_FIELD_CHECK  // diagnostic build only: the hash encoding evaluated twice; differing lanes are counted
+    if constexpr (FCHK) {
+        float f2[16];
+        hash_levels8<INTERP>(em, log2T, h, x0, x1, x2, f2);
+        bool bad = false;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) bad |= __float_as_uint(f2[i]) != __float_as_uint(feat[i]);
+        const uint64_t bm = __ballot(bad);
+        if (bm && lane == 0) {
+            atomicAdd(&g_fchk[0], 1u);
+            atomicOr(&g_fchk[1], (uint32_t)bm);
+            atomicOr(&g_fchk[2], (uint32_t)(bm >> 32));
+        }
+        if (bad) {   // per differing lane: lane, table pointer, unit point, both feature vectors
+            const unsigned q = atomicAdd(&g_fchk_n, 1u);
+            if (q < kFchkMax) {
+                float* o = g_fchk_rec + 40 * q;
+                const uint64_t tp = (uint64_t)(uintptr_t)em.table;
+                o[0] = __uint_as_float((uint32_t)lane); o[1] = __uint_as_float((uint32_t)tp);
+                o[2] = __uint_as_float((uint32_t)(tp >> 32)); o[3] = x0; o[4] = x1; o[5] = x2;
+                o[6] = __uint_as_float((uint32_t)log2T); o[7] = __uint_as_float((uint32_t)h);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) { o[8 + i] = feat[i]; o[24 + i] = f2[i]; }
+            }
+        }
+    }
 #endif
 #if ACN_DIAG_PHASE
     {
@@ -1380,7 +1416,7 @@ __device__ __forceinline__ void slots_field(const FieldCfg& cfg, const RenderPar
                     fold_sh_bias(Wk, shv, lane, cbk);
                     folded |= 1u << sl;
                 }
-                field_tile<INTERP, FOLD>(Wk, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbk, lane, yr,
+                field_tile<INTERP, FOLD, false, ACN_FIELD_CHECK != 0>(Wk, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbk, lane, yr,
                                          yg, yb, sg);
             } else {
                 const float* Wg = p.packed + (size_t)k * PK_FLOATS;
@@ -1388,7 +1424,7 @@ __device__ __forceinline__ void slots_field(const FieldCfg& cfg, const RenderPar
                     fold_sh_bias(Wg, shv, lane, cbg);
                     folded = cbg_set(folded, k);
                 }
-                field_tile<INTERP, FOLD>(Wg, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbg, lane, yr,
+                field_tile<INTERP, FOLD, false, ACN_FIELD_CHECK != 0>(Wg, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbg, lane, yr,
                                          yg, yb, sg);
             }
             ys = trunc_exp(sg);
@@ -1413,7 +1449,7 @@ __device__ __forceinline__ void slots_field(const FieldCfg& cfg, const RenderPar
                     fold_sh_bias(Wk, shv, lane, cbk);
                     folded |= 1u << sl;
                 }
-                field_tile<INTERP, FOLD>(Wk, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbk, lane, r, g,
+                field_tile<INTERP, FOLD, false, ACN_FIELD_CHECK != 0>(Wk, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbk, lane, r, g,
                                          b, sg);
             } else {
     #if ACN_SLOTS_NOFALLBACK  // diagnostic only: non-resident experts skipped
@@ -1424,7 +1460,7 @@ __device__ __forceinline__ void slots_field(const FieldCfg& cfg, const RenderPar
                     fold_sh_bias(Wg, shv, lane, cbg);
                     folded = cbg_set(folded, k);
                 }
-                field_tile<INTERP, FOLD>(Wg, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbg, lane, r, g,
+                field_tile<INTERP, FOLD, false, ACN_FIELD_CHECK != 0>(Wg, cfg.ex[k], cfg.log2T, px, py, pz, shv, cbg, lane, r, g,
                                          b, sg);
     #endif
             }
@@ -3002,6 +3038,24 @@ extern "C" int acn_debug_cmblk_fetch(unsigned long long* host, int max_blocks) {
     const int m = max_blocks < 4096 ? max_blocks : 4096;
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_cmblk), (size_t)m * 4 * sizeof(unsigned long long)) == hipSuccess
                ? m : -1;
+}
+#endif
+#if ACN_FIELD_CHECK
+extern "C" int acn_debug_fchk_fetch(uint32_t* host) {
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fchk), 3 * sizeof(uint32_t)) != hipSuccess) return -1;
+    const uint32_t z[3] = {0u, 0u, 0u};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_fchk), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+// records of the differing lanes (40 floats each); returns how many were recorded, clears the count
+extern "C" int acn_debug_fchk_records(float* host, int max_records) {
+    unsigned n = 0;
+    if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_fchk_n), sizeof(n)) != hipSuccess) return -1;
+    n = n < kFchkMax ? n : kFchkMax;
+    const unsigned m = n < (unsigned)max_records ? n : (unsigned)max_records;
+    if (m && hipMemcpyFromSymbol(host, HIP_SYMBOL(g_fchk_rec), (size_t)m * 40 * sizeof(float)) != hipSuccess) return -1;
+    const unsigned z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_fchk_n), &z, sizeof(z)) != hipSuccess) return -1;
+    return (int)m;
 }
 #endif
 #if ACN_SLOTS_CHECK > 1

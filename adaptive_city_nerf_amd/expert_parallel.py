@@ -325,6 +325,7 @@ class ExpertParallelRenderer:
         self._graph_wanted = bool(graph)
         self.replays = 0
         self.owner = owner
+        _GRAPH_OWNERS.add(self)
         self.last_exchange = None    # bytes this rank sent in the last call: {"sent": .., "live": ..}
 
     def _run(self, n: int) -> None:
@@ -443,6 +444,16 @@ class ExpertParallelRenderer:
                 self.graph = g
         w = self.weights[:n] if self.weights is not None else None
         return self.rgb[:n], self.depth[:n], w, self.acc[:n]
+
+    def close(self) -> int:
+        """Destroy the captured graph (its RCCL resources go with it); the next full call captures again.
+        Returns 1 when a graph was released."""
+        if self.graph is None:
+            return 0
+        torch.cuda.synchronize(self.device)
+        self.graph.reset()
+        self.graph = None
+        return 1
 
     def overflowed(self) -> bool:
         """True when the last call's pairs of some expert exceeded the capacity (host read of the counts)."""
@@ -608,6 +619,44 @@ def render_image_expert_parallel(model, *, H: int, W: int, fx: float, fy: float,
 
 # ============================================================================ sync-free expert-parallel step
 FORCE_COLLECTIVES = False   # tests: the exchanges through the process group even at world size 1 (RCCL on one GPU)
+
+# Owners of HIP graphs that captured collectives (ExpertParallelRenderer / ExpertParallelAdaptStep).  RCCL ties a
+# communicator's resources to every graph that captured one of its collectives and releases them only when that
+# graph is destroyed; ncclCommDestroy waits for them, so destroy_process_group() (and the interpreter's exit
+# handlers that run it) never return while such a graph is alive.  shutdown() releases them first.
+import weakref as _weakref
+_GRAPH_OWNERS = _weakref.WeakSet()
+
+
+def release_collective_graphs() -> int:
+    """Destroy every live graph held by an ExpertParallelRenderer / ExpertParallelAdaptStep (they recapture on
+    their next full call).  Returns how many were released."""
+    n = 0
+    for o in list(_GRAPH_OWNERS):
+        n += o.close()
+    return n
+
+
+def shutdown(group=None, timeout: float = 120.0) -> bool:
+    """Release the collective-capturing graphs, synchronize, then destroy_process_group(group) -- bounded: a
+    teardown that does not return within ``timeout`` seconds is reported (False) instead of hanging the caller.
+    Reference: the process group's lifetime in scripts/create_clusters.py:224-238."""
+    import gc
+    import threading
+    release_collective_graphs()
+    gc.collect()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    done = threading.Event()
+
+    def _destroy():
+        dist.destroy_process_group(group)
+        done.set()
+    t = threading.Thread(target=_destroy, daemon=True, name="acn-pg-teardown")
+    t.start()
+    t.join(timeout)
+    return done.is_set()
+
 
 
 class _Comm:
@@ -841,6 +890,7 @@ class ExpertParallelAdaptStep:
         self.steps_done = 0
         self.graph = None
         self._eager_left = max(1, int(warmup)) if graph else 0
+        _GRAPH_OWNERS.add(self)
 
     def _set_caps(self, caps) -> None:
         """Per-expert segment capacities (identical on every rank) and the layouts / split sizes they imply."""
@@ -978,9 +1028,24 @@ class ExpertParallelAdaptStep:
             new = [max(a, b) for a, b in zip(new, self.caps)]
         self._set_caps(new)
         if self.graph is not None:
-            self.graph = None
+            self._drop_graph()
             self._eager_left = 1
             self.recaptures += 1
+
+    def _drop_graph(self) -> None:
+        torch.cuda.synchronize(self.device)
+        self.graph.reset()
+        self.graph = None
+
+    def close(self) -> int:
+        """Settle the last step (flush), then destroy the captured graph and its RCCL resources; the next full
+        step is captured again after one eager step.  Returns 1 when a graph was released."""
+        self.flush()
+        if self.graph is None:
+            return 0
+        self._drop_graph()
+        self._eager_left = 1
+        return 1
 
     def _capture(self) -> None:
         dev = self.device

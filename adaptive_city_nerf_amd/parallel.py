@@ -31,6 +31,9 @@ from torch import Tensor
 from .color_space import color_space_transformer
 
 
+FORCE_COLLECTIVES = False   # tests: the all-gather and the PSNR all-reduce through the group even at world size 1
+
+
 def _world_rank(group) -> Tuple[int, int]:
     if dist.is_available() and dist.is_initialized():
         return dist.get_world_size(group), dist.get_rank(group)
@@ -140,7 +143,7 @@ def gather_rendered(local: Tensor, plan: ShardPlan, group=None) -> Tensor:
     C = local.shape[1]
     buf = torch.zeros(plan.chunk, C, device=local.device, dtype=local.dtype)
     buf[: local.shape[0]] = local
-    if world == 1:
+    if world == 1 and not FORCE_COLLECTIVES:
         full = buf
     elif buf.is_cuda and dist.get_backend(group) == "gloo":
         # gloo has no device all-gather: stage through the host (tests run two ranks on one GPU this way)
@@ -159,7 +162,7 @@ def psnr_reduce(sse: float, count: float, device, group=None) -> float:
     """Global PSNR from per-rank sums: -10 log10(clamp_min(SSE/count, 1e-8)) (runtime_adapt.py:156-157)."""
     world, _ = _world_rank(group)
     t = torch.tensor([sse, count], dtype=torch.float64, device=device)
-    if world > 1:
+    if world > 1 or FORCE_COLLECTIVES:
         if t.is_cuda and dist.get_backend(group) == "gloo":
             t = t.cpu()
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)

@@ -1294,7 +1294,14 @@ def main():
                     line["amp_scaler"] = meta_scaler.state_dict()
         print(json.dumps(line))
     if world > 1:
-        dist.destroy_process_group()
+        # release every graph that captured an RCCL collective (--ep-graph), then destroy the group, bounded:
+        # RCCL's teardown waits for such graphs
+        from adaptive_city_nerf_amd.expert_parallel import shutdown
+        if not shutdown(timeout=120.0):
+            print(f"bench.py rank {rank}: destroy_process_group did not return within 120 s", file=sys.stderr,
+                  flush=True)
+            sys.stdout.flush()
+            os._exit(0)
 
 
 if __name__ == "__main__":
