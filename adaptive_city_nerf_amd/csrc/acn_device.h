@@ -97,50 +97,52 @@ __device__ __forceinline__ float lerp_t(float start, float end, float w) {
 }
 
 // models/encodings.py:27-81 components_from_spherical_harmonics, float32 op order of the torch
-// expressions (scalar * tensor evaluated left to right).
+// expressions (scalar * tensor evaluated left to right).  kz: an opaque +0.0f (c + 0.0f == c for every nonzero
+// coefficient) from callers inside a loop, so the coefficient pairs of packed multiplies are formed per call instead
+// of being hoisted out of the loop into VGPRs (render_ws_kernel spilled them); 0 elsewhere.
 template <int DEGREE>
-__device__ __forceinline__ void sh_components(float x, float y, float z, float* c) {
+__device__ __forceinline__ void sh_components(float x, float y, float z, float* c, float kz = 0.0f) {
     const float xx = x * x, yy = y * y, zz = z * z;
-    c[0] = 0.28209479177387814f;
+    c[0] = (0.28209479177387814f + kz);
     if (DEGREE > 0) {
-        c[1] = 0.4886025119029199f * y;
-        c[2] = 0.4886025119029199f * z;
-        c[3] = 0.4886025119029199f * x;
+        c[1] = (0.4886025119029199f + kz) * y;
+        c[2] = (0.4886025119029199f + kz) * z;
+        c[3] = (0.4886025119029199f + kz) * x;
     }
     if (DEGREE > 1) {
-        c[4] = (1.0925484305920792f * x) * y;
-        c[5] = (1.0925484305920792f * y) * z;
-        c[6] = 0.9461746957575601f * zz - 0.31539156525251999f;
-        c[7] = (1.0925484305920792f * x) * z;
-        c[8] = 0.5462742152960396f * (xx - yy);
+        c[4] = ((1.0925484305920792f + kz) * x) * y;
+        c[5] = ((1.0925484305920792f + kz) * y) * z;
+        c[6] = (0.9461746957575601f + kz) * zz - (0.31539156525251999f + kz);
+        c[7] = ((1.0925484305920792f + kz) * x) * z;
+        c[8] = (0.5462742152960396f + kz) * (xx - yy);
     }
     if (DEGREE > 2) {
-        c[9] = (0.5900435899266435f * y) * (3.0f * xx - yy);
-        c[10] = ((2.890611442640554f * x) * y) * z;
-        c[11] = (0.4570457994644658f * y) * (5.0f * zz - 1.0f);
-        c[12] = (0.3731763325901154f * z) * (5.0f * zz - 3.0f);
-        c[13] = (0.4570457994644658f * x) * (5.0f * zz - 1.0f);
-        c[14] = (1.445305721320277f * z) * (xx - yy);
-        c[15] = (0.5900435899266435f * x) * (xx - 3.0f * yy);
+        c[9] = ((0.5900435899266435f + kz) * y) * (3.0f * xx - yy);
+        c[10] = (((2.890611442640554f + kz) * x) * y) * z;
+        c[11] = ((0.4570457994644658f + kz) * y) * (5.0f * zz - (1.0f + kz));
+        c[12] = ((0.3731763325901154f + kz) * z) * (5.0f * zz - (3.0f + kz));
+        c[13] = ((0.4570457994644658f + kz) * x) * (5.0f * zz - (1.0f + kz));
+        c[14] = ((1.445305721320277f + kz) * z) * (xx - yy);
+        c[15] = ((0.5900435899266435f + kz) * x) * (xx - (3.0f + kz) * yy);
     }
     if (DEGREE > 3) {
-        c[16] = ((2.5033429417967046f * x) * y) * (xx - yy);
-        c[17] = ((1.7701307697799304f * y) * z) * (3.0f * xx - yy);
-        c[18] = ((0.9461746957575601f * x) * y) * (7.0f * zz - 1.0f);
-        c[19] = ((0.6690465435572892f * y) * z) * (7.0f * zz - 3.0f);
-        c[20] = 0.10578554691520431f * (((35.0f * zz) * zz - 30.0f * zz) + 3.0f);
-        c[21] = ((0.6690465435572892f * x) * z) * (7.0f * zz - 3.0f);
-        c[22] = (0.47308734787878004f * (xx - yy)) * (7.0f * zz - 1.0f);
-        c[23] = ((1.7701307697799304f * x) * z) * (xx - 3.0f * yy);
-        c[24] = 0.6258357354491761f * (xx * (xx - 3.0f * yy) - yy * (3.0f * xx - yy));
+        c[16] = (((2.5033429417967046f + kz) * x) * y) * (xx - yy);
+        c[17] = (((1.7701307697799304f + kz) * y) * z) * (3.0f * xx - yy);
+        c[18] = (((0.9461746957575601f + kz) * x) * y) * (7.0f * zz - (1.0f + kz));
+        c[19] = (((0.6690465435572892f + kz) * y) * z) * (7.0f * zz - (3.0f + kz));
+        c[20] = (0.10578554691520431f + kz) * (((35.0f * zz) * zz - (30.0f + kz) * zz) + (3.0f + kz));
+        c[21] = (((0.6690465435572892f + kz) * x) * z) * (7.0f * zz - (3.0f + kz));
+        c[22] = ((0.47308734787878004f + kz) * (xx - yy)) * (7.0f * zz - (1.0f + kz));
+        c[23] = (((1.7701307697799304f + kz) * x) * z) * (xx - (3.0f + kz) * yy);
+        c[24] = (0.6258357354491761f + kz) * (xx * (xx - (3.0f + kz) * yy) - yy * (3.0f * xx - yy));
     }
 }
 
 // SHEncoder.forward (encodings.py:144-151): d / norm(d).clamp_min(1e-9), then components
 template <int DEGREE>
-__device__ __forceinline__ void sh_encode(float dx, float dy, float dz, float* c) {
+__device__ __forceinline__ void sh_encode(float dx, float dy, float dz, float* c, float kz = 0.0f) {
     const float n = clamp_min_nan(norm3(dx, dy, dz), 1e-9f);
-    sh_components<DEGREE>(dx / n, dy / n, dz / n, c);
+    sh_components<DEGREE>(dx / n, dy / n, dz / n, c, kz);
 }
 
 // One level of HashGridEncoder._torch_forward split in two halves so that callers can keep the
@@ -318,6 +320,49 @@ __device__ __forceinline__ void hash_issue_x(__amdgpu_buffer_rsrc_t rs, uint32_t
     p.sel = sel;
 }
 
+// Buffer-resource form of hash_issue, one 8-byte gather per corner (the render's default, ACN_XPAIR == 3): the
+// row offsets are 32-bit (lvbase + 8 * row from the expert's table base in the resource), so no 64-bit address
+// is formed per corner.  The gathers of the global-address form (hash_issue) returned a wrong row to lanes 48-63
+// of one level now and then inside the render kernels; this form never did.
+template <int INTERP>
+__device__ __forceinline__ void hash_issue_b(__amdgpu_buffer_rsrc_t rs, uint32_t lvbase, float sx, float sy, float sz,
+                                             uint32_t mask, HashPending& p) {
+    auto ld = [&](uint32_t row) {
+        const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(rs, lvbase + (row << 3), 0, 0);
+        return make_float2(__uint_as_float(v[0]), __uint_as_float(v[1]));
+    };
+    if (INTERP == 0) {
+        const uint32_t ix = (uint32_t)(int)rintf(sx), iy = (uint32_t)(int)rintf(sy), iz = (uint32_t)(int)rintf(sz);
+        p.f[0] = ld((ix ^ (iy * kP1) ^ (iz * kP2)) & mask);
+        return;
+    }
+    const float fx = floorf(sx), fy = floorf(sy), fz = floorf(sz);
+    float wx = sx - fx, wy = sy - fy, wz = sz - fz;
+    const uint32_t x0 = (uint32_t)(int)fx;
+    const uint32_t y0 = (uint32_t)(int)fy * kP1, y1 = y0 + kP1;
+    const uint32_t z0 = (uint32_t)(int)fz * kP2, z1 = z0 + kP2;
+    const uint32_t x1 = x0 + 1u;
+    if (INTERP == 2) {   // the constants offset by an opaque +0.0f: formed here, not hoisted into VGPR pairs
+        float k3 = 3.0f, k2 = 2.0f;
+        asm volatile("" : "+s"(k3), "+s"(k2));
+        wx = (wx * wx) * (k3 - k2 * wx);
+        wy = (wy * wy) * (k3 - k2 * wy);
+        wz = (wz * wz) * (k3 - k2 * wz);
+    }
+    const uint32_t a00 = y0 ^ z0, a01 = y0 ^ z1, a10 = y1 ^ z0, a11 = y1 ^ z1;
+    p.f[0] = ld((x0 ^ a00) & mask);
+    p.f[1] = ld((x1 ^ a00) & mask);
+    p.f[2] = ld((x0 ^ a01) & mask);
+    p.f[3] = ld((x1 ^ a01) & mask);
+    p.f[4] = ld((x0 ^ a10) & mask);
+    p.f[5] = ld((x1 ^ a10) & mask);
+    p.f[6] = ld((x0 ^ a11) & mask);
+    p.f[7] = ld((x1 ^ a11) & mask);
+    p.wx = wx;
+    p.wy = wy;
+    p.wz = wz;
+}
+
 template <int INTERP>
 __device__ __forceinline__ void hash_finish_x(const HashPendingX& p, float& o0, float& o1) {
     HashPending h;
@@ -474,9 +519,9 @@ __device__ __forceinline__ float route_weight(const Cfg& cfg, const RouteState& 
 }
 
 // colour-branch direction encoding (meta_ngp.py:165-168 then encodings.py:144-151)
-__device__ __forceinline__ void dir_sh(float dx, float dy, float dz, float (&sh)[16]) {
+__device__ __forceinline__ void dir_sh(float dx, float dy, float dz, float (&sh)[16], float kz = 0.0f) {
     const float n = clamp_min_nan(norm3(dx, dy, dz), 1e-9f);
-    sh_encode<3>(dx / n, dy / n, dz / n, sh);
+    sh_encode<3>(dx / n, dy / n, dz / n, sh, kz);
 }
 
 // t value of sample s (stratified_t_vals, ray_rendering.py:278-287); linspace as torch CPU

@@ -29,6 +29,10 @@ using namespace acn;
 #define ACN_SLOTS 1  // routed K > 2: stage the two most needed experts per workgroup (render_slots_kernel)
 #endif
 
+#ifndef ACN_XPAIR
+#define ACN_XPAIR 2  // hash gathers: 2 buffer loads of x-paired 16-B blocks (default); 3 buffer loads,
+                     // one 8-B row per corner; 0 global loads from 64-bit addresses (round 5: wrong rows in lanes 48-63)
+#endif
 #ifndef ACN_LEVEL_PARITY
 #define ACN_LEVEL_PARITY 0  // 1: half h encodes levels 2i+h (instruction i = two adjacent levels)
 #endif
@@ -388,7 +392,7 @@ __device__ __forceinline__ int level_of(int i, int h) { return ACN_LEVEL_PARITY 
 template <int INTERP>
 __device__ __forceinline__ void hash_levels8(const ExpertMeta& em, int log2T, int h, float x0, float x1, float x2,
                                              float (&feat)[16]) {
-    constexpr int D = ACN_HASH_DEPTH;
+    constexpr int D = INTERP == 2 ? 1 : ACN_HASH_DEPTH;   // Smoothstep: one level in flight (its spill-free depth)
     const uint32_t mask = (uint32_t)((1ull << log2T) - 1ull);
 #if ACN_XPAIR == 2
     if (INTERP != 0) {
@@ -414,10 +418,19 @@ __device__ __forceinline__ void hash_levels8(const ExpertMeta& em, int log2T, in
     }
 #endif
     HashPending pend[D];
+#if ACN_XPAIR == 3
+    // the expert's 16 level tables (F = 2) in one buffer resource: level lv starts at byte lv << (log2T + 3)
+    const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)em.table, (short)0, (int)(uint32_t)((16ull << log2T) * 8ull), 0x00020000);
+#endif
     auto issue = [&](int i, HashPending& pp) {
         const int lv = level_of(i, h);
         const float res = (float)(ACN_LEVEL_PARITY ? (h ? em.res[2 * i + 1] : em.res[2 * i])
                                                    : (h ? em.res[8 + i] : em.res[i]));
+#if ACN_XPAIR == 3
+        hash_issue_b<INTERP>(rsb, (uint32_t)lv << (log2T + 3), x0 * res, x1 * res, x2 * res, mask, pp);
+        return;
+#endif
         const float2* tl = reinterpret_cast<const float2*>(em.table) + ((size_t)lv << log2T);
         if (i >= ACN_FINE_FROM)
             hash_issue<INTERP, ACN_FINE_POL>(tl, x0 * res, x1 * res, x2 * res, mask, pp);
@@ -888,8 +901,11 @@ __device__ __forceinline__ void background(const BgArgs& bg, float dx, float dy,
     if (bg.mode != ACN_BG_MLP) { out[0] = out[1] = out[2] = 0.0f; return; }
     const float n = clamp_min_nan(norm3(dx, dy, dz), 1e-12f);
     float sh[16];
-    sh_encode<3>(dx / n, dy / n, dz / n, sh);
+    sh_encode<3>(dx / n, dy / n, dz / n, sh, __int_as_float(opaque_s(0)));   // +0.0f, opaque (acn_device.h)
     float hv = 0.0f;
+    // an opaque lane index: the per-lane weight addresses below are formed here, per call, not hoisted out of
+    // the callers' ray loops by LICM (four 64-bit addresses held across render_ws_kernel's loop spilled)
+    lane = opaque_v(lane);
     if (lane < bg.hidden) {
         float s = 0.0f;
         for (int k = 0; k < 16; ++k) s = fmaf(sh[k], bg.w1[lane * 16 + k], s);
@@ -1194,7 +1210,6 @@ __global__ void __launch_bounds__(1024, 4) render_ws_kernel(FieldCfg cfg, BgArgs
     __shared__ int done[16];
     stage_weights<1>(smem, p.packed);
     const float* W = smem;
-    const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     float* cb = FOLD ? cbuf + wave * 64 : nullptr;
     const int S = p.S;
@@ -1214,16 +1229,21 @@ __global__ void __launch_bounds__(1024, 4) render_ws_kernel(FieldCfg cfg, BgArgs
         stride = (int64_t)gridDim.x * 16;
     }
     for (; base < hi; base += stride) {   // block-uniform
+        // the lane index re-derived per round through an opaque copy: the per-lane LDS addresses and constants
+        // formed from it stay inside the loop instead of being hoisted into registers held across it (spilled)
+        const int tid = opaque_v((int)threadIdx.x);
+        const int lane = tid & 63, j = lane & 31, h = lane >> 5;
+        const float kz = __int_as_float(opaque_s(0));   // +0.0f for the SH coefficients (acn_device.h)
         const int nr = (int)min((int64_t)16, hi - base);
-        if (threadIdx.x == 0) qhead = 0;
-        if (threadIdx.x < 16) done[threadIdx.x] = 0;
+        if (tid == 0) qhead = 0;
+        if (tid < 16) done[tid] = 0;
         constexpr bool PRE = FOLD && ACN_WS_PREFOLD;
         if (PRE && wave < nr) {
             // wave w folds round slot w's colour bias into cbuf[w] once; every tile of that ray reads it there
             const int64_t r0 = p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[base + wave]) : base + wave;
             const float* rp = p.rays + r0 * 8;
             float sh[16], sv[8];
-            dir_sh(rp[3], rp[4], rp[5], sh);
+            dir_sh(rp[3], rp[4], rp[5], sh, kz);
             sh_rows_for_half(sh, h, sv);
             fold_sh_bias(W, sv, lane, cbuf + wave * 64);
         }
@@ -1247,7 +1267,7 @@ __global__ void __launch_bounds__(1024, 4) render_ws_kernel(FieldCfg cfg, BgArgs
                 jit = p.jitter ? p.jitter + ray * S : nullptr;
                 if (!PRE || ACN_WS_CHECK) {
                     float sh[16];
-                    dir_sh(dx, dy, dz, sh);
+                    dir_sh(dx, dy, dz, sh, kz);
                     sh_rows_for_half(sh, h, shv);
                     if (!PRE) folded = 0u;
                 }
@@ -1640,11 +1660,12 @@ __global__ void __launch_bounds__(kRtThreads, 4) ep_field_kernel(FieldCfg cfg, c
                                                                   float* __restrict__ ret) {
     __shared__ __attribute__((aligned(16))) float Wsl[PK_FLOATS];
     __shared__ int64_t pre[kEpMaxSeg];   // cap == 0 (compact layout): start of segment (w, e), row-major
-    const int tid = threadIdx.x, lane = tid & 63, j = lane & 31, h = lane >> 5;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // lane from mbcnt (re-derivable anywhere): threadIdx.x is not held across the expert loop (it was spilled)
+    const int lane = (int)__lane_id(), j = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t G = (int64_t)gridDim.x * kRtWaves;
     const bool compact = cap == 0;
-    if (compact && tid == 0) {
+    if (compact && wave == 0 && lane == 0) {
         int64_t o = 0;
         for (int q = 0; q < W * E; ++q) {
             pre[q] = o;
@@ -1665,7 +1686,8 @@ __global__ void __launch_bounds__(kRtThreads, 4) ep_field_kernel(FieldCfg cfg, c
             __syncthreads();   // every wave is done with the previous expert's image
             const f32x4* src = reinterpret_cast<const f32x4*>(packed + (size_t)e * PK_FLOATS);
             f32x4* dst = reinterpret_cast<f32x4*>(Wsl);
-            for (int i = tid; i < PK_FLOATS / 4; i += kRtThreads) dst[i] = src[i];
+            // opaque thread index: the unrolled copy's per-lane offsets are formed here, not held across the loop
+            for (int i = opaque_v(wave * 64 + (int)__lane_id()); i < PK_FLOATS / 4; i += kRtThreads) dst[i] = src[i];
             __syncthreads();
             slot = e;
         }
