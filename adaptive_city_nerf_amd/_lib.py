@@ -208,14 +208,31 @@ def lib():
                                f"adaptive_city_nerf_amd/csrc)")
             L = C.CDLL(str(LIB_PATH))
             variant = "ACNERF_LIB" in os.environ   # a developer build (tools/build_variants.sh) may predate an entry
+            missing = []
             for name, (args, res) in SIGNATURES.items():
                 if variant and not hasattr(L, name):
+                    missing.append(name)
                     continue
                 fn = getattr(L, name)
                 fn.argtypes = args
                 fn.restype = res
+            if missing:
+                _disable_fused_paths(missing)
             _lib = L
     return _lib
+
+
+def _disable_fused_paths(missing) -> None:
+    """A variant library without the fused entry points the defaults select: switch those paths off, loudly,
+    instead of failing later with an AttributeError."""
+    import warnings
+    from . import optim, routed_train
+    if "acn_grad_clip_slots" in missing and optim.FUSED_CLIP:
+        optim.FUSED_CLIP = False
+        warnings.warn(f"{LIB_PATH} lacks acn_grad_clip_slots: FUSED_CLIP switched off")
+    if "acn_routed_composite_mse_train" in missing and routed_train.FUSED_COMPOSITE:
+        routed_train.FUSED_COMPOSITE = False
+        warnings.warn(f"{LIB_PATH} lacks acn_routed_composite_mse_train: FUSED_COMPOSITE switched off")
 
 
 def exported_symbols():

@@ -1918,8 +1918,10 @@ __global__ void __launch_bounds__(256) volume_render_bwd_kernel(
 //   rgb = volume_render(rs, t, bg) (ray_rendering.py:137-165), the linear-space MSE's gradient
 //         (mse_linear_bwd_kernel; losses.py:10-32), volume_render's backward (vr_bwd_ray) and the blend's
 //         backward into the pair slots (blend_bwd_kernel; padding slots below the live count get zeros)
-// -- the arithmetic of those kernels, in one launch instead of eight.  The reported loss: a double sum per
-// workgroup in ray order, the last workgroup to finish adds the G partials in index order (deterministic).
+// -- the arithmetic of those kernels, in one launch instead of eight (the gradients bitwise those kernels').  The
+// reported loss: a double sum per workgroup in ray order, the last workgroup to finish adds the G partials in index
+// order (deterministic; mse_linear_fwd_ws sums element-strided, so the two losses agree after the float cast at the
+// tested sizes, not by construction).
 constexpr int kCmThreads = 256;
 constexpr int kCmMaxBlocks = 4096;
 #ifndef ACN_CM_PROF

@@ -359,7 +359,7 @@ class ExpertParallelRenderer:
                                  C.byref(self.bg_spec), 1.0, 0.0, ptr(self.rgb), ptr(self.depth), ptr(self.weights),
                                  ptr(self.acc), s), "acn_ep_composite")
 
-    def _run_planned(self, n: int, counts, recv_cnt: Tensor) -> None:
+    def _run_planned(self, n: int, counts, recv_cnt: Tensor, pack: bool = True) -> None:
         """One batch with the exchange sized by ``counts`` (host (W, K) ints: every rank's pair counts of this
         batch, the capacities of its segments): compact layouts on both sides, no padding slot crosses a link.
         ``recv_cnt``: the (W, E) counts of the owned experts on the device (int64; read by the field kernel)."""
@@ -381,8 +381,9 @@ class ExpertParallelRenderer:
         recv = [sum(rc[w * E:(w + 1) * E]) for w in range(W)]
         ps, pr = sum(send), sum(recv)
         comm.all_to_all(self.recv_xd[:pr], self.xd[:ps], recv, send)
-        check(L.acn_pack_experts(self._own_arr, C.byref(self.own_routing), -1, ptr(self.packed),
-                                 self.packed.numel() * 4, s), "acn_pack_experts")
+        if pack:   # the owned experts' images: constant within a frame, packed by its first batch
+            check(L.acn_pack_experts(self._own_arr, C.byref(self.own_routing), -1, ptr(self.packed),
+                                     self.packed.numel() * 4, s), "acn_pack_experts")
         if pr > 0:
             from . import ops
             hook = ops.EVENT_HOOK   # bench.py timing (eager only: this path is never captured)
@@ -405,7 +406,7 @@ class ExpertParallelRenderer:
         self.last_exchange = {"sent": 24 * ps + 16 * pr, "live": 24 * ps + 16 * pr, "pairs_sent": ps,
                               "pairs_evaluated": pr}
 
-    def render_planned(self, rays: Tensor, counts, recv_cnt: Optional[Tensor] = None):
+    def render_planned(self, rays: Tensor, counts, recv_cnt: Optional[Tensor] = None, pack: bool = True):
         """As __call__, with the exchange sized by ``counts`` (host (W, K): every rank's pair counts of this batch,
         acn_routed_count_batches).  Eager (the split sizes change per batch); collective over the group.
         ``recv_cnt``: counts[w][own[e]] as a device int64 (W * E) tensor, if the caller already holds one."""
@@ -417,7 +418,7 @@ class ExpertParallelRenderer:
         if recv_cnt is None:   # a fresh device tensor per call: a reused pinned buffer could be rewritten before
             recv_cnt = torch.tensor([int(counts[w][k]) for w in range(self.W) for k in self.own],   # its copy ran
                                     dtype=torch.int64).to(self.device)
-        self._run_planned(n, counts, recv_cnt)
+        self._run_planned(n, counts, recv_cnt, pack)
         w = self.weights[:n] if self.weights is not None else None
         return self.rgb[:n], self.depth[:n], w, self.acc[:n]
 
@@ -566,7 +567,7 @@ def _render_planned(model, rays: Tensor, S: int, group, batch: int, nb: int, sta
     for b in range(nb):
         lo, hi = b * batch, min(n, (b + 1) * batch)
         counts = [host[w][b] for w in range(world)]
-        o = r.render_planned(rays[lo:hi] if hi > lo else dummy, counts, rc_all[b])
+        o = r.render_planned(rays[lo:hi] if hi > lo else dummy, counts, rc_all[b], pack=b == 0)
         if hi > lo:
             rgb[lo:hi], depth[lo:hi], acc[lo:hi] = o[0], o[1], o[3]
             seen[b] = r.seg[K + 1: 2 * K + 1]

@@ -67,7 +67,9 @@ ADAM_EARLY = os.environ.get("ACN_ADAM_EARLY", "0") != "0"   # measured slower (D
 BG_SIDE = os.environ.get("ACN_BG_SIDE", "0") != "0"   # measured within noise: off
 # The compositing glue of the step in one launch (acn_routed_composite_mse_train: blend, background forward,
 # compositing, the linear MSE and the backward of all three down to the pair outputs) instead of eight launches
-# and a copy; same arithmetic (tests/test_routed_glue.py compares the two bitwise)
+# and a copy; same arithmetic for every gradient (per-element; tests/test_routed_glue.py compares them bitwise).  The
+# loss is a double sum whose order differs (per ray per workgroup here, element-strided in mse_linear_fwd_ws): it is
+# equal after the float cast at the tested sizes, not by construction
 FUSED_COMPOSITE = os.environ.get("ACN_FUSED_COMPOSITE", "1") != "0"
 
 

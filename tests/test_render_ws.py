@@ -63,9 +63,11 @@ def test_work_shared_render_bitwise_equal_render_kernel(tag, active, S, jitter, 
     with torch.no_grad():
         new = ops.render_stratified(rays, S, specs, routing, active, bg[0], tau=0.0, jitter=jit)
         old = ops.render_stratified(rays, S, specs, routing, active, bg[0], tau=TAU_OLD, jitter=jit)
-    # strict: one differing ray fails.  The two one-off differences recorded in round 4 came from stale MFMA
-    # operands (v_cvt_pk_f16_f32 -> MFMA with 2 wait states, the fold had no pad at all); every fp16 B fragment
-    # now passes the operand fence (acn_device.h) and tools/hazard_audit.py checks the ISA
+    # strict: one differing ray fails.  The run-to-run differences of rounds 4-5 were hash-table gathers issued as
+    # global loads from 64-bit addresses returning a wrong row to lanes 48-63 of one level (the self-check builds'
+    # hash-feature records); the renders now gather through buffer loads with 32-bit offsets, which
+    # showed no wrong row in the same detectors.  tools/hazard_audit.py (tests/test_hazard_audit.py) checks the
+    # ISA's MFMA hazard classes separately.
     assert (msg := _mismatch(new, old, n)) is None, f"{tag} S={S} n={n} jitter={jitter}: {msg}"
 
 
