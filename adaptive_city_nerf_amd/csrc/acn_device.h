@@ -542,40 +542,25 @@ __device__ __forceinline__ float tval(float near, float far, int s, int S, const
     return lo + (hi - lo) * jit[s];
 }
 
-// ---- VALU -> MFMA operand fence.  The fp16 B fragments of every MLP layer are written by
-// v_cvt_pk_f16_f32 (VALU).  hipcc (ROCm 7.2) leaves the 2 wait states of its gfx950 VALU -> MFMA rule between
-// such a conversion and the MFMA reading it, and on MI355X that left rare, timing-dependent stale operands
-// (round 4: 16 columns of a tile off by ~1e-4; a 1-ulp render difference when the stale register held the
-// neighbouring ray's nearly equal value).  A pad placed by position is not enough: the compiler sinks the
-// last conversions past a scheduling barrier (tools/hazard_audit.py found 1031 such sites in render.hip).
-// So the fence takes the fragments as "+v" operands of ONE asm statement holding the pad: every conversion
-// must have retired into the fragments before it, every MFMA reads the asm's outputs after it, and the
-// audit checks that no VALU writes an MFMA A/B operand fewer than 16 wait states before it.
+// ---- VALU -> MFMA operand fence (round 5; OFF by default since round 6, §4l).  Round 5 took the
+// rare run-to-run differences of the renders (16 columns of one MFMA tile) for stale fp16 B operands and put every
+// B fragment through ONE asm statement holding 16 wait states.  Round 6 found their cause elsewhere: the hash-table
+// gathers, issued as global loads from 64-bit addresses, now and then returned a wrong row to lanes 48-63 of one
+// level (self-check records of the hash features); with the gathers on buffer loads the field repeats, the slots
+// self-check builds and the training-MLP repeats show no difference with or without the fence, and hipcc's own
+// padding (>= 2 wait states; the box probe needs 1) holds in every kernel (tests/test_hazard_audit.py).  The fence
+// cost the meta step 5%, so it is compiled out; -DACN_OPND_FENCE_ON restores it for A/B runs.
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-#ifndef ACN_OPND_FENCE
-#define ACN_OPND_FENCE 1   // 0: diagnostic build only, the fence compiled out (the round-4 state without its pad)
-#endif
-#if ACN_OPND_FENCE
+#ifdef ACN_OPND_FENCE_ON
 #define ACN_OPND_PAD "s_nop 7\n\ts_nop 7"
+#define ACN_OPND_SB0 __builtin_amdgcn_sched_barrier(0);
+#define ACN_OPND_ASM(...) asm volatile(__VA_ARGS__)
 #else
 #define ACN_OPND_PAD ""
-#endif
-#ifndef ACN_OPND_SB
-#define ACN_OPND_SB 1   // scheduling barriers around the fence (0: measured run-to-run differences in field_kernel)
-#endif
-#define ACN_OPND_CLOB
-#if ACN_OPND_SB
-#define ACN_OPND_SB0 __builtin_amdgcn_sched_barrier(0);
-#else
-#define ACN_OPND_SB0
-#endif
-#ifdef ACN_OPND_OFF   // diagnostic A/B builds only: no fence statement at all
-#undef ACN_OPND_SB0
 #define ACN_OPND_SB0
 #define ACN_OPND_ASM(...)
-#else
-#define ACN_OPND_ASM(...) asm volatile(__VA_ARGS__)
 #endif
+#define ACN_OPND_CLOB
 __device__ __forceinline__ void opnd_fence(f16x8& a) { ACN_OPND_SB0 ACN_OPND_ASM(ACN_OPND_PAD : "+v"(a) : ACN_OPND_CLOB); ACN_OPND_SB0 }
 __device__ __forceinline__ void opnd_fence(f16x8& a, f16x8& b) {
     ACN_OPND_SB0 ACN_OPND_ASM(ACN_OPND_PAD : "+v"(a), "+v"(b) : ACN_OPND_CLOB); ACN_OPND_SB0

@@ -4,8 +4,9 @@ Compiles render.hip and mlp_train.hip to gfx950 assembly with the Makefile's fla
 GPU) and runs tools/hazard_audit.py over every kernel: no MFMA may have a VALU write of its A / B / C operands, a
 reader or writer of its result, a partial-overlap accumulator or a write of its C operand within the wait states
 gfx950 requires (LLVM's gfx940 rules + 1, tools/hazard_audit.py REQ), counted along every control-flow path with
-inline-asm contents as the instructions they hold.  The round-5 operand fence is held to its own policy: 16 states
-between the fp16 conversion of a B fragment and its MFMA in the render."""
+inline-asm contents as the instructions they hold.  (The round-5 operand fence, 16 states before every fp16 B
+operand, is compiled out since round 6: the differences it was meant for came from the hash gathers, DESIGN.md §4l;
+the gap hipcc leaves, >= 2 states, is what the box probe requires, 1.)"""
 import os
 import re
 import shutil
@@ -54,13 +55,3 @@ def test_no_mfma_hazard_below_requirement(asm, src):
     assert counts["mfma"] > 1000, counts            # the kernels' MFMA code is there
     bad = {c: sites.get(c, [])[:3] for c in REQUIRED if sites.get(c)}
     assert not bad, f"{src}: MFMA hazard sites below requirement: {bad}"
-
-
-def test_render_operand_fence_policy(asm):
-    """Every VALU write of an MFMA A/B operand in the render kernels is >= 16 states before it (the fence)."""
-    import hazard_audit as H
-    funcs = H.parse(asm["render.hip"])
-    req = dict(H.REQ)
-    req["valu_ab"] = 16
-    sites, _, _ = H.audit(funcs, "", req)
-    assert not sites.get("valu_ab"), sites.get("valu_ab")[:3]
