@@ -233,6 +233,9 @@ __device__ __forceinline__ void hash_issue(const float2* __restrict__ tl, float 
 
 // FMA: c = fma(f1, w, f0 * (1 - w)) (one rounding fewer than the reference's f0*(1-w) + f1*w; used
 // by the fused field, whose outputs are compared within tolerance)
+#ifndef ACN_HASH_PK
+#define ACN_HASH_PK 1   // hash_finish on packed fp32 vectors (render.hip is built without the SLP vectorizer)
+#endif
 template <int INTERP, bool FMA = false>
 __device__ __forceinline__ void hash_finish(const HashPending& p, float& o0, float& o1) {
     if (INTERP == 0) {
@@ -242,6 +245,25 @@ __device__ __forceinline__ void hash_finish(const HashPending& p, float& o0, flo
     }
     const float wx = p.wx, wy = p.wy, wz = p.wz;
     const float ax = 1.0f - wx, ay = 1.0f - wy, az = 1.0f - wz;
+#if ACN_HASH_PK
+    if (!FMA) {   // both features at once on packed fp32 (v_pk_mul_f32 / v_pk_add_f32: per-component IEEE, the same
+                  // roundings as the scalar chain below), written as vectors so the packing needs no SLP pass
+        auto v2 = [](float2 f) { return f32x2_t{f.x, f.y}; };
+        auto lerp2 = [](f32x2_t a, f32x2_t b, float w, float aw) {
+            return a * f32x2_t{aw, aw} + b * f32x2_t{w, w};
+        };
+        const f32x2_t c00 = lerp2(v2(p.f[0]), v2(p.f[1]), wx, ax);
+        const f32x2_t c01 = lerp2(v2(p.f[2]), v2(p.f[3]), wx, ax);
+        const f32x2_t c10 = lerp2(v2(p.f[4]), v2(p.f[5]), wx, ax);
+        const f32x2_t c11 = lerp2(v2(p.f[6]), v2(p.f[7]), wx, ax);
+        const f32x2_t c0 = lerp2(c00, c10, wy, ay);
+        const f32x2_t c1 = lerp2(c01, c11, wy, ay);
+        const f32x2_t o = lerp2(c0, c1, wz, az);
+        o0 = o[0];
+        o1 = o[1];
+        return;
+    }
+#endif
     auto lerp = [&](float a, float b, float w, float aw) { return FMA ? fmaf(b, w, a * aw) : a * aw + b * w; };
     // f index: bit0 = x1, bit1 = z1, bit2 = y1 (issue order above)
     {

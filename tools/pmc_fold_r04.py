@@ -16,6 +16,7 @@ from collections import defaultdict
 def main():
     root, pat, samples, out, rnd, what = sys.argv[1:7]
     samples = int(samples)
+    bpu = float(sys.argv[7]) if len(sys.argv) > 7 else 1024.2   # algorithmic bytes per unit (sample / record)
     vals = defaultdict(list)
     for f in sorted(glob.glob(f"{root}/p*/**/*counter_collection.csv", recursive=True)):
         for r in csv.DictReader(open(f)):
@@ -37,7 +38,7 @@ def main():
     write = c.get("WRITE_SIZE", 0.0) * 1024
     fetch = 2 * fetch_raw                               # gfx950 half-count correction
     traffic = int(fetch + write)
-    alg = int(1024.2 * samples)
+    alg = int(bpu * samples)
     derived = {
         "tcp_accesses_per_sample": c.get("TCP_TOTAL_CACHE_ACCESSES_sum", 0) / samples,
         "l2_requests_per_sample": c.get("TCP_TCC_READ_REQ_sum", 0) / samples,
