@@ -1639,6 +1639,9 @@ __device__ __forceinline__ int lanes_below(uint64_t m) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 constexpr int kRtThreads = 512;   // ep_field_kernel: two workgroups per CU (16 waves)
+#ifndef ACN_EP_BANDS
+#define ACN_EP_BANDS 1                // ep_field_kernel: XCD bands over each expert's wave-tiles
+#endif
 constexpr int kRtWaves = kRtThreads / 64;
 constexpr int kEpMaxSeg = 1024;   // W * E segments of the compact received layout (ep_field_kernel)
 
@@ -1681,7 +1684,17 @@ __global__ void __launch_bounds__(kRtThreads, 4) ep_field_kernel(FieldCfg cfg, c
             const int64_t c = min(cnt[(int64_t)w * E + e], cap_eff);
             T += (c + 31) >> 5;
         }
-        if ((int64_t)blockIdx.x * kRtWaves >= T) continue;   // no tile of this expert for this workgroup
+        // XCD bands (as render_kernel): with the grid a multiple of 8, XCD x takes the x-th contiguous eighth of the
+        // expert's wave-tiles, so consecutive records (a ray's samples, neighbouring rays) share one XCD's L2
+        int64_t g0 = (int64_t)blockIdx.x * kRtWaves + wave, gend = T, gstep = G;
+        if (ACN_EP_BANDS && (gridDim.x & 7) == 0) {
+            const int64_t chunk = (T + 7) >> 3;
+            const int64_t lo = min(T, (int64_t)(blockIdx.x & 7) * chunk);
+            gend = min(T, lo + chunk);
+            g0 = lo + (int64_t)(blockIdx.x >> 3) * kRtWaves + wave;
+            gstep = (int64_t)(gridDim.x >> 3) * kRtWaves;
+        }
+        if (g0 - wave >= gend) continue;   // block-uniform: no tile of this expert for this workgroup
         if (slot != e) {
             __syncthreads();   // every wave is done with the previous expert's image
             const f32x4* src = reinterpret_cast<const f32x4*>(packed + (size_t)e * PK_FLOATS);
@@ -1691,7 +1704,7 @@ __global__ void __launch_bounds__(kRtThreads, 4) ep_field_kernel(FieldCfg cfg, c
             __syncthreads();
             slot = e;
         }
-        for (int64_t g = (int64_t)blockIdx.x * kRtWaves + wave; g < T; g += G) {
+        for (int64_t g = g0; g < gend; g += gstep) {
             int64_t tl = g, c = 0;
             int w = 0;
             for (; w < W; ++w) {   // sender of wave-tile g

@@ -56,6 +56,10 @@ def main():
     s = int(torch.cuda.current_stream(dev).cuda_stream)
     for e in ranks:
         P = counts[e]
+        if P == 0:   # an idle rank: this camera's frame routes no sample to its expert
+            print(json.dumps({"what": "ep_field_kernel of one rank of the one-expert-per-GPU C4 layout",
+                              "world": a.world, "rank_expert": e, "records": 0, "pairs_per_expert": counts}), flush=True)
+            continue
         recs = xd[starts[e]:starts[e + 1]].contiguous()
         sender = (pidx[starts[e]:starts[e + 1]].to(torch.int64) // S) // chunk     # records are in sample order
         rc = torch.bincount(sender, minlength=a.world)[: a.world].to(torch.int64)
