@@ -358,12 +358,11 @@ def load_traffic(name: str = "render", rnd: str = "r01"):
 def render_traffic_profile(workload: str, S: int, layout: str):
     """Counter summary of the render line's dominant kernel (tools/pmc_r04.sh + tools/pmc_fold_r04.py: separate
     rocprofv3 --pmc passes, FETCH_SIZE doubled per the gfx950 correction of MI355X_MICROARCH.md 'HBM', plus
-    WRITE_SIZE) -- round 5, the final render build -- or None
+    WRITE_SIZE) -- round 6, the final render build (buffer-load gathers; C4 at S = 256 not re-profiled) -- or None
     when no profile of this exact configuration is committed."""
-    name = {("c2", 256, "replicated"): "r05_pmc_c2_ws.json",
-            ("c3", 256, "replicated"): "r05_pmc_c3_slots.json",
-            ("c4", 96, "replicated"): "r05_pmc_c4s96_slots.json",
-            ("c4", 256, "replicated"): "r05_pmc_c4_slots.json"}.get((workload, S, layout))
+    name = {("c2", 256, "replicated"): "r06_pmc_c2_render.json",
+            ("c3", 256, "replicated"): "r06_pmc_c3_render.json",
+            ("c4", 96, "replicated"): "r06_pmc_c4s96_render.json"}.get((workload, S, layout))
     if name is None:
         return None
     p = REPO / "profiles" / name
@@ -1276,6 +1275,31 @@ def main():
                                             "slot at the step's capacities; live = the same for the routed pairs"}
         if a.workload == "c4":
             line["psnr_vs_synthetic_gt_db"] = round(float(out[3]), 4)
+            if a.layout == "expert":
+                # the owner kernel as ONE rank of the 8-GPU layout runs it (tools/ep_owner_rank.py: the records of
+                # the busiest rank, one 128 MiB table resident), timed and counter-profiled on one GPU
+                try:
+                    pr = json.loads((REPO / "profiles" / "r06_pmc_ep_owner_rank2.json").read_text())
+                    ranks = [json.loads(l) for l in (REPO / "profiles" / "r06_ep_owner_ranks_bands.jsonl").read_text()
+                             .splitlines() if l.strip()]
+                    busy = max((r for r in ranks if r.get("records")), key=lambda r: r["records"])
+                    alg = pr["bytes_algorithmic_per_launch"]
+                    ms = pr["rocprof_avg_ns"] / 1e6
+                    line["per_rank_owner"] = {
+                        "what": "ep_field_kernel of the busiest rank of the 8-GPU one-expert-per-GPU layout (expert "
+                                f"{busy['rank_expert']}: {busy['records']} records of this frame; per-rank record "
+                                f"counts {[r.get('records', 0) for r in ranks]})",
+                        "kernel_ms_events": busy["kernel_ms"], "kernel_ms_rocprof": round(ms, 4),
+                        "roofline": {"bound": "hbm", "achieved": round(alg / (ms * 1e-3) / 1e9, 1),
+                                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                     "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                     "traffic": pr["hbm_bytes_per_launch"], "bytes_per_record": 1064,
+                                     "bytes_algorithmic_per_launch": alg,
+                                     "l2_misses_per_record": round(pr["derived"]["l2_misses_per_sample"], 2)},
+                        "source": "profiles/r06_ep_owner_ranks_bands.jsonl, profiles/r06_pmc_ep_owner_rank2.json, "
+                                  "profiles/r06_rocprof_ep_owner_rank2_kernel_stats.csv"}
+                except Exception:
+                    pass
             if a.layout == "expert" and ep_stats:
                 line["exchange"] = {"bytes_sent_per_frame_per_rank": int(ep_stats["sent"]),
                                     "live_pair_bytes_per_frame_per_rank": int(ep_stats["live"]),
