@@ -36,6 +36,12 @@ def main():
     ap.add_argument("--expert", type=int, default=None, help="rank / owned expert; -1: every rank")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--order", choices=["sample", "depth-tiled"], default="sample",
+                    help="record order inside each sender segment: as the senders produce them (sample order, "
+                         "ray-major), or depth-tiled: blocks of --block neighbouring rays, one sample index at a "
+                         "time (a wave-tile = the block's rays at one depth); the results go back by position, so "
+                         "the order is the sender's free choice")
+    ap.add_argument("--block", type=int, default=32)
     a = ap.parse_args()
     import bench
     from adaptive_city_nerf_amd import _lib, ops
@@ -61,7 +67,12 @@ def main():
                               "world": a.world, "rank_expert": e, "records": 0, "pairs_per_expert": counts}), flush=True)
             continue
         recs = xd[starts[e]:starts[e + 1]].contiguous()
-        sender = (pidx[starts[e]:starts[e + 1]].to(torch.int64) // S) // chunk     # records are in sample order
+        samp = pidx[starts[e]:starts[e + 1]].to(torch.int64)
+        sender = (samp // S) // chunk     # records are in sample order
+        if a.order == "depth-tiled":
+            ray, si = samp // S, samp % S
+            key = ((sender * ((N + a.block - 1) // a.block) + ray // a.block) * S + si) * a.block + ray % a.block
+            recs = recs[torch.argsort(key)].contiguous()
         rc = torch.bincount(sender, minlength=a.world)[: a.world].to(torch.int64)
         recv_cnt = rc.to(dev)
         rc_host = [int(v) for v in rc.tolist()]
@@ -90,7 +101,7 @@ def main():
         gbs = BYTES_PER_RECORD * P / (ms * 1e-3) / 1e9
         print(json.dumps({
             "what": "ep_field_kernel of one rank of the one-expert-per-GPU C4 layout (tools/ep_owner_rank.py)",
-            "world": a.world, "rank_expert": e, "frame": [H, W], "samples": S, "records": P,
+            "world": a.world, "rank_expert": e, "frame": [H, W], "samples": S, "records": P, "order": a.order,
             "records_per_sender": rc_host, "pairs_per_expert": counts, "kernel_ms": round(ms, 4),
             "records_per_s": P / (ms * 1e-3), "finite": finite,
             "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
