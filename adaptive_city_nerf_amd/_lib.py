@@ -91,6 +91,7 @@ SIGNATURES = {
     "acn_render_order_bytes": ([i64], sz),
     "acn_ray_order": ([vp, i64, vp, vp], C.c_int),
     "acn_routed_count_caps": ([vp, i64, i32, vp, vp, vp, vp, vp, vp, sz, vp], C.c_int),
+    "acn_routed_count_caps_tiled": ([vp, i64, i32, vp, vp, vp, i32, vp, vp, vp, sz, vp], C.c_int),
     "acn_ep_gather_caps": ([vp, vp, i32, i32, vp, i32, vp, vp, f32, f32, vp, vp, vp, vp, vp, vp, vp, vp], C.c_int),
     "acn_ep_field_fwd": ([vp, vp, i32, i32, i64, vp, vp, sz, vp, vp], C.c_int),
     "acn_ep_field_fwd_compact": ([vp, vp, i32, i32, i64, i64, vp, vp, sz, vp, vp], C.c_int),
@@ -161,6 +162,7 @@ SIGNATURES = {
     "acn_hashgrid_bwd_det_workspace_bytes": ([i64, i32, i32, i32], C.c_size_t),
     "acn_hashgrid_bwd_det": ([vp, i64, vp, vp, i32, i32, i32, i32, vp, vp, sz, vp], C.c_int),
     "acn_routed_scatter_xd": ([vp, i64, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp], C.c_int),
+    "acn_routed_scatter_xd_tiled": ([vp, i64, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp], C.c_int),
     "acn_routed_count_fixed": ([vp, i64, i32, vp, vp, i64, vp, vp, vp, sz, vp], C.c_int),
     "acn_routed_pad_pairs": ([vp, i32, i64, vp, vp, vp], C.c_int),
     "acn_ep_workspace_bytes": ([i32, i32], sz),

@@ -9,7 +9,8 @@
 //                        cdist-mm arithmetic, per-256-sample block counts of routed samples per expert,
 //                        then one workgroup scans them -> pair segment of every expert (starts[K+1]).
 //   acn_routed_scatter : one lane per sample -> for every expert k with w_k > 0, pair record at
-//                        starts[k] + (rank of the sample among expert k's samples, in sample order):
+//                        starts[k] + (rank of the sample among expert k's samples, in sample order;
+//                        the *_tiled expert-parallel forms: in depth-tile order, tile_sample):
 //                        sample index, weight, x in expert k's unit box (clamped), SH-4 of the ray
 //                        direction; pmap (M,K) = pair index or -1.  Pairs of expert k are therefore
 //                        exactly the rows the reference's index_select(nonzero(w[:,k] > 0)) gathers,
@@ -56,13 +57,30 @@ __device__ __forceinline__ void route_row(const RouteCfg& cfg, float px, float p
     }
 }
 
+// Sample at traversal position mp.  tile = 0: sample order (mp itself, ray-major).  tile > 0: depth tiles -- the
+// rays come in blocks of `tile` consecutive rays (the last one shorter), and a block's rays at sample s precede its
+// rays at s + 1.  The pair lists are built in traversal order, so with tiles a wave of an expert's records holds
+// neighbouring rays at one depth: neighbouring points, the hash rows they share stay in L2.  A
+// bijection of [0, M): every sample is visited once, whatever the order.
+__device__ __forceinline__ int64_t tile_sample(int64_t mp, int64_t N, int S, int tile) {
+    if (tile <= 0) return mp;
+    const int64_t ts = (int64_t)tile * S;
+    const int64_t bi = mp / ts;
+    const int64_t q = mp - bi * ts;
+    const int64_t r0 = bi * tile;
+    const int64_t nb = N - r0 < tile ? N - r0 : tile;
+    const int64_t s = q / nb;
+    return (r0 + (q - s * nb)) * S + s;
+}
+
 __global__ void __launch_bounds__(kBlk) routed_count_kernel(const float* __restrict__ rays, int64_t N, int S,
                                                             const float* __restrict__ jit, RouteCfg cfg,
                                                             float* __restrict__ t_out, float* __restrict__ W,
-                                                            int32_t* __restrict__ blk_cnt) {
+                                                            int32_t* __restrict__ blk_cnt, int tile) {
     __shared__ int wcnt[kBlk / 64][kMaxK];
     const int64_t M = N * (int64_t)S;
-    const int64_t m = (int64_t)blockIdx.x * kBlk + threadIdx.x;
+    const int64_t mp = (int64_t)blockIdx.x * kBlk + threadIdx.x;
+    const int64_t m = mp < M ? tile_sample(mp, N, S, tile) : mp;
     float w[kMaxK];
 #pragma unroll
     for (int k = 0; k < kMaxK; ++k) w[k] = 0.0f;
@@ -154,7 +172,7 @@ __global__ void __launch_bounds__(kBlk) routed_scatter_kernel(const float* __res
                                                               int32_t* __restrict__ pidx, float* __restrict__ pw,
                                                               float* __restrict__ x01, float* __restrict__ sh_out,
                                                               int32_t* __restrict__ pmap, int32_t* __restrict__ pk,
-                                                              int pad) {
+                                                              int pad, int tile) {
     __shared__ int wcnt[kBlk / 64][kMaxK];
     const int64_t M = N * (int64_t)S;
     if (XD == 0 && pad) {
@@ -173,8 +191,9 @@ __global__ void __launch_bounds__(kBlk) routed_scatter_kernel(const float* __res
             }
         }
     }
-    const int64_t m = (int64_t)blockIdx.x * kBlk + threadIdx.x;
-    const bool live = m < M;
+    const int64_t mp = (int64_t)blockIdx.x * kBlk + threadIdx.x;   // traversal position (tile_sample)
+    const bool live = mp < M;
+    const int64_t m = live ? tile_sample(mp, N, S, tile) : mp;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     float px = 0.0f, py = 0.0f, pz = 0.0f, sh[16];
     if (live) {
@@ -460,7 +479,7 @@ extern "C" int acn_routed_count(const float* rays, int64_t N, int S, const float
     int32_t* blk = (int32_t*)(W + M * K);
     const int64_t nblk = (M + kBlk - 1) / kBlk;
     hipLaunchKernelGGL(routed_count_kernel, dim3(blocks_for(M, kBlk)), dim3(kBlk), 0, s, rays, N, S, jitter, cfg, t_vals,
-                       W, blk);
+                       W, blk, 0);
     Caps caps{};
     hipLaunchKernelGGL(routed_scan_kernel, dim3(1), dim3(1024), 0, s, blk, nblk, K, align, caps, starts);
     return acn_check_launch("acn_routed_count");
@@ -478,7 +497,16 @@ extern "C" int acn_routed_count_fixed(const float* rays, int64_t N, int S, const
 extern "C" int acn_routed_count_caps(const float* rays, int64_t N, int S, const float* jitter,
                                      const acn_routing* routing, const int64_t* caps_host, float* t_vals,
                                      int64_t* starts, void* workspace, size_t workspace_bytes, void* stream) {
-    ACN_REQUIRE(N >= 0 && S >= 1 && routing && starts && caps_host, "acn_routed_count_caps: bad arguments");
+    return acn_routed_count_caps_tiled(rays, N, S, jitter, routing, caps_host, 0, t_vals, starts, workspace,
+                                       workspace_bytes, stream);
+}
+
+extern "C" int acn_routed_count_caps_tiled(const float* rays, int64_t N, int S, const float* jitter,
+                                           const acn_routing* routing, const int64_t* caps_host, int tile_rays,
+                                           float* t_vals, int64_t* starts, void* workspace, size_t workspace_bytes,
+                                           void* stream) {
+    ACN_REQUIRE(N >= 0 && S >= 1 && routing && starts && caps_host && tile_rays >= 0,
+                "acn_routed_count_caps: bad arguments");
     const int K = routing->K;
     ACN_REQUIRE(K >= 1 && K <= kMaxK, "acn_routed_count_caps: K = %d outside [1, %d]", K, kMaxK);
     const int64_t M = N * (int64_t)S;
@@ -505,7 +533,7 @@ extern "C" int acn_routed_count_caps(const float* rays, int64_t N, int S, const 
     if (M > 0) {
         ACN_REQUIRE(rays && t_vals, "acn_routed_count_caps: NULL pointer");
         hipLaunchKernelGGL(routed_count_kernel, dim3(blocks_for(M, kBlk)), dim3(kBlk), 0, s, rays, N, S, jitter, cfg,
-                           t_vals, W, blk);
+                           t_vals, W, blk, tile_rays);
     }
     hipLaunchKernelGGL(routed_scan_kernel, dim3(1), dim3(1024), 0, s, blk, nblk, K, 1, caps, starts);
     return acn_check_launch("acn_routed_count_caps");
@@ -532,7 +560,7 @@ extern "C" int acn_routed_scatter(const float* rays, int64_t N, int S, int K, co
     const float* W = (const float*)workspace;
     const int32_t* blk = (const int32_t*)(W + M * K);
     hipLaunchKernelGGL(routed_scatter_kernel<0>, dim3(blocks_for(M, kBlk)), dim3(kBlk), 0, (hipStream_t)stream, rays,
-                       N, S, K, t_vals, W, blk, starts, box, pidx, pw, x01, sh, pmap, pk, align > 1 ? 1 : 0);
+                       N, S, K, t_vals, W, blk, starts, box, pidx, pw, x01, sh, pmap, pk, align > 1 ? 1 : 0, 0);
     return acn_check_launch("acn_routed_scatter");
 }
 
@@ -559,7 +587,14 @@ extern "C" int acn_routed_blend_bwd(const float* g, const int32_t* pidx, const f
 extern "C" int acn_routed_scatter_xd(const float* rays, int64_t N, int S, int K, const float* t_vals, const int64_t* seg,
                                      const void* workspace, int32_t* pidx, float* pw, float* xd, int32_t* pmap,
                                      int32_t* pk, void* stream) {
-    ACN_REQUIRE(N >= 0 && S >= 1 && K >= 1 && K <= kMaxK, "acn_routed_scatter_xd: bad arguments");
+    return acn_routed_scatter_xd_tiled(rays, N, S, K, 0, t_vals, seg, workspace, pidx, pw, xd, pmap, pk, stream);
+}
+
+extern "C" int acn_routed_scatter_xd_tiled(const float* rays, int64_t N, int S, int K, int tile_rays,
+                                           const float* t_vals, const int64_t* seg, const void* workspace,
+                                           int32_t* pidx, float* pw, float* xd, int32_t* pmap, int32_t* pk,
+                                           void* stream) {
+    ACN_REQUIRE(N >= 0 && S >= 1 && K >= 1 && K <= kMaxK && tile_rays >= 0, "acn_routed_scatter_xd: bad arguments");
     const int64_t M = N * (int64_t)S;
     if (M == 0) return ACN_OK;
     ACN_REQUIRE(rays && t_vals && seg && workspace && pidx && pw && xd && pmap, "acn_routed_scatter_xd: NULL pointer");
@@ -567,7 +602,7 @@ extern "C" int acn_routed_scatter_xd(const float* rays, int64_t N, int S, int K,
     const float* W = (const float*)workspace;
     const int32_t* blk = (const int32_t*)(W + M * K);
     hipLaunchKernelGGL(routed_scatter_kernel<1>, dim3(blocks_for(M, kBlk)), dim3(kBlk), 0, (hipStream_t)stream, rays,
-                       N, S, K, t_vals, W, blk, seg, box, pidx, pw, xd, (float*)nullptr, pmap, pk, 0);
+                       N, S, K, t_vals, W, blk, seg, box, pidx, pw, xd, (float*)nullptr, pmap, pk, 0, tile_rays);
     return acn_check_launch("acn_routed_scatter_xd");
 }
 

@@ -8,7 +8,8 @@ owns experts [r K / W, (r+1) K / W)), every rank holds a shard of the rays, and 
 per-sample records:
 
     rank r: its rays -> t values + routed (sample, expert) pairs, grouped by expert in sample order
-            (routed.hip) -> 24-B records xd = [world point, ray direction] of every pair
+            (routed.hip; the renderer: in depth tiles of neighbouring rays) -> 24-B records xd = [world
+            point, ray direction] of every pair
     all-to-all #1 (forward):  records to the owner of the pair's expert (+ the expert id)
     owner:  its experts' fields on the records it received (the same per-expert forward as one GPU)
     all-to-all #2:           (rgb, sigma) 16 B back, in the sender's pair order
@@ -24,6 +25,7 @@ a CPU restatement in to check the data movement over gloo.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
@@ -33,6 +35,11 @@ from torch import Tensor
 
 from ._lib import graph_capture
 from .color_space import color_space_transformer
+
+
+# ExpertParallelRenderer's record order: depth tiles of this many neighbouring rays (0: sample order; env
+# ACN_EP_TILE overrides).  32: the busiest C4 owner rank at 0.47 of HBM against 0.25 in sample order
+EP_TILE_RAYS = 32
 
 
 def world_rank(group=None):
@@ -258,7 +265,8 @@ class ExpertParallelRenderer:
     meta_container.py:307-321).  Reference: models/inr/meta_container.py:300-337, nerfs/ray_rendering.py:577-627."""
 
     def __init__(self, model, n_rays: int, ray_samples: int, group=None, capacity: Optional[int] = None,
-                 graph: bool = False, bg_color_default: str = "white", want_weights: bool = False):
+                 graph: bool = False, bg_color_default: str = "white", want_weights: bool = False,
+                 tile_rays: Optional[int] = None):
         from . import _lib, ops
         from ._lib import AcnError
         from .meta_container import MetaContainer
@@ -281,6 +289,12 @@ class ExpertParallelRenderer:
         if Cc < 1:
             raise AcnError("ExpertParallelRenderer: capacity must be >= 1")
         self.K, self.E, self.W, self.N, self.S, self.M, self.C = K, E, W, N, S, M, Cc
+        # the order of every expert's records: depth tiles of tile_rays neighbouring rays (acn_routed_*_tiled), so
+        # the owner's waves see neighbouring points; 0: sample order.  Results go back by position,
+        # so the order changes no value.
+        self.tile_rays = int(os.environ.get("ACN_EP_TILE", EP_TILE_RAYS) if tile_rays is None else tile_rays)
+        if self.tile_rays < 0:
+            raise AcnError("ExpertParallelRenderer: tile_rays must be >= 0")
         self.own, self.eo = own, eo
         self.split_send = [e * Cc for e in eo]
         self.split_recv = [E * Cc] * W
@@ -335,11 +349,13 @@ class ExpertParallelRenderer:
         L = _lib.lib()
         s = int(torch.cuda.current_stream(self.device).cuda_stream)
         K, E, S, Cc, comm = self.K, self.E, self.S, self.C, self.comm
-        check(L.acn_routed_count_fixed(ptr(self.rays), n, S, None, C.byref(self.routing), Cc, ptr(self.t),
-                                       ptr(self.seg), ptr(self.rws), self.rws.numel(), s), "acn_routed_count_fixed")
-        check(L.acn_routed_scatter_xd(ptr(self.rays), n, S, K, ptr(self.t), ptr(self.seg), ptr(self.rws),
-                                      ptr(self.pidx), ptr(self.pw), ptr(self.xd), ptr(self.pmap), ptr(self.pk), s),
-              "acn_routed_scatter_xd")
+        caps = (C.c_int64 * K)(*([Cc] * K))
+        check(L.acn_routed_count_caps_tiled(ptr(self.rays), n, S, None, C.byref(self.routing), caps, self.tile_rays,
+                                            ptr(self.t), ptr(self.seg), ptr(self.rws), self.rws.numel(), s),
+              "acn_routed_count_caps_tiled")
+        check(L.acn_routed_scatter_xd_tiled(ptr(self.rays), n, S, K, self.tile_rays, ptr(self.t), ptr(self.seg),
+                                            ptr(self.rws), ptr(self.pidx), ptr(self.pw), ptr(self.xd), ptr(self.pmap),
+                                            ptr(self.pk), s), "acn_routed_scatter_xd_tiled")
         comm.all_to_all(self.recv_cnt, self.seg[K + 1:], self.split_cnt_recv, self.split_cnt_send)
         comm.all_to_all(self.recv_xd, self.xd, self.split_recv, self.split_send)
         check(L.acn_pack_experts(self._own_arr, C.byref(self.own_routing), -1, ptr(self.packed),
@@ -371,11 +387,12 @@ class ExpertParallelRenderer:
         K, E, W, S, comm, rank, own, owner = self.K, self.E, self.W, self.S, self.comm, self.comm.rank, self.own, self.owner
         mine = [int(c) for c in counts[rank]]
         caps = (C.c_int64 * K)(*mine)
-        check(L.acn_routed_count_caps(ptr(self.rays), n, S, None, C.byref(self.routing), caps, ptr(self.t),
-                                      ptr(self.seg), ptr(self.rws), self.rws.numel(), s), "acn_routed_count_caps")
-        check(L.acn_routed_scatter_xd(ptr(self.rays), n, S, K, ptr(self.t), ptr(self.seg), ptr(self.rws),
-                                      ptr(self.pidx), ptr(self.pw), ptr(self.xd), ptr(self.pmap), ptr(self.pk), s),
-              "acn_routed_scatter_xd")
+        check(L.acn_routed_count_caps_tiled(ptr(self.rays), n, S, None, C.byref(self.routing), caps, self.tile_rays,
+                                            ptr(self.t), ptr(self.seg), ptr(self.rws), self.rws.numel(), s),
+              "acn_routed_count_caps_tiled")
+        check(L.acn_routed_scatter_xd_tiled(ptr(self.rays), n, S, K, self.tile_rays, ptr(self.t), ptr(self.seg),
+                                            ptr(self.rws), ptr(self.pidx), ptr(self.pw), ptr(self.xd), ptr(self.pmap),
+                                            ptr(self.pk), s), "acn_routed_scatter_xd_tiled")
         send = [sum(mine[k] for k in range(K) if owner[k] == o) for o in range(W)]
         rc = [int(counts[w][k]) for w in range(W) for k in own]
         recv = [sum(rc[w * E:(w + 1) * E]) for w in range(W)]

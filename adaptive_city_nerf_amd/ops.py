@@ -718,9 +718,11 @@ def routed_blend_bwd(g: torch.Tensor, pidx: torch.Tensor, pw: torch.Tensor,
     return gy
 
 
-def routed_pairs_xd(rays: torch.Tensor, S: int, jitter: Optional[torch.Tensor], routing: acn_routing):
+def routed_pairs_xd(rays: torch.Tensor, S: int, jitter: Optional[torch.Tensor], routing: acn_routing,
+                    tile_rays: int = 0):
     """t_vals (N,S) and the routed pairs as expert-parallel records: (t_vals, counts (K host ints), pidx, pw,
-    xd (P,6) world point + direction, pmap (M,K), pk (P,)); pairs grouped by expert, in sample order."""
+    xd (P,6) world point + direction, pmap (M,K), pk (P,)); pairs grouped by expert, in sample order, or with
+    ``tile_rays`` > 0 in depth tiles of that many rays (acn_routed_*_tiled, the ExpertParallelRenderer order)."""
     require_hip(rays, "expert-parallel render")
     r = _f32(rays)
     N = r.shape[0]
@@ -742,8 +744,13 @@ def routed_pairs_xd(rays: torch.Tensor, S: int, jitter: Optional[torch.Tensor], 
     xd = torch.empty(P, 6, device=dev, dtype=torch.float32)
     pk = torch.empty(P, device=dev, dtype=torch.int32)
     pmap = torch.empty(M, K, device=dev, dtype=torch.int32)
-    check(L.acn_routed_scatter_xd(ptr(r), N, int(S), K, ptr(t), ptr(seg), ptr(ws), ptr(pidx), ptr(pw), ptr(xd),
-                                  ptr(pmap), ptr(pk), stream_of(r)), "acn_routed_scatter_xd")
+    if tile_rays:   # the same segments (capacities = the counts), laid out in depth-tile order
+        check(L.acn_routed_count_caps_tiled(ptr(r), N, int(S), ptr(jit), C.byref(routing), (C.c_int64 * K)(*counts),
+                                            int(tile_rays), ptr(t), ptr(seg), ptr(ws), ws.numel(), stream_of(r)),
+              "acn_routed_count_caps_tiled")
+    check(L.acn_routed_scatter_xd_tiled(ptr(r), N, int(S), K, int(tile_rays), ptr(t), ptr(seg), ptr(ws), ptr(pidx),
+                                        ptr(pw), ptr(xd), ptr(pmap), ptr(pk), stream_of(r)),
+          "acn_routed_scatter_xd_tiled")
     return t, counts, pidx, pw, xd, pmap, pk
 
 

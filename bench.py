@@ -1278,9 +1278,16 @@ def main():
             if a.layout == "expert":
                 # the owner kernel as ONE rank of the 8-GPU layout runs it (tools/ep_owner_rank.py: the records of
                 # the busiest rank, one 128 MiB table resident), timed and counter-profiled on one GPU
+                # the records in the order this run's renderer lays them out (depth tiles unless ACN_EP_TILE=0)
+                from adaptive_city_nerf_amd import expert_parallel as _ep
+                tile = int(os.environ.get("ACN_EP_TILE", _ep.EP_TILE_RAYS))
+                src = (("r06_ep_owner_ranks_tiled.jsonl", "r06_pmc_ep_owner_rank2_tiled.json",
+                        "r06_rocprof_ep_owner_rank2_tiled_kernel_stats.csv") if tile else
+                       ("r06_ep_owner_ranks_bands.jsonl", "r06_pmc_ep_owner_rank2.json",
+                        "r06_rocprof_ep_owner_rank2_kernel_stats.csv"))
                 try:
-                    pr = json.loads((REPO / "profiles" / "r06_pmc_ep_owner_rank2.json").read_text())
-                    ranks = [json.loads(l) for l in (REPO / "profiles" / "r06_ep_owner_ranks_bands.jsonl").read_text()
+                    pr = json.loads((REPO / "profiles" / src[1]).read_text())
+                    ranks = [json.loads(l) for l in (REPO / "profiles" / src[0]).read_text()
                              .splitlines() if l.strip()]
                     busy = max((r for r in ranks if r.get("records")), key=lambda r: r["records"])
                     alg = pr["bytes_algorithmic_per_launch"]
@@ -1289,6 +1296,7 @@ def main():
                         "what": "ep_field_kernel of the busiest rank of the 8-GPU one-expert-per-GPU layout (expert "
                                 f"{busy['rank_expert']}: {busy['records']} records of this frame; per-rank record "
                                 f"counts {[r.get('records', 0) for r in ranks]})",
+                        "record_order": f"depth tiles of {tile} rays" if tile else "sample order",
                         "kernel_ms_events": busy["kernel_ms"], "kernel_ms_rocprof": round(ms, 4),
                         "roofline": {"bound": "hbm", "achieved": round(alg / (ms * 1e-3) / 1e9, 1),
                                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -1296,8 +1304,7 @@ def main():
                                      "traffic": pr["hbm_bytes_per_launch"], "bytes_per_record": 1064,
                                      "bytes_algorithmic_per_launch": alg,
                                      "l2_misses_per_record": round(pr["derived"]["l2_misses_per_sample"], 2)},
-                        "source": "profiles/r06_ep_owner_ranks_bands.jsonl, profiles/r06_pmc_ep_owner_rank2.json, "
-                                  "profiles/r06_rocprof_ep_owner_rank2_kernel_stats.csv"}
+                        "source": ", ".join("profiles/" + f for f in src)}
                 except Exception:
                     pass
             if a.layout == "expert" and ep_stats:

@@ -580,6 +580,19 @@ int acn_routed_pad_pairs(const int64_t* seg, int K, int64_t max_pad, int32_t* pi
 int acn_routed_count_caps(const float* rays, int64_t N, int S, const float* jitter, const acn_routing* routing,
                           const int64_t* caps, float* t_vals, int64_t* seg, void* workspace, size_t workspace_bytes,
                           void* stream);
+/* Depth-tiled pair order (the expert-parallel render, expert_parallel.ExpertParallelRenderer(tile_rays=...)): as
+ * acn_routed_count_caps / acn_routed_scatter_xd, with every expert's pairs laid out in depth-tile order instead of
+ * sample order -- blocks of tile_rays consecutive rays (the last one shorter), a block's rays at sample s before its
+ * rays at s + 1.  The same pairs, counts and segments, pmap / pidx pointing at the new positions; tile_rays 0 IS
+ * the sample order of the forms above.  The owner evaluates records in arrival order, so a wave holds neighbouring
+ * rays at one depth (the busiest C4 owner rank 29.7 -> 15.5 ms).  Both calls of a batch must use the
+ * same tile_rays.  No reference counterpart (the order is the sender's free choice: results go back by position). */
+int acn_routed_count_caps_tiled(const float* rays, int64_t N, int S, const float* jitter, const acn_routing* routing,
+                                const int64_t* caps, int tile_rays, float* t_vals, int64_t* seg, void* workspace,
+                                size_t workspace_bytes, void* stream);
+int acn_routed_scatter_xd_tiled(const float* rays, int64_t N, int S, int K, int tile_rays, const float* t_vals,
+                                const int64_t* seg, const void* workspace, int32_t* pidx, float* pw, float* xd,
+                                int32_t* pmap, int32_t* pk, void* stream);
 int acn_ep_gather_caps(const float* recv_xd, const int64_t* recv_cnt, int W, int E, const int64_t* caps, int align,
                        const float* aabb_min, const float* aabb_extent, float lo, float hi, int64_t* seg,
                        void* workspace, float* x01, float* sh, int32_t* pk, int32_t* pflag, int64_t* back,

@@ -389,15 +389,54 @@ def test_ep_comm_fixed_splits_gloo_world2():
 
 # --------------------------------------------------------------- sync-free one-expert-per-GPU render (GPU)
 @pytest.mark.gpu
+@pytest.mark.parametrize("tile", [1, 7, 32, 1 << 20])
+def test_routed_pairs_depth_tiled_order(tile):
+    """acn_routed_count_caps_tiled + acn_routed_scatter_xd_tiled (the renderer's record order): the same pairs,
+    counts and t values as the sample order, every expert's segment permuted into depth-tile order -- blocks of
+    `tile` consecutive rays (the last one shorter), a block's rays at sample s before its rays at s + 1 -- with the
+    records, weights and expert ids moved bit for bit and pmap pointing at the new positions."""
+    from adaptive_city_nerf_amd import ops
+    from test_k8 import _model
+    d = G.load("render_k8")
+    m, _ = _model(d, "w:")
+    rays = torch.from_numpy(d["render:rays"]).cuda()
+    N, S = rays.shape[0], 64
+    with torch.no_grad():
+        a = ops.routed_pairs_xd(rays, S, None, m.routing_spec())
+        b = ops.routed_pairs_xd(rays, S, None, m.routing_spec(), tile_rays=tile)
+    t0, c0, pidx0, pw0, xd0, pmap0, pk0 = [x.cpu().numpy() if torch.is_tensor(x) else x for x in a]
+    t1, c1, pidx1, pw1, xd1, pmap1, pk1 = [x.cpu().numpy() if torch.is_tensor(x) else x for x in b]
+    assert c0 == c1 and sum(c0) > 0
+    np.testing.assert_array_equal(t0, t1)
+    samp = pidx0.astype(np.int64)
+    ray, s = samp // S, samp % S
+    blk = ray // tile
+    nb = np.minimum(tile, N - blk * tile)
+    pos = blk * tile * S + s * nb + (ray - blk * tile)     # traversal position of the sample (tile_sample inverse)
+    start = np.concatenate([[0], np.cumsum(c0)])
+    for k in range(len(c0)):
+        sl = slice(start[k], start[k + 1])
+        order = np.argsort(pos[sl], kind="stable")
+        np.testing.assert_array_equal(pidx1[sl], pidx0[sl][order], err_msg=f"expert {k}")
+        np.testing.assert_array_equal(xd1[sl], xd0[sl][order])
+        np.testing.assert_array_equal(pw1[sl], pw0[sl][order])
+        np.testing.assert_array_equal(pk1[sl], pk0[sl][order])
+    assert ((pmap0 < 0) == (pmap1 < 0)).all()
+    P = int(start[-1])
+    np.testing.assert_array_equal(pmap1[pidx1.astype(np.int64), pk1.astype(np.int64)], np.arange(P))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("variant", ["render", "render_hi"])
 @pytest.mark.parametrize("graph", [False, True])
-def test_ep_renderer_world1_equals_fused_render(variant, graph):
+@pytest.mark.parametrize("tile", [0, 32])
+def test_ep_renderer_world1_equals_fused_render(variant, graph, tile):
     """ExpertParallelRenderer at world size 1 (exchanges are copies; graph=True: the first full batch is run
     eagerly and captured, later calls replay it): every ray's rgb / depth / weights / acc equal the fused
     single-process routed render bit for bit (same per-(sample, expert) arithmetic, blend in expert order,
     same compositing), and the reference fixture within the north-star tolerances.  A capacity below the
     largest expert's pair count is detected (overflowed) and, re-rendered at full capacity, gives the same
-    frame."""
+    frame.  tile: the record order (0 sample order, 32 the default depth tiles): no value may change."""
     from adaptive_city_nerf_amd import render_rays
     from adaptive_city_nerf_amd.expert_parallel import ExpertParallelRenderer, render_rays_ep_batched
     from test_k8 import _model
@@ -405,7 +444,7 @@ def test_ep_renderer_world1_equals_fused_render(variant, graph):
     m, _ = _model(d, "hiw:" if variant == "render_hi" else "w:")
     rays = torch.from_numpy(d["render:rays"]).cuda()
     n = rays.shape[0]
-    r = ExpertParallelRenderer(m, n, 64, graph=graph, want_weights=True)
+    r = ExpertParallelRenderer(m, n, 64, graph=graph, want_weights=True, tile_rays=tile)
     with torch.no_grad():
         fr = render_rays(m, rays, ray_samples=64, bg_color_default="white")
         for rep in range(3):
@@ -417,7 +456,7 @@ def test_ep_renderer_world1_equals_fused_render(variant, graph):
     assert np.abs(out[0].cpu().numpy() - d[f"{variant}:rgb"]).max() <= 1e-4
     assert np.abs(out[2].cpu().numpy() - d[f"{variant}:weights"]).max() <= 1e-5
     # capacity-bounded exchange: an overflow is seen and the batch re-rendered at full capacity
-    small = ExpertParallelRenderer(m, n, 64, capacity=n * 64 // 16)
+    small = ExpertParallelRenderer(m, n, 64, capacity=n * 64 // 16, tile_rays=tile)
     with torch.no_grad():
         small(rays)
         assert small.overflowed()

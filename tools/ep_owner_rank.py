@@ -36,11 +36,11 @@ def main():
     ap.add_argument("--expert", type=int, default=None, help="rank / owned expert; -1: every rank")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--order", choices=["sample", "depth-tiled"], default="sample",
-                    help="record order inside each sender segment: as the senders produce them (sample order, "
-                         "ray-major), or depth-tiled: blocks of --block neighbouring rays, one sample index at a "
-                         "time (a wave-tile = the block's rays at one depth); the results go back by position, so "
-                         "the order is the sender's free choice")
+    ap.add_argument("--order", choices=["sample", "depth-tiled"], default="depth-tiled",
+                    help="record order inside each sender segment: sample order (ray-major), or depth-tiled (the "
+                         "renderer's order, acn_routed_*_tiled): blocks of --block neighbouring rays, one sample "
+                         "index at a time (a wave-tile = the block's rays at one depth); the results go back by "
+                         "position, so the order is the sender's free choice")
     ap.add_argument("--block", type=int, default=32)
     a = ap.parse_args()
     import bench
@@ -52,10 +52,13 @@ def main():
     rays, _ = ops.get_rays_image(H, W, *intr, c2w, gbox.aabb, dev, near_far_override=(None, None))
     N, S, K = rays.shape[0], a.samples, len(model.submodules)
     routing = model.routing_spec()
-    with torch.no_grad():
-        _, counts, pidx, _, xd, _, _ = ops.routed_pairs_xd(rays, S, None, routing)
-    starts = [sum(counts[:k]) for k in range(K + 1)]
+    tile = a.block if a.order == "depth-tiled" else 0
     chunk = (N + a.world - 1) // a.world          # sender w holds rays [w * chunk, (w + 1) * chunk)
+    if tile and chunk % tile:
+        raise SystemExit(f"--block {tile} must divide the sender chunk {chunk} (tiles may not straddle senders)")
+    with torch.no_grad():   # the senders' own kernels, in the renderer's record order (acn_routed_*_tiled)
+        _, counts, pidx, _, xd, _, _ = ops.routed_pairs_xd(rays, S, None, routing, tile_rays=tile)
+    starts = [sum(counts[:k]) for k in range(K + 1)]
     ranks = list(range(K)) if a.expert == -1 else [a.expert if a.expert is not None else
                                                    max(range(K), key=lambda k: counts[k])]
     L = _lib.lib()
@@ -68,11 +71,8 @@ def main():
             continue
         recs = xd[starts[e]:starts[e + 1]].contiguous()
         samp = pidx[starts[e]:starts[e + 1]].to(torch.int64)
-        sender = (samp // S) // chunk     # records are in sample order
-        if a.order == "depth-tiled":
-            ray, si = samp // S, samp % S
-            key = ((sender * ((N + a.block - 1) // a.block) + ray // a.block) * S + si) * a.block + ray % a.block
-            recs = recs[torch.argsort(key)].contiguous()
+        sender = (samp // S) // chunk     # ray-major tiles (or samples): grouped by sender already
+        assert bool((sender[1:] >= sender[:-1]).all())
         rc = torch.bincount(sender, minlength=a.world)[: a.world].to(torch.int64)
         recv_cnt = rc.to(dev)
         rc_host = [int(v) for v in rc.tolist()]
