@@ -30,6 +30,33 @@ __global__ void __launch_bounds__(256) hashgrid_fwd_f2(const float* __restrict__
     out[m * L + l] = make_float2(o0, o1);
 }
 
+// Linear / Smoothstep through a buffer resource over the whole table (the renders' gather form):
+// 32-bit row offsets, and the x-neighbours of each (y, z) corner pair come from one 16-B block when x0 is even
+// (hash_issue_x: 4 dwordx4 gathers, plus 4 dwordx2 only for odd x0).  The same rows and the same lerp chain as
+// hash_level_f2, so the outputs are bitwise those of hashgrid_fwd_f2.  Tables up to 2 GiB (acn_hashgrid_fwd).
+#ifndef ACN_HASH_FWD_BUF
+#define ACN_HASH_FWD_BUF 1
+#endif
+template <int INTERP>
+__global__ void __launch_bounds__(256) hashgrid_fwd_f2_buf(const float* __restrict__ x01, int64_t M,
+                                                           const float2* __restrict__ table, Res32 res, int L,
+                                                           int log2T, float2* __restrict__ out) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t m = gid / L;
+    const int l = (int)(gid - m * L);
+    if (m >= M) return;
+    const float r = (float)res.v[l];
+    const float sx = x01[3 * m] * r, sy = x01[3 * m + 1] * r, sz = x01[3 * m + 2] * r;
+    const uint32_t mask = (uint32_t)((1ull << log2T) - 1ull);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)table, (short)0, (int)((uint32_t)L << (log2T + 3)), 0x00020000);
+    acn::HashPendingX p;
+    acn::hash_issue_x<INTERP>(rs, (uint32_t)l << (log2T + 3), sx, sy, sz, mask, p);
+    float o0, o1;
+    acn::hash_finish_x<INTERP>(p, o0, o1);
+    out[m * L + l] = make_float2(o0, o1);
+}
+
 // generic feature count (F != 2)
 template <int INTERP>
 __global__ void __launch_bounds__(256) hashgrid_fwd_gen(const float* __restrict__ x01, int64_t M,
@@ -489,7 +516,10 @@ extern "C" int acn_hashgrid_fwd(const float* x01, int64_t M, const float* table,
     const dim3 grid((unsigned)((threads + 255) / 256)), block(256);
     hipStream_t s = (hipStream_t)stream;
     if (F == 2) {
-        if (interp == 0) hipLaunchKernelGGL(hashgrid_fwd_f2<0>, grid, block, 0, s, x01, M, (const float2*)table, r, L, log2T, (float2*)out);
+        const bool buf = ACN_HASH_FWD_BUF && interp != 0 && ((uint64_t)L << (log2T + 3)) <= (1ull << 31);
+        if (buf && interp == 1) hipLaunchKernelGGL(hashgrid_fwd_f2_buf<1>, grid, block, 0, s, x01, M, (const float2*)table, r, L, log2T, (float2*)out);
+        else if (buf) hipLaunchKernelGGL(hashgrid_fwd_f2_buf<2>, grid, block, 0, s, x01, M, (const float2*)table, r, L, log2T, (float2*)out);
+        else if (interp == 0) hipLaunchKernelGGL(hashgrid_fwd_f2<0>, grid, block, 0, s, x01, M, (const float2*)table, r, L, log2T, (float2*)out);
         else if (interp == 1) hipLaunchKernelGGL(hashgrid_fwd_f2<1>, grid, block, 0, s, x01, M, (const float2*)table, r, L, log2T, (float2*)out);
         else hipLaunchKernelGGL(hashgrid_fwd_f2<2>, grid, block, 0, s, x01, M, (const float2*)table, r, L, log2T, (float2*)out);
     } else {
