@@ -257,7 +257,7 @@ struct SegMaps {   // per expert: the "touched this step" byte map of its table'
     uint8_t* t[acn::kMaxK];
 };
 
-template <int INTERP>
+template <int INTERP, bool BUF = false>
 __global__ void __launch_bounds__(256) hashgrid_fwd_pairs(const float* __restrict__ x01, const int32_t* __restrict__ pk,
                                                           const int64_t* __restrict__ seg, int K, Tables tabs,
                                                           Res32 res, int L, int log2T, float2* __restrict__ out) {
@@ -268,9 +268,26 @@ __global__ void __launch_bounds__(256) hashgrid_fwd_pairs(const float* __restric
         const int l = (int)(gid - m * L);
         const float r = (float)res.v[l];
         const float sx = x01[3 * m] * r, sy = x01[3 * m + 1] * r, sz = x01[3 * m + 2] * r;
-        const float2* tl = tabs.t[pk[m]] + ((int64_t)l << log2T);
         float o0, o1;
-        acn::hash_level_f2<INTERP>(tl, sx, sy, sz, mask, o0, o1);
+        if (BUF) {
+            // buffer gathers (hashgrid_fwd_f2_buf) from the table of the lane's expert: one resource per distinct
+            // expert of the wave (a wave's slots normally share one; the loop takes each expert once)
+            const int k = pk[m];
+            for (;;) {
+                const int kw = __builtin_amdgcn_readfirstlane(k);
+                if (k == kw) {
+                    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                        (void*)tabs.t[kw], (short)0, (int)((uint32_t)L << (log2T + 3)), 0x00020000);
+                    acn::HashPendingX p;
+                    acn::hash_issue_x<INTERP>(rs, (uint32_t)l << (log2T + 3), sx, sy, sz, mask, p);
+                    acn::hash_finish_x<INTERP>(p, o0, o1);
+                    break;
+                }
+            }
+        } else {
+            const float2* tl = tabs.t[pk[m]] + ((int64_t)l << log2T);
+            acn::hash_level_f2<INTERP>(tl, sx, sy, sz, mask, o0, o1);
+        }
         out[m * L + l] = make_float2(o0, o1);
     }
 }
@@ -609,6 +626,10 @@ extern "C" int acn_hashgrid_fwd_pairs(const float* x01, const int32_t* pk, const
     const dim3 grid(2048), block(256);  // grid-stride to the device slot count
     hipStream_t s = (hipStream_t)stream;
     if (interp == 0) hipLaunchKernelGGL(hashgrid_fwd_pairs<0>, grid, block, 0, s, x01, pk, seg, K, t, r, L, log2T, (float2*)out);
+    else if (ACN_HASH_FWD_BUF && ((uint64_t)L << (log2T + 3)) <= (1ull << 31)) {
+        if (interp == 1) hipLaunchKernelGGL((hashgrid_fwd_pairs<1, true>), grid, block, 0, s, x01, pk, seg, K, t, r, L, log2T, (float2*)out);
+        else hipLaunchKernelGGL((hashgrid_fwd_pairs<2, true>), grid, block, 0, s, x01, pk, seg, K, t, r, L, log2T, (float2*)out);
+    }
     else if (interp == 1) hipLaunchKernelGGL(hashgrid_fwd_pairs<1>, grid, block, 0, s, x01, pk, seg, K, t, r, L, log2T, (float2*)out);
     else hipLaunchKernelGGL(hashgrid_fwd_pairs<2>, grid, block, 0, s, x01, pk, seg, K, t, r, L, log2T, (float2*)out);
     return acn_check_launch("acn_hashgrid_fwd_pairs");
