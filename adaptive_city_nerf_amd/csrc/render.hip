@@ -1142,6 +1142,10 @@ constexpr int kWsMaxS = 256;   // LDS field buffer: 16 rays x kWsMaxS samples x 
 #ifndef ACN_WS_PREFOLD
 #define ACN_WS_PREFOLD 1  // fold each round ray's SH colour bias once, at the round start (not per tile)
 #endif
+#ifndef ACN_WS_DTILE
+#define ACN_WS_DTILE 0    // 1: depth tiles -- a field tile = the round's 16 rays at 2 consecutive samples (lane j:
+                          // ray slot j & 15, sample 2 q + (j >> 4)) instead of one ray's 32 consecutive samples
+#endif
 
 // composite one ray from its samples' field values in LDS (ys[s] = rgb, sigma of sample s, as the field tile
 // returned them): render_ray's exact sequence without early termination -- t and dist, the volume_render
@@ -1248,6 +1252,54 @@ __global__ void __launch_bounds__(1024, 4) render_ws_kernel(FieldCfg cfg, BgArgs
             fold_sh_bias(W, sv, lane, cbuf + wave * 64);
         }
         __syncthreads();
+#if ACN_WS_DTILE
+        static_assert(!ACN_WS_DTILE || (FOLD && ACN_WS_PREFOLD && !ACN_WS_CHECK), "depth tiles read the pre-folded bias");
+        {
+            // lane j's ray is round slot (j & 15) for the whole round (both halves of the tile: the same sample);
+            // slots past the round's rays repeat its last ray and write nothing
+            const int slot = j & 15, ls = slot < nr ? slot : nr - 1;
+            const int64_t ray = p.order ? (int64_t)p.order[base + ls] : base + ls;
+            const float* rp = p.rays + ray * 8;
+            const float ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
+            const float near = rp[6], far = rp[7];
+            const float* jit = p.jitter ? p.jitter + ray * S : nullptr;
+            float* cbl = cbuf + slot * 64;
+            const float shz[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+            const int T2 = (S + 1) >> 1;
+            for (;;) {
+                int item = 0;
+                if (lane == 0) item = __hip_atomic_fetch_add(&qhead, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                item = __builtin_amdgcn_readlane(item, 0);
+                if (item >= T2) break;
+                const int s = 2 * item + (j >> 4);
+                const int sc = s < S ? s : S - 1;
+                float t;
+                if (!jit) {
+                    const int i0 = sc < S - 1 ? sc : S - 2;
+                    const float ta = tlin_sel(near, far, i0, S, step), tb = tlin_sel(near, far, i0 + 1, S, step);
+                    t = sc < S - 1 ? ta : tb;
+                } else {
+                    t = tval(near, far, sc, S, jit);
+                }
+                const float px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;
+                uint32_t fl = 1u;
+                float yr, yg, yb, ys;
+                container_tile<INTERP, 0, FOLD>(cfg, W, px, py, pz, shz, cbl, &fl, lane, yr, yg, yb, ys);
+                if (h == 0 && s < S && slot < nr) {
+                    f32x4 v;
+                    v[0] = yr, v[1] = yg, v[2] = yb, v[3] = ys;
+                    ybuf[slot * kWsMaxS + s] = v;
+                }
+            }
+            __syncthreads();   // every sample of the round's rays is in ybuf
+            if (wave < nr) {
+                const int64_t ray_w = p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[base + wave]) : base + wave;
+                composite_ray_lds(p, bg, ray_w, ybuf + wave * kWsMaxS, lane, step);
+            }
+            __syncthreads();
+            continue;
+        }
+#endif
         int64_t cur = -1;
         uint32_t folded = 0u;
         float shv[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
