@@ -1143,8 +1143,8 @@ constexpr int kWsMaxS = 256;   // LDS field buffer: 16 rays x kWsMaxS samples x 
 #define ACN_WS_PREFOLD 1  // fold each round ray's SH colour bias once, at the round start (not per tile)
 #endif
 #ifndef ACN_WS_DTILE
-#define ACN_WS_DTILE 0    // 1: depth tiles -- a field tile = the round's 16 rays at 2 consecutive samples (lane j:
-                          // ray slot j & 15, sample 2 q + (j >> 4)) instead of one ray's 32 consecutive samples
+#define ACN_WS_DTILE 0    // R > 0: depth tiles -- a field tile = R of the round's 16 rays at 32 / R consecutive
+                          // samples instead of one ray's 32 consecutive samples
 #endif
 
 // composite one ray from its samples' field values in LDS (ys[s] = rgb, sigma of sample s, as the field tile
@@ -1254,24 +1254,35 @@ __global__ void __launch_bounds__(1024, 4) render_ws_kernel(FieldCfg cfg, BgArgs
         __syncthreads();
 #if ACN_WS_DTILE
         static_assert(!ACN_WS_DTILE || (FOLD && ACN_WS_PREFOLD && !ACN_WS_CHECK), "depth tiles read the pre-folded bias");
+        static_assert(16 % (ACN_WS_DTILE > 0 ? ACN_WS_DTILE : 1) == 0, "ACN_WS_DTILE: rays per tile divide 16");
         {
-            // lane j's ray is round slot (j & 15) for the whole round (both halves of the tile: the same sample);
-            // slots past the round's rays repeat its last ray and write nothing
-            const int slot = j & 15, ls = slot < nr ? slot : nr - 1;
-            const int64_t ray = p.order ? (int64_t)p.order[base + ls] : base + ls;
-            const float* rp = p.rays + ray * 8;
-            const float ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
-            const float near = rp[6], far = rp[7];
-            const float* jit = p.jitter ? p.jitter + ray * S : nullptr;
-            float* cbl = cbuf + slot * 64;
+            // tile = R rays of one group of the round at D = 32 / R consecutive samples; lane j: slot g R + j % R,
+            // sample q D + j / R (both halves of the tile: the same sample).  Slots past the round's rays repeat
+            // its last ray and write nothing.
+            constexpr int R = ACN_WS_DTILE, D = 32 / R, NG = 16 / R;
+            const int ND = (S + D - 1) / D;
             const float shz[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-            const int T2 = (S + 1) >> 1;
+            int gcur = -1;
+            int slot = 0;
+            float ox = 0.0f, oy = 0.0f, oz = 0.0f, dx = 0.0f, dy = 0.0f, dz = 0.0f, near = 0.0f, far = 0.0f;
+            const float* jit = nullptr;
             for (;;) {
                 int item = 0;
                 if (lane == 0) item = __hip_atomic_fetch_add(&qhead, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 item = __builtin_amdgcn_readlane(item, 0);
-                if (item >= T2) break;
-                const int s = 2 * item + (j >> 4);
+                if (item >= NG * ND) break;
+                const int g = NG == 1 ? 0 : item % NG, q = NG == 1 ? item : item / NG;
+                if (g != gcur) {   // wave-uniform
+                    slot = g * R + (j % R);
+                    const int ls = slot < nr ? slot : nr - 1;
+                    const int64_t ray = p.order ? (int64_t)p.order[base + ls] : base + ls;
+                    const float* rp = p.rays + ray * 8;
+                    ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
+                    near = rp[6], far = rp[7];
+                    jit = p.jitter ? p.jitter + ray * S : nullptr;
+                    gcur = g;
+                }
+                const int s = q * D + j / R;
                 const int sc = s < S ? s : S - 1;
                 float t;
                 if (!jit) {
@@ -1284,7 +1295,7 @@ __global__ void __launch_bounds__(1024, 4) render_ws_kernel(FieldCfg cfg, BgArgs
                 const float px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;
                 uint32_t fl = 1u;
                 float yr, yg, yb, ys;
-                container_tile<INTERP, 0, FOLD>(cfg, W, px, py, pz, shz, cbl, &fl, lane, yr, yg, yb, ys);
+                container_tile<INTERP, 0, FOLD>(cfg, W, px, py, pz, shz, cbuf + slot * 64, &fl, lane, yr, yg, yb, ys);
                 if (h == 0 && s < S && slot < nr) {
                     f32x4 v;
                     v[0] = yr, v[1] = yg, v[2] = yb, v[3] = ys;
