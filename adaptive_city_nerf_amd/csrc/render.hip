@@ -1143,8 +1143,13 @@ constexpr int kWsMaxS = 256;   // LDS field buffer: 16 rays x kWsMaxS samples x 
 #define ACN_WS_PREFOLD 1  // fold each round ray's SH colour bias once, at the round start (not per tile)
 #endif
 #ifndef ACN_WS_DTILE
-#define ACN_WS_DTILE 0    // R > 0: depth tiles -- a field tile = R of the round's 16 rays at 32 / R consecutive
-                          // samples instead of one ray's 32 consecutive samples
+// R > 0: depth tiles -- a field tile = R of the round's 16 rays at 32 / R consecutive samples, instead of one ray's
+// 32 consecutive samples (0).  A wave's gathers then come from neighbouring rays at nearby depths, whose points
+// share hash lines at more levels than one ray's consecutive samples do.  C2: 3.72e9 (0) -> 3.79 (16) / 3.89 (8) /
+// 3.90 (4) / 3.86e9 (2) ray-samples/s (profiles/r06y_ws_dtile_ab.jsonl); outputs bit-identical (the field of a
+// sample does not depend on its tile-mates; compositing reads LDS per ray as before).  The self-check build
+// (ACN_WS_CHECK) keeps ray tiles.
+#define ACN_WS_DTILE (ACN_WS_CHECK ? 0 : 8)
 #endif
 
 // composite one ray from its samples' field values in LDS (ys[s] = rgb, sigma of sample s, as the field tile
