@@ -1682,6 +1682,147 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
     }
 }
 
+// Routed render in depth tiles (render_wss_kernel: C3 / C4 without early termination).  render_slots_kernel gives
+// every wave one ray and its 32-sample tiles; here, as in render_ws_kernel, the 8 rays of a workgroup round are
+// cut into tiles of R rays x 32 / R consecutive samples (ACN_WSS_DTILE), so a wave's hash gathers come from
+// neighbouring rays at nearby depths.  Per round: every wave routes its ray's samples (ray_expert_mask), the
+// counts pick the two most needed experts for the LDS slots (render_slots_kernel's rule; the others are read
+// from the packed images in global memory), the waves take tiles from an LDS counter and put each sample's
+// blended (rgb, sigma) in LDS, and after a barrier wave w composites ray w with render_ray's sequence
+// (composite_ray_lds).  A tile mixes rays, so colour layer 0 runs unfolded on each lane's own SH rows, SH k-steps
+// first (field_tile SHFIRST: bit for bit the folded layer), and the blend is the general path (for a
+// single-expert ray 0 + y * 1.0f == y): every output equals render_slots_kernel's (tests/test_k8.py).
+#ifndef ACN_RENDER_WSS
+#define ACN_RENDER_WSS 1
+#endif
+#ifndef ACN_WSS_DTILE
+#define ACN_WSS_DTILE 8
+#endif
+constexpr int kWssRays = ACN_SLOTS_THREADS / 64;   // rays per round: one per wave (routing pass)
+template <int INTERP, int ROUTE>
+__global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) render_wss_kernel(FieldCfg cfg, BgArgs bg, RenderParams p) {
+    static_assert(kWssRays % ACN_WSS_DTILE == 0 && 32 % ACN_WSS_DTILE == 0, "ACN_WSS_DTILE: rays per tile");
+    constexpr int R = ACN_WSS_DTILE, D = 32 / R, NG = kWssRays / R;
+    __shared__ __attribute__((aligned(16))) float smem[2 * PK_FLOATS];
+    __shared__ __attribute__((aligned(16))) f32x4 ybuf[kWssRays * kWsMaxS];
+    __shared__ int cnt[kMaxK];
+    __shared__ int qhead;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int S = p.S;
+    const float step = 1.0f / (float)(S - 1);
+    const int ND = (S + D - 1) / D;
+    int sk0 = -1, sk1 = -1;
+    const int64_t lim = p.norder ? (int64_t)p.norder[0] : p.N;
+    for (int64_t base = (int64_t)blockIdx.x * kWssRays; base < lim; base += (int64_t)gridDim.x * kWssRays) {
+        const int tid = opaque_v((int)threadIdx.x);
+        const int lane = tid & 63, j = lane & 31, h = lane >> 5;
+        const int nr = (int)min((int64_t)kWssRays, lim - base);
+        const bool live = wave < nr;
+        const int64_t ray = !live ? 0 : (p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[base + wave])
+                                                 : base + wave);
+        if (tid < kMaxK) cnt[tid] = 0;
+        if (tid == 0) qhead = 0;
+        __syncthreads();   // the previous round's composites are done with ybuf; counts cleared
+        const uint32_t m = ray_expert_mask(cfg, ROUTE, p, ray, live, step, lane);
+        if (lane == 0)
+            for (int k = 0; k < cfg.K; ++k)
+                if ((m >> k) & 1u) atomicAdd(&cnt[k], 1);
+        __syncthreads();
+        {   // the two most needed experts (render_slots_kernel's choice and slot keeping)
+            int b0 = -1, b1 = -1;
+            for (int k = 0; k < cfg.K; ++k) {
+                const int c = cnt[k];
+                if (c == 0) continue;
+                if (b0 < 0 || c > cnt[b0]) { b1 = b0; b0 = k; }
+                else if (b1 < 0 || c > cnt[b1]) b1 = k;
+            }
+            b0 = __builtin_amdgcn_readfirstlane(b0);
+            b1 = __builtin_amdgcn_readfirstlane(b1);
+            if (b0 == sk1 || b1 == sk0) { const int t = b0; b0 = b1; b1 = t; }
+            const bool rs0 = b0 >= 0 && b0 != sk0, rs1 = b1 >= 0 && b1 != sk1;
+            if (b0 >= 0) sk0 = b0;
+            if (b1 >= 0) sk1 = b1;
+            if (rs0 || rs1) {   // block-uniform
+                for (int sl = 0; sl < 2; ++sl) {
+                    if (sl == 0 ? !rs0 : !rs1) continue;
+                    const f32x4* src = reinterpret_cast<const f32x4*>(p.packed + (size_t)(sl == 0 ? sk0 : sk1) * PK_FLOATS);
+                    f32x4* dst = reinterpret_cast<f32x4*>(smem + sl * PK_FLOATS);
+                    for (int i = tid; i < PK_FLOATS / 4; i += blockDim.x) dst[i] = src[i];
+                }
+                __syncthreads();
+            }
+        }
+        const int k0 = sk0, k1 = sk1;
+        int gcur = -1, slot = 0;
+        float ox = 0.0f, oy = 0.0f, oz = 0.0f, dx = 0.0f, dy = 0.0f, dz = 0.0f, near = 0.0f, far = 0.0f;
+        float shv[8];
+        const float* jit = nullptr;
+        for (;;) {
+            int item = 0;
+            if (lane == 0) item = __hip_atomic_fetch_add(&qhead, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            item = __builtin_amdgcn_readlane(item, 0);
+            if (item >= NG * ND) break;
+            const int g = NG == 1 ? 0 : item % NG, q = NG == 1 ? item : item / NG;
+            if (g != gcur) {   // wave-uniform: this lane's ray of group g
+                slot = g * R + (j % R);
+                const int ls = slot < nr ? slot : nr - 1;
+                const int64_t rr = p.order ? (int64_t)p.order[base + ls] : base + ls;
+                const float* rp = p.rays + rr * 8;
+                ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
+                near = rp[6], far = rp[7];
+                jit = p.jitter ? p.jitter + rr * S : nullptr;
+                float sh[16];
+                dir_sh(dx, dy, dz, sh);
+                sh_rows_for_half(sh, h, shv);
+                gcur = g;
+            }
+            const int s = q * D + j / R;
+            const int sc = s < S ? s : S - 1;
+            float t;
+            if (!jit) {
+                const int i0 = sc < S - 1 ? sc : S - 2;
+                const float ta = tlin_sel(near, far, i0, S, step), tb = tlin_sel(near, far, i0 + 1, S, step);
+                t = sc < S - 1 ? ta : tb;
+            } else {
+                t = tval(near, far, sc, S, jit);
+            }
+            const float px = ox + dx * t, py = oy + dy * t, pz = oz + dz * t;
+            const RouteState st = route_prep<ROUTE>(cfg, px, py, pz);
+            float yr = 0.0f, yg = 0.0f, yb = 0.0f, ys = 0.0f;
+            for (int k = 0; k < cfg.K; ++k) {
+                const float wk = (ROUTE == 1) ? route_weight(cfg, st, k, px, py, pz) : 0.0f;
+                const bool need = (ROUTE == 1) ? (wk > 0.0f) : (st.hard == k);
+                if (__ballot(need) == 0ull) continue;
+                float r, gg, b, sg;
+                if (k == k0 || k == k1)   // wave-uniform; separate call sites keep LDS and global reads of the image
+                    field_tile<INTERP, false, true>(smem + (k == k0 ? 0 : PK_FLOATS), cfg.ex[k], cfg.log2T, px, py, pz,
+                                                    shv, nullptr, lane, r, gg, b, sg);
+                else
+                    field_tile<INTERP, false, true>(p.packed + (size_t)k * PK_FLOATS, cfg.ex[k], cfg.log2T, px, py, pz,
+                                                    shv, nullptr, lane, r, gg, b, sg);
+                sg = trunc_exp(sg);
+                if (need) {
+                    if (ROUTE == 1) {
+                        yr = yr + r * wk;
+                        yg = yg + gg * wk;
+                        yb = yb + b * wk;
+                        ys = ys + sg * wk;
+                    } else {
+                        yr = r; yg = gg; yb = b; ys = sg;
+                    }
+                }
+            }
+            if (h == 0 && s < S && slot < nr) {
+                f32x4 v;
+                v[0] = yr, v[1] = yg, v[2] = yb, v[3] = ys;
+                ybuf[slot * kWsMaxS + s] = v;
+            }
+        }
+        __syncthreads();   // every sample of the round's rays is in ybuf
+        if (live) composite_ray_lds(p, bg, ray, ybuf + wave * kWsMaxS, lane, step);
+    }
+}
+
 // inclusive scan over the 64 lanes of a wave on DPP: row_shr 1/2/4/8 inside each 16-lane row, then
 // row_bcast:15 / :31 carry the row totals upward (gfx9-family DPP)
 __device__ __forceinline__ int wave_incl_scan(int v) {
@@ -2749,9 +2890,11 @@ extern "C" int acn_render_stratified_fwd_ordered(const float* rays, int64_t N, i
         hipLaunchKernelGGL(ray_order_kernel, dim3(1), dim3(1024), 0, s, rays, (int)N, (int32_t*)order_scratch);
         p.order = (const int32_t*)order_scratch;
     }
+    const bool wss = ACN_RENDER_WSS && S <= kWsMaxS && !(tau > 0.0f);   // routed, no early termination: depth tiles
 #define ACN_RENDER_LAUNCH(I, KL, R)                                                                    \
     do {                                                                                              \
-        if (ACN_SLOTS && KL == 0 && R != 0) hipLaunchKernelGGL((render_slots_kernel<I, (R == 0 ? 1 : R)>), grid, dim3(ACN_SLOTS_THREADS), 0, s, cfg, b, p); \
+        if (ACN_SLOTS && KL == 0 && R != 0 && wss) hipLaunchKernelGGL((render_wss_kernel<I, (R == 0 ? 1 : R)>), grid, dim3(ACN_SLOTS_THREADS), 0, s, cfg, b, p); \
+        else if (ACN_SLOTS && KL == 0 && R != 0) hipLaunchKernelGGL((render_slots_kernel<I, (R == 0 ? 1 : R)>), grid, dim3(ACN_SLOTS_THREADS), 0, s, cfg, b, p); \
         else hipLaunchKernelGGL((render_kernel<I, KL, R>), grid, block, 0, s, cfg, b, p);            \
     } while (0)
     if (ACN_RENDER_WS && cfg.routing == 0 && S <= kWsMaxS && !(tau > 0.0f)) {

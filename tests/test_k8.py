@@ -102,6 +102,24 @@ def test_render_rays_k8_vs_reference(variant, tau):
     assert np.abs(w.cpu().numpy() - d[f"{variant}:weights"]).max() <= 1e-5
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["render", "render_hi"])
+@pytest.mark.parametrize("S", [64, 96])
+def test_depth_tiled_routed_render_equals_ray_tiles(variant, S):
+    """render_wss_kernel (tau = 0: depth tiles of 8 rays x 4 samples, unfolded SH-first colour layer, LDS compositing)
+    renders every ray bit for bit like render_slots_kernel (taken with an early-termination threshold so small that
+    only an underflowed transmittance, whose later samples add exact zeros, can stop a ray): rgb, depth, weights, acc."""
+    from adaptive_city_nerf_amd import render_rays
+    d = G.load("render_k8")
+    m, _ = _model(d, "hiw:" if variant == "render_hi" else "w:")
+    rays = torch.from_numpy(d["render:rays"]).cuda()
+    with torch.no_grad():
+        a = render_rays(m, rays, ray_samples=S, bg_color_default="white")
+        b = render_rays(m, rays, ray_samples=S, bg_color_default="white", early_stop_tau=1e-37)
+    for x, y, name in zip(a, b, ("rgb", "depth", "weights", "acc")):
+        assert torch.equal(x, y), name
+
+
 def _single_expert_rays(rays, S, sc, bm):
     """Per ray: the one expert every sample routes to with weight exactly 1.0f (else -1), from the
     oracle's routing at the eval t-values (linspace as torch CPU, ray_rendering.py:278-287)."""
