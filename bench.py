@@ -358,7 +358,7 @@ def load_traffic(name: str = "render", rnd: str = "r01"):
 def render_traffic_profile(workload: str, S: int, layout: str):
     """Counter summary of the render line's dominant kernel (tools/pmc_r04.sh + tools/pmc_fold_r04.py: separate
     rocprofv3 --pmc passes, FETCH_SIZE doubled per the gfx950 correction of MI355X_MICROARCH.md 'HBM', plus
-    WRITE_SIZE) -- round 6, the final render build (buffer-load gathers; C4 at S = 256 not re-profiled) -- or None
+    WRITE_SIZE) -- round 6, the final render build (buffer-load gathers, depth tiles; C4 at S = 256 not profiled) -- or None
     when no profile of this exact configuration is committed."""
     name = {("c2", 256, "replicated"): "r06_pmc_c2_render.json",
             ("c3", 256, "replicated"): "r06_pmc_c3_render.json",
@@ -997,13 +997,15 @@ def main():
              "c5a": "adam_kernel (fused clip + Adam over the adapted expert + background head)",
              "c2": "ray_order_kernel + render_ws_kernel<1> (one acn_render_stratified_fwd_ordered call: direction "
                    "grouping of the batch, then the fused stratified render, 1 expert, the workgroup's 16 rays "
-                   "sharing their 32-sample field tiles; kernel_ms = two HIP events bracketing the K timed calls on "
-                   "the launch stream / K)",
-             "c3": "render_slots_kernel (fused stratified render, soft routing over 4 experts, two staged per round)",
+                   "sharing their field tiles, each tile 8 rays x 4 consecutive samples; kernel_ms = two HIP events "
+                   "bracketing the K timed calls on the launch stream / K)",
+             "c3": "render_wss_kernel (fused stratified render, soft routing over 4 experts, two staged per round, "
+                   "field tiles of 8 rays x 4 consecutive samples)",
              "c4": ("ep_field_kernel (the owned expert's fused MFMA field over the received per-sample records; "
                     "one-expert-per-GPU layout, kernel_ms per launch)"
                     if a.layout == "expert" else
-                    "render_slots_kernel (fused stratified render, soft routing over 8 experts, two staged per round)"),
+                    "render_wss_kernel (fused stratified render, soft routing over 8 experts, two staged per round, "
+                    "field tiles of 8 rays x 4 consecutive samples)"),
              "occ": "occ_render_kernel<1,1,0> (fused occupancy render over packed marched samples, 1 expert)",
              "meta": "adam_kernel (fused clip + Adam of the outer meta-update over the region experts + shared head)",
              "data": "route_kernel (TaskDataset region clip + DDA max-overlap micro-cell routing + keep tolerance)",
