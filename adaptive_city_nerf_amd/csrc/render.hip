@@ -1698,13 +1698,19 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
 #ifndef ACN_WSS_DTILE
 #define ACN_WSS_DTILE 8
 #endif
-constexpr int kWssRays = ACN_SLOTS_THREADS / 64;   // rays per round: one per wave (routing pass)
+#ifndef ACN_WSS_RAYS
+#define ACN_WSS_RAYS 8    // rays per round: 8 (one per wave) up to S = 256, or 16 (two per wave) up to S = 128
+#endif
+constexpr int kWssRays = ACN_WSS_RAYS;
+constexpr int kWssMaxS = kWssRays == 8 ? kWsMaxS : 128;   // LDS: 2 expert images + kWssRays x kWssMaxS x 16 B
+constexpr int kWssPerWave = kWssRays / (ACN_SLOTS_THREADS / 64);
 template <int INTERP, int ROUTE>
 __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) render_wss_kernel(FieldCfg cfg, BgArgs bg, RenderParams p) {
     static_assert(kWssRays % ACN_WSS_DTILE == 0 && 32 % ACN_WSS_DTILE == 0, "ACN_WSS_DTILE: rays per tile");
     constexpr int R = ACN_WSS_DTILE, D = 32 / R, NG = kWssRays / R;
     __shared__ __attribute__((aligned(16))) float smem[2 * PK_FLOATS];
-    __shared__ __attribute__((aligned(16))) f32x4 ybuf[kWssRays * kWsMaxS];
+    __shared__ __attribute__((aligned(16))) f32x4 ybuf[kWssRays * kWssMaxS];
+    static_assert(kWssPerWave >= 1 && kWssRays == kWssPerWave * (ACN_SLOTS_THREADS / 64), "ACN_WSS_RAYS");
     __shared__ int cnt[kMaxK];
     __shared__ int qhead;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1717,16 +1723,19 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
         const int tid = opaque_v((int)threadIdx.x);
         const int lane = tid & 63, j = lane & 31, h = lane >> 5;
         const int nr = (int)min((int64_t)kWssRays, lim - base);
-        const bool live = wave < nr;
-        const int64_t ray = !live ? 0 : (p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[base + wave])
-                                                 : base + wave);
         if (tid < kMaxK) cnt[tid] = 0;
         if (tid == 0) qhead = 0;
         __syncthreads();   // the previous round's composites are done with ybuf; counts cleared
-        const uint32_t m = ray_expert_mask(cfg, ROUTE, p, ray, live, step, lane);
-        if (lane == 0)
-            for (int k = 0; k < cfg.K; ++k)
-                if ((m >> k) & 1u) atomicAdd(&cnt[k], 1);
+        for (int u = 0; u < kWssPerWave; ++u) {   // wave w routes round slots w, w + 8, ...
+            const int sl = wave + u * (ACN_SLOTS_THREADS / 64);
+            const bool live = sl < nr;
+            const int64_t ray = !live ? 0 : (p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[base + sl])
+                                                     : base + sl);
+            const uint32_t m = ray_expert_mask(cfg, ROUTE, p, ray, live, step, lane);
+            if (lane == 0)
+                for (int k = 0; k < cfg.K; ++k)
+                    if ((m >> k) & 1u) atomicAdd(&cnt[k], 1);
+        }
         __syncthreads();
         {   // the two most needed experts (render_slots_kernel's choice and slot keeping)
             int b0 = -1, b1 = -1;
@@ -1815,11 +1824,16 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
             if (h == 0 && s < S && slot < nr) {
                 f32x4 v;
                 v[0] = yr, v[1] = yg, v[2] = yb, v[3] = ys;
-                ybuf[slot * kWsMaxS + s] = v;
+                ybuf[slot * kWssMaxS + s] = v;
             }
         }
         __syncthreads();   // every sample of the round's rays is in ybuf
-        if (live) composite_ray_lds(p, bg, ray, ybuf + wave * kWsMaxS, lane, step);
+        for (int u = 0; u < kWssPerWave; ++u) {
+            const int sl = wave + u * (ACN_SLOTS_THREADS / 64);
+            if (sl >= nr) break;
+            const int64_t ray = p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[base + sl]) : base + sl;
+            composite_ray_lds(p, bg, ray, ybuf + sl * kWssMaxS, lane, step);
+        }
     }
 }
 
@@ -2890,7 +2904,7 @@ extern "C" int acn_render_stratified_fwd_ordered(const float* rays, int64_t N, i
         hipLaunchKernelGGL(ray_order_kernel, dim3(1), dim3(1024), 0, s, rays, (int)N, (int32_t*)order_scratch);
         p.order = (const int32_t*)order_scratch;
     }
-    const bool wss = ACN_RENDER_WSS && S <= kWsMaxS && !(tau > 0.0f);   // routed, no early termination: depth tiles
+    const bool wss = ACN_RENDER_WSS && S <= kWssMaxS && !(tau > 0.0f);   // routed, no early termination: depth tiles
 #define ACN_RENDER_LAUNCH(I, KL, R)                                                                    \
     do {                                                                                              \
         if (ACN_SLOTS && KL == 0 && R != 0 && wss) hipLaunchKernelGGL((render_wss_kernel<I, (R == 0 ? 1 : R)>), grid, dim3(ACN_SLOTS_THREADS), 0, s, cfg, b, p); \
