@@ -1695,22 +1695,27 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
 #ifndef ACN_RENDER_WSS
 #define ACN_RENDER_WSS 1
 #endif
-#ifndef ACN_WSS_DTILE
-#define ACN_WSS_DTILE 8
+// Rounds (RW = rays per round, LDS ybuf = RW x kWssMaxS(RW) samples x 16 B = 32 KB beside the two expert images):
+// 16 rays (two per wave) in tiles of 16 rays x 2 samples up to S = 128, else 8 rays in tiles of 8 x 4.  C4-S96:
+// 3.12e9 (8 / 8 x 4) -> 3.17e9 (16 / 8 x 4) -> 3.27e9 (16 / 16 x 2) ray-samples/s (profiles/r06ac_wss_rounds_ab.jsonl)
+#ifndef ACN_WSS_DTILE8
+#define ACN_WSS_DTILE8 8     // rays per tile in 8-ray rounds
 #endif
-#ifndef ACN_WSS_RAYS
-#define ACN_WSS_RAYS 8    // rays per round: 8 (one per wave) up to S = 256, or 16 (two per wave) up to S = 128
+#ifndef ACN_WSS_DTILE16
+#define ACN_WSS_DTILE16 16   // rays per tile in 16-ray rounds
 #endif
-constexpr int kWssRays = ACN_WSS_RAYS;
-constexpr int kWssMaxS = kWssRays == 8 ? kWsMaxS : 128;   // LDS: 2 expert images + kWssRays x kWssMaxS x 16 B
-constexpr int kWssPerWave = kWssRays / (ACN_SLOTS_THREADS / 64);
-template <int INTERP, int ROUTE>
+#ifndef ACN_WSS_RAYS16
+#define ACN_WSS_RAYS16 1     // 0: 8-ray rounds at every S
+#endif
+constexpr int kWssMaxS(int rw) { return rw == 8 ? kWsMaxS : 128; }
+template <int INTERP, int ROUTE, int RW>
 __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) render_wss_kernel(FieldCfg cfg, BgArgs bg, RenderParams p) {
-    static_assert(kWssRays % ACN_WSS_DTILE == 0 && 32 % ACN_WSS_DTILE == 0, "ACN_WSS_DTILE: rays per tile");
-    constexpr int R = ACN_WSS_DTILE, D = 32 / R, NG = kWssRays / R;
+    constexpr int kWssRays = RW, kWssPerWave = RW / (ACN_SLOTS_THREADS / 64), kMaxS = kWssMaxS(RW);
+    constexpr int R = RW == 8 ? ACN_WSS_DTILE8 : ACN_WSS_DTILE16, D = 32 / R, NG = kWssRays / R;
+    static_assert(kWssRays % R == 0 && 32 % R == 0, "ACN_WSS_DTILE*: rays per tile");
     __shared__ __attribute__((aligned(16))) float smem[2 * PK_FLOATS];
-    __shared__ __attribute__((aligned(16))) f32x4 ybuf[kWssRays * kWssMaxS];
-    static_assert(kWssPerWave >= 1 && kWssRays == kWssPerWave * (ACN_SLOTS_THREADS / 64), "ACN_WSS_RAYS");
+    __shared__ __attribute__((aligned(16))) f32x4 ybuf[kWssRays * kMaxS];
+    static_assert(kWssPerWave >= 1 && kWssRays == kWssPerWave * (ACN_SLOTS_THREADS / 64), "rays per round");
     __shared__ int cnt[kMaxK];
     __shared__ int qhead;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1824,7 +1829,7 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
             if (h == 0 && s < S && slot < nr) {
                 f32x4 v;
                 v[0] = yr, v[1] = yg, v[2] = yb, v[3] = ys;
-                ybuf[slot * kWssMaxS + s] = v;
+                ybuf[slot * kMaxS + s] = v;
             }
         }
         __syncthreads();   // every sample of the round's rays is in ybuf
@@ -1832,7 +1837,7 @@ __global__ void __launch_bounds__(ACN_SLOTS_THREADS, ACN_SLOTS_THREADS / 256) re
             const int sl = wave + u * (ACN_SLOTS_THREADS / 64);
             if (sl >= nr) break;
             const int64_t ray = p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[base + sl]) : base + sl;
-            composite_ray_lds(p, bg, ray, ybuf + sl * kWssMaxS, lane, step);
+            composite_ray_lds(p, bg, ray, ybuf + sl * kMaxS, lane, step);
         }
     }
 }
@@ -2904,10 +2909,12 @@ extern "C" int acn_render_stratified_fwd_ordered(const float* rays, int64_t N, i
         hipLaunchKernelGGL(ray_order_kernel, dim3(1), dim3(1024), 0, s, rays, (int)N, (int32_t*)order_scratch);
         p.order = (const int32_t*)order_scratch;
     }
-    const bool wss = ACN_RENDER_WSS && S <= kWssMaxS && !(tau > 0.0f);   // routed, no early termination: depth tiles
+    const bool wss = ACN_RENDER_WSS && S <= kWssMaxS(8) && !(tau > 0.0f);   // routed, no early termination: depth tiles
+    const bool wss16 = ACN_WSS_RAYS16 && S <= kWssMaxS(16);
 #define ACN_RENDER_LAUNCH(I, KL, R)                                                                    \
     do {                                                                                              \
-        if (ACN_SLOTS && KL == 0 && R != 0 && wss) hipLaunchKernelGGL((render_wss_kernel<I, (R == 0 ? 1 : R)>), grid, dim3(ACN_SLOTS_THREADS), 0, s, cfg, b, p); \
+        if (ACN_SLOTS && KL == 0 && R != 0 && wss && wss16) hipLaunchKernelGGL((render_wss_kernel<I, (R == 0 ? 1 : R), 16>), grid, dim3(ACN_SLOTS_THREADS), 0, s, cfg, b, p); \
+        else if (ACN_SLOTS && KL == 0 && R != 0 && wss) hipLaunchKernelGGL((render_wss_kernel<I, (R == 0 ? 1 : R), 8>), grid, dim3(ACN_SLOTS_THREADS), 0, s, cfg, b, p); \
         else if (ACN_SLOTS && KL == 0 && R != 0) hipLaunchKernelGGL((render_slots_kernel<I, (R == 0 ? 1 : R)>), grid, dim3(ACN_SLOTS_THREADS), 0, s, cfg, b, p); \
         else hipLaunchKernelGGL((render_kernel<I, KL, R>), grid, block, 0, s, cfg, b, p);            \
     } while (0)

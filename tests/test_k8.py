@@ -104,9 +104,10 @@ def test_render_rays_k8_vs_reference(variant, tau):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("variant", ["render", "render_hi"])
-@pytest.mark.parametrize("S", [64, 96])
+@pytest.mark.parametrize("S", [64, 96, 200])
 def test_depth_tiled_routed_render_equals_ray_tiles(variant, S):
-    """render_wss_kernel (tau = 0: depth tiles of 8 rays x 4 samples, unfolded SH-first colour layer, LDS compositing)
+    """render_wss_kernel (tau = 0: depth tiles -- 16-ray rounds in 16 x 2 tiles up to S = 128, 8-ray rounds in 8 x 4
+    tiles above -- unfolded SH-first colour layer, LDS compositing)
     renders every ray bit for bit like render_slots_kernel (taken with an early-termination threshold so small that
     only an underflowed transmittance, whose later samples add exact zeros, can stop a ray): rgb, depth, weights, acc."""
     from adaptive_city_nerf_amd import render_rays
