@@ -1151,9 +1151,6 @@ constexpr int kWsMaxS = 256;   // LDS field buffer: 16 rays x kWsMaxS samples x 
 // (ACN_WS_CHECK) keeps ray tiles.
 #define ACN_WS_DTILE (ACN_WS_CHECK ? 0 : 8)
 #endif
-#ifndef ACN_WS_OVERLAP
-#define ACN_WS_OVERLAP 0  // depth tiles: composite a ray group's rays while the next group's tiles still run
-#endif
 
 // composite one ray from its samples' field values in LDS (ys[s] = rgb, sigma of sample s, as the field tile
 // returned them): render_ray's exact sequence without early termination -- t and dist, the volume_render
@@ -1278,24 +1275,8 @@ __global__ void __launch_bounds__(1024, 4) render_ws_kernel(FieldCfg cfg, BgArgs
                 int item = 0;
                 if (lane == 0) item = __hip_atomic_fetch_add(&qhead, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 item = __builtin_amdgcn_readlane(item, 0);
-#if ACN_WS_OVERLAP
-                // group-major tiles, then one job per ray: composite it once its group's tiles are all in ybuf (the
-                // group's tiles were all handed out before this job, so the wait ends) -- the first group's rays
-                // composite while the other waves still evaluate the last group's tiles
-                if (item >= NG * ND + nr) break;
-                if (item >= NG * ND) {
-                    const int sl = item - NG * ND, gg = sl / R;
-                    while (__hip_atomic_load(&done[gg], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < ND)
-                        __builtin_amdgcn_s_sleep(1);
-                    const int64_t ray_c = p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[base + sl]) : base + sl;
-                    composite_ray_lds(p, bg, ray_c, ybuf + sl * kWsMaxS, lane, step);
-                    continue;
-                }
-                const int g = NG == 1 ? 0 : item / ND, q = NG == 1 ? item : item % ND;
-#else
                 if (item >= NG * ND) break;
                 const int g = NG == 1 ? 0 : item % NG, q = NG == 1 ? item : item / NG;
-#endif
                 if (g != gcur) {   // wave-uniform
                     slot = g * R + (j % R);
                     const int ls = slot < nr ? slot : nr - 1;
@@ -1325,18 +1306,12 @@ __global__ void __launch_bounds__(1024, 4) render_ws_kernel(FieldCfg cfg, BgArgs
                     v[0] = yr, v[1] = yg, v[2] = yb, v[3] = ys;
                     ybuf[slot * kWsMaxS + s] = v;
                 }
-#if ACN_WS_OVERLAP
-                // the wave's ybuf writes are ordered before its count (workgroup-scope release / acquire)
-                if (lane == 0) __hip_atomic_fetch_add(&done[g], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
             }
-#if !ACN_WS_OVERLAP
             __syncthreads();   // every sample of the round's rays is in ybuf
             if (wave < nr) {
                 const int64_t ray_w = p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[base + wave]) : base + wave;
                 composite_ray_lds(p, bg, ray_w, ybuf + wave * kWsMaxS, lane, step);
             }
-#endif
             __syncthreads();
             continue;
         }
