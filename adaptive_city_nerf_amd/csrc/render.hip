@@ -47,10 +47,6 @@ using namespace acn;
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// render_ws_kernel's self-derived visiting order (defined with ray_order_kernel below)
-__device__ __forceinline__ void ws_order_setup(const float* __restrict__ rays, int N, uint16_t* key, int* start, float* red);
-__device__ __forceinline__ int ws_order_pick(const uint16_t* key, const int* start, int N, int pos, int lane);
-
 namespace {
 
 __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
@@ -947,7 +943,6 @@ struct RenderParams {
     const int32_t* order;  // optional visiting order (ray_order_kernel); NULL = rays in the given order
     const int32_t* norder; // render_slots_kernel: device count of `order` entries (the multi-expert rays of the
                            // split routed render); NULL = N
-    int32_t self_order;    // render_ws_kernel: every workgroup derives the direction-cell order itself (ws_order_*)
 };
 
 #ifndef ACN_SHFOLD
@@ -1157,12 +1152,6 @@ constexpr int kWsMaxS = 256;   // LDS field buffer: 16 rays x kWsMaxS samples x 
 #define ACN_WS_DTILE (ACN_WS_CHECK ? 0 : 8)
 #endif
 
-#ifndef ACN_WS_SELF_ORDER
-#define ACN_WS_SELF_ORDER 1   // render_ws_kernel derives the visiting order in its prologue (no ray_order_kernel)
-#endif
-constexpr int kWsOrdMax = 8192, kWsOrdBins = 4096;   // = ACN_ORDER_MAX / ACN_ORDER_BINS (ray_order_kernel)
-constexpr int kWsSelfRounds = 4;                     // rounds per workgroup the self-derived order covers
-
 // composite one ray from its samples' field values in LDS (ys[s] = rgb, sigma of sample s, as the field tile
 // returned them): render_ray's exact sequence without early termination -- t and dist, the volume_render
 // conditioning, composite_tile in tile order, weights, background, the double reductions, the outputs
@@ -1228,7 +1217,6 @@ __global__ void __launch_bounds__(1024, 4) render_ws_kernel(FieldCfg cfg, BgArgs
     __shared__ __attribute__((aligned(16))) f32x4 ybuf[16 * kWsMaxS];
     __shared__ int qhead;
     __shared__ int done[16];
-    __shared__ int ord_loc[kWsSelfRounds * 16];   // self_order: the rays at this workgroup's round positions
     stage_weights<1>(smem, p.packed);
     const float* W = smem;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1249,31 +1237,7 @@ __global__ void __launch_bounds__(1024, 4) render_ws_kernel(FieldCfg cfg, BgArgs
         base = (int64_t)blockIdx.x * 16;
         stride = (int64_t)gridDim.x * 16;
     }
-    const bool sord = ACN_WS_SELF_ORDER && p.self_order;   // block-uniform
-    if (sord) {
-        // the direction-cell order of the whole batch (ray_order_kernel's keys), derived by every workgroup from
-        // the same data with the same arithmetic, so all agree; ybuf is scratch until the first round.  Wave w
-        // then picks the ray at position base + w of each of its rounds (at most kWsSelfRounds: the host checks)
-        uint16_t* key = reinterpret_cast<uint16_t*>(ybuf);
-        int* start = reinterpret_cast<int*>(ybuf) + kWsOrdMax / 2;
-        float* red = reinterpret_cast<float*>(start + kWsOrdBins);
-        ws_order_setup(p.rays, (int)p.N, key, start, red);
-        const int lane0 = (int)(threadIdx.x & 63);
-        int r = 0;
-        for (int64_t b = base; b < hi && r < kWsSelfRounds; b += stride, ++r) {
-            const int64_t pos = b + wave;
-            if (pos < hi) {
-                const int ri = ws_order_pick(key, start, (int)p.N, (int)pos, lane0);
-                if (lane0 == 0) ord_loc[r * 16 + wave] = ri;
-            }
-        }
-        __syncthreads();   // ord_loc complete; ybuf free for the rounds
-    }
-    for (int rnd = 0; base < hi; base += stride, ++rnd) {   // block-uniform
-        // the ray at round slot sl: the self-derived order, the given order, or the position itself
-        auto ray_at = [&](int sl) -> int64_t {
-            return sord ? (int64_t)ord_loc[rnd * 16 + sl] : (p.order ? (int64_t)p.order[base + sl] : base + sl);
-        };
+    for (; base < hi; base += stride) {   // block-uniform
         // the lane index re-derived per round through an opaque copy: the per-lane LDS addresses and constants
         // formed from it stay inside the loop instead of being hoisted into registers held across it (spilled)
         const int tid = opaque_v((int)threadIdx.x);
@@ -1285,7 +1249,7 @@ __global__ void __launch_bounds__(1024, 4) render_ws_kernel(FieldCfg cfg, BgArgs
         constexpr bool PRE = FOLD && ACN_WS_PREFOLD;
         if (PRE && wave < nr) {
             // wave w folds round slot w's colour bias into cbuf[w] once; every tile of that ray reads it there
-            const int64_t r0 = __builtin_amdgcn_readfirstlane((int)ray_at(wave));
+            const int64_t r0 = p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[base + wave]) : base + wave;
             const float* rp = p.rays + r0 * 8;
             float sh[16], sv[8];
             dir_sh(rp[3], rp[4], rp[5], sh, kz);
@@ -1316,7 +1280,7 @@ __global__ void __launch_bounds__(1024, 4) render_ws_kernel(FieldCfg cfg, BgArgs
                 if (g != gcur) {   // wave-uniform
                     slot = g * R + (j % R);
                     const int ls = slot < nr ? slot : nr - 1;
-                    const int64_t ray = ray_at(ls);
+                    const int64_t ray = p.order ? (int64_t)p.order[base + ls] : base + ls;
                     const float* rp = p.rays + ray * 8;
                     ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
                     near = rp[6], far = rp[7];
@@ -1345,7 +1309,7 @@ __global__ void __launch_bounds__(1024, 4) render_ws_kernel(FieldCfg cfg, BgArgs
             }
             __syncthreads();   // every sample of the round's rays is in ybuf
             if (wave < nr) {
-                const int64_t ray_w = __builtin_amdgcn_readfirstlane((int)ray_at(wave));
+                const int64_t ray_w = p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[base + wave]) : base + wave;
                 composite_ray_lds(p, bg, ray_w, ybuf + wave * kWsMaxS, lane, step);
             }
             __syncthreads();
@@ -1363,7 +1327,7 @@ __global__ void __launch_bounds__(1024, 4) render_ws_kernel(FieldCfg cfg, BgArgs
             item = __builtin_amdgcn_readlane(item, 0);
             if (item >= nr * T) break;
             const int tile = item / nr, slot = item - tile * nr;
-            const int64_t ray = __builtin_amdgcn_readfirstlane((int)ray_at(slot));
+            const int64_t ray = p.order ? (int64_t)__builtin_amdgcn_readfirstlane(p.order[base + slot]) : base + slot;
             if (ray != cur) {
                 const float* rp = p.rays + ray * 8;
                 ox = rp[0], oy = rp[1], oz = rp[2], dx = rp[3], dy = rp[4], dz = rp[5];
@@ -2666,122 +2630,6 @@ __device__ __forceinline__ bool dir_ok(float x, float y, float z) {
     const float n2 = x * x + y * y + z * z;
     return n2 > 0.0f && n2 < 3.0e38f;  // finite, non-zero
 }
-// render_ws_kernel's self-derived visiting order (ACN_WS_SELF_ORDER): ray_order_kernel's direction cells, computed
-// in every workgroup's prologue instead of by a single-workgroup kernel launched before the render.  The order is a
-// total one -- by (cell, ray index) -- so every workgroup agrees on it: same data, same arithmetic, deterministic
-// reductions.  key[i] = cell of ray i (LDS), start[c] = first position of cell c (exclusive scan of the counts).
-static_assert(kWsOrdMax == ACN_ORDER_MAX && kWsOrdBins == ACN_ORDER_BINS, "self-order sizes");
-__device__ __forceinline__ void ws_order_setup(const float* __restrict__ rays, int N, uint16_t* key, int* start, float* red) {
-    constexpr int PER = ACN_ORDER_MAX / 1024;
-    const int tid = threadIdx.x;
-    float dxq[PER], dyq[PER], dzq[PER];
-    float sx = 0.0f, sy = 0.0f, sz = 0.0f;
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-        const int i = tid + q * 1024;
-        dxq[q] = dyq[q] = dzq[q] = 0.0f;
-        if (i < N) {
-            const float* rp = rays + (int64_t)i * 8;
-            const float x = rp[3], y = rp[4], z = rp[5];
-            dxq[q] = x, dyq[q] = y, dzq[q] = z;
-            if (dir_ok(x, y, z)) {
-                const float r = rsqrtf(x * x + y * y + z * z);
-                sx += x * r, sy += y * r, sz += z * r;
-            }
-        }
-    }
-    block_reduce3<0>(sx, sy, sz, red);
-    const float mn = sqrtf(sx * sx + sy * sy + sz * sz);
-    float mx = 0.0f, my = 0.0f, mz = 1.0f;
-    if (mn > 0.0f && mn < 3.0e38f) mx = sx / mn, my = sy / mn, mz = sz / mn;
-    float ax = 0.0f, ay = 0.0f, az = 0.0f;
-    if (fabsf(mx) <= fabsf(my) && fabsf(mx) <= fabsf(mz)) ax = 1.0f;
-    else if (fabsf(my) <= fabsf(mz)) ay = 1.0f;
-    else az = 1.0f;
-    float e1x = my * az - mz * ay, e1y = mz * ax - mx * az, e1z = mx * ay - my * ax;
-    const float e1n = rsqrtf(e1x * e1x + e1y * e1y + e1z * e1z);
-    e1x *= e1n, e1y *= e1n, e1z *= e1n;
-    const float e2x = my * e1z - mz * e1y, e2y = mz * e1x - mx * e1z, e2z = mx * e1y - my * e1x;
-    float umin = 3.0e38f, vmin = 3.0e38f, umax = -3.0e38f, vmax = -3.0e38f;
-    float cu[PER], cv[PER];
-    bool cok[PER];
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-        const int i = tid + q * 1024;
-        const float x = dxq[q], y = dyq[q], z = dzq[q];
-        cok[q] = false;
-        cu[q] = cv[q] = 0.0f;
-        if (i < N && dir_ok(x, y, z)) {
-            const float dm = x * mx + y * my + z * mz;
-            if (dm > 0.0f) {
-                const float u = (x * e1x + y * e1y + z * e1z) / dm, v = (x * e2x + y * e2y + z * e2z) / dm;
-                if (fabsf(u) < 1.0e30f && fabsf(v) < 1.0e30f) {
-                    cok[q] = true, cu[q] = u, cv[q] = v;
-                    umin = fminf(umin, u), umax = fmaxf(umax, u), vmin = fminf(vmin, v), vmax = fmaxf(vmax, v);
-                }
-            }
-        }
-    }
-    umin = -umin, vmin = -vmin;
-    block_reduce4max(umin, vmin, umax, vmax, red);
-    umin = -umin, vmin = -vmin;
-    const float su = umax > umin ? 63.999f / (umax - umin) : 0.0f;
-    const float sv = vmax > vmin ? 63.999f / (vmax - vmin) : 0.0f;
-    for (int b = tid; b < ACN_ORDER_BINS; b += 1024) start[b] = 0;
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-        const int i = tid + q * 1024;
-        if (i >= N) break;
-        int c = ACN_ORDER_BINS - 1;
-        if (cok[q]) {
-            const uint32_t qu = (uint32_t)fminf(fmaxf((cu[q] - umin) * su, 0.0f), 63.0f);
-            const uint32_t qv = (uint32_t)fminf(fmaxf((cv[q] - vmin) * sv, 0.0f), 63.0f);
-            c = (int)(spread6(qu) | (spread6(qv) << 1));
-        }
-        key[i] = (uint16_t)c;
-        atomicAdd(&start[c], 1);
-    }
-    __syncthreads();
-    // exclusive scan of the 4096 counts: 4 consecutive cells per thread, wave scans, wave totals
-    constexpr int BPT = ACN_ORDER_BINS / 1024;
-    int c[BPT], tot = 0;
-#pragma unroll
-    for (int k = 0; k < BPT; ++k) c[k] = start[tid * BPT + k], tot += c[k];
-    const int incl = wave_incl_scan(tot);
-    int* wsum = reinterpret_cast<int*>(red);
-    if ((tid & 63) == 63) wsum[tid >> 6] = incl;
-    __syncthreads();
-    int run = incl - tot;
-    for (int w = 0; w < (tid >> 6); ++w) run += wsum[w];
-#pragma unroll
-    for (int k = 0; k < BPT; ++k) start[tid * BPT + k] = run, run += c[k];
-    __syncthreads();
-}
-// the ray at position pos of the order (wave-uniform result): cell = the last with start <= pos, then the
-// (pos - start)-th ray of that cell in index order, found by one wave sweeping the keys with ballots
-__device__ __forceinline__ int ws_order_pick(const uint16_t* key, const int* start, int N, int pos, int lane) {
-    int lo = 0, hi = ACN_ORDER_BINS - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (start[mid] <= pos) lo = mid;
-        else hi = mid - 1;
-    }
-    int o = pos - start[lo];
-    for (int i0 = 0; i0 < N; i0 += 64) {
-        const int i = i0 + lane;
-        const bool m = i < N && (int)key[i] == lo;
-        const uint64_t b = __ballot(m);
-        const int c = __popcll(b);
-        if (o < c) {
-            const int below = __popcll(b & ((1ull << lane) - 1ull));
-            const uint64_t sel = __ballot(m && below == o);
-            return i0 + (int)__builtin_ctzll(sel);
-        }
-        o -= c;
-    }
-    return N - 1;   // not reached: pos < N lies in a non-empty cell
-}
 // One stable LSD radix pass over N <= ACN_ORDER_MAX 16-bit keys by digit (key >> shift) & 63, 1024 threads.
 // Wave w owns the contiguous input block [w B, (w + 1) B); per (digit, wave) counts cnt[digit * 16 + w]
 // are scanned digit-major, so the output keeps every digit's elements in input order: within a wave
@@ -3057,17 +2905,9 @@ extern "C" int acn_render_stratified_fwd_ordered(const float* rays, int64_t N, i
     if ((num_cus() & 7) == 0) wgs = (wgs + 7) & ~(int64_t)7;  // whole XCD bands (render_kernel)
     const dim3 grid((unsigned)(wgs < num_cus() ? wgs : num_cus())), block(1024);
     const bool slots = ACN_SLOTS && cfg.routing != 0 && K != 2;  // render_slots_kernel keeps its own order
-    const bool ws = ACN_RENDER_WS && cfg.routing == 0 && S <= kWsMaxS && !(tau > 0.0f);
     if (order_scratch && !slots && N <= ACN_ORDER_MAX && order_bytes >= (size_t)N * sizeof(int32_t)) {
-        // render_ws_kernel derives the order in its prologue when every workgroup's rounds fit ord_loc
-        const int64_t g = (int64_t)grid.x;
-        const int64_t rounds = (g & 7) == 0 ? (((N + 7) >> 3) + 16 * (g >> 3) - 1) / (16 * (g >> 3)) : (N + 16 * g - 1) / (16 * g);
-        if (ws && ACN_WS_SELF_ORDER && rounds <= kWsSelfRounds) {
-            p.self_order = 1;
-        } else {
-            hipLaunchKernelGGL(ray_order_kernel, dim3(1), dim3(1024), 0, s, rays, (int)N, (int32_t*)order_scratch);
-            p.order = (const int32_t*)order_scratch;
-        }
+        hipLaunchKernelGGL(ray_order_kernel, dim3(1), dim3(1024), 0, s, rays, (int)N, (int32_t*)order_scratch);
+        p.order = (const int32_t*)order_scratch;
     }
     const bool wss = ACN_RENDER_WSS && S <= kWssMaxS(8) && !(tau > 0.0f);   // routed, no early termination: depth tiles
     const bool wss16 = ACN_WSS_RAYS16 && S <= kWssMaxS(16);
@@ -3078,7 +2918,7 @@ extern "C" int acn_render_stratified_fwd_ordered(const float* rays, int64_t N, i
         else if (ACN_SLOTS && KL == 0 && R != 0) hipLaunchKernelGGL((render_slots_kernel<I, (R == 0 ? 1 : R)>), grid, dim3(ACN_SLOTS_THREADS), 0, s, cfg, b, p); \
         else hipLaunchKernelGGL((render_kernel<I, KL, R>), grid, block, 0, s, cfg, b, p);            \
     } while (0)
-    if (ws) {
+    if (ACN_RENDER_WS && cfg.routing == 0 && S <= kWsMaxS && !(tau > 0.0f)) {
         // one expert, no early termination: the workgroup shares its rays' field tiles (bit-identical outputs)
         if (interp == 1) hipLaunchKernelGGL(render_ws_kernel<1>, grid, block, 0, s, cfg, b, p);
         else if (interp == 0) hipLaunchKernelGGL(render_ws_kernel<0>, grid, block, 0, s, cfg, b, p);
