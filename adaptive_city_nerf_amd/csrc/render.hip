@@ -368,7 +368,9 @@ __device__ __forceinline__ void layer64x64(const float* W, int seg, int btile, i
 }
 
 #ifndef ACN_HASH_DEPTH
-#define ACN_HASH_DEPTH 2  // levels whose gathers are in flight together (1 = issue + wait per level)
+// levels whose gathers are in flight together (1 = issue + wait per level).  3 with the depth tiles: C2 3.89 -> 3.92e9,
+// C3 2.745 -> 2.755e9 against 2 (profiles/r06ag_hash_depth_ab.jsonl); 1 loses 3-4% on C3 / C4; 4 spills
+#define ACN_HASH_DEPTH 3
 #endif
 
 #ifndef ACN_FIELD_CHECK
