@@ -1286,7 +1286,10 @@ __global__ void __launch_bounds__(256) mlp_bwd_dw_kernel(const float* __restrict
 // accumulators of the same row / column blocks wave w - 4 owned in dw_round and contract the stage.  Per
 // layer: producers put -> barrier -> [producers: dX of the layer | consumers: dW of the layer] -> barrier,
 // so the MFMA-bound contraction overlaps the producers' VALU-bound split / ReLU / dX work instead of
-// following it, and neither role carries the other's registers.  Every wave executes the same barriers per
+// following it, and neither role carries the other's registers.  The barrier that frees the stage for the
+// next round sits at the HEAD of the producers' round (after the forward recompute), not at the end of the
+// previous one, so the consumers' last layer (sigma trunk 0) runs beside the producers' dL/dh0 and their next
+// forward recompute instead of in front of them.  Every wave executes the same barriers per
 // round and the same rounds; with the fp32 stage the sums, their order and every output are those of
 // mlp_bwd_dw_kernel bit for bit (same owners, same stage, same k order).
 //   fp16 stages: the AMP build puts fp16 values unscaled (one plane); the fp16x3 stage (ACN_DW_F16X3 in the
@@ -1304,6 +1307,12 @@ __global__ void __launch_bounds__(256) mlp_bwd_dw_kernel(const float* __restrict
 #define PC_BWD(...) __VA_ARGS__
 #endif
 __device__ __forceinline__ void pc_sync() { __syncthreads(); }
+#ifndef ACN_DW_PRIO
+#define ACN_DW_PRIO 0   // wave priority in mlp_bwd_dw_pc_kernel: 1 producers raised, 2 consumers raised (A/B)
+#endif
+#ifndef ACN_DW_HEADSYNC
+#define ACN_DW_HEADSYNC 1   // the stage-free barrier at the head of the producers' round (0: at the end, round 5)
+#endif
 constexpr bool kPcScaled = (ACN_DW_F16X3 && !ACN_TRAIN_AMP) || ACN_DW_CSPLIT;
 
 template <int NO, int NI>
@@ -1384,6 +1393,7 @@ __device__ __forceinline__ void pc_producer_round(const float* W, float* st, uin
         pc_publish<1, 2>(s0, dRg, C2, w, lane);
         pc_sync();
     }
+    if (ACN_DW_HEADSYNC) pc_sync();   // the consumers have finished the previous round's last layer: stage free
     pc_put<1, 2>(st, dRg, C2, s0, w, lane);
     pc_sync();
     f32x16 G2[2], G1[2], Gc[1];
@@ -1429,17 +1439,18 @@ __device__ __forceinline__ void pc_producer_round(const float* W, float* st, uin
     // sigma trunk 0
     pc_put<2, 1>(st, GA1, X0, s1, w, lane);
     pc_sync();
-    if (gh0) {
+    if (gh0) {   // overlaps the consumers' last layer (and the next round's forward recompute follows)
         PC_BWD(bwd_layer<1, 2, 64, 64>(W + L_W0, S32, GA1, GH, lane));
         store_tiles<1>(gh0, 32, 0, 32, m, ok, h, GH);
     }
-    pc_sync();
+    if (!ACN_DW_HEADSYNC) pc_sync();
 }
 
 __device__ __forceinline__ void pc_consumer_round(const float* st, const uint32_t* smax, int w, int lane, DwAcc& a) {
     const uint32_t* s0 = smax;
     const uint32_t* s1 = smax + 8;
     if (kPcScaled) pc_sync();
+    if (ACN_DW_HEADSYNC) pc_sync();   // stage free (the producers' round-head barrier)
     pc_sync();
     dw_blocks<1>(st, 0, X_ROW + 16 * w, a.aWC2, a.bWC2, pc_scale(s0), lane);
     pc_sync();
@@ -1457,7 +1468,7 @@ __device__ __forceinline__ void pc_consumer_round(const float* st, const uint32_
     pc_sync();
     pc_sync();
     dw_blocks<2>(st, 16 * w, X_ROW, a.aW0, a.bW0, pc_scale(s1), lane);
-    pc_sync();
+    if (!ACN_DW_HEADSYNC) pc_sync();
 }
 
 __global__ void __launch_bounds__(512) mlp_bwd_dw_pc_kernel(const float* __restrict__ img, const float* __restrict__ h0,
@@ -1476,12 +1487,14 @@ __global__ void __launch_bounds__(512) mlp_bwd_dw_pc_kernel(const float* __restr
     // rounds are uniform over the workgroup (the same 12 -- 13 with the scaled stage -- barriers per round in
     // both roles)
     if (wv < 4) {
+        if (ACN_DW_PRIO == 1) __builtin_amdgcn_s_setprio(2);   // the producers' chain is the critical path
         for (int64_t base = (int64_t)blockIdx.x * 4; base < ntiles; base += (int64_t)gridDim.x * 4) {
             const int64_t m = (base + w) * 32 + j;
             pc_producer_round(Wl + opaque_s(0), st_base + opaque_s(0), pc_smax, h0, sh, out, gout, m, m < M, w,
                               opaque_v(lane0), gh0);
         }
     } else {
+        if (ACN_DW_PRIO == 2) __builtin_amdgcn_s_setprio(2);
         DwAcc a;
         dw_zero(a);
         for (int64_t base = (int64_t)blockIdx.x * 4; base < ntiles; base += (int64_t)gridDim.x * 4)

@@ -60,6 +60,53 @@ def test_hashgrid_fwd_bit_exact_vs_reference(name):
     np.testing.assert_array_equal(y.cpu().numpy(), d[f"{name}:y"])
 
 
+@pytest.mark.parametrize("name", ["lin_L16_T20", "smooth_L16_T12", "lin_L4_T19"])
+@pytest.mark.parametrize("M", [1, 63, 65, 1000, 4095])
+def test_hashgrid_fwd_ragged_prefixes_bit_exact(name, M):
+    """Point counts off the level-major kernel's 64-point blocks (hashgrid_fwd_f2_lm) and fewer than 16 levels:
+    every prefix of the fixture batch gives the fixture's rows bit for bit."""
+    ops = _ops()
+    d = G.load("hashgrid")
+    L, mn, mx, log2T, seed, interp = [int(v) for v in d[f"{name}:cfg"]]
+    from adaptive_city_nerf_amd.synthetic import formula_table
+    tab = _t(formula_table(L, log2T, 2, seed=seed, scale=0.5))
+    y = ops.hashgrid_fwd(_t(d["x01"][:M]), tab, d[f"{name}:resolutions"].tolist(), log2T, 2, interp)
+    np.testing.assert_array_equal(y.cpu().numpy(), d[f"{name}:y"][:M])
+
+
+@pytest.mark.parametrize("interp", [1, 2])
+@pytest.mark.parametrize("counts", [(700, 0, 1301), (1, 63, 65), (4096, 5, 2)])
+def test_hashgrid_fwd_pairs_bit_exact_vs_single_table(interp, counts):
+    """The routed training forward (acn_hashgrid_fwd_pairs: slots grouped by expert, each through its expert's
+    table, hashgrid_fwd_pairs_lm) equals acn_hashgrid_fwd of each expert's slice bit for bit, at slot counts off
+    the 64-slot blocks and with an empty expert."""
+    import ctypes as C
+    from adaptive_city_nerf_amd import _lib
+    from adaptive_city_nerf_amd._lib import check, ptr
+    from adaptive_city_nerf_amd.synthetic import formula_table
+    ops = _ops()
+    L, log2T = 16, 14
+    res = O.level_resolutions(L, 16, 2048).tolist()
+    K = len(counts)
+    g = torch.Generator().manual_seed(7)
+    tabs = [_t(formula_table(L, log2T, 2, seed=11 + k, scale=0.5)) for k in range(K)]
+    M = sum(counts)
+    x01 = torch.rand(M, 3, generator=g).to(DEV)
+    pk = torch.cat([torch.full((c,), k, dtype=torch.int32) for k, c in enumerate(counts)]).to(DEV)
+    seg = torch.tensor(np.concatenate([[0], np.cumsum(counts)]), dtype=torch.int64).to(DEV)
+    out = torch.full((M, 2 * L), float("nan"), device=DEV)
+    tp = (C.c_void_p * K)(*[t.data_ptr() for t in tabs])
+    rp = (C.c_int32 * L)(*res)
+    check(_lib.lib().acn_hashgrid_fwd_pairs(ptr(x01), ptr(pk), ptr(seg), K, tp, rp, L, log2T, interp, ptr(out),
+                                            torch.cuda.current_stream().cuda_stream), "acn_hashgrid_fwd_pairs")
+    o = 0
+    for k, c in enumerate(counts):
+        if c:
+            ref = ops.hashgrid_fwd(x01[o:o + c], tabs[k], res, log2T, 2, interp)
+            assert torch.equal(out[o:o + c], ref), f"expert {k}"
+        o += c
+
+
 @pytest.mark.parametrize("name", ["near_L16_T12", "smooth_L16_T12", "lin_L8_T14_r2_512"])
 def test_hashgrid_bwd_vs_reference(name):
     ops = _ops()
