@@ -23,7 +23,9 @@ def parse(paths):
                 continue
             body = line.split("remark:", 1)[1].rsplit("[-Rpass", 1)[0].strip()
             if body.startswith("Function Name:"):
-                cur = body.split(":", 1)[1].strip()
+                # keyed by (object, kernel): the same kernel is built into several objects (the default, exact and
+                # AMP training MLPs share mlp_train.hip), and each object's copy must pass on its own
+                cur = (p, body.split(":", 1)[1].strip())
                 kernels[cur] = {"obj": p}
                 continue
             if cur is None or ":" not in body:
@@ -44,15 +46,15 @@ def main():
     a = ap.parse_args()
     ks = parse(a.remarks)
     bad = []
-    for name, r in sorted(ks.items()):
+    for (obj, name), r in sorted(ks.items(), key=lambda kv: (kv[0][1], kv[0][0])):
         hot = any(h in name for h in HOT)
         if a.all or hot:
             print(f"{'HOT ' if hot else '    '}{r.get('vgpr', '?'):>4} VGPR {r.get('agpr', 0):>3} AGPR "
                   f"{r.get('vspill', 0):>4} spilled {r.get('scratch', 0):>5} B scratch  occ {r.get('occ', '?')}  "
-                  f"{name[:110]}")
+                  f"{name[:100]}  [{obj.rsplit('/', 1)[-1].split('.', 1)[0]}]")
         if hot and (r.get("vspill", 0) or r.get("scratch", 0)):
-            bad.append(name)
-    if not any(any(h in n for h in HOT) for n in ks):
+            bad.append(f"{name} [{obj}]")
+    if not any(any(h in n for _, n in [k] for h in HOT) for k in ks):
         print("spill_guard: no hot kernel found in the remarks", file=sys.stderr)
         return 1
     if bad:
