@@ -549,6 +549,92 @@ __device__ __forceinline__ void tile_forward(const float* Wl, const float* h0, c
     fwd_layer<1, 2, 32>(Wl + L_WC2, S64, Wl + L_BC2, C2, Rg, lane);
 }
 
+#ifndef ACN_FWD_VLOAD
+#define ACN_FWD_VLOAD 0   // mlp_fwd_kernel<false>: the producers' vector h0 / SH loads below (0: per-element loads)
+#endif
+// Prefetched per-sample inputs of the producer waves (mlp_bwd_dw_pc_kernel): whole 16-B vectors at a clamped
+// sample index (no per-element exec branches), issued well ahead of their use and masked for samples past the
+// end only where they are consumed -- a scheduling barrier after the loads keeps the compiler from sinking them
+// to their uses.  The values are those load_tiles / tile_forward / dw_round's output-gradient reads take.
+struct X0Raw {
+    float4 v[4];   // h0 row elements rho(4q .. 4q + 3, h) = 8q + 4h + 0..3
+};
+__device__ __forceinline__ void load_x0raw(const float* __restrict__ h0, int64_t m, bool ok, int h, X0Raw& x) {
+    const float4* p = reinterpret_cast<const float4*>(h0 + (ok ? m : 0) * 32 + 4 * h);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) x.v[q] = p[2 * q];
+}
+__device__ __forceinline__ void x0_tile(const X0Raw& x, bool ok, f32x16 (&X)[1]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        X[0][4 * q] = ok ? x.v[q].x : 0.0f;
+        X[0][4 * q + 1] = ok ? x.v[q].y : 0.0f;
+        X[0][4 * q + 2] = ok ? x.v[q].z : 0.0f;
+        X[0][4 * q + 3] = ok ? x.v[q].w : 0.0f;
+    }
+}
+struct PcIn {      // issued after the forward's first layer (its h0 tile's registers are free by then)
+    float s[9];    // SH row value of accumulator row r = 7 .. 15 (rho(r, h) - 15, clamped; rows r < 7 are geo)
+    float o[3], g[3];   // outputs / output gradients: h == 0 lanes rgb, h == 1 lanes sigma (in all three)
+};
+template <bool OG>   // OG: also the output / output-gradient values (the backward's producers)
+__device__ __forceinline__ void load_pcin(const float* __restrict__ sh, const float* __restrict__ out,
+                                          const float* __restrict__ gout, int64_t m, bool ok, int h, PcIn& in) {
+    const int64_t mc = ok ? m : 0;
+#pragma unroll
+    for (int r = 7; r < 16; ++r) {
+        const int f = rho(r, h) - 15;
+        in.s[r - 7] = sh[mc * 16 + (f < 0 ? 0 : (f > 15 ? 15 : f))];
+    }
+    if (OG) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            in.o[c] = out[mc * 4 + (h ? 3 : c)];
+            in.g[c] = gout[mc * 4 + (h ? 3 : c)];
+        }
+    }
+}
+__device__ __forceinline__ float opaque_f(float v) {   // pins a prefetched value's first use (and its wait) here
+    asm volatile("" : "+v"(v));
+    return v;
+}
+// tile_forward on a prefetched h0 tile, issuing the SH / output loads behind the first layer (bitwise the same
+// layers and values)
+template <bool OG = true>
+__device__ __forceinline__ void tile_forward_x(const float* Wl, const X0Raw& x0, const float* __restrict__ sh,
+                                               const float* __restrict__ out, const float* __restrict__ gout,
+                                               int64_t m, bool ok, int lane, PcIn& in, f32x16 (&A1)[2],
+                                               f32x16 (&A2)[2], f32x16 (&Hd)[1], f32x16 (&Cin)[1],
+                                               f32x16 (&C1)[2], f32x16 (&C2)[2], f32x16 (&Rg)[1]) {
+    const int h = lane >> 5;
+    {
+        f32x16 X0[1];
+        x0_tile(x0, ok, X0);
+        fwd_layer<2, 1, 64>(Wl + L_W0, S32, Wl + L_B0, X0, A1, lane);
+    }
+    relu<2>(A1);
+    __builtin_amdgcn_sched_barrier(0);
+    load_pcin<OG>(sh, out, gout, m, ok, h, in);
+    __builtin_amdgcn_sched_barrier(0);
+    fwd_layer<2, 2, 64>(Wl + L_W1, S64, Wl + L_B1, A1, A2, lane);
+    relu<2>(A2);
+    fwd_layer<1, 2, 32>(Wl + L_WH, S64, Wl + L_BH, A2, Hd, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    float sv[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) sv[k] = opaque_f(in.s[k]);   // unconditional: selects below, no branches
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int f = rho(r, h);
+        Cin[0][r] = f < 15 ? Hd[0][r] : ((ok && f < 31 && r >= 7) ? sv[r >= 7 ? r - 7 : 0] : 0.0f);
+    }
+    fwd_layer<2, 1, 64>(Wl + L_WC0, S32, Wl + L_BC0, Cin, C1, lane);
+    relu<2>(C1);
+    fwd_layer<2, 2, 64>(Wl + L_WC1, S64, Wl + L_BC1, C1, C2, lane);
+    relu<2>(C2);
+    fwd_layer<1, 2, 32>(Wl + L_WC2, S64, Wl + L_BC2, C2, Rg, lane);
+}
+
 // SAVE: write the layer inputs for the split backward (keeps every activation live to the end of the tile:
 // ~250 VGPRs, 4-wave blocks).  The no-save instantiation -- every fused-path call -- needs ~124 registers, so it
 // runs 8-wave blocks: two blocks (the 72 KB weight image each) = four waves per SIMD.
@@ -569,7 +655,15 @@ __global__ void __launch_bounds__(SAVE ? 256 : 512) mlp_fwd_kernel(const float* 
         f32x16 X0[1], A1[2], A2[2], Hd[1], Cin[1], C1[2], C2[2], Rg[1];
         // opaque base: the LDS weight reads are re-issued per tile instead of hoisted out of the loop into
         // ~240 held registers (one wave per SIMD; with it the no-save form fits two)
-        tile_forward(Wl + opaque_s(0), h0, sh, m, ok, lane, X0, A1, A2, Hd, Cin, C1, C2, Rg);
+        if (!SAVE && ACN_FWD_VLOAD) {   // vector loads of h0, SH behind the first layer (no per-element branches)
+            X0Raw x0;
+            load_x0raw(h0, m, ok, h, x0);
+            PcIn in;
+            tile_forward_x<false>(Wl + opaque_s(0), x0, sh, nullptr, nullptr, m, ok, lane, in, A1, A2, Hd, Cin, C1,
+                                  C2, Rg);
+        } else {
+            tile_forward(Wl + opaque_s(0), h0, sh, m, ok, lane, X0, A1, A2, Hd, Cin, C1, C2, Rg);
+        }
         if (ok) {
             if (h == 0) {
 #pragma unroll
@@ -1310,6 +1404,9 @@ __device__ __forceinline__ void pc_sync() { __syncthreads(); }
 #ifndef ACN_DW_PRIO
 #define ACN_DW_PRIO 0   // wave priority in mlp_bwd_dw_pc_kernel: 1 producers raised, 2 consumers raised (A/B)
 #endif
+#ifndef ACN_DW_PREFETCH
+#define ACN_DW_PREFETCH 1   // producers: vector loads of h0 / SH / outputs issued ahead of their use (0: in place)
+#endif
 #ifndef ACN_DW_HEADSYNC
 #define ACN_DW_HEADSYNC 1   // the stage-free barrier at the head of the producers' round (0: at the end, round 5)
 #endif
@@ -1360,14 +1457,23 @@ __device__ __forceinline__ void pc_put(float* st, const f32x16 (&dY)[NO], const 
 __device__ __forceinline__ void pc_producer_round(const float* W, float* st, uint32_t* smax,
                                                   const float* __restrict__ h0, const float* __restrict__ sh,
                                                   const float* __restrict__ out, const float* __restrict__ gout,
-                                                  int64_t m, bool ok, int w, int lane, float* __restrict__ gh0) {
+                                                  int64_t m, bool ok, int w, int lane, float* __restrict__ gh0,
+                                                  X0Raw& X0n, int64_t mn, bool okn) {
     const int h = lane >> 5;
     uint32_t* s0 = smax;
     uint32_t* s1 = smax + 8;
     f32x16 A1[2], A2[2], Hd[1], Cin[1], C1[2], C2[2], Rg[1];
+#if ACN_DW_PREFETCH
+    // X0n holds this round's h0 tile (loaded during the previous round); the SH row and the output / output-
+    // gradient vectors are issued before the forward recompute and consumed after its first layers
+    PcIn in;
+#endif
 #if ACN_DIAG_NOPROD  // diagnostic build only: no forward recompute (zero activations): the consumers' time
     A1[0] = A1[1] = A2[0] = A2[1] = Hd[0] = Cin[0] = C1[0] = C1[1] = C2[0] = C2[1] = Rg[0] = 0.0f;
     (void)sh;
+#elif ACN_DW_PREFETCH
+    tile_forward_x(W, X0n, sh, out, gout, m, ok, lane, in, A1, A2, Hd, Cin, C1, C2, Rg);
+    __builtin_amdgcn_sched_barrier(0);
 #else
     {
         f32x16 X0[1];
@@ -1377,6 +1483,20 @@ __device__ __forceinline__ void pc_producer_round(const float* W, float* st, uin
     f32x16 dRg[1], dHd[1];
     dRg[0] = 0.0f;
     float dsig = 0.0f;
+#if ACN_DW_PREFETCH
+    {   // selects, not a branch: a branch would let the compiler sink the prefetched loads into it
+        const bool rgb = ok && h == 0, sg = ok && h != 0;
+        float gv[3], ov[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            gv[c] = opaque_f(in.g[c]);
+            ov[c] = opaque_f(in.o[c]);
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) dRg[0][c] = rgb ? grad_rgb(gv[c], ov[c]) : 0.0f;
+        dsig = sg ? grad_sigma(gv[0], ov[0]) : 0.0f;
+    }
+#else
     if (ok) {
         if (h == 0) {
 #pragma unroll
@@ -1388,6 +1508,7 @@ __device__ __forceinline__ void pc_producer_round(const float* W, float* st, uin
             dsig = grad_sigma(gout[m * 4 + 3], out[m * 4 + 3]);
         }
     }
+#endif
     // colour head
     if (kPcScaled) {
         pc_publish<1, 2>(s0, dRg, C2, w, lane);
@@ -1430,15 +1551,31 @@ __device__ __forceinline__ void pc_producer_round(const float* W, float* st, uin
     // sigma trunk 1
     pc_put<2, 2>(st, GA2, A1, s0, w, lane);
     pc_sync();
+    f32x16 X0[1];
+#if ACN_DW_PREFETCH
+    X0Raw x0c;
+    load_x0raw(h0, m, ok, h, x0c);   // reloaded (L2-hot) for the last layer, issued before this layer's dX
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     PC_BWD(bwd_layer<2, 2, 64, 64>(W + L_W1, S64, GA2, GA1, lane));
     relu_mask<2>(GA1, A1);
-    f32x16 X0[1];
+#if ACN_DW_PREFETCH
+    __builtin_amdgcn_sched_barrier(0);
+    x0_tile(x0c, ok, X0);
+#else
     load_tiles<1>(h0, 32, 0, 32, m, ok, h, X0);
+#endif
     pc_publish<2, 1>(s1, GA1, X0, w, lane);
     pc_sync();
     // sigma trunk 0
     pc_put<2, 1>(st, GA1, X0, s1, w, lane);
     pc_sync();
+#if ACN_DW_PREFETCH
+    load_x0raw(h0, mn, okn, h, X0n);   // the next round's h0 tile, behind dL/dh0 and the consumers' last layer
+    __builtin_amdgcn_sched_barrier(0);
+#else
+    (void)X0n; (void)mn; (void)okn;
+#endif
     if (gh0) {   // overlaps the consumers' last layer (and the next round's forward recompute follows)
         PC_BWD(bwd_layer<1, 2, 64, 64>(W + L_W0, S32, GA1, GH, lane));
         store_tiles<1>(gh0, 32, 0, 32, m, ok, h, GH);
@@ -1488,10 +1625,18 @@ __global__ void __launch_bounds__(512) mlp_bwd_dw_pc_kernel(const float* __restr
     // both roles)
     if (wv < 4) {
         if (ACN_DW_PRIO == 1) __builtin_amdgcn_s_setprio(2);   // the producers' chain is the critical path
-        for (int64_t base = (int64_t)blockIdx.x * 4; base < ntiles; base += (int64_t)gridDim.x * 4) {
-            const int64_t m = (base + w) * 32 + j;
+        const int64_t step = (int64_t)gridDim.x * 4;
+        X0Raw X0n;
+#if ACN_DW_PREFETCH
+        {
+            const int64_t m0 = ((int64_t)blockIdx.x * 4 + w) * 32 + j;
+            load_x0raw(h0, m0, m0 < M, lane0 >> 5, X0n);
+        }
+#endif
+        for (int64_t base = (int64_t)blockIdx.x * 4; base < ntiles; base += step) {
+            const int64_t m = (base + w) * 32 + j, mn = m + step * 32;
             pc_producer_round(Wl + opaque_s(0), st_base + opaque_s(0), pc_smax, h0, sh, out, gout, m, m < M, w,
-                              opaque_v(lane0), gh0);
+                              opaque_v(lane0), gh0, X0n, mn, mn < M);
         }
     } else {
         if (ACN_DW_PRIO == 2) __builtin_amdgcn_s_setprio(2);
