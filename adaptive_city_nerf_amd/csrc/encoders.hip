@@ -485,16 +485,22 @@ __global__ void __launch_bounds__(256) hashgrid_bwd_merge(const float* __restric
 }
 
 #ifndef ACN_HASH_BWD_MERGE
-// coarse levels merged per workgroup (0: every level on the run-merge kernel).  Off: measured slower on
-// the C5 step (hash backward 0.36 -> 0.76 / 0.79 / 0.89 ms merging 3 / 6 / 8 levels, tools/ab_c5.sh,
-// DESIGN.md 4g) -- a coarse chunk is one workgroup's serial work (few items in flight), and the runs of
-// neighbouring lanes collide on the same LDS entries
+// coarse levels merged per workgroup in the pair-list scatter (C5; 0: every level on the run-merge kernel).  Off:
+// measured slower on the C5 step (hash backward 0.36 -> 0.76 / 0.79 / 0.89 ms merging 3 / 6 / 8 levels,
+// tools/ab_c5.sh) -- a coarse chunk is one workgroup's serial work (few items in flight), and the
+// runs of neighbouring lanes collide on the same LDS entries; it also cannot telescope the clip norm or mark the
+// segment maps the C5 step needs
 #define ACN_HASH_BWD_MERGE 0
 #endif
+#ifndef ACN_HASH_BWD_MERGE_SA
+// the same for the standalone scatter (acn_hashgrid_bwd: the meta-training query step, whose batch is ~6x C5's):
+// 6 merged levels there cut the scatter 855 -> 795 us and the meta step 1.1%
+#define ACN_HASH_BWD_MERGE_SA 6
+#endif
 
-MergeCfg merge_cfg(int L, int log2T) {
+MergeCfg merge_cfg(int L, int log2T, int levels = ACN_HASH_BWD_MERGE) {
     MergeCfg c{};
-    c.LM = ACN_HASH_BWD_MERGE < L ? ACN_HASH_BWD_MERGE : L;
+    c.LM = levels < L ? levels : L;
     if (log2T > 27) c.LM = 0;  // the LDS key holds a 24-bit segment index
     // chunks sized so a chunk's distinct segments stay well under kMergeNE at the reference grid
     // (tools/hash_bwd_analysis.py on the C5 batch: level 0 ~13k segments per 104k slots ... level 5 ~230k)
@@ -562,7 +568,7 @@ extern "C" int acn_hashgrid_bwd(const float* x01, int64_t M, const float* grad_o
     hipStream_t s = (hipStream_t)stream;
     if (F == 2 && interp != 0 && ACN_HASH_BWD_PPL > 0) {
         constexpr int PPL = ACN_HASH_BWD_PPL > 0 ? ACN_HASH_BWD_PPL : 1;
-        const MergeCfg mc = merge_cfg(L, log2T);
+        const MergeCfg mc = merge_cfg(L, log2T, ACN_HASH_BWD_MERGE_SA);
         if (mc.LM > 0) {
             GradTables t{};
             t.t[0] = grad_table;
