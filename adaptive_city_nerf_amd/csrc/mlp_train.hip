@@ -552,6 +552,9 @@ __device__ __forceinline__ void tile_forward(const float* Wl, const float* h0, c
 #ifndef ACN_FWD_VLOAD
 #define ACN_FWD_VLOAD 0   // mlp_fwd_kernel<false>: the producers' vector h0 / SH loads below (0: per-element loads)
 #endif
+#ifndef ACN_DW_PIPE
+#define ACN_DW_PIPE 1   // dw_blocks (fp32 stage): next k-step's LDS reads in flight, blocks' MFMAs interleaved
+#endif
 // Prefetched per-sample inputs of the producer waves (mlp_bwd_dw_pc_kernel): whole 16-B vectors at a clamped
 // sample index (no per-element exec branches), issued well ahead of their use and masked for samples past the
 // end only where they are consumed -- a scheduling barrier after the loads keeps the compiler from sinking them
@@ -1091,6 +1094,34 @@ __device__ __forceinline__ void dw_blocks(const float* st, int arow, int xrow, f
 #else
     (void)sc;
 #endif
+#if ACN_DW_PIPE
+    // software-pipelined: the next k-step's A / B vectors are read while this one's MFMAs run, and the MFMAs
+    // of the NCB independent blocks alternate (each block's own chain keeps its k order: the same sums bit for
+    // bit as the plain loop below)
+    f32x4 a = *reinterpret_cast<const f32x4*>(pa);
+    f32x4 b[NCB];
+#pragma unroll
+    for (int n = 0; n < NCB; ++n) b[n] = *reinterpret_cast<const f32x4*>(pb + 16 * n * SW);
+#pragma unroll
+    for (int k4 = 0; k4 < 8; ++k4) {
+        f32x4 an = a, bn[NCB];
+#pragma unroll
+        for (int n = 0; n < NCB; ++n) bn[n] = b[n];
+        if (k4 < 7) {
+            an = *reinterpret_cast<const f32x4*>(pa + 4 * (k4 + 1));
+#pragma unroll
+            for (int n = 0; n < NCB; ++n) bn[n] = *reinterpret_cast<const f32x4*>(pb + 16 * n * SW + 4 * (k4 + 1));
+        }
+        bsum += (a[0] + a[1]) + (a[2] + a[3]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int n = 0; n < NCB; ++n) acc[n] = mfma16(a[e], b[n][e], acc[n]);
+        a = an;
+#pragma unroll
+        for (int n = 0; n < NCB; ++n) b[n] = bn[n];
+    }
+#else
 #pragma unroll
     for (int k4 = 0; k4 < 8; ++k4) {
         const f32x4 a = *reinterpret_cast<const f32x4*>(pa + 4 * k4);
@@ -1104,6 +1135,7 @@ __device__ __forceinline__ void dw_blocks(const float* st, int arow, int xrow, f
             acc[n] = mfma16(a[3], b[3], acc[n]);
         }
     }
+#endif
 }
 
 // one layer's stage round: barrier (previous readers done), put dY / X, barrier
@@ -1747,6 +1779,69 @@ __global__ void __launch_bounds__(256) mlp_fwd_pairs_kernel(const float* __restr
     }
 }
 
+// Producer / consumer form of the pair-list backward (the routed container's C5 step): mlp_bwd_dw_pc_kernel's
+// roles, barriers and prefetch over mlp_bwd_dw_pairs_kernel's contiguous round range per workgroup.  When the
+// expert of the next round differs, both roles pass two barriers around the restaging of that expert's image
+// (the consumers first write their running sums to copy (b, expert) and restart), so the barrier sequence
+// stays the same in both roles.  Same owners, same stage, same k order as dw_round: bitwise the outputs of
+// mlp_bwd_dw_pairs_kernel.
+#ifndef ACN_DW_PAIRS_PC
+#define ACN_DW_PAIRS_PC 0
+#endif
+__global__ void __launch_bounds__(512) mlp_bwd_dw_pairs_pc_kernel(const float* __restrict__ imgs,
+                                                                  const float* __restrict__ h0,
+                                                                  const float* __restrict__ sh,
+                                                                  const float* __restrict__ out,
+                                                                  const float* __restrict__ gout,
+                                                                  const int64_t* __restrict__ seg, int K,
+                                                                  float* __restrict__ gh0, float* __restrict__ partial) {
+    __shared__ __attribute__((aligned(16))) float Wl[L_FLOATS];
+    __shared__ __attribute__((aligned(16))) float st_base[ST_FLOATS];
+    __shared__ uint32_t pc_smax[16];
+    stage_init(st_base);   // published by the staging barriers of the first round
+    const int lane0 = threadIdx.x & 63, j = lane0 & 31;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), w = wv & 3;
+    const int64_t R = seg[K] / 128, G = gridDim.x;
+    const int64_t r0 = (int64_t)blockIdx.x * R / G, r1 = ((int64_t)blockIdx.x + 1) * R / G;
+    int cur = -1;
+    if (wv < 4) {
+        X0Raw X0n;
+#if ACN_DW_PREFETCH
+        if (r0 < r1) load_x0raw(h0, (r0 * 4 + w) * 32 + j, true, lane0 >> 5, X0n);
+#endif
+        for (int64_t rd = r0; rd < r1; ++rd) {
+            const int k = seg_expert(seg, K, rd * 128);
+            if (k != cur) {
+                __syncthreads();
+                stage_weights(imgs + (int64_t)k * L_FLOATS, Wl);
+                __syncthreads();
+                cur = k;
+            }
+            const int64_t m = (rd * 4 + w) * 32 + j, mn = m + 128;
+            pc_producer_round(Wl + opaque_s(0), st_base + opaque_s(0), pc_smax, h0, sh, out, gout, m, true, w,
+                              opaque_v(lane0), gh0, X0n, mn, rd + 1 < r1);
+        }
+    } else {
+        DwAcc a;
+        dw_zero(a);
+        for (int64_t rd = r0; rd < r1; ++rd) {
+            const int k = seg_expert(seg, K, rd * 128);
+            if (k != cur) {
+                if (cur >= 0) {
+                    dw_flush(a, partial + ((int64_t)blockIdx.x * K + cur) * NDW, w, lane0);
+                    dw_zero(a);
+                }
+                __syncthreads();
+                stage_weights(imgs + (int64_t)k * L_FLOATS, Wl);
+                __syncthreads();
+                cur = k;
+            }
+            pc_consumer_round(st_base + opaque_s(0), pc_smax, w, opaque_v(lane0), a);
+        }
+        if (cur >= 0) dw_flush(a, partial + ((int64_t)blockIdx.x * K + cur) * NDW, w, lane0);
+    }
+}
+
 // dw[k][e] = sum over the workgroups b whose round range [b R / G, (b+1) R / G) met expert k's rounds of
 // copy (b, k); zero for an expert without pairs.  grid (NDW / 32, K)
 __global__ void __launch_bounds__(256) mlp_dw_reduce_pairs_kernel(const float* __restrict__ partial,
@@ -1922,8 +2017,12 @@ extern "C" int ACN_MLP_API(acn_mlp_train_bwd_dw_pairs)(const float* h0, const fl
     const float* imgs = (const float*)workspace;
     float* partial = (float*)workspace + (size_t)K * L_FLOATS;
     hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(mlp_bwd_dw_pairs_kernel, dim3(PAIR_DW_BLOCKS), dim3(256), 0, s, imgs, h0, sh, out, gout, seg, K,
-                       gh0, partial);
+    if (ACN_DW_PAIRS_PC)
+        hipLaunchKernelGGL(mlp_bwd_dw_pairs_pc_kernel, dim3(PAIR_DW_BLOCKS), dim3(512), 0, s, imgs, h0, sh, out, gout,
+                           seg, K, gh0, partial);
+    else
+        hipLaunchKernelGGL(mlp_bwd_dw_pairs_kernel, dim3(PAIR_DW_BLOCKS), dim3(256), 0, s, imgs, h0, sh, out, gout,
+                           seg, K, gh0, partial);
     hipLaunchKernelGGL(mlp_dw_reduce_pairs_kernel, dim3((NDW + 31) / 32, K), dim3(256), 0, s, (const float*)partial,
                        seg, K, PAIR_DW_BLOCKS, dw);
     return acn_check_launch("acn_mlp_train_bwd_dw_pairs");

@@ -10,7 +10,8 @@ MLP backward.  --all lists every kernel with its VGPRs, spills and scratch.
 """
 import argparse, re, sys
 
-HOT = ("render_ws_kernel", "render_slots_kernel", "render_wss_kernel", "ep_field_kernel", "mlp_bwd_dw_pc_kernel")
+HOT = ("render_ws_kernel", "render_slots_kernel", "render_wss_kernel", "ep_field_kernel", "mlp_bwd_dw_pc_kernel",
+       "mlp_bwd_dw_pairs_pc_kernel")
 FIELDS = {"VGPRs": "vgpr", "AGPRs": "agpr", "ScratchSize [bytes/lane]": "scratch", "VGPRs Spill": "vspill",
           "SGPRs Spill": "sspill", "Occupancy [waves/SIMD]": "occ"}
 
