@@ -286,6 +286,11 @@ __device__ __forceinline__ f16x8 cat44(const f16x4& a, const f16x4& b) {
     return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
+#ifndef ACN_MLP_ILV
+// fp16x3 layer products: the output tiles' MFMA chains interleaved per k-step.  Off: meta 61.73 -> 62.03 ms with
+// it (the producers of mlp_bwd_dw_pc_kernel 214 -> 217.5 us), C5 1.743 -> 1.728 ms
+#define ACN_MLP_ILV 0
+#endif
 // Y[to] (rows 32to..) = b + W . X  (W: hi / lo planes of 32*NT padded rows, ld = stride in halves,
 // ROWS = rows of the region; X: KT input tiles)
 template <int NT, int KT, int ROWS>
@@ -319,6 +324,32 @@ __device__ __forceinline__ void fwd_layer(const float* W, int ld, const float* b
     acn::opnd_fence_n<2 * KT>(bh, bl);
     const _Float16* Wh = reinterpret_cast<const _Float16*>(W);
     const _Float16* Wlo = Wh + ROWS * ld;
+#if ACN_MLP_ILV
+    // the NT output tiles' chains interleaved, k-step by k-step, with the k-step's A operands of every tile read
+    // first (each tile's own chain keeps its order: the same sums bit for bit); Y is the accumulator
+#pragma unroll
+    for (int to = 0; to < NT; ++to) Y[to] = 0.0f;
+#pragma unroll
+    for (int s = 0; s < 2 * KT; ++s) {
+        f16x8 ahi[NT], alo[NT];
+#pragma unroll
+        for (int to = 0; to < NT; ++to) {
+            const int c0 = (32 * to + i) * ld + 32 * (s >> 1) + 16 * (s & 1) + 4 * h;
+            ahi[to] = cat44(*reinterpret_cast<const f16x4*>(Wh + c0), *reinterpret_cast<const f16x4*>(Wh + c0 + 8));
+            alo[to] = cat44(*reinterpret_cast<const f16x4*>(Wlo + c0), *reinterpret_cast<const f16x4*>(Wlo + c0 + 8));
+        }
+#pragma unroll
+        for (int to = 0; to < NT; ++to) Y[to] = mfma_h(alo[to], bh[s], Y[to]);
+#pragma unroll
+        for (int to = 0; to < NT; ++to) Y[to] = mfma_h(ahi[to], bl[s], Y[to]);
+#pragma unroll
+        for (int to = 0; to < NT; ++to) Y[to] = mfma_h(ahi[to], bh[s], Y[to]);
+    }
+#pragma unroll
+    for (int to = 0; to < NT; ++to)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) Y[to][r] = __builtin_fmaf(Y[to][r], usc, b[32 * to + rho(r, h)]);
+#else
 #pragma unroll
     for (int to = 0; to < NT; ++to) {
         const int ro = (32 * to + i) * ld;
@@ -336,6 +367,7 @@ __device__ __forceinline__ void fwd_layer(const float* W, int ld, const float* b
 #pragma unroll
         for (int r = 0; r < 16; ++r) Y[to][r] = __builtin_fmaf(acc[r], usc, b[32 * to + rho(r, h)]);
     }
+#endif
 #endif
 }
 
@@ -375,6 +407,33 @@ __device__ __forceinline__ void bwd_layer(const float* W, int ld, const f32x16 (
     const _Float16* Wlo = Wh + ROWS * ld;
 #if ACN_BWD_TR16
     const int trow = 4 * h + ((lane >> 2) & 3), tcol = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+#endif
+#if ACN_MLP_ILV && ACN_BWD_TR16 && !ACN_TRAIN_AMP
+    // as fwd_layer: the NT input tiles' chains interleaved per k-step, operands read first; dX is the accumulator
+#pragma unroll
+    for (int ti = 0; ti < NT; ++ti) dX[ti] = 0.0f;
+#pragma unroll
+    for (int s = 0; s < 2 * KT; ++s) {
+        if (32 * (s >> 1) + 16 * (s & 1) >= NROW) continue;
+        f16x8 ahi[NT], alo[NT];
+#pragma unroll
+        for (int ti = 0; ti < NT; ++ti) {
+            const int o = (32 * (s >> 1) + 16 * (s & 1) + trow) * ld + 32 * ti + tcol;
+            ahi[ti] = cat44(ds_read_tr16(Wh + o), ds_read_tr16(Wh + o + 8 * ld));
+            alo[ti] = cat44(ds_read_tr16(Wlo + o), ds_read_tr16(Wlo + o + 8 * ld));
+        }
+#pragma unroll
+        for (int ti = 0; ti < NT; ++ti) dX[ti] = mfma_h(alo[ti], bh[s], dX[ti]);
+#pragma unroll
+        for (int ti = 0; ti < NT; ++ti) dX[ti] = mfma_h(ahi[ti], bl[s], dX[ti]);
+#pragma unroll
+        for (int ti = 0; ti < NT; ++ti) dX[ti] = mfma_h(ahi[ti], bh[s], dX[ti]);
+    }
+#pragma unroll
+    for (int ti = 0; ti < NT; ++ti)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dX[ti][r] = dX[ti][r] * usc;
+    return;
 #endif
 #pragma unroll
     for (int ti = 0; ti < NT; ++ti) {
@@ -1786,8 +1845,12 @@ __global__ void __launch_bounds__(256) mlp_fwd_pairs_kernel(const float* __restr
 // stays the same in both roles.  Same owners, same stage, same k order as dw_round: bitwise the outputs of
 // mlp_bwd_dw_pairs_kernel.
 #ifndef ACN_DW_PAIRS_PC
+// Off: measured C5 1.728 -> 1.705 ms (kernel 115.8 -> 90.2 us, profiles/r06ap_*, tests green), but in this kernel the
+// register allocator renames the consumers' accumulators and leaves a VGPR write 6 wait states after an
+// MFMA that reads it as C -- LLVM's minimum, one under tests/test_hazard_audit.py's margin
 #define ACN_DW_PAIRS_PC 0
 #endif
+#if ACN_DW_PAIRS_PC
 __global__ void __launch_bounds__(512) mlp_bwd_dw_pairs_pc_kernel(const float* __restrict__ imgs,
                                                                   const float* __restrict__ h0,
                                                                   const float* __restrict__ sh,
@@ -1803,44 +1866,41 @@ __global__ void __launch_bounds__(512) mlp_bwd_dw_pairs_pc_kernel(const float* _
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), w = wv & 3;
     const int64_t R = seg[K] / 128, G = gridDim.x;
     const int64_t r0 = (int64_t)blockIdx.x * R / G, r1 = ((int64_t)blockIdx.x + 1) * R / G;
-    int cur = -1;
+    // one pass per run of rounds of one expert: both roles restage that expert's image between two barriers, the
+    // consumers zero their sums before the run and write copy (b, expert) after it (no accumulator state
+    // crosses a run, so the compiler keeps the sums in place)
+    int64_t rd = r0;
     if (wv < 4) {
         X0Raw X0n;
 #if ACN_DW_PREFETCH
         if (r0 < r1) load_x0raw(h0, (r0 * 4 + w) * 32 + j, true, lane0 >> 5, X0n);
 #endif
-        for (int64_t rd = r0; rd < r1; ++rd) {
+        while (rd < r1) {
             const int k = seg_expert(seg, K, rd * 128);
-            if (k != cur) {
-                __syncthreads();
-                stage_weights(imgs + (int64_t)k * L_FLOATS, Wl);
-                __syncthreads();
-                cur = k;
+            __syncthreads();
+            stage_weights(imgs + (int64_t)k * L_FLOATS, Wl);
+            __syncthreads();
+            for (; rd < r1 && seg_expert(seg, K, rd * 128) == k; ++rd) {
+                const int64_t m = (rd * 4 + w) * 32 + j, mn = m + 128;
+                pc_producer_round(Wl + opaque_s(0), st_base + opaque_s(0), pc_smax, h0, sh, out, gout, m, true, w,
+                                  opaque_v(lane0), gh0, X0n, mn, rd + 1 < r1);
             }
-            const int64_t m = (rd * 4 + w) * 32 + j, mn = m + 128;
-            pc_producer_round(Wl + opaque_s(0), st_base + opaque_s(0), pc_smax, h0, sh, out, gout, m, true, w,
-                              opaque_v(lane0), gh0, X0n, mn, rd + 1 < r1);
         }
     } else {
-        DwAcc a;
-        dw_zero(a);
-        for (int64_t rd = r0; rd < r1; ++rd) {
+        while (rd < r1) {
             const int k = seg_expert(seg, K, rd * 128);
-            if (k != cur) {
-                if (cur >= 0) {
-                    dw_flush(a, partial + ((int64_t)blockIdx.x * K + cur) * NDW, w, lane0);
-                    dw_zero(a);
-                }
-                __syncthreads();
-                stage_weights(imgs + (int64_t)k * L_FLOATS, Wl);
-                __syncthreads();
-                cur = k;
-            }
-            pc_consumer_round(st_base + opaque_s(0), pc_smax, w, opaque_v(lane0), a);
+            __syncthreads();
+            stage_weights(imgs + (int64_t)k * L_FLOATS, Wl);
+            __syncthreads();
+            DwAcc a;
+            dw_zero(a);
+            for (; rd < r1 && seg_expert(seg, K, rd * 128) == k; ++rd)
+                pc_consumer_round(st_base + opaque_s(0), pc_smax, w, opaque_v(lane0), a);
+            dw_flush(a, partial + ((int64_t)blockIdx.x * K + k) * NDW, w, lane0);
         }
-        if (cur >= 0) dw_flush(a, partial + ((int64_t)blockIdx.x * K + cur) * NDW, w, lane0);
     }
 }
+#endif
 
 // dw[k][e] = sum over the workgroups b whose round range [b R / G, (b+1) R / G) met expert k's rounds of
 // copy (b, k); zero for an expert without pairs.  grid (NDW / 32, K)
@@ -2017,12 +2077,13 @@ extern "C" int ACN_MLP_API(acn_mlp_train_bwd_dw_pairs)(const float* h0, const fl
     const float* imgs = (const float*)workspace;
     float* partial = (float*)workspace + (size_t)K * L_FLOATS;
     hipStream_t s = (hipStream_t)stream;
-    if (ACN_DW_PAIRS_PC)
-        hipLaunchKernelGGL(mlp_bwd_dw_pairs_pc_kernel, dim3(PAIR_DW_BLOCKS), dim3(512), 0, s, imgs, h0, sh, out, gout,
-                           seg, K, gh0, partial);
-    else
-        hipLaunchKernelGGL(mlp_bwd_dw_pairs_kernel, dim3(PAIR_DW_BLOCKS), dim3(256), 0, s, imgs, h0, sh, out, gout,
-                           seg, K, gh0, partial);
+#if ACN_DW_PAIRS_PC
+    hipLaunchKernelGGL(mlp_bwd_dw_pairs_pc_kernel, dim3(PAIR_DW_BLOCKS), dim3(512), 0, s, imgs, h0, sh, out, gout, seg, K,
+                       gh0, partial);
+#else
+    hipLaunchKernelGGL(mlp_bwd_dw_pairs_kernel, dim3(PAIR_DW_BLOCKS), dim3(256), 0, s, imgs, h0, sh, out, gout, seg, K,
+                       gh0, partial);
+#endif
     hipLaunchKernelGGL(mlp_dw_reduce_pairs_kernel, dim3((NDW + 31) / 32, K), dim3(256), 0, s, (const float*)partial,
                        seg, K, PAIR_DW_BLOCKS, dw);
     return acn_check_launch("acn_mlp_train_bwd_dw_pairs");
