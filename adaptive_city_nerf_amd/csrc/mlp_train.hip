@@ -970,7 +970,7 @@ __device__ __forceinline__ void stage_put(float* st, int row0, const f32x16 (&T)
 // acc[n] += dY[16 rows from arow] . X[16 features from xrow + 16 n]^T over the 128 staged samples,
 // bacc (column 0) += the dY rows' sums; lane (i = l & 15, q = l >> 4) supplies k-elements = samples
 // 32 q + 4 t + 0..3 of k-step t
-template <int NCB>
+template <int NCB, bool PIPE = false>   // PIPE: the fp32 stage's option (unused on the fp16 stage)
 __device__ __forceinline__ void dw_blocks(const float* st, int arow, int xrow, f32x4 (&acc)[NCB], BiasAcc& bacc,
                                           StageScale sc, int lane) {
 #if ACN_DIAG_NODW  // diagnostic build only: no weight-gradient contraction
@@ -1115,7 +1115,7 @@ __device__ __forceinline__ void split4(const f32x4& x, float sc, f16x4d& hi, f16
 // acc[n] += dY[16 rows from arow] . X[16 features from xrow + 16 n]^T over the 128 staged samples;
 // lane (i = l & 15, q = l >> 4) supplies k = sample 32 q + kk (4 k-steps per 16-B read).  bsum += this
 // lane's share of the bias row sum (the A operand is dY itself).
-template <int NCB>
+template <int NCB, bool PIPE = (ACN_DW_PIPE != 0)>
 __device__ __forceinline__ void dw_blocks(const float* st, int arow, int xrow, f32x4 (&acc)[NCB], float& bsum,
                                           StageScale sc, int lane) {
 #if ACN_DIAG_NODW  // diagnostic build only: no weight-gradient contraction
@@ -1153,7 +1153,7 @@ __device__ __forceinline__ void dw_blocks(const float* st, int arow, int xrow, f
 #else
     (void)sc;
 #endif
-#if ACN_DW_PIPE
+    if (PIPE) {
     // software-pipelined: the next k-step's A / B vectors are read while this one's MFMAs run, and the MFMAs
     // of the NCB independent blocks alternate (each block's own chain keeps its k order: the same sums bit for
     // bit as the plain loop below)
@@ -1180,7 +1180,8 @@ __device__ __forceinline__ void dw_blocks(const float* st, int arow, int xrow, f
 #pragma unroll
         for (int n = 0; n < NCB; ++n) b[n] = bn[n];
     }
-#else
+    return;
+    }
 #pragma unroll
     for (int k4 = 0; k4 < 8; ++k4) {
         const f32x4 a = *reinterpret_cast<const f32x4*>(pa + 4 * k4);
@@ -1194,7 +1195,6 @@ __device__ __forceinline__ void dw_blocks(const float* st, int arow, int xrow, f
             acc[n] = mfma16(a[3], b[3], acc[n]);
         }
     }
-#endif
 }
 
 // one layer's stage round: barrier (previous readers done), put dY / X, barrier
@@ -1674,28 +1674,29 @@ __device__ __forceinline__ void pc_producer_round(const float* W, float* st, uin
     if (!ACN_DW_HEADSYNC) pc_sync();
 }
 
+template <bool PIPE = (ACN_DW_PIPE != 0)>
 __device__ __forceinline__ void pc_consumer_round(const float* st, const uint32_t* smax, int w, int lane, DwAcc& a) {
     const uint32_t* s0 = smax;
     const uint32_t* s1 = smax + 8;
     if (kPcScaled) pc_sync();
     if (ACN_DW_HEADSYNC) pc_sync();   // stage free (the producers' round-head barrier)
     pc_sync();
-    dw_blocks<1>(st, 0, X_ROW + 16 * w, a.aWC2, a.bWC2, pc_scale(s0), lane);
+    dw_blocks<1, PIPE>(st, 0, X_ROW + 16 * w, a.aWC2, a.bWC2, pc_scale(s0), lane);
     pc_sync();
     pc_sync();
-    dw_blocks<4>(st, 16 * w, X_ROW, a.aWC1, a.bWC1, pc_scale(s1), lane);
+    dw_blocks<4, PIPE>(st, 16 * w, X_ROW, a.aWC1, a.bWC1, pc_scale(s1), lane);
     pc_sync();
     pc_sync();
-    dw_blocks<2>(st, 16 * w, X_ROW, a.aWC0, a.bWC0, pc_scale(s0), lane);
+    dw_blocks<2, PIPE>(st, 16 * w, X_ROW, a.aWC0, a.bWC0, pc_scale(s0), lane);
     pc_sync();
     pc_sync();
-    dw_blocks<1>(st, 0, X_ROW + 16 * w, a.aHD, a.bHD, pc_scale(s1), lane);
+    dw_blocks<1, PIPE>(st, 0, X_ROW + 16 * w, a.aHD, a.bHD, pc_scale(s1), lane);
     pc_sync();
     pc_sync();
-    dw_blocks<4>(st, 16 * w, X_ROW, a.aW1, a.bW1, pc_scale(s0), lane);
+    dw_blocks<4, PIPE>(st, 16 * w, X_ROW, a.aW1, a.bW1, pc_scale(s0), lane);
     pc_sync();
     pc_sync();
-    dw_blocks<2>(st, 16 * w, X_ROW, a.aW0, a.bW0, pc_scale(s1), lane);
+    dw_blocks<2, PIPE>(st, 16 * w, X_ROW, a.aW0, a.bW0, pc_scale(s1), lane);
     if (!ACN_DW_HEADSYNC) pc_sync();
 }
 
@@ -1845,10 +1846,7 @@ __global__ void __launch_bounds__(256) mlp_fwd_pairs_kernel(const float* __restr
 // stays the same in both roles.  Same owners, same stage, same k order as dw_round: bitwise the outputs of
 // mlp_bwd_dw_pairs_kernel.
 #ifndef ACN_DW_PAIRS_PC
-// Off: measured C5 1.728 -> 1.705 ms (kernel 115.8 -> 90.2 us, profiles/r06ap_*, tests green), but in this kernel the
-// register allocator renames the consumers' accumulators and leaves a VGPR write 6 wait states after an
-// MFMA that reads it as C -- LLVM's minimum, one under tests/test_hazard_audit.py's margin
-#define ACN_DW_PAIRS_PC 0
+#define ACN_DW_PAIRS_PC 1   // 0: mlp_bwd_dw_pairs_kernel (one role per wave)
 #endif
 #if ACN_DW_PAIRS_PC
 __global__ void __launch_bounds__(512) mlp_bwd_dw_pairs_pc_kernel(const float* __restrict__ imgs,
@@ -1895,7 +1893,9 @@ __global__ void __launch_bounds__(512) mlp_bwd_dw_pairs_pc_kernel(const float* _
             DwAcc a;
             dw_zero(a);
             for (; rd < r1 && seg_expert(seg, K, rd * 128) == k; ++rd)
-                pc_consumer_round(st_base + opaque_s(0), pc_smax, w, opaque_v(lane0), a);
+                // the unpipelined contraction: the pipelined one's register allocation here leaves a 6-state
+                // WAR-on-C gap under tests/test_hazard_audit.py's margin
+                pc_consumer_round<false>(st_base + opaque_s(0), pc_smax, w, opaque_v(lane0), a);
             dw_flush(a, partial + ((int64_t)blockIdx.x * K + k) * NDW, w, lane0);
         }
     }
