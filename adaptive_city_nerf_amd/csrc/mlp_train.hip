@@ -81,6 +81,8 @@ constexpr int L_W0 = 0, L_W1 = L_W0 + 64 * S32, L_WH = L_W1 + 64 * S64, L_WC0 = 
               L_WC2 = L_WC1 + 64 * S64, L_B0 = L_WC2 + 32 * S64, L_B1 = L_B0 + 64, L_BH = L_B1 + 64, L_BC0 = L_BH + 32,
               L_BC1 = L_BC0 + 64, L_BC2 = L_BC1 + 64, L_FLOATS = L_BC2 + 32;
 static_assert(L_FLOATS % 4 == 0, "16-B staging");
+static_assert(L_B0 % 4 == 0 && L_B1 % 4 == 0 && L_BH % 4 == 0 && L_BC0 % 4 == 0 && L_BC1 % 4 == 0 && L_BC2 % 4 == 0,
+              "16-B bias reads (fwd_layer)");
 
 struct MlpPtrs {
     const float *w0, *b0, *w1, *b1, *wsh, *bsh, *wg, *bg, *wc0, *bc0, *wc1, *bc1, *wc2, *bc2;
@@ -286,6 +288,9 @@ __device__ __forceinline__ f16x8 cat44(const f16x4& a, const f16x4& b) {
     return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
+#ifndef ACN_MLP_BIASV
+#define ACN_MLP_BIASV 1   // fp16x3 fwd_layer epilogue: 16-B bias reads (0: one LDS read per element)
+#endif
 #ifndef ACN_MLP_ILV
 // fp16x3 layer products: the output tiles' MFMA chains interleaved per k-step.  Off: meta 61.73 -> 62.03 ms with
 // it (the producers of mlp_bwd_dw_pc_kernel 214 -> 217.5 us), C5 1.743 -> 1.728 ms
@@ -363,9 +368,21 @@ __device__ __forceinline__ void fwd_layer(const float* W, int ld, const float* b
             acc = mfma_h(ahi, bl[s], acc);
             acc = mfma_h(ahi, bh[s], acc);
         }
-        // acc * 2^-k + b in one rounding (the scaling itself is exact)
+        // acc * 2^-k + b in one rounding (the scaling itself is exact); the bias rows rho(4q .. 4q + 3, h) are 4
+        // consecutive floats, read as one 16-B vector each (the image's bias regions are 16-B aligned)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) Y[to][r] = __builtin_fmaf(acc[r], usc, b[32 * to + rho(r, h)]);
+        for (int q = 0; q < 4; ++q) {
+#if ACN_MLP_BIASV
+            typedef float f32x4b __attribute__((ext_vector_type(4)));
+            const f32x4b bv = *reinterpret_cast<const f32x4b*>(b + 32 * to + 8 * q + 4 * h);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) Y[to][4 * q + e] = __builtin_fmaf(acc[4 * q + e], usc, bv[e]);
+#else
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                Y[to][4 * q + e] = __builtin_fmaf(acc[4 * q + e], usc, b[32 * to + rho(4 * q + e, h)]);
+#endif
+        }
     }
 #endif
 #endif
