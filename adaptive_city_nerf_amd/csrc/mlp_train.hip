@@ -288,6 +288,9 @@ __device__ __forceinline__ f16x8 cat44(const f16x4& a, const f16x4& b) {
     return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
+#ifndef ACN_MLP_KPIPE
+#define ACN_MLP_KPIPE 1   // fp16x3 fwd_layer / bwd_layer: the next k-step's A operands read ahead (0: at their k-step)
+#endif
 #ifndef ACN_MLP_BIASV
 #define ACN_MLP_BIASV 1   // fp16x3 fwd_layer epilogue: 16-B bias reads (0: one LDS read per element)
 #endif
@@ -359,6 +362,26 @@ __device__ __forceinline__ void fwd_layer(const float* W, int ld, const float* b
     for (int to = 0; to < NT; ++to) {
         const int ro = (32 * to + i) * ld;
         f32x16 acc = 0.0f;
+#if ACN_MLP_KPIPE
+        // the next k-step's A operands are read while this k-step's MFMAs run (same chain, same order)
+        auto lda = [&](int s, f16x8& ahi, f16x8& alo) {
+            const int c0 = ro + 32 * (s >> 1) + 16 * (s & 1) + 4 * h;
+            ahi = cat44(*reinterpret_cast<const f16x4*>(Wh + c0), *reinterpret_cast<const f16x4*>(Wh + c0 + 8));
+            alo = cat44(*reinterpret_cast<const f16x4*>(Wlo + c0), *reinterpret_cast<const f16x4*>(Wlo + c0 + 8));
+        };
+        f16x8 ahi, alo;
+        lda(0, ahi, alo);
+#pragma unroll
+        for (int s = 0; s < 2 * KT; ++s) {
+            f16x8 nhi = ahi, nlo = alo;
+            if (s + 1 < 2 * KT) lda(s + 1, nhi, nlo);
+            acc = mfma_h(alo, bh[s], acc);
+            acc = mfma_h(ahi, bl[s], acc);
+            acc = mfma_h(ahi, bh[s], acc);
+            ahi = nhi;
+            alo = nlo;
+        }
+#else
 #pragma unroll
         for (int s = 0; s < 2 * KT; ++s) {
             const int c0 = ro + 32 * (s >> 1) + 16 * (s & 1) + 4 * h;
@@ -368,6 +391,7 @@ __device__ __forceinline__ void fwd_layer(const float* W, int ld, const float* b
             acc = mfma_h(ahi, bl[s], acc);
             acc = mfma_h(ahi, bh[s], acc);
         }
+#endif
         // acc * 2^-k + b in one rounding (the scaling itself is exact); the bias rows rho(4q .. 4q + 3, h) are 4
         // consecutive floats, read as one 16-B vector each (the image's bias regions are 16-B aligned)
 #pragma unroll
@@ -450,6 +474,34 @@ __device__ __forceinline__ void bwd_layer(const float* W, int ld, const f32x16 (
     for (int ti = 0; ti < NT; ++ti)
 #pragma unroll
         for (int r = 0; r < 16; ++r) dX[ti][r] = dX[ti][r] * usc;
+    return;
+#endif
+#if ACN_MLP_KPIPE && ACN_BWD_TR16 && !ACN_TRAIN_AMP
+    // as fwd_layer: the next live k-step's A operands are read while this k-step's MFMAs run (same chain, order)
+#pragma unroll
+    for (int ti = 0; ti < NT; ++ti) {
+        auto ldb = [&](int s, f16x8& ahi, f16x8& alo) {
+            const int o = (32 * (s >> 1) + 16 * (s & 1) + trow) * ld + 32 * ti + tcol;
+            ahi = cat44(ds_read_tr16(Wh + o), ds_read_tr16(Wh + o + 8 * ld));
+            alo = cat44(ds_read_tr16(Wlo + o), ds_read_tr16(Wlo + o + 8 * ld));
+        };
+        f32x16 acc = 0.0f;
+        f16x8 ahi, alo;
+        ldb(0, ahi, alo);
+#pragma unroll
+        for (int s = 0; s < 2 * KT; ++s) {
+            if (32 * (s >> 1) + 16 * (s & 1) >= NROW) continue;
+            f16x8 nhi = ahi, nlo = alo;
+            if (s + 1 < 2 * KT && 32 * ((s + 1) >> 1) + 16 * ((s + 1) & 1) < NROW) ldb(s + 1, nhi, nlo);
+            acc = mfma_h(alo, bh[s], acc);
+            acc = mfma_h(ahi, bl[s], acc);
+            acc = mfma_h(ahi, bh[s], acc);
+            ahi = nhi;
+            alo = nlo;
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dX[ti][r] = acc[r] * usc;
+    }
     return;
 #endif
 #pragma unroll
